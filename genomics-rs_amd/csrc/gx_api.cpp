@@ -1,0 +1,939 @@
+// gx_api.cpp -- host side of the C ABI (include/gx.h).
+//
+// Mirrors the reference's alignment API (nlaha/genomics-rs):
+//   alignment_table  src/alignment/algo.rs:151-282  -> gx_alignment_table
+//   retrace          src/alignment/algo.rs:287-441  -> gx_retrace
+// The DP fill and the interior traceback walk run on the GPU
+// (gx_kernels.hip); this file owns device memory, the exact-int32 range
+// guard, the boundary cells (analytic, int64, algo.rs:193-220), the local
+// start search over boundary cells, and the labelling of the walk into
+// AlignmentChoice values (algo.rs:351-400).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gx.h"
+#include "gx_internal.h"
+
+namespace gx {
+hipError_t launch_fill(int W, bool local, bool planes, bool lcs, bool codes, const PairDev* d_pairs, int npairs,
+                       int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
+                       hipStream_t st);
+hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d_sres, PairRes* d_pres,
+                           hipStream_t st);
+hipError_t launch_traceback(const TbDev* d_jobs, int njobs, hipStream_t st);
+hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, hipStream_t st);
+}  // namespace gx
+
+using namespace gx;
+
+// ---------------------------------------------------------------------------
+// errors
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIPCHK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(e_ == hipErrorOutOfMemory ? GX_ENOMEM : GX_EHIP,                       \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                   \
+    } while (0)
+
+int gx_internal_fail(int code, const std::string& msg) { return fail(code, msg); }
+
+extern "C" const char* gx_last_error(void) { return g_err.c_str(); }
+extern "C" const char* gx_version(void) { return "genomics-rs_amd 0.1 (gfx950)"; }
+
+static bool log_info() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("GX_LOG");
+        v = (e && (!strcmp(e, "info") || !strcmp(e, "debug"))) ? 1 : 0;
+    }
+    return v == 1;
+}
+
+// ---------------------------------------------------------------------------
+// device buffer pool (one per context)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+struct gx_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    std::mutex mu;
+    std::vector<DevBuf> free_list;
+    // staged pairs (bench path)
+    std::vector<std::vector<uint8_t>> st_s1, st_s2;
+    DevBuf st_chars;
+    std::vector<size_t> st_off1, st_off2;
+};
+
+static int pool_get(gx_context* ctx, size_t bytes, DevBuf* out) {
+    bytes = std::max<size_t>(bytes, 256);
+    size_t best = (size_t)-1;
+    int bi = -1;
+    for (size_t k = 0; k < ctx->free_list.size(); ++k) {
+        const DevBuf& b = ctx->free_list[k];
+        if (b.cap >= bytes && b.cap < best) { best = b.cap; bi = (int)k; }
+    }
+    if (bi >= 0) {
+        *out = ctx->free_list[bi];
+        ctx->free_list.erase(ctx->free_list.begin() + bi);
+        return GX_OK;
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+        // drop cached buffers and retry once
+        (void)hipGetLastError();
+        for (auto& b : ctx->free_list) (void)hipFree(b.p);
+        ctx->free_list.clear();
+        e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            return fail(GX_ENOMEM, "hipMalloc(" + std::to_string(bytes) + " B) failed");
+        }
+    }
+    out->p = p;
+    out->cap = bytes;
+    return GX_OK;
+}
+static void pool_put(gx_context* ctx, DevBuf& b) {
+    if (b.p) ctx->free_list.push_back(b);
+    b = DevBuf{};
+}
+
+extern "C" int gx_context_create(int device, gx_context** out) {
+    if (!out) return fail(GX_EINVAL, "out is NULL");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(GX_EINVAL, "no HIP device " + std::to_string(device));
+    HIPCHK(hipSetDevice(device));
+    gx_context* c = new gx_context();
+    c->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&c->ev0));
+    HIPCHK(hipEventCreate(&c->ev1));
+    HIPCHK(hipEventCreate(&c->ev2));
+    *out = c;
+    return GX_OK;
+}
+
+extern "C" int gx_context_trim(gx_context* ctx) {
+    if (!ctx) return fail(GX_EINVAL, "ctx is NULL");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    (void)hipSetDevice(ctx->device);
+    for (auto& b : ctx->free_list) (void)hipFree(b.p);
+    ctx->free_list.clear();
+    return GX_OK;
+}
+
+extern "C" void gx_context_destroy(gx_context* ctx) {
+    if (!ctx) return;
+    gx_context_trim(ctx);
+    (void)hipSetDevice(ctx->device);
+    if (ctx->st_chars.p) (void)hipFree(ctx->st_chars.p);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->ev2) (void)hipEventDestroy(ctx->ev2);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+// ---------------------------------------------------------------------------
+// scoring: exact-int32 guard (DESIGN.md "Integer range")
+
+struct HostScores {
+    int64_t sm, smm, g, h;
+    int64_t neg_inf;  // i64::MIN + |g + h|   (algo.rs:166)
+};
+
+static int64_t wadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+static int64_t wmul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+
+static int check_scores(const gx_scores* s, size_t n, size_t m, HostScores* hs, Scores32* sc, int is_local) {
+    if (!s) return fail(GX_EINVAL, "scores is NULL");
+    hs->sm = s->s_match; hs->smm = s->s_mismatch; hs->g = s->g; hs->h = s->h;
+    const int64_t lim = (int64_t)1 << 24;
+    if (llabs(s->s_match) > lim || llabs(s->s_mismatch) > lim || llabs(s->g) > lim || llabs(s->h) > lim)
+        return fail(GX_ERANGE, "score magnitudes above 2^24 are outside the exact int32 device range");
+    const int64_t gh = s->g + s->h;
+    hs->neg_inf = wadd(INT64_MIN, gh < 0 ? -gh : gh);
+    // The reference adds g and h+g to neg_inf at the boundary; when that
+    // wraps (possible only for g < 0 < h with |g+h| < |g|) its release build
+    // produces wrapped giants that the int32 path cannot reproduce.
+    if (s->g < 0 && llabs(gh) < llabs(s->g))
+        return fail(GX_ERANGE, "g < 0 < h with |g+h| < |g|: the reference's boundary arithmetic wraps");
+    // every interior magnitude <= (n + m + 2) * (|sm| + |smm| + |g| + |h|) + |h|
+    const double bound = (double)(n + m + 2) * (double)(llabs(s->s_match) + llabs(s->s_mismatch) + llabs(s->g) +
+                                                        llabs(s->h)) + (double)llabs(s->h);
+    if (bound >= (double)(1 << 28))
+        return fail(GX_ERANGE, "|score| bound exceeds 2^28: outside the exact int32 device range");
+    if (n > (size_t)1 << 26 || m > (size_t)1 << 26) return fail(GX_ERANGE, "sequence longer than 2^26");
+    sc->sm = (int)s->s_match; sc->smm = (int)s->s_mismatch; sc->g = (int)s->g; sc->h = (int)s->h;
+    sc->hg = (int)(s->h + s->g);
+    sc->floor_ = is_local ? 0 : kNeg;
+    return GX_OK;
+}
+
+// Boundary cell of the table (algo.rs:195-220), int64.
+static void boundary_cell(const HostScores& hs, uint64_t i, uint64_t j, int64_t* I, int64_t* D, int64_t* S) {
+    if (i == 0 && j == 0) { *I = 0; *D = 0; *S = 0; }
+    else if (j == 0) { *I = hs.neg_inf; *D = wadd(hs.h, wmul((int64_t)i, hs.g)); *S = hs.neg_inf; }
+    else { *I = wadd(hs.h, wmul((int64_t)j, hs.g)); *D = hs.neg_inf; *S = hs.neg_inf; }
+}
+// score_max(cell, 0, 0, 0, is_local) (algo.rs:98-107)
+static int64_t smax(int64_t I, int64_t S, int64_t D, int local) {
+    int64_t r = std::max(std::max(I, S), D);
+    return std::max(r, local ? (int64_t)0 : INT64_MIN);
+}
+
+// Processed characters for is_match(i-1, j-1, rev) (sequence.rs:102-115).
+// Without `rev` they are the bytes themselves.  With `rev`, index k of s1
+// reads s1[m - k] and index k of s2 reads s2[n - k]; an index out of range
+// (including a wrapped usize) is None, encoded 0xFF on both sides so that
+// None == None matches.  Inputs containing 0xFF are rejected in rev mode.
+static int processed_chars(const uint8_t* s1, size_t n, const uint8_t* s2, size_t m, int rev,
+                           std::vector<uint8_t>& c1, std::vector<uint8_t>& c2) {
+    c1.assign(s1, s1 + n);
+    c2.assign(s2, s2 + m);
+    if (!rev) return GX_OK;
+    for (size_t k = 0; k < n; ++k) if (s1[k] == 0xFF) return fail(GX_EINVAL, "byte 0xFF is reserved in reverse mode");
+    for (size_t k = 0; k < m; ++k) if (s2[k] == 0xFF) return fail(GX_EINVAL, "byte 0xFF is reserved in reverse mode");
+    for (size_t k = 0; k < n; ++k) {
+        // i_processed = len(s2) - k
+        c1[k] = (k <= m && (m - k) < n) ? s1[m - k] : 0xFF;
+    }
+    for (size_t k = 0; k < m; ++k) {
+        // j_processed = len(s1) - k
+        c2[k] = (k <= n && (n - k) < m) ? s2[n - k] : 0xFF;
+    }
+    return GX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// fill orchestration
+
+static int band_waves() {
+    static int w = -1;
+    if (w < 0) {
+        const char* e = getenv("GX_BAND_WAVES");
+        w = e ? atoi(e) : 4;
+        if (w != 1 && w != 2 && w != 4) w = 4;
+    }
+    return w;
+}
+static int fill_grid_cap() {
+    static int g = -1;
+    if (g < 0) {
+        const char* e = getenv("GX_FILL_GRID");
+        g = e ? atoi(e) : 1024;
+        if (g < 1) g = 1024;
+    }
+    return g;
+}
+
+struct PairHost {
+    const uint8_t* s1;   // original bytes (traceback labels, sequence.rs:113 with rev=false)
+    const uint8_t* s2;
+    size_t n, m;
+};
+
+struct FillJob {
+    // device buffers (owned by the job until released)
+    DevBuf chars, planes, codes, feed, progress, sres, pres, pairs, counter;
+    std::vector<PairDev> pd;
+    std::vector<PairRes> res;
+    int W = 4;
+    int total_bands = 0, total_strips = 0;
+    bool planes_on = false, lcs_on = false, codes_on = false;
+    double fill_ms = 0.0;
+};
+
+static void job_release(gx_context* ctx, FillJob& j) {
+    pool_put(ctx, j.chars); pool_put(ctx, j.planes); pool_put(ctx, j.codes); pool_put(ctx, j.feed);
+    pool_put(ctx, j.progress); pool_put(ctx, j.sres); pool_put(ctx, j.pres); pool_put(ctx, j.pairs);
+    pool_put(ctx, j.counter);
+}
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// chars_dev: if non-null, device buffer already holding the processed chars
+// at offsets off1/off2 (staged path); otherwise c1/c2 are uploaded.
+static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc,
+                    const std::vector<PairHost>& ph, const Scores32& sc, int is_local, bool planes, bool lcs,
+                    bool codes, FillJob& job, const uint8_t* chars_dev = nullptr,
+                    const std::vector<size_t>* off1 = nullptr, const std::vector<size_t>* off2 = nullptr) {
+    const int W = band_waves();
+    job.W = W;
+    job.planes_on = planes; job.lcs_on = lcs; job.codes_on = codes;
+    const size_t P = ph.size();
+    job.pd.assign(P, PairDev{});
+    // -- sizes
+    size_t chars_bytes = 0, plane_elems = 0, code_elems = 0, feed_recs = 0, prog_elems = 0;
+    std::vector<size_t> c1o(P), c2o(P), po(P), co(P), fo(P), gofs(P);
+    int bands = 0, strips = 0;
+    for (size_t p = 0; p < P; ++p) {
+        const int n = (int)ph[p].n, m = (int)ph[p].m;
+        PairDev& d = job.pd[p];
+        d.n = n; d.m = m;
+        d.strips = ceil_div(n, kWave);
+        d.bands = ceil_div(d.strips, W);
+        const int T = m + kWave - 1;
+        d.t16 = ceil_div(T, 16);
+        d.t4 = d.t16 * 4;
+        d.band_base = bands;
+        d.strip_base = strips;
+        d.feed_stride = (int)align_up((size_t)m + 1 + 64, 16);
+        bands += d.bands;
+        strips += d.strips;
+        c1o[p] = chars_bytes; chars_bytes += align_up(n, 64);
+        c2o[p] = chars_bytes; chars_bytes += align_up(m, 64);
+        po[p] = plane_elems; plane_elems += (size_t)d.strips * d.t4 * kWave * 4;
+        co[p] = code_elems; code_elems += (size_t)d.strips * d.t16 * kWave;
+        fo[p] = feed_recs; feed_recs += (size_t)std::max(d.bands - 1, 0) * d.feed_stride;
+        gofs[p] = prog_elems; prog_elems += (size_t)std::max(d.bands - 1, 0);
+    }
+    job.total_bands = bands;
+    job.total_strips = strips;
+    int rc;
+    const int nplanes = lcs ? 4 : 3;
+    if (!chars_dev) {
+        if ((rc = pool_get(ctx, chars_bytes, &job.chars))) return rc;
+    }
+    if (planes && (rc = pool_get(ctx, plane_elems * sizeof(int32_t) * nplanes, &job.planes))) return rc;
+    if (codes && (rc = pool_get(ctx, code_elems * sizeof(uint32_t), &job.codes))) return rc;
+    if ((rc = pool_get(ctx, std::max<size_t>(feed_recs, 1) * sizeof(Rec), &job.feed))) return rc;
+    if ((rc = pool_get(ctx, std::max<size_t>(prog_elems, 1) * sizeof(int), &job.progress))) return rc;
+    if ((rc = pool_get(ctx, std::max(strips, 1) * sizeof(StripRes), &job.sres))) return rc;
+    if ((rc = pool_get(ctx, P * sizeof(PairRes), &job.pres))) return rc;
+    if ((rc = pool_get(ctx, P * sizeof(PairDev), &job.pairs))) return rc;
+    if ((rc = pool_get(ctx, 64, &job.counter))) return rc;
+    // -- chars upload
+    const uint8_t* cbase = chars_dev;
+    if (!chars_dev) {
+        std::vector<uint8_t> hc(chars_bytes, 0);
+        for (size_t p = 0; p < P; ++p) {
+            if (ph[p].n) memcpy(&hc[c1o[p]], proc[p].first, ph[p].n);
+            if (ph[p].m) memcpy(&hc[c2o[p]], proc[p].second, ph[p].m);
+        }
+        HIPCHK(hipMemcpyAsync(job.chars.p, hc.data(), chars_bytes, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));  // hc goes out of scope
+        cbase = (const uint8_t*)job.chars.p;
+    }
+    for (size_t p = 0; p < P; ++p) {
+        PairDev& d = job.pd[p];
+        d.c1 = cbase + (chars_dev ? (*off1)[p] : c1o[p]);
+        d.c2 = cbase + (chars_dev ? (*off2)[p] : c2o[p]);
+        int32_t* pl = (int32_t*)job.planes.p;
+        d.pI = planes ? pl + po[p] : nullptr;
+        d.pD = planes ? pl + plane_elems + po[p] : nullptr;
+        d.pS = planes ? pl + 2 * plane_elems + po[p] : nullptr;
+        d.pL = (planes && lcs) ? pl + 3 * plane_elems + po[p] : nullptr;
+        d.codes = codes ? (uint32_t*)job.codes.p + co[p] : nullptr;
+        d.feed = (Rec*)job.feed.p + fo[p];
+        d.progress = (int*)job.progress.p + gofs[p];
+    }
+    HIPCHK(hipMemcpyAsync(job.pairs.p, job.pd.data(), P * sizeof(PairDev), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemsetAsync(job.progress.p, 0, std::max<size_t>(prog_elems, 1) * sizeof(int), ctx->stream));
+    HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, ctx->stream));
+    HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), ctx->stream));
+    const int grid = std::min(bands, fill_grid_cap());
+    HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+    if (bands > 0) {
+        HIPCHK(launch_fill(W, is_local != 0, planes, lcs, codes, (const PairDev*)job.pairs.p, (int)P, bands,
+                           (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, sc, grid, ctx->stream));
+        HIPCHK(launch_finalize((const PairDev*)job.pairs.p, (int)P, (const StripRes*)job.sres.p,
+                               (PairRes*)job.pres.p, ctx->stream));
+    }
+    HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+    job.res.assign(P, PairRes{});
+    int status[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(job.res.data(), job.pres.p, P * sizeof(PairRes), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(status, job.counter.p, sizeof status, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (status[1] != 0)
+        return fail(GX_EHIP, "fill kernel: inter-wave wait timed out (status " + std::to_string(status[1]) + ")");
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    job.fill_ms = ms;
+    return GX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// tables
+
+struct gx_table {
+    gx_context* ctx = nullptr;
+    FillJob job;
+    std::vector<uint8_t> s1, s2;      // original bytes (retrace labels)
+    std::vector<uint8_t> c1, c2;      // processed chars (export of *_matches)
+    HostScores hs;
+    Scores32 sc;
+    int is_local = 0;
+    uint32_t flags = 0;
+};
+
+static int start_cell(const gx_table* t, const PairRes& r, uint64_t* si, uint64_t* sj, int64_t* score);
+
+// Interior walk + labelling + boundary continuation (algo.rs:306-422).
+struct Walk {
+    std::vector<gx_step> steps;
+    gx_result res{};
+};
+
+static bool tb_match(const uint8_t* s1, size_t n, const uint8_t* s2, size_t m, uint64_t i, uint64_t j) {
+    // is_match(i, j, false) with unshifted indices: nth() past the end is None
+    const int a = i < n ? (int)s1[i] : 0x1FF;
+    const int b = j < m ? (int)s2[j] : 0x1FF;
+    return a == b;
+}
+
+static int label_walk(const HostScores& hs, int is_local, const uint8_t* s1, size_t n, const uint8_t* s2, size_t m,
+                      uint64_t si, uint64_t sj, const uint8_t* moves, size_t nmoves, Walk& w) {
+    uint64_t i = si, j = sj;
+    int last = GX_MATCH;
+    gx_result& r = w.res;
+    r.matches = r.mismatches = r.gap_extensions = r.opening_gaps = 0;
+    w.steps.clear();
+    w.steps.reserve(nmoves + (size_t)si + (size_t)sj + 2);
+    bool done = false;
+    // interior part, decided on the device
+    for (size_t k = 0; k < nmoves; ++k) {
+        gx_step st{};
+        st.i = i; st.j = j;
+        const uint8_t c = moves[k];
+        if (c == 0) {
+            const bool mt = tb_match(s1, n, s2, m, i, j);
+            st.choice = mt ? GX_MATCH : GX_MISMATCH;
+            if (mt) r.matches++; else r.mismatches++;
+            last = st.choice;
+            --i; --j;
+        } else if (c == 1) {
+            if (last == GX_INSERT) { st.choice = GX_INSERT; r.gap_extensions++; }
+            else { st.choice = GX_OPEN_INSERT; r.opening_gaps++; }
+            last = GX_INSERT;
+            --j;
+        } else {
+            if (last == GX_DELETE) { st.choice = GX_DELETE; r.gap_extensions++; }
+            else { st.choice = GX_OPEN_DELETE; r.opening_gaps++; }
+            last = GX_DELETE;
+            --i;
+        }
+        w.steps.push_back(st);
+        if (i == 0 && j == 0) { done = true; break; }
+    }
+    // boundary part: the reference loop on analytic cells
+    while (!done) {
+        int64_t I, D, S;
+        boundary_cell(hs, i, j, &I, &D, &S);
+        const int64_t mx = smax(I, S, D, is_local);
+        gx_step st{};
+        st.i = i; st.j = j;
+        bool di, dj;
+        if (mx == S) {
+            const bool mt = tb_match(s1, n, s2, m, i, j);
+            st.choice = mt ? GX_MATCH : GX_MISMATCH;
+            if (mt) r.matches++; else r.mismatches++;
+            last = st.choice;
+            di = dj = true;
+        } else if (mx == I) {
+            if (last == GX_INSERT) { st.choice = GX_INSERT; r.gap_extensions++; }
+            else { st.choice = GX_OPEN_INSERT; r.opening_gaps++; }
+            last = GX_INSERT;
+            di = false; dj = true;
+        } else if (mx == D) {
+            if (last == GX_DELETE) { st.choice = GX_DELETE; r.gap_extensions++; }
+            else { st.choice = GX_OPEN_DELETE; r.opening_gaps++; }
+            last = GX_DELETE;
+            di = true; dj = false;
+        } else {
+            if (is_local && mx == 0) break;
+            return fail(GX_EPANIC, "Unexpected score during retrace: " + std::to_string(mx) + " at (" +
+                                       std::to_string(i) + ", " + std::to_string(j) + ")");
+        }
+        w.steps.push_back(st);
+        const bool inone = di && i == 0, jnone = dj && j == 0;
+        if (inone && jnone) break;
+        i = inone ? 0 : i - (di ? 1 : 0);
+        j = jnone ? 0 : j - (dj ? 1 : 0);
+        if (i == 0 && j == 0) break;
+    }
+    r.n_steps = w.steps.size();
+    return GX_OK;
+}
+
+// Device walk for a set of jobs; returns moves per job.
+struct TbOut {
+    std::vector<std::vector<uint8_t>> moves;
+    std::vector<int> end_i, end_j;
+    double ms = 0;
+};
+
+static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<std::pair<int, int>>& starts,
+                         TbOut& out) {
+    const size_t P = starts.size();
+    std::vector<TbDev> jobs(P);
+    std::vector<size_t> mo(P);
+    size_t mtot = 0;
+    for (size_t p = 0; p < P; ++p) {
+        mo[p] = mtot;
+        mtot += align_up((size_t)job.pd[p].n + job.pd[p].m + 64, 64);
+    }
+    DevBuf moves, jb, cnt;
+    int rc;
+    if ((rc = pool_get(ctx, mtot, &moves))) return rc;
+    if ((rc = pool_get(ctx, P * sizeof(TbDev), &jb))) { pool_put(ctx, moves); return rc; }
+    if ((rc = pool_get(ctx, P * 4 * sizeof(int), &cnt))) { pool_put(ctx, moves); pool_put(ctx, jb); return rc; }
+    for (size_t p = 0; p < P; ++p) {
+        TbDev& t = jobs[p];
+        t.codes = job.pd[p].codes;
+        t.n = job.pd[p].n; t.m = job.pd[p].m; t.t16 = job.pd[p].t16;
+        t.start_i = starts[p].first; t.start_j = starts[p].second;
+        t.moves = (uint8_t*)moves.p + mo[p];
+        t.nmoves = (int*)cnt.p + 4 * p;
+        t.end_ij = (int*)cnt.p + 4 * p + 1;
+    }
+    auto cleanup = [&]() { pool_put(ctx, moves); pool_put(ctx, jb); pool_put(ctx, cnt); };
+    hipError_t e = hipMemcpyAsync(jb.p, jobs.data(), P * sizeof(TbDev), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(ctx->ev1, ctx->stream);
+    if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(ctx->ev2, ctx->stream);
+    std::vector<int> c(4 * P);
+    if (e == hipSuccess) e = hipMemcpyAsync(c.data(), cnt.p, 4 * P * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) { cleanup(); return fail(GX_EHIP, std::string("traceback: ") + hipGetErrorString(e)); }
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, ctx->ev1, ctx->ev2);
+    out.ms = ms;
+    out.moves.resize(P);
+    out.end_i.resize(P);
+    out.end_j.resize(P);
+    // one D2H for all moves
+    std::vector<uint8_t> hm(mtot);
+    e = hipMemcpyAsync(hm.data(), moves.p, mtot, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    cleanup();
+    if (e != hipSuccess) return fail(GX_EHIP, std::string("traceback copy: ") + hipGetErrorString(e));
+    for (size_t p = 0; p < P; ++p) {
+        const int k = c[4 * p];
+        out.moves[p].assign(hm.begin() + mo[p], hm.begin() + mo[p] + k);
+        out.end_i[p] = c[4 * p + 1];
+        out.end_j[p] = c[4 * p + 2];
+    }
+    return GX_OK;
+}
+
+// Start cell + score (algo.rs:306-331).
+static int start_cell_common(const HostScores& hs, int is_local, size_t n, size_t m, const PairRes& r,
+                             uint64_t* si, uint64_t* sj, int64_t* score) {
+    if (!is_local) {
+        *si = n; *sj = m;
+        if (n >= 1 && m >= 1) *score = r.end_SM;
+        else {
+            int64_t I, D, S;
+            boundary_cell(hs, n, m, &I, &D, &S);
+            *score = smax(I, S, D, 0);
+        }
+        return GX_OK;
+    }
+    // local: LAST maximum of score_max over all cells in row-major order
+    int64_t best = INT64_MIN;
+    uint64_t bi = 0, bj = 0;
+    auto consider = [&](int64_t v, uint64_t i, uint64_t j) {
+        if (v > best || (v == best && (i > bi || (i == bi && j > bj)))) { best = v; bi = i; bj = j; }
+    };
+    for (uint64_t j = 0; j <= m; ++j) {  // row 0
+        int64_t I, D, S;
+        boundary_cell(hs, 0, j, &I, &D, &S);
+        consider(smax(I, S, D, 1), 0, j);
+    }
+    for (uint64_t i = 1; i <= n; ++i) {  // column 0
+        int64_t I, D, S;
+        boundary_cell(hs, i, 0, &I, &D, &S);
+        consider(smax(I, S, D, 1), i, 0);
+    }
+    if (n >= 1 && m >= 1) consider(r.lmax_val, (uint64_t)r.lmax_i, (uint64_t)r.lmax_j);
+    *si = bi; *sj = bj; *score = best;
+    return GX_OK;
+}
+
+static int start_cell(const gx_table* t, const PairRes& r, uint64_t* si, uint64_t* sj, int64_t* score) {
+    return start_cell_common(t->hs, t->is_local, t->s1.size(), t->s2.size(), r, si, sj, score);
+}
+
+extern "C" int gx_alignment_table(gx_context* ctx, const uint8_t* s1, size_t n, const uint8_t* s2, size_t m,
+                                  const gx_scores* scores, int is_local, int reverse_sequences, uint32_t flags,
+                                  gx_table** table_out, uint64_t* matches_at_max) {
+    if (!ctx || !table_out) return fail(GX_EINVAL, "ctx/table_out is NULL");
+    if ((n && !s1) || (m && !s2)) return fail(GX_EINVAL, "sequence pointer is NULL");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    gx_table* t = new gx_table();
+    t->ctx = ctx;
+    t->is_local = is_local;
+    t->flags = flags;
+    int rc = check_scores(scores, n, m, &t->hs, &t->sc, is_local);
+    if (!rc) rc = processed_chars(s1, n, s2, m, reverse_sequences, t->c1, t->c2);
+    if (rc) { delete t; return rc; }
+    t->s1.assign(s1, s1 + n);
+    t->s2.assign(s2, s2 + m);
+    if (log_info()) {
+        fprintf(stderr, "[gx INFO] Sequence table shape: [%zu, %zu]\n", n + 1, m + 1);
+    }
+    std::vector<PairHost> ph{PairHost{t->s1.data(), t->s2.data(), n, m}};
+    std::vector<std::pair<const uint8_t*, const uint8_t*>> proc{{t->c1.data(), t->c2.data()}};
+    const bool planes = (flags & (GX_TABLE_PLANES | GX_TABLE_MATCHES)) != 0;
+    const bool lcs = (flags & GX_TABLE_MATCHES) != 0;
+    if (n >= 1 && m >= 1) {
+        rc = run_fill(ctx, proc, ph, t->sc, is_local, planes, lcs, true, t->job);
+        if (rc) { job_release(ctx, t->job); delete t; return rc; }
+    } else {
+        t->job.res.assign(1, PairRes{});
+        t->job.pd.assign(1, PairDev{});
+        t->job.pd[0].n = (int)n; t->job.pd[0].m = (int)m;
+    }
+    if (log_info())
+        fprintf(stderr, "[gx INFO] Table initialization complete, time taken: %lldus\n",
+                (long long)(t->job.fill_ms * 1000.0));
+    if (matches_at_max) *matches_at_max = (n >= 1 && m >= 1) ? (uint64_t)t->job.res[0].mam : 0;
+    *table_out = t;
+    return GX_OK;
+}
+
+extern "C" int gx_table_info(const gx_table* t, uint64_t* n_rows, uint64_t* n_cols, uint64_t* max_cell_i,
+                             uint64_t* max_cell_j, int64_t* fill_us) {
+    if (!t) return fail(GX_EINVAL, "table is NULL");
+    const bool interior = t->s1.size() >= 1 && t->s2.size() >= 1;
+    if (n_rows) *n_rows = t->s1.size() + 1;
+    if (n_cols) *n_cols = t->s2.size() + 1;
+    if (max_cell_i) *max_cell_i = interior ? (uint64_t)t->job.res[0].max_i : 0;
+    if (max_cell_j) *max_cell_j = interior ? (uint64_t)t->job.res[0].max_j : 0;
+    if (fill_us) *fill_us = (int64_t)(t->job.fill_ms * 1000.0);
+    return GX_OK;
+}
+
+// Interior of one plane as int32 row-major (n+1)x(m+1) (boundary slots undefined).
+static int fetch_plane32(const gx_table* t, int which, std::vector<int32_t>& out) {
+    const size_t n = t->s1.size(), m = t->s2.size();
+    out.assign((n + 1) * (m + 1), 0);
+    if (n == 0 || m == 0) return GX_OK;
+    const PairDev& d = t->job.pd[0];
+    const int32_t* src = which == 0 ? d.pI : which == 1 ? d.pD : which == 2 ? d.pS : d.pL;
+    if (!src) return fail(GX_EINVAL, "plane not kept: build the table with GX_TABLE_PLANES / GX_TABLE_MATCHES");
+    gx_context* ctx = t->ctx;
+    DevBuf tmp;
+    int rc = pool_get(ctx, out.size() * sizeof(int32_t), &tmp);
+    if (rc) return rc;
+    hipError_t e = launch_export(src, (int32_t*)tmp.p, (int)n, (int)m, d.t4, ctx->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(out.data(), tmp.p, out.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    pool_put(ctx, tmp);
+    if (e != hipSuccess) return fail(GX_EHIP, std::string("export: ") + hipGetErrorString(e));
+    return GX_OK;
+}
+
+extern "C" int gx_table_export_plane(const gx_table* t, int which, int64_t* out, size_t out_cells, int colmajor) {
+    if (!t || !out) return fail(GX_EINVAL, "NULL argument");
+    if (which < 0 || which > 2) return fail(GX_EINVAL, "which must be 0 (insert), 1 (delete) or 2 (sub)");
+    const size_t n = t->s1.size(), m = t->s2.size();
+    if (out_cells < (n + 1) * (m + 1)) return fail(GX_ECAP, "out too small");
+    std::lock_guard<std::mutex> lk(t->ctx->mu);
+    HIPCHK(hipSetDevice(t->ctx->device));
+    std::vector<int32_t> p32;
+    int rc = fetch_plane32(t, which, p32);
+    if (rc) return rc;
+    for (size_t i = 0; i <= n; ++i)
+        for (size_t j = 0; j <= m; ++j) {
+            int64_t v;
+            if (i == 0 || j == 0) {
+                int64_t I, D, S;
+                boundary_cell(t->hs, i, j, &I, &D, &S);
+                v = which == 0 ? I : which == 1 ? D : S;
+            } else {
+                v = p32[i * (m + 1) + j];
+            }
+            out[colmajor ? i + j * (n + 1) : i * (m + 1) + j] = v;
+        }
+    return GX_OK;
+}
+
+extern "C" int gx_table_export(const gx_table* t, gx_cell* out, size_t out_cells) {
+    if (!t || !out) return fail(GX_EINVAL, "NULL argument");
+    const size_t n = t->s1.size(), m = t->s2.size();
+    if (out_cells < (n + 1) * (m + 1)) return fail(GX_ECAP, "out too small");
+    std::lock_guard<std::mutex> lk(t->ctx->mu);
+    HIPCHK(hipSetDevice(t->ctx->device));
+    std::vector<int32_t> pI, pD, pS, pL;
+    int rc;
+    if ((rc = fetch_plane32(t, 0, pI)) || (rc = fetch_plane32(t, 1, pD)) || (rc = fetch_plane32(t, 2, pS))) return rc;
+    const bool have_l = t->job.lcs_on;
+    if (have_l && (rc = fetch_plane32(t, 3, pL))) return rc;
+    auto L = [&](size_t i, size_t j) -> uint64_t {
+        if (i == 0 || j == 0 || !have_l) return 0;
+        return (uint64_t)pL[i * (m + 1) + j];
+    };
+    for (size_t i = 0; i <= n; ++i)
+        for (size_t j = 0; j <= m; ++j) {
+            gx_cell c{};
+            if (i == 0 || j == 0) {
+                boundary_cell(t->hs, i, j, &c.insert_score, &c.delete_score, &c.sub_score);
+            } else {
+                const size_t o = i * (m + 1) + j;
+                c.insert_score = pI[o]; c.delete_score = pD[o]; c.sub_score = pS[o];
+                if (have_l) {
+                    // A.5: Im = L(i,j-1), Dm = L(i-1,j), Sm = L(i-1,j-1) + is_match(i-1,j-1)
+                    c.insert_matches = L(i, j - 1);
+                    c.delete_matches = L(i - 1, j);
+                    c.sub_matches = L(i - 1, j - 1) + (t->c1[i - 1] == t->c2[j - 1] ? 1 : 0);
+                }
+            }
+            out[i + j * (n + 1)] = c;   // column-major, algo.rs:172 `.f()`
+        }
+    return GX_OK;
+}
+
+extern "C" void gx_table_free(gx_table* t) {
+    if (!t) return;
+    if (t->ctx) {
+        std::lock_guard<std::mutex> lk(t->ctx->mu);
+        job_release(t->ctx, t->job);
+    }
+    delete t;
+}
+
+static int copy_steps(const Walk& w, gx_step* steps, size_t cap) {
+    if (!steps) return GX_OK;
+    if (w.steps.size() > cap) return fail(GX_ECAP, "steps capacity " + std::to_string(cap) + " < " +
+                                                       std::to_string(w.steps.size()));
+    memcpy(steps, w.steps.data(), w.steps.size() * sizeof(gx_step));
+    return GX_OK;
+}
+
+extern "C" int gx_retrace(gx_table* t, int is_local, gx_step* steps, size_t cap, gx_result* out) {
+    if (!t) return fail(GX_EINVAL, "table is NULL");
+    gx_context* ctx = t->ctx;
+    int rc = GX_OK;
+    Walk w;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        (void)hipSetDevice(ctx->device);
+        const size_t n = t->s1.size(), m = t->s2.size();
+        const auto t0 = std::chrono::steady_clock::now();
+        t->is_local = is_local;
+        uint64_t si, sj;
+        int64_t score;
+        const PairRes r = t->job.res[0];
+        start_cell(t, r, &si, &sj, &score);
+        if (log_info()) fprintf(stderr, "[gx INFO] Starting at (%llu, %llu)\n", (unsigned long long)si,
+                                (unsigned long long)sj);
+        TbOut tb;
+        if (si >= 1 && sj >= 1 && n >= 1 && m >= 1) {
+            rc = run_traceback(ctx, t->job, {{(int)si, (int)sj}}, tb);
+        } else {
+            tb.moves.assign(1, {});
+        }
+        if (!rc) rc = label_walk(t->hs, is_local, t->s1.data(), n, t->s2.data(), m, si, sj, tb.moves[0].data(),
+                                 tb.moves[0].size(), w);
+        const auto t1 = std::chrono::steady_clock::now();
+        w.res.score = score;
+        w.res.start_i = si; w.res.start_j = sj;
+        const bool interior = n >= 1 && m >= 1;
+        w.res.max_cell_i = interior ? (uint64_t)r.max_i : 0;
+        w.res.max_cell_j = interior ? (uint64_t)r.max_j : 0;
+        w.res.matches_at_max = interior ? (uint64_t)r.mam : 0;
+        w.res.fill_us = (int64_t)(t->job.fill_ms * 1000.0);
+        w.res.retrace_us = std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
+        if (log_info()) {
+            fprintf(stderr, "[gx INFO] Retrace complete, time taken: %lldus\n", (long long)w.res.retrace_us);
+            fprintf(stderr, "[gx INFO] Retrace alignment size: %zu\n", w.steps.size());
+        }
+        job_release(ctx, t->job);
+    }
+    delete t;  // consumed, like the by-value Array2 in the reference
+    if (rc) return rc;
+    if (out) *out = w.res;
+    return copy_steps(w, steps, cap);
+}
+
+extern "C" int gx_align(gx_context* ctx, const uint8_t* s1, size_t n, const uint8_t* s2, size_t m,
+                        const gx_scores* scores, int is_local, int reverse_sequences, gx_step* steps, size_t cap,
+                        gx_result* out) {
+    gx_table* t = nullptr;
+    int rc = gx_alignment_table(ctx, s1, n, s2, m, scores, is_local, reverse_sequences, 0, &t, nullptr);
+    if (rc) return rc;
+    return gx_retrace(t, is_local, steps, cap, out);
+}
+
+// ---------------------------------------------------------------------------
+// batch of independent pairs (config 4 / 5)
+
+static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
+                      const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc, const HostScores& hs,
+                      const Scores32& sc, int is_local, bool planes, std::vector<Walk>& walks, double* fill_ms,
+                      const uint8_t* chars_dev = nullptr, const std::vector<size_t>* off1 = nullptr,
+                      const std::vector<size_t>* off2 = nullptr) {
+    const size_t P = ph.size();
+    // pairs with an interior go to the device
+    std::vector<size_t> idx;
+    for (size_t p = 0; p < P; ++p) if (ph[p].n >= 1 && ph[p].m >= 1) idx.push_back(p);
+    std::vector<PairHost> dph;
+    std::vector<std::pair<const uint8_t*, const uint8_t*>> dproc;
+    std::vector<size_t> o1, o2;
+    for (size_t p : idx) {
+        dph.push_back(ph[p]);
+        dproc.push_back(proc[p]);
+        if (chars_dev) { o1.push_back((*off1)[p]); o2.push_back((*off2)[p]); }
+    }
+    FillJob job;
+    std::vector<PairRes> res(P, PairRes{});
+    TbOut tb;
+    std::vector<std::pair<int, int>> starts(idx.size());
+    std::vector<uint64_t> si(P), sj(P);
+    std::vector<int64_t> score(P);
+    int rc = GX_OK;
+    if (!idx.empty()) {
+        rc = run_fill(ctx, dproc, dph, sc, is_local, planes, false, true, job, chars_dev, chars_dev ? &o1 : nullptr,
+                      chars_dev ? &o2 : nullptr);
+        if (rc) { job_release(ctx, job); return rc; }
+        for (size_t k = 0; k < idx.size(); ++k) res[idx[k]] = job.res[k];
+    }
+    for (size_t p = 0; p < P; ++p) start_cell_common(hs, is_local, ph[p].n, ph[p].m, res[p], &si[p], &sj[p], &score[p]);
+    if (!idx.empty()) {
+        for (size_t k = 0; k < idx.size(); ++k) {
+            const size_t p = idx[k];
+            starts[k] = (si[p] >= 1 && sj[p] >= 1) ? std::make_pair((int)si[p], (int)sj[p]) : std::make_pair(0, 0);
+        }
+        rc = run_traceback(ctx, job, starts, tb);
+    }
+    if (fill_ms) *fill_ms = job.fill_ms;
+    job_release(ctx, job);
+    if (rc) return rc;
+    walks.assign(P, Walk{});
+    std::vector<int> dev_of(P, -1);
+    for (size_t k = 0; k < idx.size(); ++k) dev_of[idx[k]] = (int)k;
+    for (size_t p = 0; p < P; ++p) {
+        const uint8_t* mv = nullptr;
+        size_t nm = 0;
+        if (dev_of[p] >= 0) { mv = tb.moves[dev_of[p]].data(); nm = tb.moves[dev_of[p]].size(); }
+        rc = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], mv, nm, walks[p]);
+        if (rc) return rc;
+        Walk& w = walks[p];
+        const bool interior = ph[p].n >= 1 && ph[p].m >= 1;
+        w.res.score = score[p];
+        w.res.start_i = si[p]; w.res.start_j = sj[p];
+        w.res.max_cell_i = interior ? (uint64_t)res[p].max_i : 0;
+        w.res.max_cell_j = interior ? (uint64_t)res[p].max_j : 0;
+        w.res.matches_at_max = interior ? (uint64_t)res[p].mam : 0;
+        w.res.fill_us = (int64_t)(job.fill_ms * 1000.0);
+        w.res.retrace_us = (int64_t)(tb.ms * 1000.0);
+    }
+    return GX_OK;
+}
+
+extern "C" int gx_align_batch(gx_context* ctx, const uint8_t* const* s1, const size_t* n, const uint8_t* const* s2,
+                              const size_t* m, size_t npairs, const gx_scores* scores, int is_local,
+                              gx_step* const* steps, const size_t* caps, gx_result* out) {
+    if (!ctx || !s1 || !n || !s2 || !m || !out) return fail(GX_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    size_t nmax = 0, mmax = 0;
+    for (size_t p = 0; p < npairs; ++p) { nmax = std::max(nmax, n[p]); mmax = std::max(mmax, m[p]); }
+    HostScores hs;
+    Scores32 sc;
+    int rc = check_scores(scores, nmax, mmax, &hs, &sc, is_local);
+    if (rc) return rc;
+    std::vector<PairHost> ph(npairs);
+    std::vector<std::pair<const uint8_t*, const uint8_t*>> proc(npairs);
+    for (size_t p = 0; p < npairs; ++p) {
+        ph[p] = PairHost{s1[p], s2[p], n[p], m[p]};
+        proc[p] = {s1[p], s2[p]};
+    }
+    std::vector<Walk> walks;
+    rc = batch_core(ctx, ph, proc, hs, sc, is_local, false, walks, nullptr);
+    if (rc) return rc;
+    for (size_t p = 0; p < npairs; ++p) {
+        out[p] = walks[p].res;
+        if (steps && steps[p]) {
+            rc = copy_steps(walks[p], steps[p], caps ? caps[p] : 0);
+            if (rc) return rc;
+        }
+    }
+    return GX_OK;
+}
+
+// ---------------------------------------------------------------------------
+// staged (device-resident inputs) path for benchmarking
+
+extern "C" int gx_stage_pairs(gx_context* ctx, const uint8_t* const* s1, const size_t* n, const uint8_t* const* s2,
+                              const size_t* m, size_t npairs) {
+    if (!ctx || !s1 || !n || !s2 || !m) return fail(GX_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    ctx->st_s1.assign(npairs, {});
+    ctx->st_s2.assign(npairs, {});
+    ctx->st_off1.assign(npairs, 0);
+    ctx->st_off2.assign(npairs, 0);
+    size_t tot = 0;
+    for (size_t p = 0; p < npairs; ++p) {
+        ctx->st_s1[p].assign(s1[p], s1[p] + n[p]);
+        ctx->st_s2[p].assign(s2[p], s2[p] + m[p]);
+        ctx->st_off1[p] = tot; tot += align_up(n[p], 64);
+        ctx->st_off2[p] = tot; tot += align_up(m[p], 64);
+    }
+    std::vector<uint8_t> hc(std::max<size_t>(tot, 1), 0);
+    for (size_t p = 0; p < npairs; ++p) {
+        if (n[p]) memcpy(&hc[ctx->st_off1[p]], s1[p], n[p]);
+        if (m[p]) memcpy(&hc[ctx->st_off2[p]], s2[p], m[p]);
+    }
+    if (ctx->st_chars.p) { (void)hipFree(ctx->st_chars.p); ctx->st_chars = DevBuf{}; }
+    HIPCHK(hipMalloc(&ctx->st_chars.p, hc.size()));
+    ctx->st_chars.cap = hc.size();
+    HIPCHK(hipMemcpy(ctx->st_chars.p, hc.data(), hc.size(), hipMemcpyHostToDevice));
+    return GX_OK;
+}
+
+extern "C" int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes,
+                             gx_result* out, double* fill_ms_out) {
+    if (!ctx || !out) return fail(GX_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    const size_t P = ctx->st_s1.size();
+    size_t nmax = 0, mmax = 0;
+    for (size_t p = 0; p < P; ++p) { nmax = std::max(nmax, ctx->st_s1[p].size()); mmax = std::max(mmax, ctx->st_s2[p].size()); }
+    HostScores hs;
+    Scores32 sc;
+    int rc = check_scores(scores, nmax, mmax, &hs, &sc, is_local);
+    if (rc) return rc;
+    std::vector<PairHost> ph(P);
+    std::vector<std::pair<const uint8_t*, const uint8_t*>> proc(P);
+    for (size_t p = 0; p < P; ++p) {
+        ph[p] = PairHost{ctx->st_s1[p].data(), ctx->st_s2[p].data(), ctx->st_s1[p].size(), ctx->st_s2[p].size()};
+        proc[p] = {ph[p].s1, ph[p].s2};
+    }
+    std::vector<Walk> walks;
+    double fms = 0;
+    rc = batch_core(ctx, ph, proc, hs, sc, is_local, keep_planes != 0, walks, &fms,
+                    (const uint8_t*)ctx->st_chars.p, &ctx->st_off1, &ctx->st_off2);
+    if (rc) return rc;
+    for (size_t p = 0; p < P; ++p) out[p] = walks[p].res;
+    if (fill_ms_out) *fill_ms_out = fms;
+    return GX_OK;
+}

@@ -1,0 +1,87 @@
+// gx_internal.h -- structures shared by the HIP kernels and the C++ host code.
+//
+// Device data layout (DESIGN.md "HBM layout"):
+//   A pair (s1: n rows, s2: m columns) is cut into STRIPS of 64 interior rows
+//   (strip k = rows 64k+1 .. 64k+64, lane l = row 64k+l+1).  One wave sweeps a
+//   strip along the anti-diagonal skew: at step t lane l computes column
+//   j = t - l + 1, so a strip takes T = m + 63 steps.  WAVES_PER_BAND strips
+//   form a BAND, processed by one workgroup (one wave per strip + one I/O wave).
+//
+//   Score planes (int32, one each for insert/delete/sub score):
+//       plane[strip][t/4][lane][t%4]        (16 B per lane per 4 steps)
+//   so each wave stores 1 KiB contiguous per plane every 4 steps.
+//   Traceback direction codes (2 bit/cell, 0=sub 1=insert 2=delete):
+//       codes[strip][t/16][lane]  (uint32, step t%16 at bits 2*(15 - t%16))
+#pragma once
+#include <stdint.h>
+
+namespace gx {
+
+constexpr int kWave = 64;
+constexpr int kNeg = -(1 << 30);   // int32 stand-in for negative_inf (algo.rs:166)
+constexpr int kRing = 256;         // LDS ring records per strip boundary (power of two)
+constexpr int kSub = 16;           // steps per flow-control sub-block (multiple of 16)
+constexpr int kIoChunk = 16;       // columns per I/O-wave transfer
+constexpr int kMaxBandWaves = 8;
+
+// Scores narrowed to int32 after the host range guard (DESIGN.md "Integer range").
+struct Scores32 {
+    int sm;      // s_match
+    int smm;     // s_mismatch
+    int g;       // per-residue gap
+    int h;       // gap open
+    int hg;      // h + g
+    int floor_;  // local ? 0 : kNeg  (the 4th lane of score_max, algo.rs:103)
+};
+
+// One inter-strip record: the bottom-row cell (r, j) of a strip, as needed by
+// the strip below.  dd = its delete-successor max(max(I,S)+h+g, D+g, floor),
+// sm = score_max(cell), l = max_matches(cell), c2 = s2[j-1].
+struct __attribute__((aligned(16))) Rec {
+    int dd, sm, l, c2;
+};
+
+struct __attribute__((aligned(16))) StripRes {
+    int best, bi, bj, bl;      // first max of score_max in row-major order + LCS there
+    int lbest, li, lj, valid;  // last max (local start search)
+};
+
+struct __attribute__((aligned(16))) PairRes {
+    int max_val, max_i, max_j, mam;       // first max over interior (algo.rs:258-262, 279)
+    int lmax_val, lmax_i, lmax_j, nstrips;// last max over interior (algo.rs:310-322)
+    int end_SM, pad0, pad1, pad2;         // score_max of cell (n, m)
+};
+
+struct PairDev {
+    const uint8_t* c1;   // processed row chars, n   (is_match row operand)
+    const uint8_t* c2;   // processed col chars, m
+    int n, m;
+    int strips;          // ceil(n / 64)
+    int bands;           // ceil(strips / W)
+    int t4;              // plane step-groups per strip (multiple of 4)
+    int t16;             // code words per lane per strip
+    int band_base;       // global index of this pair's band 0
+    int strip_base;      // index of this pair's strip 0 in the StripRes array
+    int32_t* pI;         // planes (nullptr: score-only)
+    int32_t* pD;
+    int32_t* pS;
+    int32_t* pL;         // optional LCS plane (full AlignmentCell export)
+    uint32_t* codes;     // traceback codes (nullptr: none)
+    Rec* feed;           // [bands-1][feed_stride] band-boundary rows
+    int* progress;       // [bands-1] columns published per boundary
+    int feed_stride;
+    int pad;
+};
+
+struct TbDev {           // per-pair traceback job
+    const uint32_t* codes;
+    int n, m, t16;
+    int start_i, start_j;  // interior start cell (1-based), or 0 = nothing to walk
+    uint8_t* moves;        // out: one code per move
+    int* nmoves;           // out
+    int* end_ij;           // out: [2] position where the walk left the interior
+};
+
+inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace gx

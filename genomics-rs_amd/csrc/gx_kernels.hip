@@ -1,0 +1,470 @@
+// gx_kernels.hip -- CDNA4 (gfx950) kernels for the Gotoh-style affine-gap
+// fill of nlaha/genomics-rs (src/alignment/algo.rs:151-282) and the
+// per-cell-max traceback walk (algo.rs:339-422).
+//
+// Fill: one workgroup = one BAND of W strips (W compute waves) + 1 I/O wave.
+//   * lane l of a compute wave owns row i = 64*strip + l + 1 and sweeps the
+//     columns on the anti-diagonal skew (step t -> column t - l + 1);
+//   * the row above arrives through a 64-lane DPP wave_shr:1 (lane l reads
+//     lane l-1's cell of the previous step); lane 0 takes it from an LDS ring
+//     filled by the wave above (or by the I/O wave at a band boundary);
+//   * lane 63's cell is pushed into the LDS ring of the wave below;
+//   * the three int32 score planes are written 16 B/lane every 4 steps into
+//     the strip-major anti-diagonal layout (gx_internal.h) -- every store is a
+//     1 KiB contiguous wave store;
+//   * bands are taken from a global atomic queue in order, so the band a
+//     workgroup waits on is always held by a running workgroup (no residency
+//     assumption); band-to-band rows go through HBM with write-through (sc1)
+//     8-byte agent atomics and a per-boundary progress counter
+//     (cdna_hip_programming.md Guideline 16, "8-B agent atomics both sides").
+// No MFMA: the recurrence is an integer max-plus, not a contraction.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <limits.h>
+#include "gx_internal.h"
+
+namespace gx {
+
+#define DPP_WAVE_SHR1 0x138
+
+__device__ __forceinline__ int shr1(int old, int src) {
+    // lane l <- src[l-1]; lane 0 keeps `old` (bound_ctrl off)
+    return __builtin_amdgcn_update_dpp(old, src, DPP_WAVE_SHR1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
+
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Every spin is bounded (~2^25 sleeps, seconds): on expiry the wave records a
+// timeout in *status and carries on, so the grid always drains; the host
+// turns a non-zero status into GX_EHIP.
+constexpr unsigned kSpinLimit = 1u << 25;
+
+__device__ __forceinline__ void wait_ge(volatile int* p, int v, int* status) {
+    for (unsigned it = 0; *p < v; ++it) {
+        if (it > kSpinLimit) { __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ int ld_agent(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ Rec ld_rec_agent(const Rec* p) {
+    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+    unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    Rec r;
+    r.dd = (int)(a & 0xffffffffu); r.sm = (int)(a >> 32);
+    r.l = (int)(b & 0xffffffffu);  r.c2 = (int)(b >> 32);
+    return r;
+}
+__device__ __forceinline__ void st_rec_agent(Rec* p, Rec r) {
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    __hip_atomic_store(q, (unsigned long long)(unsigned)r.dd | ((unsigned long long)(unsigned)r.sm << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, (unsigned long long)(unsigned)r.l | ((unsigned long long)(unsigned)r.c2 << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct LaneState {
+    int I, SD, Dd, SM, L, c2c, SMtl, Ltl;
+    int best, bstep, bl, lbest, lstep;
+    uint32_t cacc;
+};
+
+// One anti-diagonal step of a compute wave.  MASKED: some lanes are outside
+// columns 1..m this step (ramp-up / ramp-down of the skew).
+template <bool LOCAL, bool MASKED, bool CODES>
+__device__ __forceinline__ void dp_step(LaneState& st, const Rec r, const int t, const int lane, const int m,
+                                        const int c1v, const Scores32& sc, int& oI, int& oD, int& oS, int& oL) {
+    // row above (i-1, j): lane 0 from the ring, others from lane-1 (wave_shr:1)
+    const int dd_in = shr1(r.dd, st.Dd);   // == D(i, j): delete score of the new cell
+    const int sm_in = shr1(r.sm, st.SM);   // score_max(i-1, j)
+    const int l_in = shr1(r.l, st.L);      // max_matches(i-1, j)
+    const int c2 = shr1(r.c2, st.c2c);     // s2[j-1]
+    // algo.rs:231-236  insert_score = top.score_max(g, h+g, h+g)
+    const int In = max3i(st.I + sc.g, st.SD + sc.hg, sc.floor_);
+    const bool mt = c2 == c1v;             // sequence.rs:113-114
+    // algo.rs:245-248  sub_score = s_(mis)match + top_left.score_max(0,0,0)
+    const int Sn = st.SMtl + (mt ? sc.sm : sc.smm);
+    const int Dn = dd_in;                  // algo.rs:238-243 (computed by the lane above)
+    const int IS = max(In, Sn);
+    const int SMn = max(IS, Dn);           // cell.score_max(0,0,0); >= floor since In >= floor
+    const int SDn = max(Sn, Dn);
+    const int Ddn = max3i(IS + sc.hg, Dn + sc.g, sc.floor_);
+    const int Ln = max3i(st.L, l_in, st.Ltl + (mt ? 1 : 0));   // algo.rs:250-255
+    bool act = true;
+    if (MASKED) act = (unsigned)(t - lane) < (unsigned)m;
+    if (!MASKED || act) {
+        st.I = In; st.SD = SDn; st.Dd = Ddn; st.SM = SMn; st.L = Ln;
+    }
+    st.SMtl = sm_in; st.Ltl = l_in; st.c2c = c2;
+    // algo.rs:258-262: first strict maximum in row-major order
+    if (act && SMn > st.best) { st.best = SMn; st.bstep = t; st.bl = Ln; }
+    // algo.rs:310-322: max_by keeps the LAST maximum
+    if (LOCAL && act && SMn >= st.lbest) { st.lbest = SMn; st.lstep = t; }
+    if (CODES) {
+        // retrace priority S > I > D against the cell max (algo.rs:351-400)
+        const uint32_t code = (SMn == Sn) ? 0u : ((SMn == In) ? 1u : 2u);
+        st.cacc = (st.cacc << 2) | code;
+    }
+    oI = In; oD = Dn; oS = Sn; oL = Ln;
+}
+
+template <bool LOCAL, bool PLANES, bool LCSP, bool CODES>
+__device__ void compute_wave(const PairDev& P, const int s, const int lane, const Scores32& sc,
+                             const Rec* ring_in, Rec* ring_out, volatile int* wcnt_in, volatile int* rcnt_in,
+                             volatile int* wcnt_out, volatile int* rcnt_out, const bool has_consumer,
+                             StripRes* sres, PairRes* pres, int* status) {
+    const int n = P.n, m = P.m;
+    const int i = s * kWave + lane + 1;
+    const bool row_ok = i <= n;
+    const int c1v = row_ok ? (int)P.c1[i - 1] : 0x1FF;   // 0x1FF never equals a byte
+    LaneState st;
+    // cell (i, 0): algo.rs:204-211
+    const int D0 = sc.h + i * sc.g;
+    st.I = kNeg;
+    st.SD = D0;                                   // max(sub=neg_inf, delete)
+    st.SM = max(D0, sc.floor_);
+    st.Dd = max3i(kNeg + sc.hg, D0 + sc.g, sc.floor_);
+    st.L = 0;
+    st.c2c = 0;
+    st.SMtl = 0; st.Ltl = 0;
+    st.best = row_ok ? INT_MIN : INT_MAX; st.bstep = 0; st.bl = 0;
+    st.lbest = row_ok ? INT_MIN : INT_MAX; st.lstep = 0;
+    st.cacc = 0;
+
+    if (has_consumer) {
+        if (lane == kWave - 1) ring_out[0] = Rec{st.Dd, st.SM, st.L, 0};
+        lds_wait();
+        if (lane == 0) *wcnt_out = 1;
+    }
+
+    const int T = m + kWave - 1;
+    const size_t strip_off4 = (size_t)s * P.t4;       // in 4-step groups
+    const size_t strip_off16 = (size_t)s * P.t16;
+    for (int t0 = 0; t0 < T; t0 += kSub) {
+        wait_ge(wcnt_in, min(t0 + kSub, m) + 1, status);
+        if (has_consumer) {
+            const int hi = t0 + kSub - 1 - (kWave - 2);
+            if (hi >= kRing) wait_ge(rcnt_out, hi - kRing + 1, status);
+        }
+        if (t0 == 0) { const Rec r0 = ring_in[0]; st.SMtl = r0.sm; st.Ltl = r0.l; }
+        const bool full = (t0 >= kWave - 1) && (t0 + kSub - 1 <= m - 1);
+#pragma unroll
+        for (int q = 0; q < kSub; q += 4) {
+            int bI[4], bD[4], bS[4], bL[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int t = t0 + q + u;
+                const Rec r = ring_in[(t + 1) & (kRing - 1)];
+                if (full) dp_step<LOCAL, false, CODES>(st, r, t, lane, m, c1v, sc, bI[u], bD[u], bS[u], bL[u]);
+                else dp_step<LOCAL, true, CODES>(st, r, t, lane, m, c1v, sc, bI[u], bD[u], bS[u], bL[u]);
+                if (has_consumer && lane == kWave - 1 && (full || (unsigned)(t - lane) < (unsigned)m))
+                    ring_out[(t - (kWave - 2)) & (kRing - 1)] = Rec{st.Dd, st.SM, st.L, st.c2c};
+            }
+            if (PLANES) {
+                const size_t o = ((strip_off4 + ((t0 + q) >> 2)) * kWave + lane) * 4;
+                *reinterpret_cast<int4*>(P.pI + o) = make_int4(bI[0], bI[1], bI[2], bI[3]);
+                *reinterpret_cast<int4*>(P.pD + o) = make_int4(bD[0], bD[1], bD[2], bD[3]);
+                *reinterpret_cast<int4*>(P.pS + o) = make_int4(bS[0], bS[1], bS[2], bS[3]);
+                if (LCSP) *reinterpret_cast<int4*>(P.pL + o) = make_int4(bL[0], bL[1], bL[2], bL[3]);
+            }
+        }
+        if (CODES) P.codes[(strip_off16 + (t0 >> 4)) * kWave + lane] = st.cacc;
+        // publish: consumed input columns, produced output columns
+        lds_wait();
+        if (lane == 0) {
+            const int t_end = t0 + kSub - 1;
+            *rcnt_in = min(t_end + 2, m + 1);
+            if (has_consumer) {
+                const int w = min(t_end - (kWave - 2), m) + 1;
+                if (w > 1) *wcnt_out = w;
+            }
+        }
+    }
+
+    // ---- strip reduction of the max trackers ----
+    int best = row_ok ? st.best : INT_MIN;
+    int lbest = row_ok ? st.lbest : INT_MIN;
+    int mx = best, lmx = lbest;
+    for (int off = 32; off > 0; off >>= 1) {
+        mx = max(mx, __shfl_xor(mx, off));
+        lmx = max(lmx, __shfl_xor(lmx, off));
+    }
+    const unsigned long long fmask = __ballot(row_ok && best == mx);
+    const unsigned long long lmask = __ballot(row_ok && lbest == lmx);
+    const int fl = fmask ? (__ffsll((long long)fmask) - 1) : 0;           // lowest row
+    const int ll = lmask ? (63 - __clzll((long long)lmask)) : 0;          // highest row
+    const int f_step = __shfl(st.bstep, fl), f_l = __shfl(st.bl, fl);
+    const int l_step = __shfl(st.lstep, ll);
+    if (lane == 0) {
+        StripRes r;
+        r.best = mx; r.bi = s * kWave + fl + 1; r.bj = f_step - fl + 1; r.bl = f_l;
+        r.lbest = lmx; r.li = s * kWave + ll + 1; r.lj = l_step - ll + 1; r.valid = 1;
+        sres[P.strip_base + s] = r;
+    }
+    // cell (n, m) for the global-mode start (algo.rs:308, 331)
+    if (row_ok && i == n) pres->end_SM = st.SM;
+}
+
+// I/O wave of a band: feeds ring 0 (row 0 analytic, or the previous band's
+// published bottom row) and drains ring W to HBM for the next band.
+__device__ void io_wave(const PairDev& P, const int lb, const int lane, const Scores32& sc,
+                        Rec* ring0, const Rec* ringW, volatile int* wcnt0, volatile int* rcnt0,
+                        volatile int* wcntW, volatile int* rcntW, const bool do_out, int* status) {
+    const int m = P.m;
+    int in_next = 0, out_next = 0;
+    const Rec* feed_in = lb > 0 ? P.feed + (size_t)(lb - 1) * P.feed_stride : nullptr;
+    Rec* feed_out = do_out ? P.feed + (size_t)lb * P.feed_stride : nullptr;
+    const int* prog_in = lb > 0 ? P.progress + (lb - 1) : nullptr;
+    int* prog_out = do_out ? P.progress + lb : nullptr;
+    unsigned idle = 0;
+    while (in_next <= m || (do_out && out_next <= m)) {
+        bool moved = false;
+        if (in_next <= m) {
+            const int chunk = min(kIoChunk, m + 1 - in_next);
+            const int last = in_next + chunk - 1;
+            bool ok = last < *rcnt0 + kRing;
+            if (ok && lb > 0) ok = ld_agent(prog_in) > last;
+            if (ok) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const int j = in_next + lane;
+                if (lane < chunk) {
+                    Rec r;
+                    if (lb == 0) {
+                        // row 0 (algo.rs:195-202, 213-220): I = h + j g, D = S = neg_inf
+                        if (j == 0) { r.dd = 0; r.sm = 0; r.l = 0; r.c2 = 0; }
+                        else {
+                            const int I0 = sc.h + j * sc.g;
+                            r.dd = max(I0 + sc.hg, sc.floor_);
+                            r.sm = max(I0, sc.floor_);
+                            r.l = 0;
+                            r.c2 = P.c2[j - 1];
+                        }
+                    } else {
+                        r = ld_rec_agent(feed_in + j);
+                    }
+                    ring0[j & (kRing - 1)] = r;
+                }
+                lds_wait();
+                if (lane == 0) *wcnt0 = last + 1;
+                in_next = last + 1;
+                moved = true;
+            }
+        }
+        if (do_out && out_next <= m) {
+            const int avail = *wcntW;
+            const int chunk = min(kIoChunk, avail - out_next);
+            if (chunk == kIoChunk || (avail == m + 1 && chunk > 0)) {
+                const int j = out_next + lane;
+                if (lane < chunk) st_rec_agent(feed_out + j, ringW[j & (kRing - 1)]);
+                vm_wait();
+                lds_wait();
+                if (lane == 0) {
+                    *rcntW = out_next + chunk;
+                    st_agent(prog_out, out_next + chunk);
+                }
+                out_next += chunk;
+                moved = true;
+            }
+        }
+        if (moved) idle = 0;
+        else if (++idle > kSpinLimit) {
+            __hip_atomic_store(status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        } else {
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+template <int W, bool LOCAL, bool PLANES, bool LCSP, bool CODES>
+__global__ __launch_bounds__((W + 1) * kWave) void fill_kernel(const PairDev* __restrict__ pairs, const int npairs,
+                                                              const int total_bands, int* band_counter,
+                                                              StripRes* sres, PairRes* pres, const Scores32 sc) {
+    __shared__ Rec rings[W + 1][kRing];
+    __shared__ int wcnt[W + 1];
+    __shared__ int rcnt[W + 1];
+    __shared__ int band_sh;
+    const int wave = threadIdx.x / kWave;
+    const int lane = threadIdx.x & (kWave - 1);
+    for (;;) {
+        if (threadIdx.x == 0) band_sh = atomicAdd(band_counter, 1);
+        if (threadIdx.x < W + 1) { wcnt[threadIdx.x] = 0; rcnt[threadIdx.x] = 0; }
+        __syncthreads();
+        const int b = band_sh;
+        if (b >= total_bands) return;
+        int p = 0;
+        while (p + 1 < npairs && pairs[p + 1].band_base <= b) ++p;
+        const PairDev& P = pairs[p];
+        const int lb = b - P.band_base;
+        const int s0 = lb * W;
+        if (wave < W) {
+            const int s = s0 + wave;
+            if (s < P.strips) {
+                const bool last_in_band = wave == W - 1;
+                const bool has_consumer = last_in_band ? (lb + 1 < P.bands) : (s + 1 < P.strips);
+                compute_wave<LOCAL, PLANES, LCSP, CODES>(P, s, lane, sc, rings[wave], rings[wave + 1],
+                                                         &wcnt[wave], &rcnt[wave], &wcnt[wave + 1],
+                                                         &rcnt[wave + 1], has_consumer, sres, pres + p,
+                                                         band_counter + 1);
+            }
+        } else {
+            io_wave(P, lb, lane, sc, rings[0], rings[W], &wcnt[0], &rcnt[0], &wcnt[W], &rcnt[W],
+                    lb + 1 < P.bands, band_counter + 1);
+        }
+        __syncthreads();
+    }
+}
+
+// Per-pair reduction of the strip results (first max: lowest strip wins ties;
+// last max: highest strip wins ties).
+__global__ void finalize_kernel(const PairDev* __restrict__ pairs, const StripRes* __restrict__ sres,
+                                PairRes* pres) {
+    const int p = blockIdx.x;
+    const PairDev& P = pairs[p];
+    if (threadIdx.x != 0) return;
+    int best = INT_MIN, bi = 0, bj = 0, bl = 0, lbest = INT_MIN, li = 0, lj = 0;
+    for (int s = 0; s < P.strips; ++s) {
+        const StripRes r = sres[P.strip_base + s];
+        if (r.best > best) { best = r.best; bi = r.bi; bj = r.bj; bl = r.bl; }
+        if (r.lbest >= lbest) { lbest = r.lbest; li = r.li; lj = r.lj; }
+    }
+    PairRes& o = pres[p];
+    o.max_val = best; o.max_i = bi; o.max_j = bj; o.mam = bl;
+    o.lmax_val = lbest; o.lmax_i = li; o.lmax_j = lj; o.nstrips = P.strips;
+}
+
+// Traceback walk over the 2-bit direction codes (algo.rs:339-422), interior
+// cells only; the host finishes the boundary part and labels the moves.
+// One wave per pair; the walk state is wave-uniform.  A 64-step x 64-row
+// chunk of codes is held in 4 VGPRs (lane = row) and read with readlane.
+__global__ __launch_bounds__(64) void traceback_kernel(const TbDev* __restrict__ jobs) {
+    const TbDev J = jobs[blockIdx.x];
+    const int lane = threadIdx.x;
+    int i = J.start_i, j = J.start_j;
+    int k = 0;
+    uint32_t mvbuf = 0;
+    if (i < 1 || j < 1) {
+        if (lane == 0) { *J.nmoves = 0; J.end_ij[0] = i; J.end_ij[1] = j; }
+        return;
+    }
+    int cur_s = -1, cur_q = -1;  // chunk = strip s, words q..q+3 (t in [16q, 16q+64))
+    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    while (i >= 1 && j >= 1) {
+        const int s = (i - 1) >> 6;
+        const int l = (i - 1) & 63;
+        const int t = j - 1 + l;
+        const int tq = t >> 4;
+        if (s != cur_s || tq < cur_q || tq > cur_q + 3) {
+            cur_s = s;
+            cur_q = max(tq - 3, 0);
+            const uint32_t* base = J.codes + ((size_t)s * J.t16 + cur_q) * kWave + lane;
+            w0 = base[0];
+            w1 = (cur_q + 1 < J.t16) ? base[kWave] : 0u;
+            w2 = (cur_q + 2 < J.t16) ? base[2 * kWave] : 0u;
+            w3 = (cur_q + 3 < J.t16) ? base[3 * kWave] : 0u;
+        }
+        const int d = tq - cur_q;
+        uint32_t word;
+        if (d == 0) word = __builtin_amdgcn_readlane(w0, l);
+        else if (d == 1) word = __builtin_amdgcn_readlane(w1, l);
+        else if (d == 2) word = __builtin_amdgcn_readlane(w2, l);
+        else word = __builtin_amdgcn_readlane(w3, l);
+        const uint32_t code = (word >> (2 * (15 - (t & 15)))) & 3u;
+        if (lane == (k & 63)) mvbuf = code;
+        ++k;
+        if ((k & 63) == 0) J.moves[k - 64 + lane] = (uint8_t)mvbuf;
+        if (code == 0) { --i; --j; }
+        else if (code == 1) { --j; }
+        else { --i; }
+    }
+    const int rem = k & 63;
+    if (rem && lane < rem) J.moves[k - rem + lane] = (uint8_t)mvbuf;
+    if (lane == 0) { *J.nmoves = k; J.end_ij[0] = i; J.end_ij[1] = j; }
+}
+
+// Export: strip-major anti-diagonal planes -> row-major (n+1) x (m+1) int32
+// (interior only; the host fills the boundary in int64).
+__global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __restrict__ out, int n, int m, int t4) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t total = (size_t)n * m;
+    if (idx >= total) return;
+    const int i = (int)(idx / m) + 1;
+    const int j = (int)(idx % m) + 1;
+    const int s = (i - 1) >> 6, l = (i - 1) & 63, t = j - 1 + l;
+    const size_t o = (((size_t)s * t4 + (t >> 2)) * kWave + l) * 4 + (t & 3);
+    out[(size_t)i * (m + 1) + j] = plane[o];
+}
+
+}  // namespace gx
+
+// ---- explicit launch wrappers (C++ linkage, used by gx_api.cpp) ----
+namespace gx {
+
+template <int W, bool LOCAL, bool PLANES, bool LCSP, bool CODES>
+static hipError_t launch_fill_t(const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
+                                StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
+    hipLaunchKernelGGL((fill_kernel<W, LOCAL, PLANES, LCSP, CODES>), dim3(grid), dim3((W + 1) * kWave), 0, st,
+                       d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill(int W, bool local, bool planes, bool lcs, bool codes, const PairDev* d_pairs, int npairs,
+                       int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
+                       hipStream_t st) {
+#define GX_FILL_CASE(WW, LO, PL, CO)                                                                     \
+    if (W == WW && local == LO && planes == PL && codes == CO && !lcs)                                   \
+        return launch_fill_t<WW, LO, PL, false, CO>(d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, \
+                                                    sc, grid, st);
+#define GX_FILL_W(WW)                 \
+    GX_FILL_CASE(WW, false, false, false) \
+    GX_FILL_CASE(WW, false, false, true)  \
+    GX_FILL_CASE(WW, false, true, false)  \
+    GX_FILL_CASE(WW, false, true, true)   \
+    GX_FILL_CASE(WW, true, false, false)  \
+    GX_FILL_CASE(WW, true, false, true)   \
+    GX_FILL_CASE(WW, true, true, false)   \
+    GX_FILL_CASE(WW, true, true, true)
+    GX_FILL_W(1)
+    GX_FILL_W(2)
+    GX_FILL_W(4)
+    // full-fidelity export (LCS plane): one configuration per mode
+    if (W == 4 && planes && codes && lcs)
+        return local ? launch_fill_t<4, true, true, true, true>(d_pairs, npairs, total_bands, d_counter, d_sres,
+                                                                 d_pres, sc, grid, st)
+                     : launch_fill_t<4, false, true, true, true>(d_pairs, npairs, total_bands, d_counter, d_sres,
+                                                                  d_pres, sc, grid, st);
+#undef GX_FILL_W
+#undef GX_FILL_CASE
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d_sres, PairRes* d_pres,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(finalize_kernel, dim3(npairs), dim3(64), 0, st, d_pairs, d_sres, d_pres);
+    return hipGetLastError();
+}
+
+hipError_t launch_traceback(const TbDev* d_jobs, int njobs, hipStream_t st) {
+    hipLaunchKernelGGL(traceback_kernel, dim3(njobs), dim3(64), 0, st, d_jobs);
+    return hipGetLastError();
+}
+
+hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, hipStream_t st) {
+    const size_t total = (size_t)n * m;
+    if (total == 0) return hipSuccess;
+    const int blk = 256;
+    hipLaunchKernelGGL(export_kernel, dim3((unsigned)((total + blk - 1) / blk)), dim3(blk), 0, st, plane, out, n, m,
+                       t4);
+    return hipGetLastError();
+}
+
+}  // namespace gx

@@ -1,0 +1,180 @@
+/*
+ * gx.h -- C ABI of genomics-rs_amd: an MI355X (gfx950) drop-in for the
+ * affine-gap alignment path of nlaha/genomics-rs.
+ *
+ * Every entry point replaces one item of the reference's public Rust API
+ * (src/lib.rs:3-6 re-exports alignment, config, sequence).  A Rust shim binds
+ * these 1:1 with `extern "C"`.  Plain pointers and sizes
+ * only; host memory unless a name says `_device`.  All calls return 0 on
+ * success or a GX_E* code; gx_last_error() (thread-local) describes the last
+ * failure.  The library never aborts the process.
+ */
+#ifndef GX_H
+#define GX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------- */
+#define GX_OK 0
+#define GX_EINVAL 1       /* bad argument (NULL, size mismatch)                        */
+#define GX_ESEQ 2         /* fewer than 2 sequences: the reference panics (algo.rs:169) */
+#define GX_ERANGE 3       /* scores/lengths outside the exact int32 device range        */
+#define GX_ENOMEM 4       /* device or host allocation failed                           */
+#define GX_EHIP 5         /* HIP runtime error                                          */
+#define GX_EPANIC 6       /* the reference would panic (retrace, algo.rs:407-408)       */
+#define GX_ECAP 7         /* caller buffer too small (needed size reported)             */
+#define GX_EIO 8          /* file could not be read                                     */
+#define GX_EPARSE 9       /* config could not be parsed                                 */
+
+/* ---- config.rs:6-13  Scores ------------------------------------------ */
+typedef struct gx_scores {
+    int64_t s_match;
+    int64_t s_mismatch;
+    int64_t g; /* per-residue gap */
+    int64_t h; /* gap opening     */
+} gx_scores;
+
+/* ---- algo.rs:25-35  #[repr(C)] AlignmentCell (48 B, same field order) - */
+typedef struct gx_cell {
+    int64_t insert_score;
+    int64_t delete_score;
+    int64_t sub_score;
+    uint64_t insert_matches;
+    uint64_t delete_matches;
+    uint64_t sub_matches;
+} gx_cell;
+
+/* ---- algo.rs:124-133  #[repr(u8)] AlignmentChoice ---------------------- */
+enum {
+    GX_MATCH = 0,
+    GX_MISMATCH = 1,
+    GX_INSERT = 2,
+    GX_DELETE = 3,
+    GX_OPEN_INSERT = 4,
+    GX_OPEN_DELETE = 5
+};
+
+/* one element of AlignedSequences.alignment: (AlignmentChoice, usize, usize) */
+typedef struct gx_step {
+    uint8_t choice;
+    uint8_t pad[7];
+    uint64_t i;
+    uint64_t j;
+} gx_step;
+
+/* ---- algo.rs:135-146  AlignedSequences stats (+ where the walk started) - */
+typedef struct gx_result {
+    int64_t score;
+    uint64_t matches;
+    uint64_t mismatches;
+    uint64_t gap_extensions;
+    uint64_t opening_gaps;
+    uint64_t n_steps;        /* alignment.len()                                  */
+    uint64_t start_i;        /* retrace start cell (algo.rs:306-323)             */
+    uint64_t start_j;
+    uint64_t max_cell_i;     /* alignment_table's running max cell (algo.rs:258) */
+    uint64_t max_cell_j;
+    uint64_t matches_at_max; /* alignment_table's second return (algo.rs:279)    */
+    int64_t fill_us;         /* device fill time (µs), for the info! log lines    */
+    int64_t retrace_us;      /* traceback time (µs)                              */
+} gx_result;
+
+typedef struct gx_context gx_context; /* one per GPU (device memory cache + stream) */
+typedef struct gx_table gx_table;     /* a device-resident Array2<AlignmentCell>     */
+
+const char* gx_last_error(void);
+const char* gx_version(void);
+
+/* Create a context on HIP device `device`. */
+int gx_context_create(int device, gx_context** out);
+void gx_context_destroy(gx_context* ctx);
+/* Release cached device buffers (they are otherwise reused across calls). */
+int gx_context_trim(gx_context* ctx);
+
+/* ---- alignment_table (algo.rs:151-156) --------------------------------
+ * Fills the table of the first two sequences on the GPU.  The table stays in
+ * HBM (the reference's (n+1)x(m+1) 48 B cells need 42.9 GB at 30k; planes
+ * here take 12 B/cell).  `reverse_sequences` has the semantics of
+ * is_match(.., true) (sequence.rs:102-115).  On success *table_out owns the
+ * table and *matches_at_max holds the second tuple element.
+ * flags: GX_TABLE_PLANES keeps the three score planes (needed for export);
+ *        GX_TABLE_MATCHES additionally keeps the LCS plane so that the
+ *        *_matches fields can be exported (full AlignmentCell fidelity).   */
+#define GX_TABLE_PLANES 1u
+#define GX_TABLE_MATCHES 2u
+int gx_alignment_table(gx_context* ctx, const uint8_t* s1, size_t n, const uint8_t* s2, size_t m,
+                       const gx_scores* scores, int is_local, int reverse_sequences, uint32_t flags,
+                       gx_table** table_out, uint64_t* matches_at_max);
+
+/* Shape and running-max bookkeeping of a table. */
+int gx_table_info(const gx_table* t, uint64_t* n_rows /* n+1 */, uint64_t* n_cols /* m+1 */,
+                  uint64_t* max_cell_i, uint64_t* max_cell_j, int64_t* fill_us);
+
+/* Copy the whole table into caller memory as the reference's Array2
+ * (column-major `.f()`, element (i,j) at i + j*(n+1), algo.rs:172).
+ * Requires GX_TABLE_PLANES (and GX_TABLE_MATCHES for the *_matches fields,
+ * which are otherwise written as 0). */
+int gx_table_export(const gx_table* t, gx_cell* out, size_t out_cells);
+
+/* Copy one score plane (0 = insert, 1 = delete, 2 = sub) as int64, row-major
+ * (i*(m+1)+j) when colmajor = 0, column-major otherwise. */
+int gx_table_export_plane(const gx_table* t, int which, int64_t* out, size_t out_cells, int colmajor);
+
+/* ---- retrace (algo.rs:287-291) -----------------------------------------
+ * Walks the table and consumes it (the reference moves the Array2 in); the
+ * handle is invalid afterwards whatever the return code.  steps[] receives
+ * AlignedSequences.alignment in the reference's order (end -> start);
+ * cap = n + m + 1 always suffices.  GX_ECAP reports out->n_steps needed.  */
+int gx_retrace(gx_table* t, int is_local, gx_step* steps, size_t cap, gx_result* out);
+
+/* Frees a table without retracing. */
+void gx_table_free(gx_table* t);
+
+/* ---- fused alignment_table + retrace (main.rs:143-150) ---------------- */
+int gx_align(gx_context* ctx, const uint8_t* s1, size_t n, const uint8_t* s2, size_t m,
+             const gx_scores* scores, int is_local, int reverse_sequences, gx_step* steps, size_t cap,
+             gx_result* out);
+
+/* ---- many independent pairs in one device launch -----------------------
+ * Pair p aligns s1[p] (n[p]) with s2[p] (m[p]).  Score planes are not kept
+ * (only the traceback codes), so the batch fits HBM.  steps may be NULL
+ * (stats only); otherwise steps[p] has caps[p] entries. */
+int gx_align_batch(gx_context* ctx, const uint8_t* const* s1, const size_t* n, const uint8_t* const* s2,
+                   const size_t* m, size_t npairs, const gx_scores* scores, int is_local, gx_step* const* steps,
+                   const size_t* caps, gx_result* out);
+
+/* ---- device-resident benchmarking path ---------------------------------
+ * Stage one pair per slot in HBM once (gx_stage_pairs), then run the hot
+ * path (fill with score planes + traceback) on the staged inputs with no
+ * host->device traffic.  Used by bench.py; results as gx_align. */
+int gx_stage_pairs(gx_context* ctx, const uint8_t* const* s1, const size_t* n, const uint8_t* const* s2,
+                   const size_t* m, size_t npairs);
+int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes, gx_result* out,
+                  double* fill_ms_out);
+
+/* ---- sequence.rs / config.rs mirrors ----------------------------------- */
+/* from_fasta (sequence.rs:45-95) on a file: records are appended to the
+ * caller's buffers.  Returns GX_OK and sets *n_records; names/sequences are
+ * concatenated into `buf` (cap bytes) with offsets/lengths in the arrays
+ * (rec_cap entries).  An unreadable file logs and yields 0 records (the
+ * reference swallows the error, sequence.rs:84-86). */
+int gx_fasta_load(const char* path, uint8_t* buf, size_t cap, uint64_t* name_off, uint64_t* name_len,
+                  uint64_t* seq_off, uint64_t* seq_len, size_t rec_cap, size_t* n_records, size_t* bytes_needed);
+/* get_config (config.rs:21-40): reads [scores] s_match, s_mismatch, g, h. */
+int gx_config_load(const char* path, gx_scores* out);
+
+/* Display for AlignedSequences (display.rs:9-127) into `out` (NUL-terminated).
+ * *needed receives the full length + 1. */
+int gx_format_alignment(const uint8_t* s1, size_t n, const uint8_t* s2, size_t m, const gx_step* steps,
+                        size_t n_steps, const gx_result* res, char* out, size_t cap, size_t* needed);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GX_H */

@@ -1,0 +1,111 @@
+"""Generate the committed golden fixtures from the CPU oracle.
+
+    python tests/golden/make_golden.py [--large]
+
+oracle_vectors.json : full outputs (alignment vectors) for small inputs --
+                      config 1 (s1.fasta x s2.fasta), the multi-record
+                      test_data files, both modes, both scoring configs.
+large_digests.json  : (--large) digests for the big pairs: BRCA2 (config 3)
+                      and Covid_Wuhan x Covid_USA-CA4 (config 2): score,
+                      stats, start, max_cell, matches_at_max, n_steps, the
+                      sha256 of the alignment vector and weighted checksums
+                      of the three score planes.
+
+The oracle (oracle/gx_oracle.c) is pinned by the reference's own vectors
+(tests/test_oracle.py).  The FASTA inputs are the reference's data files,
+copied under tests/golden/fasta and tests/golden/comparison_data.
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import oracle as o  # noqa: E402
+
+CONFIG = (1, -2, -1, -5)
+TEST = (1, -2, -2, -5)
+
+
+def recs(path):
+    with open(path, "rb") as f:
+        return o.fasta_parse(f.read())
+
+
+def alignment_digest(choices, si, sj):
+    h = hashlib.sha256()
+    h.update(bytes(choices.astype("uint8")))
+    h.update(si.astype("<u8").tobytes())
+    h.update(sj.astype("<u8").tobytes())
+    return h.hexdigest()
+
+
+def small_cases():
+    cases = []
+    fa = os.path.join(HERE, "fasta")
+    pairs = [("config1_s1_s2", recs(os.path.join(fa, "s1.fasta"))[0][1], recs(os.path.join(fa, "s2.fasta"))[0][1])]
+    for name in ("test1", "test2_short", "test3_short", "test4", "Opsin1_colorblindness_gene"):
+        r = recs(os.path.join(fa, name + ".fasta"))
+        pairs.append((name, r[0][1], r[1][1]))
+    # s3 x s4 and simple x repeat (single-record files paired, as config 1)
+    pairs.append(("s3_s4", recs(os.path.join(fa, "s3.fasta"))[0][1], recs(os.path.join(fa, "s4.fasta"))[0][1]))
+    pairs.append(("simple_repeat", recs(os.path.join(fa, "simple.fasta"))[0][1],
+                  recs(os.path.join(fa, "repeat.fasta"))[0][1]))
+    for name, a, b in pairs:
+        for loc in (False, True):
+            for sc in (CONFIG, TEST):
+                r = o.align(a, b, sc, is_local=loc)
+                assert r.status == 0
+                cases.append({
+                    "name": f"{name}/{'local' if loc else 'global'}/{sc}",
+                    "s1": a.decode("latin-1"), "s2": b.decode("latin-1"), "scores": list(sc), "is_local": loc,
+                    "score": r.score, "stats": [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps],
+                    "start": list(r.start), "max_cell": list(r.max_cell), "matches_at_max": r.matches_at_max,
+                    "alignment": [list(x) for x in r.alignment()],
+                })
+    return cases
+
+
+def large_cases():
+    fa = os.path.join(HERE, "fasta")
+    cd = os.path.join(HERE, "comparison_data")
+    brca = recs(os.path.join(fa, "Human-Mouse-BRCA2-cds.fasta"))
+    wuhan = recs(os.path.join(cd, "Covid_Wuhan.fasta"))[0][1]
+    usa = recs(os.path.join(cd, "Covid_USA-CA4.fasta"))[0][1]
+    jobs = [("brca2", brca[0][1], brca[1][1], True), ("brca2", brca[0][1], brca[1][1], False),
+            ("covid_wuhan_usa", wuhan, usa, False), ("covid_wuhan_usa", wuhan, usa, True)]
+    out = []
+    for name, a, b, loc in jobs:
+        r = o.align_lean(a, b, CONFIG, is_local=loc)
+        assert r.status == 0
+        out.append({
+            "name": f"{name}/{'local' if loc else 'global'}", "n": len(a), "m": len(b), "is_local": loc,
+            "scores": list(CONFIG), "score": r.score,
+            "stats": [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps],
+            "start": list(r.start), "max_cell": list(r.max_cell), "matches_at_max": r.matches_at_max,
+            "n_steps": int(len(r.choices)), "alignment_sha256": alignment_digest(r.choices, r.steps_i, r.steps_j),
+            "plane_sums": [str(x) for x in r.extra["plane_sums"]],
+        })
+        print(out[-1]["name"], out[-1]["score"], out[-1]["n_steps"], flush=True)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--large", action="store_true")
+    args = ap.parse_args()
+    o.build()
+    with open(os.path.join(HERE, "oracle_vectors.json"), "w") as f:
+        json.dump({"_source": "tests/golden/make_golden.py (oracle restatement, pinned by "
+                              "tests/test_alignment.rs vectors)", "cases": small_cases()}, f)
+    if args.large:
+        with open(os.path.join(HERE, "large_digests.json"), "w") as f:
+            json.dump({"_source": "tests/golden/make_golden.py --large (oracle_align_lean)",
+                       "cases": large_cases()}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,148 @@
+"""CPU: the C-ABI library loads and exports every symbol declared in
+include/gx.h; host-only entry points (FASTA, config, Display) work without a
+GPU.  No compute calls."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import COMPARISON, FASTA, GOLDEN, ROOT, read_fasta_records
+
+HEADER = os.path.join(ROOT, "include", "gx.h")
+LIB = os.path.join(ROOT, "genomics-rs_amd", "libgx_amd.so")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]*?\b(gx_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_api():
+    syms = declared_symbols()
+    for s in ("gx_alignment_table", "gx_retrace", "gx_align", "gx_align_batch", "gx_table_export",
+              "gx_fasta_load", "gx_config_load", "gx_last_error"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol(gx):
+    lib = gx.lib()
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (gx_\w+)$", out, re.M))
+    missing = [s for s in declared_symbols() if s not in exported]
+    assert not missing, missing
+    for s in declared_symbols():
+        assert getattr(lib, s) is not None
+    assert sorted(gx.EXPORTED) == declared_symbols()
+
+
+def test_struct_layouts(gx):
+    # #[repr(C)] AlignmentCell is 48 B (algo.rs:25-35); gx_step mirrors (u8, usize, usize)
+    assert ctypes.sizeof(gx.CCell) == 48
+    assert ctypes.sizeof(gx.CStep) == 24
+    assert gx.CELL_DTYPE.itemsize == 48 and gx.STEP_DTYPE.itemsize == 24
+    assert [int(c) for c in gx.AlignmentChoice] == [0, 1, 2, 3, 4, 5]
+
+
+def test_version_and_error(gx):
+    assert b"gfx950" in gx.lib().gx_version()
+    with pytest.raises(gx.GxError):
+        gx.get_config("/nonexistent/config.toml")
+    assert b"Could not read config file" in gx.lib().gx_last_error()
+
+
+def test_fasta_loader_matches_oracle(gx):
+    """from_fasta (sequence.rs:45-95): product loader == oracle restatement
+    on every FASTA fixture."""
+    files = [os.path.join(FASTA, f) for f in sorted(os.listdir(FASTA))] + \
+            [os.path.join(COMPARISON, f) for f in sorted(os.listdir(COMPARISON))]
+    for path in files:
+        sc = gx.SequenceContainer()
+        sc.from_fasta(path)
+        want = read_fasta_records(path)
+        got = [(s.name.encode(), s.sequence.encode()) for s in sc.sequences]
+        assert got == want, path
+
+
+def test_fasta_appends_and_edge_cases(gx, tmp_path):
+    p = tmp_path / "e.fasta"
+    p.write_bytes(b"orphan\n>  a b \r\nAC GT \n\n   \n>b\n\tAAA\t\n>empty\n")
+    sc = gx.SequenceContainer()
+    sc.from_fasta(str(p))
+    sc.from_fasta(str(p))                       # appends (sequence.rs:94)
+    assert [(s.name, s.sequence) for s in sc.sequences] == [("a b", "AC GT"), ("b", "AAA"), ("empty", "")] * 2
+    q = tmp_path / "bad.fasta"
+    q.write_bytes(b">a\nAC\n\xff\xfe\nGG\n")
+    sc = gx.SequenceContainer()
+    sc.from_fasta(str(q))
+    assert [(s.name, s.sequence) for s in sc.sequences] == [("a", "AC")]
+    sc = gx.SequenceContainer()
+    sc.from_fasta(str(tmp_path / "missing.fasta"))   # swallowed (sequence.rs:84-86)
+    assert sc.sequences == []
+
+
+def test_config_loader(gx, tmp_path):
+    c = gx.get_config(os.path.join(GOLDEN, "config.toml"))
+    assert (c.scores.s_match, c.scores.s_mismatch, c.scores.g, c.scores.h) == (1, -2, -1, -5)
+    p = tmp_path / "c.toml"
+    p.write_text("# comment\ntitle = 'x'\n[scores]\ns_match = +2 # two\ns_mismatch = -1_0\ng = -1\nh = -3\n"
+                 "extra = 7\n[other]\ng = 99\n")
+    c = gx.get_config(str(p))
+    assert (c.scores.s_match, c.scores.s_mismatch, c.scores.g, c.scores.h) == (2, -10, -1, -3)
+    p.write_text("scores = { s_match = 1, s_mismatch = -2, g = -2, h = -5 }\n")
+    c = gx.get_config(str(p))
+    assert (c.scores.g, c.scores.h) == (-2, -5)
+    for bad in ("[scores]\ns_match = 1\ns_mismatch = -2\ng = -1\n",          # missing h
+                "[scores]\ns_match = 1.5\ns_mismatch = -2\ng = -1\nh = -5\n",   # not an integer
+                "[scores]\ns_match = 1\ns_match = 2\ns_mismatch = -2\ng = -1\nh = -5\n"):
+        p.write_text(bad)
+        with pytest.raises(gx.GxError):
+            gx.get_config(str(p))
+
+
+def _display_restatement(s1, s2, alignment, score, matches, mismatches, ext, opens):
+    """Python restatement of display.rs:9-127 (the writeln! output)."""
+    W = 200
+    out, a1, al, a2 = [], "", "", ""
+    i1 = i2 = hl = ai = 0
+    for c, _, _ in reversed(alignment):
+        if hl > W:
+            out.append(f"\n\n{ai - W}-{ai}:\n\n{a1}\n{al}\n{a2}\n")
+            a1 = al = a2 = ""
+            hl = 0
+        if c in ("Insert", "OpenInsert"):
+            a1 += "-"
+        elif i1 < len(s1):
+            a1 += s1[i1]; i1 += 1
+        al += {"Match": "|", "Mismatch": "x", "Insert": " ", "Delete": " "}.get(c, "%")
+        if c in ("Delete", "OpenDelete"):
+            a2 += "-"
+        elif i2 < len(s2):
+            a2 += s2[i2]; i2 += 1
+        hl += 1
+        ai += 1
+    out.append(f"\n\n{ai - len(a1)}-{ai}:\n\n{a1}\n{al}\n{a2}\n")
+    out.append(f"\n\nAlignment Score: {score}\n")
+    for lab, v in (("Matches", matches), ("Mismatches", mismatches), ("Gap Extensions", ext),
+                   ("Opening Gaps", opens)):
+        out.append(f"{lab}: {v}/{ai} ({v / ai * 100:.2f}%)\n")
+    pid = matches / ai * 100
+    pid_s = repr(pid)
+    if pid_s.endswith(".0"):
+        pid_s = pid_s[:-2]          # Rust Display of an integral f64 omits ".0"
+    out.append(f"Percent Identity {pid_s}%\n")
+    return "".join(out)
+
+
+def test_display_matches_restatement(gx, oracle):
+    import json
+    with open(os.path.join(GOLDEN, "oracle_vectors.json")) as f:
+        cases = json.load(f)["cases"]
+    for c in cases[:40]:
+        aln = [(x[0], x[1], x[2]) for x in c["alignment"]]
+        a = gx.AlignedSequences(gx.Sequence("s1", c["s1"]), gx.Sequence("s2", c["s2"]),
+                                [(gx.AlignmentChoice[x[0]], x[1], x[2]) for x in aln], c["score"],
+                                c["stats"][0], c["stats"][1], c["stats"][2], c["stats"][3])
+        want = _display_restatement(c["s1"], c["s2"], aln, c["score"], *c["stats"])
+        assert str(a) == want, c["name"]
