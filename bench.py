@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""bench.py -- GCUPS of the MI355X affine-gap aligner on synthetic 30k x 30k
+DNA pairs (BASELINE.json metric), 1..8 GPUs, one process per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs-per-gpu P]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A STEP is one pass of the hot path over one batch: for each of the P
+synthetic 30k x 30k pairs resident on this GPU, the full-table fill that
+writes the three int32 score planes (alignment_table, algo.rs:151-282) plus
+the traceback (retrace, algo.rs:287-441) down to the labelled alignment on
+the host.  Inputs are staged in HBM before the timed region.  Each rank
+aligns its own pairs (weak scaling); RCCL (torch.distributed "nccl") carries
+only the barrier, the max-over-ranks time and the gather of per-pair
+results.  value = all ranks' cells / max-over-ranks time (GCUPS).
+
+roofline: the fill kernel, HBM-bound: 12 B of score-plane writes per cell
+(SURVEY.md 8(d)); achieved = 12 * cells / average fill-kernel time from HIP
+events on the kernel's own stream.  cpu_baseline: the reference-layout C
+restatement (oracle/, 48-B cells, column-major, i-outer/j-inner, one core)
+on the first R rows of the same synthetic pair.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "genomics-rs_amd"))
+
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MEASURED_HBM_GBS = 6290.0  # float4 copy ceiling (same source)
+BYTES_PER_CELL = 12        # one int32 write each of the insert/delete/sub planes
+SCORES = (1, -2, -1, -5)   # config.toml:1-5
+
+
+def splitmix64_bases(seed: int, length: int) -> bytes:
+    """bytes i.i.d. over ACGT from SplitMix64, base = "ACGT"[x >> 62]."""
+    with np.errstate(over="ignore"):
+        k = np.arange(1, length + 1, dtype=np.uint64)
+        z = np.uint64(seed) + k * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return np.frombuffer(b"ACGT", np.uint8)[(z >> np.uint64(62)).astype(np.int64)].tobytes()
+
+
+def synth_pair(k: int, length: int):
+    return (splitmix64_bases(0x5EED0001 + 0x10000 * k, length),
+            splitmix64_bases(0x5EED0002 + 0x10000 * k, length))
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(s1: bytes, s2: bytes, target_s: float, is_local: bool):
+    """Reference-layout restatement timed on this host, one core, on the first
+    R rows of the pair (bounded sample; the per-row access pattern -- a
+    (n+1)*48-B column stride per j step -- is that of the full table)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test/measurement infrastructure, CPU baseline only
+    import tempfile
+    path = os.path.join(tempfile.mkdtemp(prefix="gx_cpu_"), "liboracle_native.so")
+    try:
+        oracle.build(native=True, out=path)
+        kind_note = "gcc -O3 -march=native"
+    except Exception as e:  # no compiler: fall back to the shipped portable build
+        log("cpu_baseline: native build failed (%s); using oracle/liboracle.so" % e)
+        oracle.build()
+        path = oracle.LIB_PATH
+        kind_note = "gcc -O3 -march=x86-64-v3"
+    try:
+        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+    except Exception:
+        pass
+    # grow the sample until one run takes >= half the target (the per-row cost
+    # falls as rows share pages of the column-major table, so extrapolating
+    # from a few rows would overshoot); the touched part of the table stays
+    # under ~24 GB
+    max_rows = min(len(s1) + 1, int(24e9 / (48 * (len(s2) + 1))))
+    rows = 64
+    while True:
+        t0 = time.perf_counter()
+        cells, ck = oracle.ref_layout_fill_rows(s1, s2, rows, SCORES, is_local, lib_path=path)
+        dt = time.perf_counter() - t0
+        if dt >= target_s / 2 or rows >= max_rows:
+            break
+        rows = int(min(max_rows, rows * min(8.0, max(2.0, target_s / max(dt, 1e-3)))))
+    return {
+        "value": round(cells / dt / 1e9, 6),
+        "unit": "GCUPS",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"alignment_table fill, reference layout (48-B AoS cells, column-major (n+1)x(m+1), "
+                  f"i-outer/j-inner, int64; C restatement, {kind_note}) over the first {rows - 1} interior rows "
+                  f"x {len(s2)} columns of synthetic pair 0 ({len(s1)}x{len(s2)}); {cells} cells in {dt:.2f} s",
+        "seconds": round(dt, 3),
+        "cpu": _cpu_model(),
+    }
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def load_traffic(workload: str):
+    """HBM bytes per fill launch from the committed PMC profile of this
+    workload (profiles/pmc_fill_*.json, made by tools/pmc_traffic.py)."""
+    for name in sorted(os.listdir(os.path.join(ROOT, "profiles")), reverse=True) if os.path.isdir(
+            os.path.join(ROOT, "profiles")) else []:
+        if name.startswith("pmc_fill") and name.endswith(".json"):
+            try:
+                with open(os.path.join(ROOT, "profiles", name)) as f:
+                    d = json.load(f)
+                if d.get("workload") == workload:
+                    return d.get("hbm_bytes_per_launch"), name
+            except Exception:
+                continue
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs-per-gpu", type=int, default=int(os.environ.get("GX_BENCH_PAIRS", "4")))
+    ap.add_argument("--length", type=int, default=30000)
+    ap.add_argument("--local", action="store_true", help="Smith-Waterman mode (default: global NW)")
+    ap.add_argument("--no-planes", action="store_true", help="score+traceback only (not the headline)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group(backend="nccl")       # RCCL over xGMI
+        dist = tdist
+
+    import gxamd as gx
+    ctx = gx.Context(local_rank)
+    P, L = args.pairs_per_gpu, args.length
+    pairs = [synth_pair(rank * P + p, L) for p in range(P)]
+    staged = gx.StagedPairs(pairs, ctx=ctx)             # inputs resident in HBM
+    scores = gx.Scores(*SCORES)
+    keep_planes = not args.no_planes
+    cells_rank = sum(len(a) * len(b) for a, b in pairs)
+
+    def barrier():
+        if dist is not None:
+            import torch
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    ref = None
+    for _ in range(args.warmup):
+        res, _ = staged.run(scores, args.local, keep_planes)
+        ref = [(r.score, r.n_steps, r.matches) for r in res]
+    barrier()
+    fill_ms = []
+    tb_us = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res, fms = staged.run(scores, args.local, keep_planes)
+        fill_ms.append(fms)
+        tb_us.append(res[0].retrace_us)
+        got = [(r.score, r.n_steps, r.matches) for r in res]
+        if ref is not None and got != ref:
+            raise RuntimeError("non-deterministic result between steps")
+        ref = got
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    # max over ranks (time) and gather of per-pair results, over RCCL
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        mine = torch.tensor([[r.score, r.n_steps, r.matches] for r in res], dtype=torch.int64, device="cuda")
+        gathered = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(gathered, mine)
+    total_cells = cells_rank * world
+    ms_per_step = elapsed / args.steps * 1e3
+    gcups = total_cells * args.steps / elapsed / 1e9
+    avg_fill_ms = float(np.mean(fill_ms))
+    workload = f"synthetic {L}x{L} DNA pairs (SplitMix64), {P} per GPU, {'local SW' if args.local else 'global NW'}, " \
+               f"scores {SCORES}, {'score planes + traceback' if keep_planes else 'traceback only (no planes)'}"
+    fill_bytes = BYTES_PER_CELL * cells_rank
+    achieved = fill_bytes / (avg_fill_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(workload)
+
+    out = {
+        "metric": "GCUPS (DP cell updates/s) at 30k×30k NW, 1/2/4/8 MI355X; % HBM roofline",
+        "value": round(gcups, 3),
+        "unit": "GCUPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {"workload": workload, "pairs_per_gpu": P, "seq_len": L,
+                   "cells_per_step": total_cells, "parallelism": f"pairs sharded over {world} GPU(s)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if keep_planes else None,
+                     "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_HBM_GBS, 4) if keep_planes else None,
+                     "frac_of_measured_copy_ceiling": round(achieved / MEASURED_HBM_GBS, 4) if keep_planes else None,
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": "gx::fill_kernel", "fill_ms_avg": round(avg_fill_ms, 3),
+                     "algorithmic_bytes_per_launch": fill_bytes},
+        "fill_gcups_per_gpu": round(cells_rank / (avg_fill_ms * 1e-3) / 1e9, 3),
+        "traceback_us_pair0": int(np.mean(tb_us)),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(pairs[0][0], pairs[0][1], args.cpu_seconds, args.local)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

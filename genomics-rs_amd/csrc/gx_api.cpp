@@ -189,6 +189,8 @@ static int check_scores(const gx_scores* s, size_t n, size_t m, HostScores* hs, 
     sc->sm = (int)s->s_match; sc->smm = (int)s->s_mismatch; sc->g = (int)s->g; sc->h = (int)s->h;
     sc->hg = (int)(s->h + s->g);
     sc->floor_ = is_local ? 0 : kNeg;
+    const char* dbg = getenv("GX_DEBUG_FLAGS");
+    sc->dbg = dbg ? atoi(dbg) : 0;
     return GX_OK;
 }
 
@@ -295,7 +297,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         d.n = n; d.m = m;
         d.strips = ceil_div(n, kWave);
         d.bands = ceil_div(d.strips, W);
-        const int T = m + kWave - 1;
+        const int T = m + kWave;   // steps per strip (lane 63 pushes column m at step m + 63)
         d.t16 = ceil_div(T, 16);
         d.t4 = d.t16 * 4;
         d.band_base = bands;
@@ -350,19 +352,34 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         d.feed = (Rec*)job.feed.p + fo[p];
         d.progress = (int*)job.progress.p + gofs[p];
     }
+    const char* trace_file = getenv("GX_TRACE_FILE");
+    DevBuf trace;
+    if (trace_file && *trace_file) {
+        if ((rc = pool_get(ctx, (size_t)std::max(strips, 1) * sizeof(StripTrace), &trace))) return rc;
+        HIPCHK(hipMemsetAsync(trace.p, 0, (size_t)std::max(strips, 1) * sizeof(StripTrace), ctx->stream));
+        for (size_t p = 0; p < P; ++p) job.pd[p].trace = (StripTrace*)trace.p + job.pd[p].strip_base;
+    }
+    const char* dbg_file = getenv("GX_DEBUG_RECS");
+    DevBuf dbgb;
+    if (dbg_file && *dbg_file && P > 0) {
+        const size_t nrec = 2 * ((size_t)job.pd[0].m + 1);
+        if ((rc = pool_get(ctx, nrec * sizeof(Rec), &dbgb))) return rc;
+        HIPCHK(hipMemsetAsync(dbgb.p, 0xFF, nrec * sizeof(Rec), ctx->stream));
+        job.pd[0].dbg = (Rec*)dbgb.p;
+    }
     HIPCHK(hipMemcpyAsync(job.pairs.p, job.pd.data(), P * sizeof(PairDev), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemsetAsync(job.progress.p, 0, std::max<size_t>(prog_elems, 1) * sizeof(int), ctx->stream));
     HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, ctx->stream));
     HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), ctx->stream));
     const int grid = std::min(bands, fill_grid_cap());
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
-    if (bands > 0) {
+    if (bands > 0)
         HIPCHK(launch_fill(W, is_local != 0, planes, lcs, codes, (const PairDev*)job.pairs.p, (int)P, bands,
                            (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, sc, grid, ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));   // ev0..ev1 brackets the fill kernel alone
+    if (bands > 0)
         HIPCHK(launch_finalize((const PairDev*)job.pairs.p, (int)P, (const StripRes*)job.sres.p,
                                (PairRes*)job.pres.p, ctx->stream));
-    }
-    HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
     job.res.assign(P, PairRes{});
     int status[2] = {0, 0};
     HIPCHK(hipMemcpyAsync(job.res.data(), job.pres.p, P * sizeof(PairRes), hipMemcpyDeviceToHost, ctx->stream));
@@ -373,6 +390,30 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     job.fill_ms = ms;
+    if (dbgb.p) {
+        std::vector<Rec> d(2 * ((size_t)job.pd[0].m + 1));
+        HIPCHK(hipMemcpy(d.data(), dbgb.p, d.size() * sizeof(Rec), hipMemcpyDeviceToHost));
+        pool_put(ctx, dbgb);
+        if (FILE* f = fopen(dbg_file, "wb")) {
+            fwrite(d.data(), sizeof(Rec), d.size(), f);
+            fclose(f);
+        }
+    }
+    if (trace.p) {
+        std::vector<StripTrace> tr((size_t)strips);
+        HIPCHK(hipMemcpy(tr.data(), trace.p, tr.size() * sizeof(StripTrace), hipMemcpyDeviceToHost));
+        pool_put(ctx, trace);
+        if (FILE* f = fopen(trace_file, "w")) {
+            fprintf(f, "pair,strip,t_start,t_first,t_end,wait_in,wait_out,W,fill_ms\n");
+            for (size_t p = 0; p < P; ++p)
+                for (int s = 0; s < job.pd[p].strips; ++s) {
+                    const StripTrace& t = tr[job.pd[p].strip_base + s];
+                    fprintf(f, "%zu,%d,%lld,%lld,%lld,%d,%d,%d,%.4f\n", p, s, t.t_start, t.t_first, t.t_end, t.wait_in,
+                            t.wait_out, W, ms);
+                }
+            fclose(f);
+        }
+    }
     return GX_OK;
 }
 

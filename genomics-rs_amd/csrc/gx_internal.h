@@ -10,8 +10,9 @@
 //   Score planes (int32, one each for insert/delete/sub score):
 //       plane[strip][t/4][lane][t%4]        (16 B per lane per 4 steps)
 //   so each wave stores 1 KiB contiguous per plane every 4 steps.
-//   Traceback direction codes (2 bit/cell, 0=sub 1=insert 2=delete):
-//       codes[strip][t/16][lane]  (uint32, step t%16 at bits 2*(15 - t%16))
+//   Traceback direction codes (2 bit/cell), two bit-planes per word:
+//       codes[strip][t/16][lane]  (uint32; for k = t%16 bit 31-k = "delete beats
+//       insert and sub", bit 15-k = "insert beats sub"; decode D ? 2 : I ? 1 : 0)
 #pragma once
 #include <stdint.h>
 
@@ -32,6 +33,7 @@ struct Scores32 {
     int h;       // gap open
     int hg;      // h + g
     int floor_;  // local ? 0 : kNeg  (the 4th lane of score_max, algo.rs:103)
+    int dbg;     // GX_DEBUG_FLAGS: bit0 = rolled path only, bit1 = never trust speculative ring reads
 };
 
 // One inter-strip record: the bottom-row cell (r, j) of a strip, as needed by
@@ -52,6 +54,18 @@ struct __attribute__((aligned(16))) PairRes {
     int end_SM, pad0, pad1, pad2;         // score_max of cell (n, m)
 };
 
+// Optional per-strip timeline (GX_TRACE_FILE): s_memrealtime ticks (100 MHz)
+// and spin iterations, for the diagnostic runs behind DESIGN.md's numbers.
+struct __attribute__((aligned(16))) StripTrace {
+    long long t_start;   // wave starts the strip
+    long long t_first;   // first input sub-block available
+    long long t_end;     // strip done
+    int wait_in;         // spin iterations waiting for the row above
+    int wait_out;        // spin iterations waiting for ring space below
+    int band, wave;
+    int pad0, pad1;
+};
+
 struct PairDev {
     const uint8_t* c1;   // processed row chars, n   (is_match row operand)
     const uint8_t* c2;   // processed col chars, m
@@ -69,6 +83,8 @@ struct PairDev {
     uint32_t* codes;     // traceback codes (nullptr: none)
     Rec* feed;           // [bands-1][feed_stride] band-boundary rows
     int* progress;       // [bands-1] columns published per boundary
+    StripTrace* trace;   // per strip, or nullptr
+    Rec* dbg;            // GX_DEBUG_RECS: [2][m+1] pushed by strip 0 / consumed by strip 1
     int feed_stride;
     int pad;
 };

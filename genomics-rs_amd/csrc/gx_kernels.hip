@@ -25,6 +25,13 @@
 
 namespace gx {
 
+// Explicit address spaces.  Generic (flat) accesses count on both vmcnt and
+// lgkmcnt, so a flat LDS poll would also wait for every outstanding HBM
+// store; LDS counters are therefore AS3 and global words AS1.
+typedef __attribute__((address_space(1))) int gint;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(3))) volatile int lds_int;
+
 #define DPP_WAVE_SHR1 0x138
 
 __device__ __forceinline__ int shr1(int old, int src) {
@@ -41,22 +48,24 @@ __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::
 // turns a non-zero status into GX_EHIP.
 constexpr unsigned kSpinLimit = 1u << 25;
 
-__device__ __forceinline__ void wait_ge(volatile int* p, int v, int* status) {
-    for (unsigned it = 0; *p < v; ++it) {
-        if (it > kSpinLimit) { __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
+__device__ __forceinline__ unsigned wait_ge(lds_int* p, int v, int* status) {
+    unsigned it = 0;
+    for (; *p < v; ++it) {
+        if (it > kSpinLimit) { __hip_atomic_store((gint*)status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
         __builtin_amdgcn_s_sleep(1);
     }
     asm volatile("" ::: "memory");
+    return it;
 }
 
 __device__ __forceinline__ int ld_agent(const int* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load((gint*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st_agent(int* p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gint*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ Rec ld_rec_agent(const Rec* p) {
-    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+    const gu64* q = (const gu64*)p;
     unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     Rec r;
@@ -65,31 +74,71 @@ __device__ __forceinline__ Rec ld_rec_agent(const Rec* p) {
     return r;
 }
 __device__ __forceinline__ void st_rec_agent(Rec* p, Rec r) {
-    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    gu64* q = (gu64*)p;
     __hip_atomic_store(q, (unsigned long long)(unsigned)r.dd | ((unsigned long long)(unsigned)r.sm << 32),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(q + 1, (unsigned long long)(unsigned)r.l | ((unsigned long long)(unsigned)r.c2 << 32),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Ring slot of column c.  The producer pushes column c at step c + 63 and the
+// consumer reads it at step c - 1, so with 16-step sub-blocks both touch 16
+// consecutive, 16-aligned slots per sub-block (constant LDS offsets).
+__device__ __forceinline__ int ring_slot(int c) { return (c + 15) & (kRing - 1); }
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)p;   // low 32 bits of a generic LDS address = LDS offset
+}
+
+// Global-address-space views: stores through them compile to global_store
+// (counted on vmcnt only).  Through a generic pointer they become flat_store,
+// which also counts on lgkmcnt and makes every LDS wait wait for HBM stores.
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) v4i gv4i;
+typedef __attribute__((address_space(1))) uint32_t guint;
+__device__ __forceinline__ void gstore4(int32_t* p, int4 v) {
+    v4i x = {v.x, v.y, v.z, v.w};
+    *(gv4i*)p = x;
+}
+__device__ __forceinline__ void gstore1(uint32_t* p, uint32_t v) { *(guint*)p = v; }
+
 struct LaneState {
+    int strip;
     int I, SD, Dd, SM, L, c2c, SMtl, Ltl;
     int best, bstep, bl, lbest, lstep;
-    uint32_t cacc;
+    uint32_t cI, cD;   // traceback code bit-planes (16 steps each)
 };
+
+// Lane 63 pushes its cell (the strip's bottom row) into the LDS ring of the
+// wave below: two ds_write2_b32 under a lane-63 exec mask.  Written in asm so
+// that no branch or register tuple is needed.  Compute waves call it only
+// with all 64 lanes active (no divergent region), so exec is restored to -1
+// rather than saved (saves an SGPR pair per push).
+template <int U>
+__device__ __forceinline__ void push63(uint32_t base, int a, int b, int c, int d, unsigned long long m63) {
+    asm volatile(
+        "s_mov_b64 exec, %0\n\t"
+        "ds_write2_b32 %1, %2, %3 offset0:%6 offset1:%7\n\t"
+        "ds_write2_b32 %1, %4, %5 offset0:%8 offset1:%9\n\t"
+        "s_mov_b64 exec, -1\n\t"
+        "s_nop 1"   // store-data hazard: the compiler may overwrite a data VGPR right after
+        :
+        : "s"(m63), "v"(base), "v"(a), "v"(b), "v"(c), "v"(d), "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2),
+          "i"(4 * U + 3));
+}
 
 // One anti-diagonal step of a compute wave.  MASKED: some lanes are outside
 // columns 1..m this step (ramp-up / ramp-down of the skew).
 template <bool LOCAL, bool MASKED, bool CODES>
 __device__ __forceinline__ void dp_step(LaneState& st, const Rec r, const int t, const int lane, const int m,
                                         const int c1v, const Scores32& sc, int& oI, int& oD, int& oS, int& oL) {
-    // row above (i-1, j): lane 0 from the ring, others from lane-1 (wave_shr:1)
+    // row above (i-1, j): lane 0 from the ring record, others from lane-1 (wave_shr:1)
     const int dd_in = shr1(r.dd, st.Dd);   // == D(i, j): delete score of the new cell
     const int sm_in = shr1(r.sm, st.SM);   // score_max(i-1, j)
     const int l_in = shr1(r.l, st.L);      // max_matches(i-1, j)
     const int c2 = shr1(r.c2, st.c2c);     // s2[j-1]
     // algo.rs:231-236  insert_score = top.score_max(g, h+g, h+g)
-    const int In = max3i(st.I + sc.g, st.SD + sc.hg, sc.floor_);
+    const int In = LOCAL ? max3i(st.I + sc.g, st.SD + sc.hg, 0) : max(st.I + sc.g, st.SD + sc.hg);
     const bool mt = c2 == c1v;             // sequence.rs:113-114
     // algo.rs:245-248  sub_score = s_(mis)match + top_left.score_max(0,0,0)
     const int Sn = st.SMtl + (mt ? sc.sm : sc.smm);
@@ -97,36 +146,190 @@ __device__ __forceinline__ void dp_step(LaneState& st, const Rec r, const int t,
     const int IS = max(In, Sn);
     const int SMn = max(IS, Dn);           // cell.score_max(0,0,0); >= floor since In >= floor
     const int SDn = max(Sn, Dn);
-    const int Ddn = max3i(IS + sc.hg, Dn + sc.g, sc.floor_);
+    const int Ddn = LOCAL ? max3i(IS + sc.hg, Dn + sc.g, 0) : max(IS + sc.hg, Dn + sc.g);
     const int Ln = max3i(st.L, l_in, st.Ltl + (mt ? 1 : 0));   // algo.rs:250-255
     bool act = true;
     if (MASKED) act = (unsigned)(t - lane) < (unsigned)m;
-    if (!MASKED || act) {
+    if (MASKED) {
+        st.I = act ? In : st.I; st.SD = act ? SDn : st.SD; st.Dd = act ? Ddn : st.Dd;
+        st.SM = act ? SMn : st.SM; st.L = act ? Ln : st.L;
+    } else {
         st.I = In; st.SD = SDn; st.Dd = Ddn; st.SM = SMn; st.L = Ln;
     }
     st.SMtl = sm_in; st.Ltl = l_in; st.c2c = c2;
     // algo.rs:258-262: first strict maximum in row-major order
-    if (act && SMn > st.best) { st.best = SMn; st.bstep = t; st.bl = Ln; }
+    const bool nb = act && SMn > st.best;
+    st.best = nb ? SMn : st.best; st.bstep = nb ? t : st.bstep; st.bl = nb ? Ln : st.bl;
     // algo.rs:310-322: max_by keeps the LAST maximum
-    if (LOCAL && act && SMn >= st.lbest) { st.lbest = SMn; st.lstep = t; }
+    if (LOCAL) {
+        const bool nl = act && SMn >= st.lbest;
+        st.lbest = nl ? SMn : st.lbest; st.lstep = nl ? t : st.lstep;
+    }
     if (CODES) {
-        // retrace priority S > I > D against the cell max (algo.rs:351-400)
-        const uint32_t code = (SMn == Sn) ? 0u : ((SMn == In) ? 1u : 2u);
-        st.cacc = (st.cacc << 2) | code;
+        // retrace priority S > I > D against the cell max (algo.rs:351-400),
+        // two bit-planes: D beats both / I beats S.  Decode: D ? delete : I ? insert : sub.
+        st.cD = st.cD + st.cD + (Dn > IS ? 1u : 0u);
+        st.cI = st.cI + st.cI + (In > Sn ? 1u : 0u);
     }
     oI = In; oD = Dn; oS = Sn; oL = Ln;
 }
 
+// GX_DEBUG_RECS: strip 0 lane 63 logs what it pushes, strip 1 lane 0 what it consumes.
+__device__ __forceinline__ void dbg_log(const PairDev& P, const LaneState& st, int lane, int t, int m, const Rec r) {
+    const int pc = t - (kWave - 1);
+    if (st.strip == 0 && lane == kWave - 1 && pc >= 0 && pc <= m) P.dbg[pc] = Rec{st.Dd, st.SM, st.L, st.c2c};
+    if (st.strip == 1 && lane == 0 && t + 1 <= m) P.dbg[(m + 1) + t + 1] = r;
+}
+
+template <bool LOCAL, bool MASKED, bool PLANES, bool LCSP, bool CODES, int G4>
+__device__ __forceinline__ void step4(LaneState& st, const Rec (&cur)[4], const uint32_t out_base,
+                                      const unsigned long long m63, const int t0, const int lane, const int m,
+                                      const int c1v, const Scores32& sc, const PairDev& P, const size_t strip_off4) {
+    int bI[4], bD[4], bS[4], bL[4];
+#define GX_STEP(U)                                                                                     \
+    {                                                                                                  \
+        const int t = t0 + G4 * 4 + (U);                                                               \
+        /* lane 63 holds column t-63 before this step: push it to the strip below (m63 = 0 when    */  \
+        /* there is no consumer).  Full sub-blocks only push columns 1..m-64.                      */  \
+        push63<G4 * 4 + (U)>(out_base, st.Dd, st.SM, st.L, st.c2c, m63);                               \
+        if (P.dbg) dbg_log(P, st, lane, t, m, cur[U]);                                                  \
+        dp_step<LOCAL, MASKED, CODES>(st, cur[U], t, lane, m, c1v, sc, bI[U], bD[U], bS[U], bL[U]);    \
+    }
+    GX_STEP(0) GX_STEP(1) GX_STEP(2) GX_STEP(3)
+#undef GX_STEP
+    if (PLANES) {
+        // sub-block base (per lane) + G4 KiB: the constant folds into the store's immediate offset
+        const size_t o = ((strip_off4 + (t0 >> 2)) * kWave + lane) * 4 + G4 * kWave * 4;
+        gstore4(P.pI + o, make_int4(bI[0], bI[1], bI[2], bI[3]));
+        gstore4(P.pD + o, make_int4(bD[0], bD[1], bD[2], bD[3]));
+        gstore4(P.pS + o, make_int4(bS[0], bS[1], bS[2], bS[3]));
+        if (LCSP) gstore4(P.pL + o, make_int4(bL[0], bL[1], bL[2], bL[3]));
+    }
+}
+
+// The ring pointers are deliberately NOT __restrict__: another wave writes the
+// ring, and with noalias the compiler may fold the re-read after a wait into
+// the earlier speculative read of the same slots (stale records).
+__device__ __forceinline__ void read4(Rec (&r)[4], const Rec* rin) {
+    r[0] = rin[0]; r[1] = rin[1]; r[2] = rin[2]; r[3] = rin[3];
+}
+
+// One lane stores an LDS counter (exec = lane 0 only, no branch).  LDS executes a
+// wave's DS operations in order, so a counter written after ring pushes is seen
+// after them by every other wave: publication needs no s_waitcnt.
+// (Compute waves only, full exec, like push63.)
+__device__ __forceinline__ void lds_store_lane0(lds_int* p, int v) {
+    asm volatile(
+        "s_mov_b64 exec, 1\n\t"
+        "ds_write_b32 %0, %1\n\t"
+        "s_mov_b64 exec, -1\n\t"
+        "s_nop 1"
+        :
+        : "v"((uint32_t)(uintptr_t)p), "v"(v)
+        : "memory");
+}
+
+// One 4-step group.  `nxt` holds the validated ring records for these steps;
+// the producer's counter is observed and the next group's records are read
+// (in that LDS order) before computing, so the read latency hides behind the
+// group and the records are valid whenever the observed counter covers them.
+template <bool LOCAL, bool MASKED, bool PLANES, bool LCSP, bool CODES, int G4>
+__device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], const Rec* ring_in,
+                                       const uint32_t out_base, const unsigned long long m63, const bool push,
+                                       const int t0, const int lane, const int m, const int c1v, const Scores32& sc,
+                                       const PairDev& P, const size_t strip_off4, lds_int* wcnt_in,
+                                       lds_int* wcnt_out, int* status, unsigned& tr_win) {
+    const int t = t0 + 4 * G4;
+    Rec cur[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
+    const int need = min(t + 8, m) + 1;                       // columns of the next group: t+5 .. t+8
+    const int seen = __builtin_amdgcn_readfirstlane(*wcnt_in);
+    asm volatile("" ::: "memory");
+    read4(nxt, ring_in + ring_slot(t + 5));
+    step4<LOCAL, MASKED, PLANES, LCSP, CODES, G4>(st, cur, out_base, m63, t0, lane, m, c1v, sc, P, strip_off4);
+    if (push) lds_store_lane0(wcnt_out, min(t + 3 - (kWave - 1), m) + 1);
+    if (seen < need || (sc.dbg & 2)) {                        // producer was behind: wait, re-read
+        tr_win += wait_ge(wcnt_in, need, status);
+        read4(nxt, ring_in + ring_slot(t + 5));
+    }
+}
+
+// Same lane-63 push with a runtime LDS address (ramp path).
+__device__ __forceinline__ void push63_rt(uint32_t addr, int a, int b, int c, int d, unsigned long long m63) {
+    asm volatile(
+        "s_mov_b64 exec, %0\n\t"
+        "ds_write2_b32 %1, %2, %3 offset1:1\n\t"
+        "ds_write2_b32 %1, %4, %5 offset0:2 offset1:3\n\t"
+        "s_mov_b64 exec, -1\n\t"
+        "s_nop 1"
+        :
+        : "s"(m63), "v"(addr), "v"(a), "v"(b), "v"(c), "v"(d));
+}
+
+// Ramp-up / ramp-down sub-block (some lanes outside columns 1..m): a rolled
+// loop, blocking on the whole sub-block's input, scalar plane stores.  At the
+// end `nxt` is re-primed with the first group of the next sub-block.
+template <bool LOCAL, bool PLANES, bool LCSP, bool CODES>
+__device__ __forceinline__ void ramp_block(LaneState& st, Rec (&nxt)[4], const Rec* ring_in,
+                                        Rec* ring_out, const unsigned long long m63, const bool push,
+                                        const int t0, const int lane, const int m, const int c1v,
+                                        const Scores32& sc, const PairDev& P, const size_t strip_off4,
+                                        lds_int* wcnt_in, lds_int* wcnt_out, int* status, unsigned& tr_win) {
+    tr_win += wait_ge(wcnt_in, min(t0 + kSub, m) + 1, status);
+#pragma unroll 1
+    for (int u = 0; u < kSub; ++u) {
+        const int t = t0 + u;
+        const Rec r = ring_in[ring_slot(t + 1)];
+        // push only columns 0..m: a push past m would land on the slot of column
+        // c - 256, which a lagging consumer may not have read yet
+        const int col = t - (kWave - 1);
+        const unsigned long long mk =
+            (unsigned long long)__builtin_amdgcn_readfirstlane((col >= 0 && col <= m) ? (unsigned)(m63 >> 32) : 0u)
+            << 32;
+        push63_rt(lds_addr(ring_out + ring_slot(col)), st.Dd, st.SM, st.L, st.c2c, mk);
+        if (P.dbg) dbg_log(P, st, lane, t, m, r);
+        int oI, oD, oS, oL;
+        dp_step<LOCAL, true, CODES>(st, r, t, lane, m, c1v, sc, oI, oD, oS, oL);
+        if (PLANES) {
+            const size_t o = ((strip_off4 + (t >> 2)) * kWave + lane) * 4 + (t & 3);
+            ((gint*)P.pI)[o] = oI;
+            ((gint*)P.pD)[o] = oD;
+            ((gint*)P.pS)[o] = oS;
+            if (LCSP) ((gint*)P.pL)[o] = oL;
+        }
+    }
+    if (push) lds_store_lane0(wcnt_out, min(t0 + kSub - 1 - (kWave - 1), m) + 1);
+    tr_win += wait_ge(wcnt_in, min(t0 + kSub + 4, m) + 1, status);
+    read4(nxt, ring_in + ring_slot(t0 + kSub + 1));
+}
+
+template <bool LOCAL, bool MASKED, bool PLANES, bool LCSP, bool CODES>
+__device__ __forceinline__ void sub_block(LaneState& st, Rec (&nxt)[4], const Rec* ring_in,
+                                          const uint32_t out_base, const unsigned long long m63, const bool push,
+                                          const int t0, const int lane, const int m, const int c1v,
+                                          const Scores32& sc, const PairDev& P, const size_t strip_off4,
+                                          lds_int* wcnt_in, lds_int* wcnt_out, int* status, unsigned& tr_win) {
+    group4<LOCAL, MASKED, PLANES, LCSP, CODES, 0>(st, nxt, ring_in, out_base, m63, push, t0, lane, m, c1v, sc, P,
+                                                  strip_off4, wcnt_in, wcnt_out, status, tr_win);
+    group4<LOCAL, MASKED, PLANES, LCSP, CODES, 1>(st, nxt, ring_in, out_base, m63, push, t0, lane, m, c1v, sc, P,
+                                                  strip_off4, wcnt_in, wcnt_out, status, tr_win);
+    group4<LOCAL, MASKED, PLANES, LCSP, CODES, 2>(st, nxt, ring_in, out_base, m63, push, t0, lane, m, c1v, sc, P,
+                                                  strip_off4, wcnt_in, wcnt_out, status, tr_win);
+    group4<LOCAL, MASKED, PLANES, LCSP, CODES, 3>(st, nxt, ring_in, out_base, m63, push, t0, lane, m, c1v, sc, P,
+                                                  strip_off4, wcnt_in, wcnt_out, status, tr_win);
+}
+
 template <bool LOCAL, bool PLANES, bool LCSP, bool CODES>
 __device__ void compute_wave(const PairDev& P, const int s, const int lane, const Scores32& sc,
-                             const Rec* ring_in, Rec* ring_out, volatile int* wcnt_in, volatile int* rcnt_in,
-                             volatile int* wcnt_out, volatile int* rcnt_out, const bool has_consumer,
-                             StripRes* sres, PairRes* pres, int* status) {
+                             const Rec* ring_in, Rec* ring_out, lds_int* wcnt_in,
+                             lds_int* rcnt_in, lds_int* wcnt_out, lds_int* rcnt_out,
+                             const bool has_consumer, StripRes* sres, PairRes* pres, int* status) {
+    static_assert(kSub == 16, "16-step sub-blocks (code words, ring alignment)");
     const int n = P.n, m = P.m;
     const int i = s * kWave + lane + 1;
     const bool row_ok = i <= n;
     const int c1v = row_ok ? (int)P.c1[i - 1] : 0x1FF;   // 0x1FF never equals a byte
     LaneState st;
+    st.strip = s;
     // cell (i, 0): algo.rs:204-211
     const int D0 = sc.h + i * sc.g;
     st.I = kNeg;
@@ -135,59 +338,50 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     st.Dd = max3i(kNeg + sc.hg, D0 + sc.g, sc.floor_);
     st.L = 0;
     st.c2c = 0;
-    st.SMtl = 0; st.Ltl = 0;
     st.best = row_ok ? INT_MIN : INT_MAX; st.bstep = 0; st.bl = 0;
     st.lbest = row_ok ? INT_MIN : INT_MAX; st.lstep = 0;
-    st.cacc = 0;
+    st.cI = 0; st.cD = 0;
 
     if (has_consumer) {
-        if (lane == kWave - 1) ring_out[0] = Rec{st.Dd, st.SM, st.L, 0};
+        if (lane == kWave - 1) ring_out[ring_slot(0)] = Rec{st.Dd, st.SM, st.L, 0};
         lds_wait();
         if (lane == 0) *wcnt_out = 1;
     }
-
-    const int T = m + kWave - 1;
+    const bool tracing = P.trace != nullptr;
+    long long tr_start = 0, tr_first = 0;
+    unsigned tr_win = 0, tr_wout = 0;
+    if (tracing) tr_start = __builtin_amdgcn_s_memrealtime();
+    // column 0 of the row above seeds the top-left of column 1; columns 1..4
+    // feed the first step group
+    tr_win += wait_ge(wcnt_in, min(4, m) + 1, status);
+    Rec nxt[4];
+    {
+        const Rec r0 = ring_in[ring_slot(0)];
+        st.SMtl = r0.sm;
+        st.Ltl = r0.l;
+        read4(nxt, ring_in + ring_slot(1));
+    }
+    if (tracing) tr_first = __builtin_amdgcn_s_memrealtime();
+    const int T = m + kWave;                          // lane 63 pushes column m at step m + 63
     const size_t strip_off4 = (size_t)s * P.t4;       // in 4-step groups
     const size_t strip_off16 = (size_t)s * P.t16;
     for (int t0 = 0; t0 < T; t0 += kSub) {
-        wait_ge(wcnt_in, min(t0 + kSub, m) + 1, status);
-        if (has_consumer) {
-            const int hi = t0 + kSub - 1 - (kWave - 2);
-            if (hi >= kRing) wait_ge(rcnt_out, hi - kRing + 1, status);
-        }
-        if (t0 == 0) { const Rec r0 = ring_in[0]; st.SMtl = r0.sm; st.Ltl = r0.l; }
-        const bool full = (t0 >= kWave - 1) && (t0 + kSub - 1 <= m - 1);
-#pragma unroll
-        for (int q = 0; q < kSub; q += 4) {
-            int bI[4], bD[4], bS[4], bL[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int t = t0 + q + u;
-                const Rec r = ring_in[(t + 1) & (kRing - 1)];
-                if (full) dp_step<LOCAL, false, CODES>(st, r, t, lane, m, c1v, sc, bI[u], bD[u], bS[u], bL[u]);
-                else dp_step<LOCAL, true, CODES>(st, r, t, lane, m, c1v, sc, bI[u], bD[u], bS[u], bL[u]);
-                if (has_consumer && lane == kWave - 1 && (full || (unsigned)(t - lane) < (unsigned)m))
-                    ring_out[(t - (kWave - 2)) & (kRing - 1)] = Rec{st.Dd, st.SM, st.L, st.c2c};
-            }
-            if (PLANES) {
-                const size_t o = ((strip_off4 + ((t0 + q) >> 2)) * kWave + lane) * 4;
-                *reinterpret_cast<int4*>(P.pI + o) = make_int4(bI[0], bI[1], bI[2], bI[3]);
-                *reinterpret_cast<int4*>(P.pD + o) = make_int4(bD[0], bD[1], bD[2], bD[3]);
-                *reinterpret_cast<int4*>(P.pS + o) = make_int4(bS[0], bS[1], bS[2], bS[3]);
-                if (LCSP) *reinterpret_cast<int4*>(P.pL + o) = make_int4(bL[0], bL[1], bL[2], bL[3]);
-            }
-        }
-        if (CODES) P.codes[(strip_off16 + (t0 >> 4)) * kWave + lane] = st.cacc;
-        // publish: consumed input columns, produced output columns
-        lds_wait();
-        if (lane == 0) {
-            const int t_end = t0 + kSub - 1;
-            *rcnt_in = min(t_end + 2, m + 1);
-            if (has_consumer) {
-                const int w = min(t_end - (kWave - 2), m) + 1;
-                if (w > 1) *wcnt_out = w;
-            }
-        }
+        const uint32_t out_base = lds_addr(ring_out + ring_slot(t0 - (kWave - 1)));
+        const int last_col = min(t0 + kSub - 1 - (kWave - 1), m);   // last column pushed here
+        const bool push = has_consumer && last_col >= 1;
+        if (push && last_col >= kRing) tr_wout += wait_ge(rcnt_out, last_col - kRing + 1, status);
+        const unsigned long long m63 =
+            (unsigned long long)__builtin_amdgcn_readfirstlane(push ? 0x80000000u : 0u) << 32;   // lane-63 exec
+        const bool full = (t0 >= kWave) && (t0 + kSub - 1 <= m - 1) && !(sc.dbg & 1);
+        if (full)
+            sub_block<LOCAL, false, PLANES, LCSP, CODES>(st, nxt, ring_in, out_base, m63, push, t0, lane, m, c1v, sc,
+                                                         P, strip_off4, wcnt_in, wcnt_out, status, tr_win);
+        else
+            ramp_block<LOCAL, PLANES, LCSP, CODES>(st, nxt, ring_in, ring_out, m63, push, t0, lane, m, c1v, sc, P,
+                                                   strip_off4, wcnt_in, wcnt_out, status, tr_win);
+        if (CODES) gstore1(P.codes + (strip_off16 + (t0 >> 4)) * kWave + lane, (st.cD << 16) | (st.cI & 0xFFFFu));
+        // every ring read up to column t0+20 (incl. the next group's) was issued before this store
+        lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
     }
 
     // ---- strip reduction of the max trackers ----
@@ -212,13 +406,20 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     }
     // cell (n, m) for the global-mode start (algo.rs:308, 331)
     if (row_ok && i == n) pres->end_SM = st.SM;
+    if (tracing && lane == 0) {
+        StripTrace tr;
+        tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
+        tr.wait_in = (int)tr_win; tr.wait_out = (int)tr_wout;
+        tr.band = s / 4; tr.wave = s % 4; tr.pad0 = 0; tr.pad1 = 0;
+        P.trace[s] = tr;
+    }
 }
 
 // I/O wave of a band: feeds ring 0 (row 0 analytic, or the previous band's
 // published bottom row) and drains ring W to HBM for the next band.
 __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Scores32& sc,
-                        Rec* ring0, const Rec* ringW, volatile int* wcnt0, volatile int* rcnt0,
-                        volatile int* wcntW, volatile int* rcntW, const bool do_out, int* status) {
+                        Rec* ring0, const Rec* ringW, lds_int* wcnt0, lds_int* rcnt0,
+                        lds_int* wcntW, lds_int* rcntW, const bool do_out, int* status) {
     const int m = P.m;
     int in_next = 0, out_next = 0;
     const Rec* feed_in = lb > 0 ? P.feed + (size_t)(lb - 1) * P.feed_stride : nullptr;
@@ -251,7 +452,7 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
                     } else {
                         r = ld_rec_agent(feed_in + j);
                     }
-                    ring0[j & (kRing - 1)] = r;
+                    ring0[ring_slot(j)] = r;
                 }
                 lds_wait();
                 if (lane == 0) *wcnt0 = last + 1;
@@ -264,7 +465,7 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
             const int chunk = min(kIoChunk, avail - out_next);
             if (chunk == kIoChunk || (avail == m + 1 && chunk > 0)) {
                 const int j = out_next + lane;
-                if (lane < chunk) st_rec_agent(feed_out + j, ringW[j & (kRing - 1)]);
+                if (lane < chunk) st_rec_agent(feed_out + j, ringW[ring_slot(j)]);
                 vm_wait();
                 lds_wait();
                 if (lane == 0) {
@@ -277,7 +478,7 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
         }
         if (moved) idle = 0;
         else if (++idle > kSpinLimit) {
-            __hip_atomic_store(status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((gint*)status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
         } else {
             __builtin_amdgcn_s_sleep(1);
@@ -286,7 +487,7 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
 }
 
 template <int W, bool LOCAL, bool PLANES, bool LCSP, bool CODES>
-__global__ __launch_bounds__((W + 1) * kWave) void fill_kernel(const PairDev* __restrict__ pairs, const int npairs,
+__global__ __launch_bounds__((W + 1) * kWave, 2) void fill_kernel(const PairDev* __restrict__ pairs, const int npairs,
                                                               const int total_bands, int* band_counter,
                                                               StripRes* sres, PairRes* pres, const Scores32 sc) {
     __shared__ Rec rings[W + 1][kRing];
@@ -312,12 +513,14 @@ __global__ __launch_bounds__((W + 1) * kWave) void fill_kernel(const PairDev* __
                 const bool last_in_band = wave == W - 1;
                 const bool has_consumer = last_in_band ? (lb + 1 < P.bands) : (s + 1 < P.strips);
                 compute_wave<LOCAL, PLANES, LCSP, CODES>(P, s, lane, sc, rings[wave], rings[wave + 1],
-                                                         &wcnt[wave], &rcnt[wave], &wcnt[wave + 1],
-                                                         &rcnt[wave + 1], has_consumer, sres, pres + p,
+                                                         (lds_int*)&wcnt[wave], (lds_int*)&rcnt[wave],
+                                                         (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1],
+                                                         has_consumer, sres, pres + p,
                                                          band_counter + 1);
             }
         } else {
-            io_wave(P, lb, lane, sc, rings[0], rings[W], &wcnt[0], &rcnt[0], &wcnt[W], &rcnt[W],
+            io_wave(P, lb, lane, sc, rings[0], rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0],
+                    (lds_int*)&wcnt[W], (lds_int*)&rcnt[W],
                     lb + 1 < P.bands, band_counter + 1);
         }
         __syncthreads();
@@ -378,7 +581,9 @@ __global__ __launch_bounds__(64) void traceback_kernel(const TbDev* __restrict__
         else if (d == 1) word = __builtin_amdgcn_readlane(w1, l);
         else if (d == 2) word = __builtin_amdgcn_readlane(w2, l);
         else word = __builtin_amdgcn_readlane(w3, l);
-        const uint32_t code = (word >> (2 * (15 - (t & 15)))) & 3u;
+        // bit-planes: bit 31-k = "delete beats both", bit 15-k = "insert beats sub" (k = t % 16)
+        const int ks = t & 15;
+        const uint32_t code = ((word >> (31 - ks)) & 1u) ? 2u : ((word >> (15 - ks)) & 1u);
         if (lane == (k & 63)) mvbuf = code;
         ++k;
         if ((k & 63) == 0) J.moves[k - 64 + lane] = (uint8_t)mvbuf;
