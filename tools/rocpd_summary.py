@@ -41,12 +41,12 @@ def main():
     stats = os.path.join(out_dir, f"{tag}_kernel_stats.csv")
     with open(stats, "w", newline="") as f:
         w = csv.writer(f)
-        w.writerow(["kernel", "calls", "total_ns", "avg_ns", "percent"])
+        w.writerow(["kernel", "calls", "total_us", "avg_us", "percent"])
         for r in rows:
             w.writerow([r[0], r[1], round(r[2], 1), round(r[3], 1), round(r[4], 3)])
     print("wrote", stats)
     for r in rows[:4]:
-        print(f"  {r[0][:70]:70s} calls {r[1]:4d} avg {r[3] / 1e6:10.3f} ms  {r[4]:.1f}%")
+        print(f"  {r[0][:70]:70s} calls {r[1]:4d} avg {r[3] / 1e3:10.3f} ms  {r[4]:.1f}%")
 
     pmc = {}
     for sub, name in (("pw", "WRITE_SIZE"), ("pf", "FETCH_SIZE")):
