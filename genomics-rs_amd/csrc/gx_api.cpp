@@ -23,7 +23,7 @@
 #include "gx_internal.h"
 
 namespace gx {
-hipError_t launch_fill(int W, bool local, bool planes, bool lcs, bool codes, const PairDev* d_pairs, int npairs,
+hipError_t launch_fill(bool local, bool planes, bool track, bool lcs, const PairDev* d_pairs, int npairs,
                        int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                        hipStream_t st);
 hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d_sres, PairRes* d_pres,
@@ -232,15 +232,7 @@ static int processed_chars(const uint8_t* s1, size_t n, const uint8_t* s2, size_
 // ---------------------------------------------------------------------------
 // fill orchestration
 
-static int band_waves() {
-    static int w = -1;
-    if (w < 0) {
-        const char* e = getenv("GX_BAND_WAVES");
-        w = e ? atoi(e) : 4;
-        if (w != 1 && w != 2 && w != 4) w = 4;
-    }
-    return w;
-}
+constexpr int kBandWaves = 4;   // compute waves per band (gx_kernels.hip)
 static int fill_grid_cap() {
     static int g = -1;
     if (g < 0) {
@@ -264,7 +256,7 @@ struct FillJob {
     std::vector<PairRes> res;
     int W = 4;
     int total_bands = 0, total_strips = 0;
-    bool planes_on = false, lcs_on = false, codes_on = false;
+    bool planes_on = false, lcs_on = false, track_on = false;
     double fill_ms = 0.0;
 };
 
@@ -278,13 +270,18 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // chars_dev: if non-null, device buffer already holding the processed chars
 // at offsets off1/off2 (staged path); otherwise c1/c2 are uploaded.
+// track: first max cell + LCS field (alignment_table's max_cell and
+// matches_at_max, algo.rs:258-262, 279); lcs: also keep the LCS plane.
 static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc,
-                    const std::vector<PairHost>& ph, const Scores32& sc, int is_local, bool planes, bool lcs,
-                    bool codes, FillJob& job, const uint8_t* chars_dev = nullptr,
+                    const std::vector<PairHost>& ph, const Scores32& sc, int is_local, bool planes, bool track,
+                    bool lcs, FillJob& job, const uint8_t* chars_dev = nullptr,
                     const std::vector<size_t>* off1 = nullptr, const std::vector<size_t>* off2 = nullptr) {
-    const int W = band_waves();
+    const int W = kBandWaves;
+    const bool codes = true;
+    lcs = lcs && planes;
+    track = track || lcs;
     job.W = W;
-    job.planes_on = planes; job.lcs_on = lcs; job.codes_on = codes;
+    job.planes_on = planes; job.lcs_on = lcs; job.track_on = track;
     const size_t P = ph.size();
     job.pd.assign(P, PairDev{});
     // -- sizes
@@ -359,14 +356,6 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         HIPCHK(hipMemsetAsync(trace.p, 0, (size_t)std::max(strips, 1) * sizeof(StripTrace), ctx->stream));
         for (size_t p = 0; p < P; ++p) job.pd[p].trace = (StripTrace*)trace.p + job.pd[p].strip_base;
     }
-    const char* dbg_file = getenv("GX_DEBUG_RECS");
-    DevBuf dbgb;
-    if (dbg_file && *dbg_file && P > 0) {
-        const size_t nrec = 2 * ((size_t)job.pd[0].m + 1);
-        if ((rc = pool_get(ctx, nrec * sizeof(Rec), &dbgb))) return rc;
-        HIPCHK(hipMemsetAsync(dbgb.p, 0xFF, nrec * sizeof(Rec), ctx->stream));
-        job.pd[0].dbg = (Rec*)dbgb.p;
-    }
     HIPCHK(hipMemcpyAsync(job.pairs.p, job.pd.data(), P * sizeof(PairDev), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemsetAsync(job.progress.p, 0, std::max<size_t>(prog_elems, 1) * sizeof(int), ctx->stream));
     HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, ctx->stream));
@@ -374,7 +363,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     const int grid = std::min(bands, fill_grid_cap());
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     if (bands > 0)
-        HIPCHK(launch_fill(W, is_local != 0, planes, lcs, codes, (const PairDev*)job.pairs.p, (int)P, bands,
+        HIPCHK(launch_fill(is_local != 0, planes, track, lcs, (const PairDev*)job.pairs.p, (int)P, bands,
                            (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, sc, grid, ctx->stream));
     HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));   // ev0..ev1 brackets the fill kernel alone
     if (bands > 0)
@@ -390,15 +379,6 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     job.fill_ms = ms;
-    if (dbgb.p) {
-        std::vector<Rec> d(2 * ((size_t)job.pd[0].m + 1));
-        HIPCHK(hipMemcpy(d.data(), dbgb.p, d.size() * sizeof(Rec), hipMemcpyDeviceToHost));
-        pool_put(ctx, dbgb);
-        if (FILE* f = fopen(dbg_file, "wb")) {
-            fwrite(d.data(), sizeof(Rec), d.size(), f);
-            fclose(f);
-        }
-    }
     if (trace.p) {
         std::vector<StripTrace> tr((size_t)strips);
         HIPCHK(hipMemcpy(tr.data(), trace.p, tr.size() * sizeof(StripTrace), hipMemcpyDeviceToHost));
@@ -643,7 +623,7 @@ extern "C" int gx_alignment_table(gx_context* ctx, const uint8_t* s1, size_t n, 
     const bool planes = (flags & (GX_TABLE_PLANES | GX_TABLE_MATCHES)) != 0;
     const bool lcs = (flags & GX_TABLE_MATCHES) != 0;
     if (n >= 1 && m >= 1) {
-        rc = run_fill(ctx, proc, ph, t->sc, is_local, planes, lcs, true, t->job);
+        rc = run_fill(ctx, proc, ph, t->sc, is_local, planes, matches_at_max != nullptr, lcs, t->job);
         if (rc) { job_release(ctx, t->job); delete t; return rc; }
     } else {
         t->job.res.assign(1, PairRes{});
@@ -661,7 +641,7 @@ extern "C" int gx_alignment_table(gx_context* ctx, const uint8_t* s1, size_t n, 
 extern "C" int gx_table_info(const gx_table* t, uint64_t* n_rows, uint64_t* n_cols, uint64_t* max_cell_i,
                              uint64_t* max_cell_j, int64_t* fill_us) {
     if (!t) return fail(GX_EINVAL, "table is NULL");
-    const bool interior = t->s1.size() >= 1 && t->s2.size() >= 1;
+    const bool interior = t->s1.size() >= 1 && t->s2.size() >= 1 && t->job.track_on;
     if (n_rows) *n_rows = t->s1.size() + 1;
     if (n_cols) *n_cols = t->s2.size() + 1;
     if (max_cell_i) *max_cell_i = interior ? (uint64_t)t->job.res[0].max_i : 0;
@@ -796,7 +776,7 @@ extern "C" int gx_retrace(gx_table* t, int is_local, gx_step* steps, size_t cap,
         const auto t1 = std::chrono::steady_clock::now();
         w.res.score = score;
         w.res.start_i = si; w.res.start_j = sj;
-        const bool interior = n >= 1 && m >= 1;
+        const bool interior = n >= 1 && m >= 1 && t->job.track_on;
         w.res.max_cell_i = interior ? (uint64_t)r.max_i : 0;
         w.res.max_cell_j = interior ? (uint64_t)r.max_j : 0;
         w.res.matches_at_max = interior ? (uint64_t)r.mam : 0;
@@ -815,10 +795,12 @@ extern "C" int gx_retrace(gx_table* t, int is_local, gx_step* steps, size_t cap,
 }
 
 extern "C" int gx_align(gx_context* ctx, const uint8_t* s1, size_t n, const uint8_t* s2, size_t m,
-                        const gx_scores* scores, int is_local, int reverse_sequences, gx_step* steps, size_t cap,
-                        gx_result* out) {
+                        const gx_scores* scores, int is_local, int reverse_sequences, uint32_t flags,
+                        gx_step* steps, size_t cap, gx_result* out) {
     gx_table* t = nullptr;
-    int rc = gx_alignment_table(ctx, s1, n, s2, m, scores, is_local, reverse_sequences, 0, &t, nullptr);
+    uint64_t mam = 0;
+    int rc = gx_alignment_table(ctx, s1, n, s2, m, scores, is_local, reverse_sequences, 0, &t,
+                                (flags & GX_ALIGN_MAX_CELL) ? &mam : nullptr);
     if (rc) return rc;
     return gx_retrace(t, is_local, steps, cap, out);
 }
@@ -828,8 +810,8 @@ extern "C" int gx_align(gx_context* ctx, const uint8_t* s1, size_t n, const uint
 
 static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
                       const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc, const HostScores& hs,
-                      const Scores32& sc, int is_local, bool planes, std::vector<Walk>& walks, double* fill_ms,
-                      const uint8_t* chars_dev = nullptr, const std::vector<size_t>* off1 = nullptr,
+                      const Scores32& sc, int is_local, bool planes, bool track, std::vector<Walk>& walks,
+                      double* fill_ms, const uint8_t* chars_dev = nullptr, const std::vector<size_t>* off1 = nullptr,
                       const std::vector<size_t>* off2 = nullptr) {
     const size_t P = ph.size();
     // pairs with an interior go to the device
@@ -851,7 +833,7 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
     std::vector<int64_t> score(P);
     int rc = GX_OK;
     if (!idx.empty()) {
-        rc = run_fill(ctx, dproc, dph, sc, is_local, planes, false, true, job, chars_dev, chars_dev ? &o1 : nullptr,
+        rc = run_fill(ctx, dproc, dph, sc, is_local, planes, track, false, job, chars_dev, chars_dev ? &o1 : nullptr,
                       chars_dev ? &o2 : nullptr);
         if (rc) { job_release(ctx, job); return rc; }
         for (size_t k = 0; k < idx.size(); ++k) res[idx[k]] = job.res[k];
@@ -877,7 +859,7 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
         rc = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], mv, nm, walks[p]);
         if (rc) return rc;
         Walk& w = walks[p];
-        const bool interior = ph[p].n >= 1 && ph[p].m >= 1;
+        const bool interior = ph[p].n >= 1 && ph[p].m >= 1 && track;
         w.res.score = score[p];
         w.res.start_i = si[p]; w.res.start_j = sj[p];
         w.res.max_cell_i = interior ? (uint64_t)res[p].max_i : 0;
@@ -891,7 +873,7 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
 
 extern "C" int gx_align_batch(gx_context* ctx, const uint8_t* const* s1, const size_t* n, const uint8_t* const* s2,
                               const size_t* m, size_t npairs, const gx_scores* scores, int is_local,
-                              gx_step* const* steps, const size_t* caps, gx_result* out) {
+                              uint32_t flags, gx_step* const* steps, const size_t* caps, gx_result* out) {
     if (!ctx || !s1 || !n || !s2 || !m || !out) return fail(GX_EINVAL, "NULL argument");
     std::lock_guard<std::mutex> lk(ctx->mu);
     HIPCHK(hipSetDevice(ctx->device));
@@ -908,7 +890,7 @@ extern "C" int gx_align_batch(gx_context* ctx, const uint8_t* const* s1, const s
         proc[p] = {s1[p], s2[p]};
     }
     std::vector<Walk> walks;
-    rc = batch_core(ctx, ph, proc, hs, sc, is_local, false, walks, nullptr);
+    rc = batch_core(ctx, ph, proc, hs, sc, is_local, false, (flags & GX_ALIGN_MAX_CELL) != 0, walks, nullptr);
     if (rc) return rc;
     for (size_t p = 0; p < npairs; ++p) {
         out[p] = walks[p].res;
@@ -952,7 +934,7 @@ extern "C" int gx_stage_pairs(gx_context* ctx, const uint8_t* const* s1, const s
 }
 
 extern "C" int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes,
-                             gx_result* out, double* fill_ms_out) {
+                             uint32_t flags, gx_result* out, double* fill_ms_out) {
     if (!ctx || !out) return fail(GX_EINVAL, "NULL argument");
     std::lock_guard<std::mutex> lk(ctx->mu);
     HIPCHK(hipSetDevice(ctx->device));
@@ -971,7 +953,7 @@ extern "C" int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_lo
     }
     std::vector<Walk> walks;
     double fms = 0;
-    rc = batch_core(ctx, ph, proc, hs, sc, is_local, keep_planes != 0, walks, &fms,
+    rc = batch_core(ctx, ph, proc, hs, sc, is_local, keep_planes != 0, (flags & GX_ALIGN_MAX_CELL) != 0, walks, &fms,
                     (const uint8_t*)ctx->st_chars.p, &ctx->st_off1, &ctx->st_off2);
     if (rc) return rc;
     for (size_t p = 0; p < P; ++p) out[p] = walks[p].res;

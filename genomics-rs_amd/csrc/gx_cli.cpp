@@ -65,7 +65,7 @@ int main(int argc, char** argv) {
     const size_t n = sl[0], m = sl[1];
     std::vector<gx_step> steps(n + m + 2);
     gx_result res{};
-    int rc = gx_align(ctx, s1, n, s2, m, &sc, is_local, 0, steps.data(), steps.size(), &res);
+    int rc = gx_align(ctx, s1, n, s2, m, &sc, is_local, 0, 0, steps.data(), steps.size(), &res);
     if (rc != GX_OK) {
         fprintf(stderr, "[ERROR] %s\n", gx_last_error());
         gx_context_destroy(ctx);

@@ -33,14 +33,15 @@ struct Scores32 {
     int h;       // gap open
     int hg;      // h + g
     int floor_;  // local ? 0 : kNeg  (the 4th lane of score_max, algo.rs:103)
-    int dbg;     // GX_DEBUG_FLAGS: bit0 = rolled path only, bit1 = never trust speculative ring reads
+    int dbg;     // GX_DEBUG_FLAGS: bit0 = rolled (ramp) path only
 };
 
 // One inter-strip record: the bottom-row cell (r, j) of a strip, as needed by
 // the strip below.  dd = its delete-successor max(max(I,S)+h+g, D+g, floor),
-// sm = score_max(cell), l = max_matches(cell), c2 = s2[j-1].
+// sm = score_max(cell), c2 = s2[j-1], l = max_matches(cell) (only with LCS
+// tracking; the three leading words are then one ds_read_b96).
 struct __attribute__((aligned(16))) Rec {
-    int dd, sm, l, c2;
+    int dd, sm, c2, l;
 };
 
 struct __attribute__((aligned(16))) StripRes {
@@ -84,7 +85,6 @@ struct PairDev {
     Rec* feed;           // [bands-1][feed_stride] band-boundary rows
     int* progress;       // [bands-1] columns published per boundary
     StripTrace* trace;   // per strip, or nullptr
-    Rec* dbg;            // GX_DEBUG_RECS: [2][m+1] pushed by strip 0 / consumed by strip 1
     int feed_stride;
     int pad;
 };

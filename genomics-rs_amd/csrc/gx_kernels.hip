@@ -101,41 +101,136 @@ __device__ __forceinline__ void gstore4(int32_t* p, int4 v) {
     *(gv4i*)p = x;
 }
 __device__ __forceinline__ void gstore1(uint32_t* p, uint32_t v) { *(guint*)p = v; }
+// Uniform base + 32-bit per-lane byte offset: selects the saddr form
+// (global_store_dwordx4 voff, data, s[base] offset:imm), no 64-bit VALU math.
+typedef __attribute__((address_space(1))) char gchar;
+__device__ __forceinline__ void gstore4_at(int32_t* base, uint32_t byte_off, int4 v) {
+    v4i x = {v.x, v.y, v.z, v.w};
+    *(gv4i*)((gchar*)base + byte_off) = x;
+}
 
+
+// Compute waves per band and the occupancy floor (waves per SIMD) that caps
+// the fill kernel's VGPRs (512 / 4 = 128).
+constexpr int kBandWaves = 4;
+#ifndef GX_FILL_MIN_WAVES
+#define GX_FILL_MIN_WAVES 4
+#endif
+
+// Per-lane DP state of row i = 64*strip + lane + 1 (the cell left of the one
+// being computed, i.e. (i, j-1) in the reference's "top" naming, algo.rs:225).
 struct LaneState {
-    int strip;
-    int I, SD, Dd, SM, L, c2c, SMtl, Ltl;
-    int best, bstep, bl, lbest, lstep;
-    uint32_t cI, cD;   // traceback code bit-planes (16 steps each)
+    int I, SD, Dd, SM, c2c, SMtl;   // insert, max(sub, delete), delete-successor, score_max, s2[j-1], SM(i-1, j-1)
+    int L, Ltl;                     // LCS field (TRACK only)
+    int best, bstep, bl;            // first strict max of the row (TRACK only)
+    int lbest, lstep;               // last max of the row (LOCAL only)
+    uint32_t cI, cD;                // traceback code bit-planes (16 steps each)
 };
 
 // Lane 63 pushes its cell (the strip's bottom row) into the LDS ring of the
-// wave below: two ds_write2_b32 under a lane-63 exec mask.  Written in asm so
-// that no branch or register tuple is needed.  Compute waves call it only
-// with all 64 lanes active (no divergent region), so exec is restored to -1
-// rather than saved (saves an SGPR pair per push).
-template <int U>
-__device__ __forceinline__ void push63(uint32_t base, int a, int b, int c, int d, unsigned long long m63) {
-    asm volatile(
-        "s_mov_b64 exec, %0\n\t"
-        "ds_write2_b32 %1, %2, %3 offset0:%6 offset1:%7\n\t"
-        "ds_write2_b32 %1, %4, %5 offset0:%8 offset1:%9\n\t"
-        "s_mov_b64 exec, -1\n\t"
-        "s_nop 1"   // store-data hazard: the compiler may overwrite a data VGPR right after
-        :
-        : "s"(m63), "v"(base), "v"(a), "v"(b), "v"(c), "v"(d), "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2),
-          "i"(4 * U + 3));
+// wave below, under a lane-63 exec mask (no branch, no register tuple).
+// Record = {dd, sm, c2, l}; without TRACK the l word is not written.  Compute
+// waves run with all 64 lanes active, so exec is restored to -1, not saved.
+// U = step within the 16-step sub-block (the ring slot's constant offset).
+template <int U, bool TRACK>
+__device__ __forceinline__ void push63(uint32_t base, const LaneState& st, unsigned long long m63) {
+    if (TRACK)
+        asm volatile(
+            "s_mov_b64 exec, %0\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%6 offset1:%7\n\t"
+            "ds_write2_b32 %1, %4, %5 offset0:%8 offset1:%9\n\t"
+            "s_mov_b64 exec, -1"
+            :
+            : "s"(m63), "v"(base), "v"(st.Dd), "v"(st.SM), "v"(st.c2c), "v"(st.L), "i"(4 * U), "i"(4 * U + 1),
+              "i"(4 * U + 2), "i"(4 * U + 3));
+    else
+        asm volatile(
+            "s_mov_b64 exec, %0\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%5 offset1:%6\n\t"
+            "ds_write_b32 %1, %4 offset:%7\n\t"
+            "s_mov_b64 exec, -1"
+            :
+            : "s"(m63), "v"(base), "v"(st.Dd), "v"(st.SM), "v"(st.c2c), "i"(4 * U), "i"(4 * U + 1),
+              "i"(16 * U + 8));
 }
 
-// One anti-diagonal step of a compute wave.  MASKED: some lanes are outside
-// columns 1..m this step (ramp-up / ramp-down of the skew).
-template <bool LOCAL, bool MASKED, bool CODES>
-__device__ __forceinline__ void dp_step(LaneState& st, const Rec r, const int t, const int lane, const int m,
+// The same push followed, in the same lane-63 window, by the store of the
+// ring's write counter: LDS executes one wave's DS operations in order, so a
+// consumer that sees the counter also sees every record pushed before it.
+template <int U, bool TRACK>
+__device__ __forceinline__ void push63_pub(uint32_t base, const LaneState& st, unsigned long long m63,
+                                           uint32_t cnt_addr, int cnt) {
+    if (TRACK)
+        asm volatile(
+            "s_mov_b64 exec, %0\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%8 offset1:%9\n\t"
+            "ds_write2_b32 %1, %4, %5 offset0:%10 offset1:%11\n\t"
+            "ds_write_b32 %6, %7\n\t"
+            "s_mov_b64 exec, -1"
+            :
+            : "s"(m63), "v"(base), "v"(st.Dd), "v"(st.SM), "v"(st.c2c), "v"(st.L), "v"(cnt_addr), "v"(cnt),
+              "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2), "i"(4 * U + 3)
+            : "memory");
+    else
+        asm volatile(
+            "s_mov_b64 exec, %0\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%7 offset1:%8\n\t"
+            "ds_write_b32 %1, %4 offset:%9\n\t"
+            "ds_write_b32 %5, %6\n\t"
+            "s_mov_b64 exec, -1"
+            :
+            : "s"(m63), "v"(base), "v"(st.Dd), "v"(st.SM), "v"(st.c2c), "v"(cnt_addr), "v"(cnt), "i"(4 * U),
+              "i"(4 * U + 1), "i"(16 * U + 8)
+            : "memory");
+}
+
+// exec mask selecting lane 63 (or no lane), forced into an SGPR pair: the
+// "s" asm operand of the pushes must not be given a VGPR.
+__device__ __forceinline__ unsigned long long lane63_mask(bool on) {
+    return (unsigned long long)__builtin_amdgcn_readfirstlane(on ? 0x80000000u : 0u) << 32;
+}
+
+// Ramp-path push with a runtime slot address.
+template <bool TRACK>
+__device__ __forceinline__ void push63_rt(uint32_t addr, const LaneState& st, unsigned long long m63) {
+    if (TRACK)
+        asm volatile(
+            "s_mov_b64 exec, %0\n\t"
+            "ds_write2_b32 %1, %2, %3 offset1:1\n\t"
+            "ds_write2_b32 %1, %4, %5 offset0:2 offset1:3\n\t"
+            "s_mov_b64 exec, -1"
+            :
+            : "s"(m63), "v"(addr), "v"(st.Dd), "v"(st.SM), "v"(st.c2c), "v"(st.L));
+    else
+        asm volatile(
+            "s_mov_b64 exec, %0\n\t"
+            "ds_write2_b32 %1, %2, %3 offset1:1\n\t"
+            "ds_write_b32 %1, %4 offset:8\n\t"
+            "s_mov_b64 exec, -1"
+            :
+            : "s"(m63), "v"(addr), "v"(st.Dd), "v"(st.SM), "v"(st.c2c));
+}
+
+// One lane stores an LDS counter (exec = lane 0 only, no branch).
+__device__ __forceinline__ void lds_store_lane0(lds_int* p, int v) {
+    asm volatile(
+        "s_mov_b64 exec, 1\n\t"
+        "ds_write_b32 %0, %1\n\t"
+        "s_mov_b64 exec, -1"
+        :
+        : "v"((uint32_t)(uintptr_t)p), "v"(v)
+        : "memory");
+}
+
+// One anti-diagonal step of a compute wave (algo.rs:222-268 for every lane's
+// cell).  MASKED: some lanes are outside columns 1..m this step (ramp-up /
+// ramp-down of the skew); their state is left unchanged.
+template <bool LOCAL, bool MASKED, bool CODES, bool TRACK>
+__device__ __forceinline__ void dp_step(LaneState& st, const Rec& r, const int t, const int lane, const int m,
                                         const int c1v, const Scores32& sc, int& oI, int& oD, int& oS, int& oL) {
     // row above (i-1, j): lane 0 from the ring record, others from lane-1 (wave_shr:1)
-    const int dd_in = shr1(r.dd, st.Dd);   // == D(i, j): delete score of the new cell
+    const int dd_in = shr1(r.dd, st.Dd);   // == D(i, j): the delete score of the new cell
     const int sm_in = shr1(r.sm, st.SM);   // score_max(i-1, j)
-    const int l_in = shr1(r.l, st.L);      // max_matches(i-1, j)
     const int c2 = shr1(r.c2, st.c2c);     // s2[j-1]
     // algo.rs:231-236  insert_score = top.score_max(g, h+g, h+g)
     const int In = LOCAL ? max3i(st.I + sc.g, st.SD + sc.hg, 0) : max(st.I + sc.g, st.SD + sc.hg);
@@ -146,65 +241,44 @@ __device__ __forceinline__ void dp_step(LaneState& st, const Rec r, const int t,
     const int IS = max(In, Sn);
     const int SMn = max(IS, Dn);           // cell.score_max(0,0,0); >= floor since In >= floor
     const int SDn = max(Sn, Dn);
+    // delete-successor, i.e. D(i+1, j) = this.score_max(hg, g, hg) (algo.rs:238-243)
     const int Ddn = LOCAL ? max3i(IS + sc.hg, Dn + sc.g, 0) : max(IS + sc.hg, Dn + sc.g);
-    const int Ln = max3i(st.L, l_in, st.Ltl + (mt ? 1 : 0));   // algo.rs:250-255
+    int Ln = 0, l_in = 0;
+    if (TRACK) {
+        l_in = shr1(r.l, st.L);            // max_matches(i-1, j)
+        Ln = max3i(st.L, l_in, st.Ltl + (mt ? 1 : 0));   // algo.rs:250-255
+    }
     bool act = true;
     if (MASKED) act = (unsigned)(t - lane) < (unsigned)m;
     if (MASKED) {
-        st.I = act ? In : st.I; st.SD = act ? SDn : st.SD; st.Dd = act ? Ddn : st.Dd;
-        st.SM = act ? SMn : st.SM; st.L = act ? Ln : st.L;
+        st.I = act ? In : st.I; st.SD = act ? SDn : st.SD; st.Dd = act ? Ddn : st.Dd; st.SM = act ? SMn : st.SM;
+        if (TRACK) st.L = act ? Ln : st.L;
     } else {
-        st.I = In; st.SD = SDn; st.Dd = Ddn; st.SM = SMn; st.L = Ln;
+        st.I = In; st.SD = SDn; st.Dd = Ddn; st.SM = SMn;
+        if (TRACK) st.L = Ln;
     }
-    st.SMtl = sm_in; st.Ltl = l_in; st.c2c = c2;
-    // algo.rs:258-262: first strict maximum in row-major order
-    const bool nb = act && SMn > st.best;
-    st.best = nb ? SMn : st.best; st.bstep = nb ? t : st.bstep; st.bl = nb ? Ln : st.bl;
-    // algo.rs:310-322: max_by keeps the LAST maximum
+    st.SMtl = sm_in; st.c2c = c2;
+    if (TRACK) {
+        st.Ltl = l_in;
+        // algo.rs:258-262: first strict maximum in row-major order
+        const bool nb = act && SMn > st.best;
+        st.best = nb ? SMn : st.best; st.bstep = nb ? t : st.bstep; st.bl = nb ? Ln : st.bl;
+    }
     if (LOCAL) {
+        // algo.rs:310-322: max_by keeps the LAST maximum
         const bool nl = act && SMn >= st.lbest;
         st.lbest = nl ? SMn : st.lbest; st.lstep = nl ? t : st.lstep;
     }
     if (CODES) {
-        // retrace priority S > I > D against the cell max (algo.rs:351-400),
-        // two bit-planes: D beats both / I beats S.  Decode: D ? delete : I ? insert : sub.
-        st.cD = st.cD + st.cD + (Dn > IS ? 1u : 0u);
-        st.cI = st.cI + st.cI + (In > Sn ? 1u : 0u);
+        // retrace priority S > I > D against the cell max (algo.rs:351-400), two
+        // bit-planes: D beats both / I beats S.  Decode: D ? delete : I ? insert : sub.
+        // The bit is the sign of a difference (|values| < 2^29 under the host's
+        // range guard), shifted in with v_alignbit: no compare masks, which the
+        // compiler would otherwise park in SGPR pairs across the sub-block.
+        st.cD = __builtin_amdgcn_alignbit(st.cD, (uint32_t)(IS - Dn), 31);   // Dn > IS
+        st.cI = __builtin_amdgcn_alignbit(st.cI, (uint32_t)(Sn - In), 31);   // In > Sn
     }
     oI = In; oD = Dn; oS = Sn; oL = Ln;
-}
-
-// GX_DEBUG_RECS: strip 0 lane 63 logs what it pushes, strip 1 lane 0 what it consumes.
-__device__ __forceinline__ void dbg_log(const PairDev& P, const LaneState& st, int lane, int t, int m, const Rec r) {
-    const int pc = t - (kWave - 1);
-    if (st.strip == 0 && lane == kWave - 1 && pc >= 0 && pc <= m) P.dbg[pc] = Rec{st.Dd, st.SM, st.L, st.c2c};
-    if (st.strip == 1 && lane == 0 && t + 1 <= m) P.dbg[(m + 1) + t + 1] = r;
-}
-
-template <bool LOCAL, bool MASKED, bool PLANES, bool LCSP, bool CODES, int G4>
-__device__ __forceinline__ void step4(LaneState& st, const Rec (&cur)[4], const uint32_t out_base,
-                                      const unsigned long long m63, const int t0, const int lane, const int m,
-                                      const int c1v, const Scores32& sc, const PairDev& P, const size_t strip_off4) {
-    int bI[4], bD[4], bS[4], bL[4];
-#define GX_STEP(U)                                                                                     \
-    {                                                                                                  \
-        const int t = t0 + G4 * 4 + (U);                                                               \
-        /* lane 63 holds column t-63 before this step: push it to the strip below (m63 = 0 when    */  \
-        /* there is no consumer).  Full sub-blocks only push columns 1..m-64.                      */  \
-        push63<G4 * 4 + (U)>(out_base, st.Dd, st.SM, st.L, st.c2c, m63);                               \
-        if (P.dbg) dbg_log(P, st, lane, t, m, cur[U]);                                                  \
-        dp_step<LOCAL, MASKED, CODES>(st, cur[U], t, lane, m, c1v, sc, bI[U], bD[U], bS[U], bL[U]);    \
-    }
-    GX_STEP(0) GX_STEP(1) GX_STEP(2) GX_STEP(3)
-#undef GX_STEP
-    if (PLANES) {
-        // sub-block base (per lane) + G4 KiB: the constant folds into the store's immediate offset
-        const size_t o = ((strip_off4 + (t0 >> 2)) * kWave + lane) * 4 + G4 * kWave * 4;
-        gstore4(P.pI + o, make_int4(bI[0], bI[1], bI[2], bI[3]));
-        gstore4(P.pD + o, make_int4(bD[0], bD[1], bD[2], bD[3]));
-        gstore4(P.pS + o, make_int4(bS[0], bS[1], bS[2], bS[3]));
-        if (LCSP) gstore4(P.pL + o, make_int4(bL[0], bL[1], bL[2], bL[3]));
-    }
 }
 
 // The ring pointers are deliberately NOT __restrict__: another wave writes the
@@ -214,146 +288,152 @@ __device__ __forceinline__ void read4(Rec (&r)[4], const Rec* rin) {
     r[0] = rin[0]; r[1] = rin[1]; r[2] = rin[2]; r[3] = rin[3];
 }
 
-// One lane stores an LDS counter (exec = lane 0 only, no branch).  LDS executes a
-// wave's DS operations in order, so a counter written after ring pushes is seen
-// after them by every other wave: publication needs no s_waitcnt.
-// (Compute waves only, full exec, like push63.)
-__device__ __forceinline__ void lds_store_lane0(lds_int* p, int v) {
-    asm volatile(
-        "s_mov_b64 exec, 1\n\t"
-        "ds_write_b32 %0, %1\n\t"
-        "s_mov_b64 exec, -1\n\t"
-        "s_nop 1"
-        :
-        : "v"((uint32_t)(uintptr_t)p), "v"(v)
-        : "memory");
-}
+// Uniform per-strip values of a compute wave, hoisted out of the pair
+// descriptor (which lives in global memory the plane stores could alias).
+struct WaveCtx {
+    int32_t* pI; int32_t* pD; int32_t* pS; int32_t* pL;   // plane bases of this strip
+    uint32_t* codes;                                        // code words of this strip
+    const Rec* ring_in;
+    Rec* ring_out;
+    lds_int* wcnt_in;
+    lds_int* wcnt_out;
+    int* status;
+    int m, lane, c1v;
+    unsigned tr_win;
+};
 
-// One 4-step group.  `nxt` holds the validated ring records for these steps;
-// the producer's counter is observed and the next group's records are read
-// (in that LDS order) before computing, so the read latency hides behind the
-// group and the records are valid whenever the observed counter covers them.
-template <bool LOCAL, bool MASKED, bool PLANES, bool LCSP, bool CODES, int G4>
-__device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], const Rec* ring_in,
-                                       const uint32_t out_base, const unsigned long long m63, const bool push,
-                                       const int t0, const int lane, const int m, const int c1v, const Scores32& sc,
-                                       const PairDev& P, const size_t strip_off4, lds_int* wcnt_in,
-                                       lds_int* wcnt_out, int* status, unsigned& tr_win) {
+// One 4-step group of a full sub-block.  `nxt` holds validated ring records
+// for these steps.  The producer's counter is observed and the next group's
+// records are read (in that LDS order) before computing, so the read latency
+// hides behind the group; if the observed counter did not cover them, they
+// are re-read after waiting.
+template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP, int G4>
+__device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w, const Scores32& sc,
+                                       const int t0, const uint32_t out_base, const unsigned long long m63,
+                                       const size_t sb_off) {
     const int t = t0 + 4 * G4;
     Rec cur[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
-    const int need = min(t + 8, m) + 1;                       // columns of the next group: t+5 .. t+8
-    const int seen = __builtin_amdgcn_readfirstlane(*wcnt_in);
+    const int need = min(t + 8, w.m) + 1;                     // columns of the next group: t+5 .. t+8
+    const int seen_v = *w.wcnt_in;                            // consumed only at the end of the group
     asm volatile("" ::: "memory");
-    read4(nxt, ring_in + ring_slot(t + 5));
-    step4<LOCAL, MASKED, PLANES, LCSP, CODES, G4>(st, cur, out_base, m63, t0, lane, m, c1v, sc, P, strip_off4);
-    if (push) lds_store_lane0(wcnt_out, min(t + 3 - (kWave - 1), m) + 1);
-    if (seen < need || (sc.dbg & 2)) {                        // producer was behind: wait, re-read
-        tr_win += wait_ge(wcnt_in, need, status);
-        read4(nxt, ring_in + ring_slot(t + 5));
+    read4(nxt, w.ring_in + ring_slot(t + 5));
+    int bI[4], bD[4], bS[4], bL[4];
+    // lane 63 holds column t+U-63 before step U: push it (m63 = 0 when there is
+    // no consumer); the last push of the group also publishes the counter
+    push63<4 * G4 + 0, TRACK>(out_base, st, m63);
+    dp_step<LOCAL, false, CODES, TRACK>(st, cur[0], t + 0, w.lane, w.m, w.c1v, sc, bI[0], bD[0], bS[0], bL[0]);
+    push63<4 * G4 + 1, TRACK>(out_base, st, m63);
+    dp_step<LOCAL, false, CODES, TRACK>(st, cur[1], t + 1, w.lane, w.m, w.c1v, sc, bI[1], bD[1], bS[1], bL[1]);
+    push63<4 * G4 + 2, TRACK>(out_base, st, m63);
+    dp_step<LOCAL, false, CODES, TRACK>(st, cur[2], t + 2, w.lane, w.m, w.c1v, sc, bI[2], bD[2], bS[2], bL[2]);
+    push63_pub<4 * G4 + 3, TRACK>(out_base, st, m63, lds_addr((const void*)w.wcnt_out), t + 3 - (kWave - 1) + 1);
+    dp_step<LOCAL, false, CODES, TRACK>(st, cur[3], t + 3, w.lane, w.m, w.c1v, sc, bI[3], bD[3], bS[3], bL[3]);
+    if (PLANES) {
+        // 16 B per lane, 1 KiB per wave: base (uniform) + lane*16 B + G4 KiB immediate
+        const uint32_t o = (uint32_t)w.lane * 16u + G4 * kWave * 16;
+        gstore4_at(w.pI + sb_off, o, make_int4(bI[0], bI[1], bI[2], bI[3]));
+        gstore4_at(w.pD + sb_off, o, make_int4(bD[0], bD[1], bD[2], bD[3]));
+        gstore4_at(w.pS + sb_off, o, make_int4(bS[0], bS[1], bS[2], bS[3]));
+        if (LCSP) gstore4_at(w.pL + sb_off, o, make_int4(bL[0], bL[1], bL[2], bL[3]));
     }
-}
-
-// Same lane-63 push with a runtime LDS address (ramp path).
-__device__ __forceinline__ void push63_rt(uint32_t addr, int a, int b, int c, int d, unsigned long long m63) {
-    asm volatile(
-        "s_mov_b64 exec, %0\n\t"
-        "ds_write2_b32 %1, %2, %3 offset1:1\n\t"
-        "ds_write2_b32 %1, %4, %5 offset0:2 offset1:3\n\t"
-        "s_mov_b64 exec, -1\n\t"
-        "s_nop 1"
-        :
-        : "s"(m63), "v"(addr), "v"(a), "v"(b), "v"(c), "v"(d));
+    if (__builtin_amdgcn_readfirstlane(seen_v) < need) {      // producer was behind: wait, re-read
+        w.tr_win += wait_ge(w.wcnt_in, need, w.status);
+        read4(nxt, w.ring_in + ring_slot(t + 5));
+    }
 }
 
 // Ramp-up / ramp-down sub-block (some lanes outside columns 1..m): a rolled
-// loop, blocking on the whole sub-block's input, scalar plane stores.  At the
-// end `nxt` is re-primed with the first group of the next sub-block.
-template <bool LOCAL, bool PLANES, bool LCSP, bool CODES>
-__device__ __forceinline__ void ramp_block(LaneState& st, Rec (&nxt)[4], const Rec* ring_in,
-                                        Rec* ring_out, const unsigned long long m63, const bool push,
-                                        const int t0, const int lane, const int m, const int c1v,
-                                        const Scores32& sc, const PairDev& P, const size_t strip_off4,
-                                        lds_int* wcnt_in, lds_int* wcnt_out, int* status, unsigned& tr_win) {
-    tr_win += wait_ge(wcnt_in, min(t0 + kSub, m) + 1, status);
+// loop that waits for the whole sub-block's input first and masks the state
+// updates and the pushes.  At the end `nxt` is re-primed with the first group
+// of the next sub-block.
+template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP>
+__device__ __forceinline__ void ramp_block(LaneState& st, Rec (&nxt)[4], WaveCtx& w, const Scores32& sc, const int t0,
+                                        const bool has_consumer, const size_t sb_off) {
+    const int m = w.m;
+    w.tr_win += wait_ge(w.wcnt_in, min(t0 + kSub, m) + 1, w.status);
 #pragma unroll 1
     for (int u = 0; u < kSub; ++u) {
         const int t = t0 + u;
-        const Rec r = ring_in[ring_slot(t + 1)];
+        const Rec r = w.ring_in[ring_slot(t + 1)];
         // push only columns 0..m: a push past m would land on the slot of column
         // c - 256, which a lagging consumer may not have read yet
         const int col = t - (kWave - 1);
-        const unsigned long long mk =
-            (unsigned long long)__builtin_amdgcn_readfirstlane((col >= 0 && col <= m) ? (unsigned)(m63 >> 32) : 0u)
-            << 32;
-        push63_rt(lds_addr(ring_out + ring_slot(col)), st.Dd, st.SM, st.L, st.c2c, mk);
-        if (P.dbg) dbg_log(P, st, lane, t, m, r);
+        const unsigned long long mk = lane63_mask(has_consumer && col >= 0 && col <= m);
+        push63_rt<TRACK>(lds_addr(w.ring_out + ring_slot(col)), st, mk);
         int oI, oD, oS, oL;
-        dp_step<LOCAL, true, CODES>(st, r, t, lane, m, c1v, sc, oI, oD, oS, oL);
+        dp_step<LOCAL, true, CODES, TRACK>(st, r, t, w.lane, m, w.c1v, sc, oI, oD, oS, oL);
         if (PLANES) {
-            const size_t o = ((strip_off4 + (t >> 2)) * kWave + lane) * 4 + (t & 3);
-            ((gint*)P.pI)[o] = oI;
-            ((gint*)P.pD)[o] = oD;
-            ((gint*)P.pS)[o] = oS;
-            if (LCSP) ((gint*)P.pL)[o] = oL;
+            const size_t o = sb_off + (size_t)w.lane * 4 + (u >> 2) * (kWave * 4) + (u & 3);
+            ((gint*)w.pI)[o] = oI;
+            ((gint*)w.pD)[o] = oD;
+            ((gint*)w.pS)[o] = oS;
+            if (LCSP) ((gint*)w.pL)[o] = oL;
         }
     }
-    if (push) lds_store_lane0(wcnt_out, min(t0 + kSub - 1 - (kWave - 1), m) + 1);
-    tr_win += wait_ge(wcnt_in, min(t0 + kSub + 4, m) + 1, status);
-    read4(nxt, ring_in + ring_slot(t0 + kSub + 1));
+    const int last_col = min(t0 + kSub - 1 - (kWave - 1), m);
+    if (has_consumer && last_col >= 0) lds_store_lane0(w.wcnt_out, last_col + 1);
+    w.tr_win += wait_ge(w.wcnt_in, min(t0 + kSub + 4, m) + 1, w.status);
+    read4(nxt, w.ring_in + ring_slot(t0 + kSub + 1));
 }
 
-template <bool LOCAL, bool MASKED, bool PLANES, bool LCSP, bool CODES>
-__device__ __forceinline__ void sub_block(LaneState& st, Rec (&nxt)[4], const Rec* ring_in,
-                                          const uint32_t out_base, const unsigned long long m63, const bool push,
-                                          const int t0, const int lane, const int m, const int c1v,
-                                          const Scores32& sc, const PairDev& P, const size_t strip_off4,
-                                          lds_int* wcnt_in, lds_int* wcnt_out, int* status, unsigned& tr_win) {
-    group4<LOCAL, MASKED, PLANES, LCSP, CODES, 0>(st, nxt, ring_in, out_base, m63, push, t0, lane, m, c1v, sc, P,
-                                                  strip_off4, wcnt_in, wcnt_out, status, tr_win);
-    group4<LOCAL, MASKED, PLANES, LCSP, CODES, 1>(st, nxt, ring_in, out_base, m63, push, t0, lane, m, c1v, sc, P,
-                                                  strip_off4, wcnt_in, wcnt_out, status, tr_win);
-    group4<LOCAL, MASKED, PLANES, LCSP, CODES, 2>(st, nxt, ring_in, out_base, m63, push, t0, lane, m, c1v, sc, P,
-                                                  strip_off4, wcnt_in, wcnt_out, status, tr_win);
-    group4<LOCAL, MASKED, PLANES, LCSP, CODES, 3>(st, nxt, ring_in, out_base, m63, push, t0, lane, m, c1v, sc, P,
-                                                  strip_off4, wcnt_in, wcnt_out, status, tr_win);
+template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP>
+__device__ __forceinline__ void sub_block(LaneState& st, Rec (&nxt)[4], WaveCtx& w, const Scores32& sc, const int t0,
+                                          const uint32_t out_base, const unsigned long long m63, const size_t sb_off) {
+    group4<LOCAL, PLANES, CODES, TRACK, LCSP, 0>(st, nxt, w, sc, t0, out_base, m63, sb_off);
+    group4<LOCAL, PLANES, CODES, TRACK, LCSP, 1>(st, nxt, w, sc, t0, out_base, m63, sb_off);
+    group4<LOCAL, PLANES, CODES, TRACK, LCSP, 2>(st, nxt, w, sc, t0, out_base, m63, sb_off);
+    group4<LOCAL, PLANES, CODES, TRACK, LCSP, 3>(st, nxt, w, sc, t0, out_base, m63, sb_off);
 }
 
-template <bool LOCAL, bool PLANES, bool LCSP, bool CODES>
-__device__ void compute_wave(const PairDev& P, const int s, const int lane, const Scores32& sc,
-                             const Rec* ring_in, Rec* ring_out, lds_int* wcnt_in,
-                             lds_int* rcnt_in, lds_int* wcnt_out, lds_int* rcnt_out,
+template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP>
+__device__ void compute_wave(const PairDev& P, const int s, const int lane, const Scores32& sc, const Rec* ring_in,
+                             Rec* ring_out, lds_int* wcnt_in, lds_int* rcnt_in, lds_int* wcnt_out, lds_int* rcnt_out,
                              const bool has_consumer, StripRes* sres, PairRes* pres, int* status) {
     static_assert(kSub == 16, "16-step sub-blocks (code words, ring alignment)");
     const int n = P.n, m = P.m;
     const int i = s * kWave + lane + 1;
     const bool row_ok = i <= n;
-    const int c1v = row_ok ? (int)P.c1[i - 1] : 0x1FF;   // 0x1FF never equals a byte
+    WaveCtx w;
+    {
+        const size_t strip_planes = (size_t)s * P.t4 * kWave * 4;   // ints per plane per strip
+        w.pI = PLANES ? P.pI + strip_planes : nullptr;
+        w.pD = PLANES ? P.pD + strip_planes : nullptr;
+        w.pS = PLANES ? P.pS + strip_planes : nullptr;
+        w.pL = LCSP ? P.pL + strip_planes : nullptr;
+        w.codes = CODES ? P.codes + (size_t)s * P.t16 * kWave : nullptr;
+    }
+    w.ring_in = ring_in; w.ring_out = ring_out; w.wcnt_in = wcnt_in; w.wcnt_out = wcnt_out; w.status = status;
+    w.m = m; w.lane = lane;
+    w.c1v = row_ok ? (int)P.c1[i - 1] : 0x1FF;   // 0x1FF never equals a byte
+    w.tr_win = 0;
+    StripTrace* const trace = P.trace;
+    const int strip_base = P.strip_base;
+
     LaneState st;
-    st.strip = s;
     // cell (i, 0): algo.rs:204-211
     const int D0 = sc.h + i * sc.g;
     st.I = kNeg;
     st.SD = D0;                                   // max(sub=neg_inf, delete)
     st.SM = max(D0, sc.floor_);
     st.Dd = max3i(kNeg + sc.hg, D0 + sc.g, sc.floor_);
-    st.L = 0;
+    st.L = 0; st.Ltl = 0;
     st.c2c = 0;
     st.best = row_ok ? INT_MIN : INT_MAX; st.bstep = 0; st.bl = 0;
     st.lbest = row_ok ? INT_MIN : INT_MAX; st.lstep = 0;
     st.cI = 0; st.cD = 0;
 
     if (has_consumer) {
-        if (lane == kWave - 1) ring_out[ring_slot(0)] = Rec{st.Dd, st.SM, st.L, 0};
+        if (lane == kWave - 1) ring_out[ring_slot(0)] = Rec{st.Dd, st.SM, 0, st.L};
         lds_wait();
         if (lane == 0) *wcnt_out = 1;
     }
-    const bool tracing = P.trace != nullptr;
+    const bool tracing = trace != nullptr;
     long long tr_start = 0, tr_first = 0;
-    unsigned tr_win = 0, tr_wout = 0;
+    unsigned tr_wout = 0;
     if (tracing) tr_start = __builtin_amdgcn_s_memrealtime();
     // column 0 of the row above seeds the top-left of column 1; columns 1..4
     // feed the first step group
-    tr_win += wait_ge(wcnt_in, min(4, m) + 1, status);
+    w.tr_win += wait_ge(wcnt_in, min(4, m) + 1, status);
     Rec nxt[4];
     {
         const Rec r0 = ring_in[ring_slot(0)];
@@ -363,55 +443,55 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     }
     if (tracing) tr_first = __builtin_amdgcn_s_memrealtime();
     const int T = m + kWave;                          // lane 63 pushes column m at step m + 63
-    const size_t strip_off4 = (size_t)s * P.t4;       // in 4-step groups
-    const size_t strip_off16 = (size_t)s * P.t16;
+    const bool rolled_only = (sc.dbg & 1) != 0;
     for (int t0 = 0; t0 < T; t0 += kSub) {
-        const uint32_t out_base = lds_addr(ring_out + ring_slot(t0 - (kWave - 1)));
         const int last_col = min(t0 + kSub - 1 - (kWave - 1), m);   // last column pushed here
-        const bool push = has_consumer && last_col >= 1;
-        if (push && last_col >= kRing) tr_wout += wait_ge(rcnt_out, last_col - kRing + 1, status);
-        const unsigned long long m63 =
-            (unsigned long long)__builtin_amdgcn_readfirstlane(push ? 0x80000000u : 0u) << 32;   // lane-63 exec
-        const bool full = (t0 >= kWave) && (t0 + kSub - 1 <= m - 1) && !(sc.dbg & 1);
-        if (full)
-            sub_block<LOCAL, false, PLANES, LCSP, CODES>(st, nxt, ring_in, out_base, m63, push, t0, lane, m, c1v, sc,
-                                                         P, strip_off4, wcnt_in, wcnt_out, status, tr_win);
-        else
-            ramp_block<LOCAL, PLANES, LCSP, CODES>(st, nxt, ring_in, ring_out, m63, push, t0, lane, m, c1v, sc, P,
-                                                   strip_off4, wcnt_in, wcnt_out, status, tr_win);
-        if (CODES) gstore1(P.codes + (strip_off16 + (t0 >> 4)) * kWave + lane, (st.cD << 16) | (st.cI & 0xFFFFu));
+        if (has_consumer && last_col >= kRing) tr_wout += wait_ge(rcnt_out, last_col - kRing + 1, status);
+        const size_t sb_off = (size_t)(t0 >> 2) * kWave * 4;          // this sub-block's plane offset (ints)
+        const bool full = (t0 >= kWave) && (t0 + kSub - 1 <= m - 1) && !rolled_only;
+        if (full) {
+            const unsigned long long m63 = lane63_mask(has_consumer);
+            sub_block<LOCAL, PLANES, CODES, TRACK, LCSP>(st, nxt, w, sc, t0,
+                                                         lds_addr(ring_out + ring_slot(t0 - (kWave - 1))), m63,
+                                                         sb_off);
+        } else {
+            ramp_block<LOCAL, PLANES, CODES, TRACK, LCSP>(st, nxt, w, sc, t0, has_consumer, sb_off);
+        }
+        if (CODES) gstore1(w.codes + (size_t)(t0 >> 4) * kWave + lane, (st.cD << 16) | (st.cI & 0xFFFFu));
         // every ring read up to column t0+20 (incl. the next group's) was issued before this store
         lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
     }
 
     // ---- strip reduction of the max trackers ----
-    int best = row_ok ? st.best : INT_MIN;
-    int lbest = row_ok ? st.lbest : INT_MIN;
-    int mx = best, lmx = lbest;
-    for (int off = 32; off > 0; off >>= 1) {
-        mx = max(mx, __shfl_xor(mx, off));
-        lmx = max(lmx, __shfl_xor(lmx, off));
-    }
-    const unsigned long long fmask = __ballot(row_ok && best == mx);
-    const unsigned long long lmask = __ballot(row_ok && lbest == lmx);
-    const int fl = fmask ? (__ffsll((long long)fmask) - 1) : 0;           // lowest row
-    const int ll = lmask ? (63 - __clzll((long long)lmask)) : 0;          // highest row
-    const int f_step = __shfl(st.bstep, fl), f_l = __shfl(st.bl, fl);
-    const int l_step = __shfl(st.lstep, ll);
-    if (lane == 0) {
-        StripRes r;
-        r.best = mx; r.bi = s * kWave + fl + 1; r.bj = f_step - fl + 1; r.bl = f_l;
-        r.lbest = lmx; r.li = s * kWave + ll + 1; r.lj = l_step - ll + 1; r.valid = 1;
-        sres[P.strip_base + s] = r;
+    if (TRACK || LOCAL) {
+        const int best = (TRACK && row_ok) ? st.best : INT_MIN;
+        const int lbest = (LOCAL && row_ok) ? st.lbest : INT_MIN;
+        int mx = best, lmx = lbest;
+        for (int off = 32; off > 0; off >>= 1) {
+            mx = max(mx, __shfl_xor(mx, off));
+            lmx = max(lmx, __shfl_xor(lmx, off));
+        }
+        const unsigned long long fmask = __ballot(row_ok && best == mx);
+        const unsigned long long lmask = __ballot(row_ok && lbest == lmx);
+        const int fl = fmask ? (__ffsll((long long)fmask) - 1) : 0;           // lowest row
+        const int ll = lmask ? (63 - __clzll((long long)lmask)) : 0;          // highest row
+        const int f_step = __shfl(st.bstep, fl), f_l = __shfl(st.bl, fl);
+        const int l_step = __shfl(st.lstep, ll);
+        if (lane == 0) {
+            StripRes r;
+            r.best = mx; r.bi = s * kWave + fl + 1; r.bj = f_step - fl + 1; r.bl = f_l;
+            r.lbest = lmx; r.li = s * kWave + ll + 1; r.lj = l_step - ll + 1; r.valid = 1;
+            sres[strip_base + s] = r;
+        }
     }
     // cell (n, m) for the global-mode start (algo.rs:308, 331)
     if (row_ok && i == n) pres->end_SM = st.SM;
     if (tracing && lane == 0) {
         StripTrace tr;
         tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
-        tr.wait_in = (int)tr_win; tr.wait_out = (int)tr_wout;
+        tr.wait_in = (int)w.tr_win; tr.wait_out = (int)tr_wout;
         tr.band = s / 4; tr.wave = s % 4; tr.pad0 = 0; tr.pad1 = 0;
-        P.trace[s] = tr;
+        trace[s] = tr;
     }
 }
 
@@ -486,21 +566,23 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
     }
 }
 
-template <int W, bool LOCAL, bool PLANES, bool LCSP, bool CODES>
-__global__ __launch_bounds__((W + 1) * kWave, 2) void fill_kernel(const PairDev* __restrict__ pairs, const int npairs,
-                                                              const int total_bands, int* band_counter,
-                                                              StripRes* sres, PairRes* pres, const Scores32 sc) {
+template <int W, bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP>
+__global__ __launch_bounds__((W + 1) * kWave, GX_FILL_MIN_WAVES) void fill_kernel(
+    const PairDev* __restrict__ pairs, const int npairs, const int total_bands, int* band_counter, StripRes* sres,
+    PairRes* pres, const Scores32 sc) {
     __shared__ Rec rings[W + 1][kRing];
     __shared__ int wcnt[W + 1];
     __shared__ int rcnt[W + 1];
     __shared__ int band_sh;
-    const int wave = threadIdx.x / kWave;
+    // readfirstlane: tell the compiler these are wave-uniform, so the pair
+    // descriptor, plane bases and exec masks live in SGPRs
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int lane = threadIdx.x & (kWave - 1);
     for (;;) {
         if (threadIdx.x == 0) band_sh = atomicAdd(band_counter, 1);
         if (threadIdx.x < W + 1) { wcnt[threadIdx.x] = 0; rcnt[threadIdx.x] = 0; }
         __syncthreads();
-        const int b = band_sh;
+        const int b = __builtin_amdgcn_readfirstlane(band_sh);
         if (b >= total_bands) return;
         int p = 0;
         while (p + 1 < npairs && pairs[p + 1].band_base <= b) ++p;
@@ -512,16 +594,14 @@ __global__ __launch_bounds__((W + 1) * kWave, 2) void fill_kernel(const PairDev*
             if (s < P.strips) {
                 const bool last_in_band = wave == W - 1;
                 const bool has_consumer = last_in_band ? (lb + 1 < P.bands) : (s + 1 < P.strips);
-                compute_wave<LOCAL, PLANES, LCSP, CODES>(P, s, lane, sc, rings[wave], rings[wave + 1],
-                                                         (lds_int*)&wcnt[wave], (lds_int*)&rcnt[wave],
-                                                         (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1],
-                                                         has_consumer, sres, pres + p,
-                                                         band_counter + 1);
+                compute_wave<LOCAL, PLANES, CODES, TRACK, LCSP>(
+                    P, s, lane, sc, rings[wave], rings[wave + 1], (lds_int*)&wcnt[wave], (lds_int*)&rcnt[wave],
+                    (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1], has_consumer, sres, pres + p,
+                    band_counter + 1);
             }
         } else {
-            io_wave(P, lb, lane, sc, rings[0], rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0],
-                    (lds_int*)&wcnt[W], (lds_int*)&rcnt[W],
-                    lb + 1 < P.bands, band_counter + 1);
+            io_wave(P, lb, lane, sc, rings[0], rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0], (lds_int*)&wcnt[W],
+                    (lds_int*)&rcnt[W], lb + 1 < P.bands, band_counter + 1);
         }
         __syncthreads();
     }
@@ -614,40 +694,33 @@ __global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __rest
 // ---- explicit launch wrappers (C++ linkage, used by gx_api.cpp) ----
 namespace gx {
 
-template <int W, bool LOCAL, bool PLANES, bool LCSP, bool CODES>
+template <bool LOCAL, bool PLANES, bool TRACK, bool LCSP>
 static hipError_t launch_fill_t(const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
                                 StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
-    hipLaunchKernelGGL((fill_kernel<W, LOCAL, PLANES, LCSP, CODES>), dim3(grid), dim3((W + 1) * kWave), 0, st,
+    constexpr int W = kBandWaves;
+    hipLaunchKernelGGL((fill_kernel<W, LOCAL, PLANES, true, TRACK, LCSP>), dim3(grid), dim3((W + 1) * kWave), 0, st,
                        d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc);
     return hipGetLastError();
 }
 
-hipError_t launch_fill(int W, bool local, bool planes, bool lcs, bool codes, const PairDev* d_pairs, int npairs,
+// Variants: mode (global/local) x planes x {no max tracking, first max + LCS
+// field, first max + LCS plane}.  Traceback codes are always produced.
+hipError_t launch_fill(bool local, bool planes, bool track, bool lcs, const PairDev* d_pairs, int npairs,
                        int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                        hipStream_t st) {
-#define GX_FILL_CASE(WW, LO, PL, CO)                                                                     \
-    if (W == WW && local == LO && planes == PL && codes == CO && !lcs)                                   \
-        return launch_fill_t<WW, LO, PL, false, CO>(d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, \
-                                                    sc, grid, st);
-#define GX_FILL_W(WW)                 \
-    GX_FILL_CASE(WW, false, false, false) \
-    GX_FILL_CASE(WW, false, false, true)  \
-    GX_FILL_CASE(WW, false, true, false)  \
-    GX_FILL_CASE(WW, false, true, true)   \
-    GX_FILL_CASE(WW, true, false, false)  \
-    GX_FILL_CASE(WW, true, false, true)   \
-    GX_FILL_CASE(WW, true, true, false)   \
-    GX_FILL_CASE(WW, true, true, true)
-    GX_FILL_W(1)
-    GX_FILL_W(2)
-    GX_FILL_W(4)
-    // full-fidelity export (LCS plane): one configuration per mode
-    if (W == 4 && planes && codes && lcs)
-        return local ? launch_fill_t<4, true, true, true, true>(d_pairs, npairs, total_bands, d_counter, d_sres,
-                                                                 d_pres, sc, grid, st)
-                     : launch_fill_t<4, false, true, true, true>(d_pairs, npairs, total_bands, d_counter, d_sres,
-                                                                  d_pres, sc, grid, st);
-#undef GX_FILL_W
+#define GX_FILL_CASE(LO, PL, TR, LC)                                                                  \
+    if (local == LO && planes == PL && track == TR && lcs == LC)                                      \
+        return launch_fill_t<LO, PL, TR, LC>(d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc, grid, st);
+    GX_FILL_CASE(false, false, false, false)
+    GX_FILL_CASE(false, false, true, false)
+    GX_FILL_CASE(false, true, false, false)
+    GX_FILL_CASE(false, true, true, false)
+    GX_FILL_CASE(false, true, true, true)
+    GX_FILL_CASE(true, false, false, false)
+    GX_FILL_CASE(true, false, true, false)
+    GX_FILL_CASE(true, true, false, false)
+    GX_FILL_CASE(true, true, true, false)
+    GX_FILL_CASE(true, true, true, true)
 #undef GX_FILL_CASE
     return hipErrorInvalidValue;
 }

@@ -25,6 +25,7 @@ LIB_PATH = os.environ.get("GX_LIB", os.path.join(_HERE, "libgx_amd.so"))
 
 GX_TABLE_PLANES = 1
 GX_TABLE_MATCHES = 2
+GX_ALIGN_MAX_CELL = 4
 
 # status codes (include/gx.h)
 _CODES = {0: "GX_OK", 1: "GX_EINVAL", 2: "GX_ESEQ", 3: "GX_ERANGE", 4: "GX_ENOMEM", 5: "GX_EHIP",
@@ -97,11 +98,12 @@ def lib():
     L.gx_retrace.argtypes = [vp, ctypes.c_int, vp, sz, ctypes.POINTER(CResult)]
     L.gx_table_free.argtypes = [vp]
     L.gx_table_free.restype = None
-    L.gx_align.argtypes = [vp, vp, sz, vp, sz, ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int, vp, sz,
-                           ctypes.POINTER(CResult)]
-    L.gx_align_batch.argtypes = [vp, vp, vp, vp, vp, sz, ctypes.POINTER(CScores), ctypes.c_int, vp, vp, vp]
+    L.gx_align.argtypes = [vp, vp, sz, vp, sz, ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int,
+                           ctypes.c_uint32, vp, sz, ctypes.POINTER(CResult)]
+    L.gx_align_batch.argtypes = [vp, vp, vp, vp, vp, sz, ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_uint32,
+                                 vp, vp, vp]
     L.gx_stage_pairs.argtypes = [vp, vp, vp, vp, vp, sz]
-    L.gx_run_staged.argtypes = [vp, ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int, vp,
+    L.gx_run_staged.argtypes = [vp, ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int, ctypes.c_uint32, vp,
                                 ctypes.POINTER(ctypes.c_double)]
     L.gx_fasta_load.argtypes = [ctypes.c_char_p, vp, sz, vp, vp, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.gx_config_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(CScores)]
@@ -382,8 +384,9 @@ def _aligned(a: Sequence, b: Sequence, steps: np.ndarray, r: CResult) -> Aligned
 
 
 def align_raw(s1: bytes, s2: bytes, scores: Scores, is_local: bool, reverse_sequences: bool = False,
-              ctx: Optional[Context] = None):
-    """Fused alignment_table + retrace on bytes -> (steps structured array, CResult)."""
+              ctx: Optional[Context] = None, max_cell: bool = True):
+    """Fused alignment_table + retrace on bytes -> (steps structured array, CResult).
+    max_cell: also report alignment_table's max cell / matches_at_max."""
     ctx = ctx or default_context()
     x, px = _buf(s1)
     y, py = _buf(s2)
@@ -391,12 +394,13 @@ def align_raw(s1: bytes, s2: bytes, scores: Scores, is_local: bool, reverse_sequ
     steps = np.zeros(cap, STEP_DTYPE)
     r = CResult()
     _check(lib().gx_align(ctx.ptr, px, len(s1), py, len(s2), ctypes.byref(scores.c()), int(is_local),
-                          int(reverse_sequences), steps.ctypes.data, cap, ctypes.byref(r)))
+                          int(reverse_sequences), GX_ALIGN_MAX_CELL if max_cell else 0, steps.ctypes.data, cap,
+                          ctypes.byref(r)))
     return steps[: r.n_steps], r
 
 
 def align_batch(pairs: Seq[Tuple[bytes, bytes]], scores: Scores, is_local: bool, with_steps: bool = True,
-                ctx: Optional[Context] = None):
+                ctx: Optional[Context] = None, max_cell: bool = True):
     """Many independent pairs in one device launch -> list of (steps, CResult)."""
     ctx = ctx or default_context()
     P = len(pairs)
@@ -409,7 +413,8 @@ def align_batch(pairs: Seq[Tuple[bytes, bytes]], scores: Scores, is_local: bool,
     steps_arr = [np.zeros(len(a) + len(b) + 2, STEP_DTYPE) for a, b in pairs] if with_steps else None
     stp = (ctypes.c_void_p * P)(*[s.ctypes.data for s in steps_arr]) if with_steps else None
     caps = (ctypes.c_size_t * P)(*[s.size for s in steps_arr]) if with_steps else None
-    _check(lib().gx_align_batch(ctx.ptr, s1p, n, s2p, m, P, ctypes.byref(scores.c()), int(is_local), stp, caps, res))
+    _check(lib().gx_align_batch(ctx.ptr, s1p, n, s2p, m, P, ctypes.byref(scores.c()), int(is_local),
+                                GX_ALIGN_MAX_CELL if max_cell else 0, stp, caps, res))
     out = []
     for p in range(P):
         st = steps_arr[p][: res[p].n_steps] if with_steps else None
@@ -430,9 +435,9 @@ class StagedPairs:
         m = (ctypes.c_size_t * self.P)(*[len(b) for _, b in pairs])
         _check(lib().gx_stage_pairs(self.ctx.ptr, s1p, n, s2p, m, self.P))
 
-    def run(self, scores: Scores, is_local: bool, keep_planes: bool = True):
+    def run(self, scores: Scores, is_local: bool, keep_planes: bool = True, max_cell: bool = False):
         res = (CResult * self.P)()
         fms = ctypes.c_double(0)
-        _check(lib().gx_run_staged(self.ctx.ptr, ctypes.byref(scores.c()), int(is_local), int(keep_planes), res,
-                                   ctypes.byref(fms)))
+        _check(lib().gx_run_staged(self.ctx.ptr, ctypes.byref(scores.c()), int(is_local), int(keep_planes),
+                                   GX_ALIGN_MAX_CELL if max_cell else 0, res, ctypes.byref(fms)))
         return list(res), fms.value

@@ -101,7 +101,9 @@ int gx_context_trim(gx_context* ctx);
  * HBM (the reference's (n+1)x(m+1) 48 B cells need 42.9 GB at 30k; planes
  * here take 12 B/cell).  `reverse_sequences` has the semantics of
  * is_match(.., true) (sequence.rs:102-115).  On success *table_out owns the
- * table and *matches_at_max holds the second tuple element.
+ * table and *matches_at_max holds the second tuple element.  Passing
+ * matches_at_max = NULL skips the running-max/LCS tracking (gx_table_info
+ * then reports max cell (0, 0)) unless GX_TABLE_MATCHES is set.
  * flags: GX_TABLE_PLANES keeps the three score planes (needed for export);
  *        GX_TABLE_MATCHES additionally keeps the LCS plane so that the
  *        *_matches fields can be exported (full AlignmentCell fidelity).   */
@@ -135,27 +137,32 @@ int gx_retrace(gx_table* t, int is_local, gx_step* steps, size_t cap, gx_result*
 /* Frees a table without retracing. */
 void gx_table_free(gx_table* t);
 
-/* ---- fused alignment_table + retrace (main.rs:143-150) ---------------- */
+/* ---- fused alignment_table + retrace (main.rs:143-150) ----------------
+ * main.rs discards alignment_table's matches_at_max, so the fused paths do
+ * not track the running max cell unless asked: with GX_ALIGN_MAX_CELL in
+ * `flags` the result's max_cell_i/j and matches_at_max are filled as
+ * gx_alignment_table would; otherwise they are 0.                         */
+#define GX_ALIGN_MAX_CELL 4u
 int gx_align(gx_context* ctx, const uint8_t* s1, size_t n, const uint8_t* s2, size_t m,
-             const gx_scores* scores, int is_local, int reverse_sequences, gx_step* steps, size_t cap,
-             gx_result* out);
+             const gx_scores* scores, int is_local, int reverse_sequences, uint32_t flags, gx_step* steps,
+             size_t cap, gx_result* out);
 
 /* ---- many independent pairs in one device launch -----------------------
  * Pair p aligns s1[p] (n[p]) with s2[p] (m[p]).  Score planes are not kept
  * (only the traceback codes), so the batch fits HBM.  steps may be NULL
- * (stats only); otherwise steps[p] has caps[p] entries. */
+ * (stats only); otherwise steps[p] has caps[p] entries.  flags as gx_align. */
 int gx_align_batch(gx_context* ctx, const uint8_t* const* s1, const size_t* n, const uint8_t* const* s2,
-                   const size_t* m, size_t npairs, const gx_scores* scores, int is_local, gx_step* const* steps,
-                   const size_t* caps, gx_result* out);
+                   const size_t* m, size_t npairs, const gx_scores* scores, int is_local, uint32_t flags,
+                   gx_step* const* steps, const size_t* caps, gx_result* out);
 
 /* ---- device-resident benchmarking path ---------------------------------
  * Stage one pair per slot in HBM once (gx_stage_pairs), then run the hot
  * path (fill with score planes + traceback) on the staged inputs with no
- * host->device traffic.  Used by bench.py; results as gx_align. */
+ * host->device traffic.  Used by bench.py; results and flags as gx_align. */
 int gx_stage_pairs(gx_context* ctx, const uint8_t* const* s1, const size_t* n, const uint8_t* const* s2,
                    const size_t* m, size_t npairs);
-int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes, gx_result* out,
-                  double* fill_ms_out);
+int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes, uint32_t flags,
+                  gx_result* out, double* fill_ms_out);
 
 /* ---- sequence.rs / config.rs mirrors ----------------------------------- */
 /* from_fasta (sequence.rs:45-95) on a file: records are appended to the
