@@ -98,6 +98,8 @@ static int pool_get(gx_context* ctx, size_t bytes, DevBuf* out) {
         return GX_OK;
     }
     void* p = nullptr;
+    if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug"))
+        fprintf(stderr, "[gx DEBUG] pool miss: hipMalloc %zu B (%zu cached)\n", bytes, ctx->free_list.size());
     hipError_t e = hipMalloc(&p, bytes);
     if (e != hipSuccess) {
         // drop cached buffers and retry once
@@ -232,7 +234,6 @@ static int processed_chars(const uint8_t* s1, size_t n, const uint8_t* s2, size_
 // ---------------------------------------------------------------------------
 // fill orchestration
 
-constexpr int kBandWaves = 4;   // compute waves per band (gx_kernels.hip)
 static int fill_grid_cap() {
     static int g = -1;
     if (g < 0) {
@@ -361,6 +362,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, ctx->stream));
     HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), ctx->stream));
     const int grid = std::min(bands, fill_grid_cap());
+    const auto h_launch = std::chrono::steady_clock::now();
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     if (bands > 0)
         HIPCHK(launch_fill(is_local != 0, planes, track, lcs, (const PairDev*)job.pairs.p, (int)P, bands,
@@ -374,6 +376,9 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     HIPCHK(hipMemcpyAsync(job.res.data(), job.pres.p, P * sizeof(PairRes), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipMemcpyAsync(status, job.counter.p, sizeof status, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug"))
+        fprintf(stderr, "[gx DEBUG] fill: launch..sync %.3f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h_launch).count());
     if (status[1] != 0)
         return fail(GX_EHIP, "fill kernel: inter-wave wait timed out (status " + std::to_string(status[1]) + ")");
     float ms = 0.f;
@@ -512,14 +517,14 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     const size_t P = starts.size();
     std::vector<TbDev> jobs(P);
     std::vector<size_t> mo(P);
-    size_t mtot = 0;
+    size_t mtot = 0;   // records (uint32): at most one per row + the final run
     for (size_t p = 0; p < P; ++p) {
         mo[p] = mtot;
-        mtot += align_up((size_t)job.pd[p].n + job.pd[p].m + 64, 64);
+        mtot += align_up((size_t)job.pd[p].n + 64, 64);
     }
     DevBuf moves, jb, cnt;
     int rc;
-    if ((rc = pool_get(ctx, mtot, &moves))) return rc;
+    if ((rc = pool_get(ctx, mtot * sizeof(uint32_t), &moves))) return rc;
     if ((rc = pool_get(ctx, P * sizeof(TbDev), &jb))) { pool_put(ctx, moves); return rc; }
     if ((rc = pool_get(ctx, P * 4 * sizeof(int), &cnt))) { pool_put(ctx, moves); pool_put(ctx, jb); return rc; }
     for (size_t p = 0; p < P; ++p) {
@@ -527,8 +532,8 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
         t.codes = job.pd[p].codes;
         t.n = job.pd[p].n; t.m = job.pd[p].m; t.t16 = job.pd[p].t16;
         t.start_i = starts[p].first; t.start_j = starts[p].second;
-        t.moves = (uint8_t*)moves.p + mo[p];
-        t.nmoves = (int*)cnt.p + 4 * p;
+        t.recs = (uint32_t*)moves.p + mo[p];
+        t.nrecs = (int*)cnt.p + 4 * p;
         t.end_ij = (int*)cnt.p + 4 * p + 1;
     }
     auto cleanup = [&]() { pool_put(ctx, moves); pool_put(ctx, jb); pool_put(ctx, cnt); };
@@ -546,15 +551,22 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     out.moves.resize(P);
     out.end_i.resize(P);
     out.end_j.resize(P);
-    // one D2H for all moves
-    std::vector<uint8_t> hm(mtot);
-    e = hipMemcpyAsync(hm.data(), moves.p, mtot, hipMemcpyDeviceToHost, ctx->stream);
+    // one D2H for all records
+    std::vector<uint32_t> hm(mtot);
+    e = hipMemcpyAsync(hm.data(), moves.p, mtot * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     cleanup();
     if (e != hipSuccess) return fail(GX_EHIP, std::string("traceback copy: ") + hipGetErrorString(e));
     for (size_t p = 0; p < P; ++p) {
+        // expand the per-row records into per-move codes (0 sub, 1 insert, 2 delete)
         const int k = c[4 * p];
-        out.moves[p].assign(hm.begin() + mo[p], hm.begin() + mo[p] + k);
+        std::vector<uint8_t>& mv = out.moves[p];
+        mv.clear();
+        for (int r = 0; r < k; ++r) {
+            const uint32_t rec = hm[mo[p] + r];
+            mv.insert(mv.end(), rec >> 2, (uint8_t)1);
+            if ((rec & 3u) != 1u) mv.push_back((uint8_t)(rec & 3u));
+        }
         out.end_i[p] = c[4 * p + 1];
         out.end_j[p] = c[4 * p + 2];
     }
@@ -832,12 +844,15 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
     std::vector<uint64_t> si(P), sj(P);
     std::vector<int64_t> score(P);
     int rc = GX_OK;
+    using clk = std::chrono::steady_clock;
+    const auto c0 = clk::now();
     if (!idx.empty()) {
         rc = run_fill(ctx, dproc, dph, sc, is_local, planes, track, false, job, chars_dev, chars_dev ? &o1 : nullptr,
                       chars_dev ? &o2 : nullptr);
         if (rc) { job_release(ctx, job); return rc; }
         for (size_t k = 0; k < idx.size(); ++k) res[idx[k]] = job.res[k];
     }
+    const auto c1 = clk::now();
     for (size_t p = 0; p < P; ++p) start_cell_common(hs, is_local, ph[p].n, ph[p].m, res[p], &si[p], &sj[p], &score[p]);
     if (!idx.empty()) {
         for (size_t k = 0; k < idx.size(); ++k) {
@@ -846,9 +861,24 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
         }
         rc = run_traceback(ctx, job, starts, tb);
     }
+    const auto c2 = clk::now();
     if (fill_ms) *fill_ms = job.fill_ms;
     job_release(ctx, job);
     if (rc) return rc;
+    struct PhaseLog {   // GX_LOG=debug: host-side phase times of the batch path
+        clk::time_point c0, c1, c2;
+        double fill_ms, tb_ms;
+        size_t P;
+        ~PhaseLog() {
+            const char* e = getenv("GX_LOG");
+            if (!e || strcmp(e, "debug")) return;
+            auto ms = [](clk::time_point a, clk::time_point b) {
+                return std::chrono::duration<double, std::milli>(b - a).count();
+            };
+            fprintf(stderr, "[gx DEBUG] batch P=%zu fill %.3f ms (kernel %.3f) traceback %.3f ms (kernel %.3f) "
+                            "label %.3f ms\n", P, ms(c0, c1), fill_ms, ms(c1, c2), tb_ms, ms(c2, clk::now()));
+        }
+    } plog{c0, c1, c2, job.fill_ms, tb.ms, P};
     walks.assign(P, Walk{});
     std::vector<int> dev_of(P, -1);
     for (size_t k = 0; k < idx.size(); ++k) dev_of[idx[k]] = (int)k;

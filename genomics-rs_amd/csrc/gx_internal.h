@@ -23,7 +23,11 @@ constexpr int kNeg = -(1 << 30);   // int32 stand-in for negative_inf (algo.rs:1
 constexpr int kRing = 256;         // LDS ring records per strip boundary (power of two)
 constexpr int kSub = 16;           // steps per flow-control sub-block (multiple of 16)
 constexpr int kIoChunk = 16;       // columns per I/O-wave transfer
-constexpr int kMaxBandWaves = 8;
+// Compute waves per band (workgroup = kBandWaves compute waves + 1 I/O wave).
+#ifndef GX_BAND_WAVES
+#define GX_BAND_WAVES 7
+#endif
+constexpr int kBandWaves = GX_BAND_WAVES;
 
 // Scores narrowed to int32 after the host range guard (DESIGN.md "Integer range").
 struct Scores32 {
@@ -93,8 +97,8 @@ struct TbDev {           // per-pair traceback job
     const uint32_t* codes;
     int n, m, t16;
     int start_i, start_j;  // interior start cell (1-based), or 0 = nothing to walk
-    uint8_t* moves;        // out: one code per move
-    int* nmoves;           // out
+    uint32_t* recs;        // out: one record per row, (insert run << 2) | kind (gx_kernels.hip)
+    int* nrecs;            // out
     int* end_ij;           // out: [2] position where the walk left the interior
 };
 

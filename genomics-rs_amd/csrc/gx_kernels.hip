@@ -110,9 +110,8 @@ __device__ __forceinline__ void gstore4_at(int32_t* base, uint32_t byte_off, int
 }
 
 
-// Compute waves per band and the occupancy floor (waves per SIMD) that caps
-// the fill kernel's VGPRs (512 / 4 = 128).
-constexpr int kBandWaves = 4;
+// Occupancy floor (waves per SIMD) that caps the fill kernel's VGPRs
+// (512 / 4 = 128): with 8-wave workgroups, two bands per CU.
 #ifndef GX_FILL_MIN_WAVES
 #define GX_FILL_MIN_WAVES 4
 #endif
@@ -490,7 +489,7 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         StripTrace tr;
         tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
         tr.wait_in = (int)w.tr_win; tr.wait_out = (int)tr_wout;
-        tr.band = s / 4; tr.wave = s % 4; tr.pad0 = 0; tr.pad1 = 0;
+        tr.band = s / kBandWaves; tr.wave = s % kBandWaves; tr.pad0 = 0; tr.pad1 = 0;
         trace[s] = tr;
     }
 }
@@ -625,55 +624,141 @@ __global__ void finalize_kernel(const PairDev* __restrict__ pairs, const StripRe
     o.lmax_val = lbest; o.lmax_i = li; o.lmax_j = lj; o.nstrips = P.strips;
 }
 
-// Traceback walk over the 2-bit direction codes (algo.rs:339-422), interior
-// cells only; the host finishes the boundary part and labels the moves.
-// One wave per pair; the walk state is wave-uniform.  A 64-step x 64-row
-// chunk of codes is held in 4 VGPRs (lane = row) and read with readlane.
+// Traceback walk over the direction codes (algo.rs:339-422), interior cells
+// only; the host finishes the boundary part and labels the moves.
+//
+// The walk is done a ROW at a time: on row i the path is a run of insert
+// moves (j-1) that ends at the nearest cell to the left whose code is not
+// "insert", followed by one sub (i-1, j-1) or delete (i-1, j) move.  Cells of
+// one row are consecutive steps of one lane's code words, so the run is a
+// bit-scan of the "not insert" mask (D | ~I) -- O(1) per word, not per move.
+// Output: one record per row, (run << 2) | kind, kind 0 = sub, 2 = delete,
+// 1 = the run reached column 0 (walk ends at (i, 0)).
+//
+// One wave per pair, walk state wave-uniform.  The code window of the current
+// strip (kTbWin words = 256 steps of every lane) sits in VGPRs and is read
+// with readlane.  The window of the strip above is prefetched by LDS-DMA
+// (global_load_lds) while this one is walked -- no VGPR has a load in flight
+// during the walk, so the dynamically indexed reads never wait on it.  The
+// path's step index only decreases inside a strip, and it enters the strip
+// above at lane 63 no further right than the current column.
+constexpr int kTbWin = 16;
+
+// (readfirstlane: keeps the walk state provably uniform, so the window index
+// is an SGPR and the indexed VGPR read needs no waterfall loop)
+__device__ __forceinline__ int tb_q0(int t) {
+    return __builtin_amdgcn_readfirstlane(max((t >> 4) - (kTbWin - 1), 0));
+}
+
+typedef __attribute__((address_space(1))) const void gcvoid;
+typedef __attribute__((address_space(3))) void lvoid;
+
+// async: words q0 .. q0+kTbWin-1 of strip s, all lanes -> buf[k][lane]
+__device__ __forceinline__ void tb_prefetch(uint32_t* buf, const TbDev& J, int s, int q0, int lane) {
+    const uint32_t* base = J.codes + ((size_t)s * J.t16 + q0) * kWave + lane;
+#pragma unroll
+    for (int k = 0; k < kTbWin; ++k)
+        if (q0 + k < J.t16)
+            __builtin_amdgcn_global_load_lds((gcvoid*)(base + (size_t)k * kWave), (lvoid*)(buf + k * kWave), 4, 0, 0);
+}
+
+__device__ __forceinline__ void tb_take(uint32_t (&w)[kTbWin], const uint32_t* buf, int lane) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the LDS-DMA writes have landed
+    typedef __attribute__((address_space(3))) const uint32_t lu32;
+    const lu32* b = (const lu32*)(uintptr_t)lds_addr(buf);
+#pragma unroll
+    for (int k = 0; k < kTbWin; ++k) w[k] = b[k * kWave + lane];
+}
+
 __global__ __launch_bounds__(64) void traceback_kernel(const TbDev* __restrict__ jobs) {
+    __shared__ uint32_t tbuf[2][kTbWin * kWave];
     const TbDev J = jobs[blockIdx.x];
     const int lane = threadIdx.x;
     int i = J.start_i, j = J.start_j;
-    int k = 0;
-    uint32_t mvbuf = 0;
-    if (i < 1 || j < 1) {
-        if (lane == 0) { *J.nmoves = 0; J.end_ij[0] = i; J.end_ij[1] = j; }
-        return;
-    }
-    int cur_s = -1, cur_q = -1;  // chunk = strip s, words q..q+3 (t in [16q, 16q+64))
-    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-    while (i >= 1 && j >= 1) {
-        const int s = (i - 1) >> 6;
-        const int l = (i - 1) & 63;
-        const int t = j - 1 + l;
-        const int tq = t >> 4;
-        if (s != cur_s || tq < cur_q || tq > cur_q + 3) {
-            cur_s = s;
-            cur_q = max(tq - 3, 0);
-            const uint32_t* base = J.codes + ((size_t)s * J.t16 + cur_q) * kWave + lane;
-            w0 = base[0];
-            w1 = (cur_q + 1 < J.t16) ? base[kWave] : 0u;
-            w2 = (cur_q + 2 < J.t16) ? base[2 * kWave] : 0u;
-            w3 = (cur_q + 3 < J.t16) ? base[3 * kWave] : 0u;
+    int nrec = 0;
+    uint32_t recbuf = 0;
+    guint* const recs = (guint*)J.recs;
+    if (i >= 1 && j >= 1) {
+        int cb = 0;
+        int s = (i - 1) >> 6;
+        int q0 = tb_q0(j - 1 + ((i - 1) & 63));
+        tb_prefetch(tbuf[cb], J, s, q0, lane);
+        int qn = tb_q0(j - 1 + (kWave - 1));   // window of the strip above, for an entry at lane 63
+        bool want_next = s > 0;
+        bool done = false;
+        bool resume = false;                   // continue a run scan after a reload
+        int t_in = 0, t = 0;
+        // outer loop: one window (a strip, or a reload lower in the same strip);
+        // `cur` is written only here, so the row loop keeps it in place
+        while (!done) {
+            uint32_t cur[kTbWin];
+            tb_take(cur, tbuf[cb], lane);
+            if (want_next) {                   // after the take: its wait must not cover this prefetch
+                tb_prefetch(tbuf[cb ^ 1], J, s - 1, qn, lane);
+                want_next = false;
+            }
+            for (;;) {
+                const int l = (i - 1) & 63;
+                if (!resume) { t_in = j - 1 + l; t = t_in; }
+                resume = false;
+                int tf = -1;           // step of the nearest non-insert cell (column >= 1), if any
+                uint32_t w = 0;
+                bool reload = false;
+                while (t >= l) {
+                    const int qq = t >> 4;
+                    if (qq < q0) { reload = true; break; }   // the run left the window (rare)
+                    w = __builtin_amdgcn_readlane(cur[__builtin_amdgcn_readfirstlane(qq - q0)], l);
+                    const int k = t & 15;
+                    // bit 15-k: "insert beats sub"; bit 31-k: "delete beats both" (step 16q + k)
+                    const uint32_t nonI = ((w >> 16) | ~w) & ((0xFFFFu << (15 - k)) & 0xFFFFu);
+                    if (nonI) {
+                        tf = (t & ~15) + (15 - __builtin_ctz(nonI));
+                        break;
+                    }
+                    t = (t & ~15) - 1;
+                }
+                if (reload) {          // window [.., t]: the scan resumes at t
+                    q0 = tb_q0(t);
+                    tb_prefetch(tbuf[cb], J, s, q0, lane);
+                    resume = true;
+                    break;
+                }
+                uint32_t rec;
+                if (tf < l) {          // all of (i, j..1) insert: the walk leaves at (i, 0)
+                    rec = ((uint32_t)j << 2) | 1u;
+                    j = 0;
+                    done = true;
+                } else {
+                    const bool del = (w >> (31 - (tf & 15))) & 1u;
+                    rec = ((uint32_t)(t_in - tf) << 2) | (del ? 2u : 0u);
+                    j = tf - l + 1 - (del ? 0 : 1);
+                    i -= 1;
+                    done = i < 1 || j < 1;
+                }
+                if (lane == (nrec & 63)) recbuf = rec;
+                ++nrec;
+                if ((nrec & 63) == 0) recs[nrec - 64 + lane] = recbuf;
+                if (done) break;
+                if (l == 0) {          // into the strip above, at lane 63
+                    s -= 1;
+                    cb ^= 1;
+                    const int te = j - 1 + (kWave - 1);
+                    if ((te >> 4) >= qn && (te >> 4) < qn + kTbWin) {
+                        q0 = qn;
+                    } else {           // entered left of the prefetched window
+                        q0 = tb_q0(te);
+                        tb_prefetch(tbuf[cb], J, s, q0, lane);
+                    }
+                    qn = tb_q0(te);
+                    want_next = s > 0;
+                    break;
+                }
+            }
         }
-        const int d = tq - cur_q;
-        uint32_t word;
-        if (d == 0) word = __builtin_amdgcn_readlane(w0, l);
-        else if (d == 1) word = __builtin_amdgcn_readlane(w1, l);
-        else if (d == 2) word = __builtin_amdgcn_readlane(w2, l);
-        else word = __builtin_amdgcn_readlane(w3, l);
-        // bit-planes: bit 31-k = "delete beats both", bit 15-k = "insert beats sub" (k = t % 16)
-        const int ks = t & 15;
-        const uint32_t code = ((word >> (31 - ks)) & 1u) ? 2u : ((word >> (15 - ks)) & 1u);
-        if (lane == (k & 63)) mvbuf = code;
-        ++k;
-        if ((k & 63) == 0) J.moves[k - 64 + lane] = (uint8_t)mvbuf;
-        if (code == 0) { --i; --j; }
-        else if (code == 1) { --j; }
-        else { --i; }
     }
-    const int rem = k & 63;
-    if (rem && lane < rem) J.moves[k - rem + lane] = (uint8_t)mvbuf;
-    if (lane == 0) { *J.nmoves = k; J.end_ij[0] = i; J.end_ij[1] = j; }
+    const int rem = nrec & 63;
+    if (rem && lane < rem) recs[nrec - rem + lane] = recbuf;
+    if (lane == 0) { *J.nrecs = nrec; J.end_ij[0] = i; J.end_ij[1] = j; }
 }
 
 // Export: strip-major anti-diagonal planes -> row-major (n+1) x (m+1) int32
