@@ -130,6 +130,27 @@ def load_traffic(workload: str):
     return None, None
 
 
+def rank_pairs(rank: int, pairs_per_rank: int, length: int):
+    """Weak-scaling shard: rank r aligns synthetic pairs r*P .. r*P+P-1 (no
+    data-path collective; every rank generates its own inputs)."""
+    return [synth_pair(rank * pairs_per_rank + p, length) for p in range(pairs_per_rank)]
+
+
+def combine_over_ranks(dist, elapsed: float, rows, device: str):
+    """Max-over-ranks time and all-gather of per-pair (score, steps, matches)
+    rows.  `dist` is torch.distributed (RCCL on the GPU box, gloo in tests) or
+    None for a single process."""
+    if dist is None:
+        return elapsed, [list(map(tuple, rows))]
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    mine = torch.tensor(rows, dtype=torch.int64, device=device).reshape(-1, 3)
+    gathered = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(gathered, mine)
+    return float(t.item()), [[tuple(int(x) for x in r) for r in g.cpu().tolist()] for g in gathered]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,7 +178,7 @@ def main():
     import gxamd as gx
     ctx = gx.Context(local_rank)
     P, L = args.pairs_per_gpu, args.length
-    pairs = [synth_pair(rank * P + p, L) for p in range(P)]
+    pairs = rank_pairs(rank, P, L)
     staged = gx.StagedPairs(pairs, ctx=ctx)             # inputs resident in HBM
     scores = gx.Scores(*SCORES)
     keep_planes = not args.no_planes
@@ -189,14 +210,7 @@ def main():
     elapsed = time.perf_counter() - t0
 
     # max over ranks (time) and gather of per-pair results, over RCCL
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        mine = torch.tensor([[r.score, r.n_steps, r.matches] for r in res], dtype=torch.int64, device="cuda")
-        gathered = [torch.zeros_like(mine) for _ in range(world)]
-        dist.all_gather(gathered, mine)
+    elapsed, _gathered = combine_over_ranks(dist, elapsed, [[r.score, r.n_steps, r.matches] for r in res], "cuda")
     total_cells = cells_rank * world
     ms_per_step = elapsed / args.steps * 1e3
     gcups = total_cells * args.steps / elapsed / 1e9
