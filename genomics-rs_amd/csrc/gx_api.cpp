@@ -569,6 +569,8 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
         }
         out.end_i[p] = c[4 * p + 1];
         out.end_j[p] = c[4 * p + 2];
+        if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug") && p == 0)
+            fprintf(stderr, "[gx DEBUG] traceback pair 0: %d row records, %d fixed-point rounds\n", k, c[4 * p + 3]);
     }
     return GX_OK;
 }

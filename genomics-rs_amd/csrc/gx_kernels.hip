@@ -627,31 +627,34 @@ __global__ void finalize_kernel(const PairDev* __restrict__ pairs, const StripRe
 // Traceback walk over the direction codes (algo.rs:339-422), interior cells
 // only; the host finishes the boundary part and labels the moves.
 //
-// The walk is done a ROW at a time: on row i the path is a run of insert
-// moves (j-1) that ends at the nearest cell to the left whose code is not
-// "insert", followed by one sub (i-1, j-1) or delete (i-1, j) move.  Cells of
-// one row are consecutive steps of one lane's code words, so the run is a
-// bit-scan of the "not insert" mask (D | ~I) -- O(1) per word, not per move.
-// Output: one record per row, (run << 2) | kind, kind 0 = sub, 2 = delete,
-// 1 = the run reached column 0 (walk ends at (i, 0)).
+// Row view of the walk: on row i the path is a run of insert moves (j-1)
+// that ends at the nearest cell to the left whose code is not "insert",
+// followed by one sub (i-1, j-1) or delete (i-1, j) move.  The cells of one
+// row are consecutive steps of one lane's code words, so a row is a bit-scan
+// of the "not insert" mask D | ~I.  Output: one record per row,
+// (run << 2) | kind, kind 0 = sub, 2 = delete, 1 = the run reached column 0.
 //
-// One wave per pair, walk state wave-uniform.  The code window of the current
-// strip (kTbWin words = 256 steps of every lane) sits in VGPRs and is read
-// with readlane.  The window of the strip above is prefetched by LDS-DMA
-// (global_load_lds) while this one is walked -- no VGPR has a load in flight
-// during the walk, so the dynamically indexed reads never wait on it.  The
-// path's step index only decreases inside a strip, and it enters the strip
-// above at lane 63 no further right than the current column.
-constexpr int kTbWin = 16;
+// Lane-parallel fixed point, one wave per pair and one strip (64 rows) at a
+// time: lane k guesses the column at which the path enters its row (first
+// guess: the diagonal from the strip's entry), every lane scans its own row
+// at once, and each lane's next guess becomes the exit column of the lane
+// above (DPP wave_shl:1).  The top lane's entry is known, so after round r the
+// top r lanes are exact; in practice paths started from wrong columns merge
+// with the true path within a few rows, so the iteration reaches the fixed
+// point -- which IS the sequential walk -- in far fewer than 64 rounds.
+// The strip's code window (kTbWin words = 512 steps of every lane) is read
+// from LDS, filled by LDS-DMA (global_load_lds) while the previous strip was
+// walked; words below the window are read from HBM.
+constexpr int kTbWin = 32;
 
-// (readfirstlane: keeps the walk state provably uniform, so the window index
-// is an SGPR and the indexed VGPR read needs no waterfall loop)
 __device__ __forceinline__ int tb_q0(int t) {
     return __builtin_amdgcn_readfirstlane(max((t >> 4) - (kTbWin - 1), 0));
 }
 
 typedef __attribute__((address_space(1))) const void gcvoid;
 typedef __attribute__((address_space(3))) void lvoid;
+typedef __attribute__((address_space(3))) const uint32_t lu32;
+typedef __attribute__((address_space(1))) const uint32_t gcu32;
 
 // async: words q0 .. q0+kTbWin-1 of strip s, all lanes -> buf[k][lane]
 __device__ __forceinline__ void tb_prefetch(uint32_t* buf, const TbDev& J, int s, int q0, int lane) {
@@ -662,103 +665,92 @@ __device__ __forceinline__ void tb_prefetch(uint32_t* buf, const TbDev& J, int s
             __builtin_amdgcn_global_load_lds((gcvoid*)(base + (size_t)k * kWave), (lvoid*)(buf + k * kWave), 4, 0, 0);
 }
 
-__device__ __forceinline__ void tb_take(uint32_t (&w)[kTbWin], const uint32_t* buf, int lane) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the LDS-DMA writes have landed
-    typedef __attribute__((address_space(3))) const uint32_t lu32;
-    const lu32* b = (const lu32*)(uintptr_t)lds_addr(buf);
-#pragma unroll
-    for (int k = 0; k < kTbWin; ++k) w[k] = b[k * kWave + lane];
-}
-
 __global__ __launch_bounds__(64) void traceback_kernel(const TbDev* __restrict__ jobs) {
     __shared__ uint32_t tbuf[2][kTbWin * kWave];
     const TbDev J = jobs[blockIdx.x];
     const int lane = threadIdx.x;
     int i = J.start_i, j = J.start_j;
-    int nrec = 0;
-    uint32_t recbuf = 0;
+    int nrec = 0, rounds = 0;
     guint* const recs = (guint*)J.recs;
+    gcu32* const codes = (gcu32*)J.codes;
     if (i >= 1 && j >= 1) {
+        int s = __builtin_amdgcn_readfirstlane((i - 1) >> 6);
+        int R = __builtin_amdgcn_readfirstlane((i - 1) & 63);   // path's top lane in this strip
+        int ce = __builtin_amdgcn_readfirstlane(j);              // its entry column
         int cb = 0;
-        int s = (i - 1) >> 6;
-        int q0 = tb_q0(j - 1 + ((i - 1) & 63));
+        int q0 = tb_q0(ce - 1 + R);
         tb_prefetch(tbuf[cb], J, s, q0, lane);
-        int qn = tb_q0(j - 1 + (kWave - 1));   // window of the strip above, for an entry at lane 63
-        bool want_next = s > 0;
-        bool done = false;
-        bool resume = false;                   // continue a run scan after a reload
-        int t_in = 0, t = 0;
-        // outer loop: one window (a strip, or a reload lower in the same strip);
-        // `cur` is written only here, so the row loop keeps it in place
-        while (!done) {
-            uint32_t cur[kTbWin];
-            tb_take(cur, tbuf[cb], lane);
-            if (want_next) {                   // after the take: its wait must not cover this prefetch
-                tb_prefetch(tbuf[cb ^ 1], J, s - 1, qn, lane);
-                want_next = false;
-            }
+        for (;;) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this strip's window has landed
+            const lu32* win = (const lu32*)(uintptr_t)lds_addr(tbuf[cb]);
+            // the strip above is entered at lane 63, no further right than column ce
+            const int qn = tb_q0(ce - 1 + (kWave - 1));
+            if (s > 0) tb_prefetch(tbuf[cb ^ 1], J, s - 1, qn, lane);
+            const size_t strip_w = (size_t)s * J.t16;
+            const bool act = lane <= R;
+            int g = ce - (R - lane);           // diagonal guess of this row's entry column
+            int rec = 0, nj = 0;
+            bool end = true, run_end = false;
+            bool changed = act;
             for (;;) {
-                const int l = (i - 1) & 63;
-                if (!resume) { t_in = j - 1 + l; t = t_in; }
-                resume = false;
-                int tf = -1;           // step of the nearest non-insert cell (column >= 1), if any
-                uint32_t w = 0;
-                bool reload = false;
-                while (t >= l) {
-                    const int qq = t >> 4;
-                    if (qq < q0) { reload = true; break; }   // the run left the window (rare)
-                    w = __builtin_amdgcn_readlane(cur[__builtin_amdgcn_readfirstlane(qq - q0)], l);
-                    const int k = t & 15;
-                    // bit 15-k: "insert beats sub"; bit 31-k: "delete beats both" (step 16q + k)
-                    const uint32_t nonI = ((w >> 16) | ~w) & ((0xFFFFu << (15 - k)) & 0xFFFFu);
-                    if (nonI) {
-                        tf = (t & ~15) + (15 - __builtin_ctz(nonI));
-                        break;
+                if (changed) {                 // re-scan only rows whose entry moved
+                    end = true; run_end = false; nj = 0; rec = 0;
+                    if (g >= 1) {
+                        const int t_in = g - 1 + lane;
+                        int t = t_in, tf = -1;
+                        uint32_t w = 0;
+                        while (t >= lane) {
+                            const int q = t >> 4;
+                            w = q >= q0 ? win[(q - q0) * kWave + lane] : codes[(strip_w + q) * kWave + lane];
+                            // bit 15-k: "insert beats sub"; bit 31-k: "delete beats both" (step 16q + k)
+                            const uint32_t nonI = ((w >> 16) | ~w) & ((0xFFFFu << (15 - (t & 15))) & 0xFFFFu);
+                            if (nonI) {
+                                tf = (t & ~15) + (15 - __builtin_ctz(nonI));
+                                break;
+                            }
+                            t = (t & ~15) - 1;
+                        }
+                        if (tf < lane) {       // (i, g..1) all insert: the walk leaves at (i, 0)
+                            rec = (g << 2) | 1;
+                            run_end = true;
+                        } else {
+                            const bool del = (w >> (31 - (tf & 15))) & 1u;
+                            rec = ((t_in - tf) << 2) | (del ? 2 : 0);
+                            nj = tf - lane + 1 - (del ? 0 : 1);
+                            end = nj < 1 || (s == 0 && lane == 0);   // next cell (i-1, nj) off the interior
+                        }
                     }
-                    t = (t & ~15) - 1;
                 }
-                if (reload) {          // window [.., t]: the scan resumes at t
-                    q0 = tb_q0(t);
-                    tb_prefetch(tbuf[cb], J, s, q0, lane);
-                    resume = true;
-                    break;
-                }
-                uint32_t rec;
-                if (tf < l) {          // all of (i, j..1) insert: the walk leaves at (i, 0)
-                    rec = ((uint32_t)j << 2) | 1u;
-                    j = 0;
-                    done = true;
-                } else {
-                    const bool del = (w >> (31 - (tf & 15))) & 1u;
-                    rec = ((uint32_t)(t_in - tf) << 2) | (del ? 2u : 0u);
-                    j = tf - l + 1 - (del ? 0 : 1);
-                    i -= 1;
-                    done = i < 1 || j < 1;
-                }
-                if (lane == (nrec & 63)) recbuf = rec;
-                ++nrec;
-                if ((nrec & 63) == 0) recs[nrec - 64 + lane] = recbuf;
-                if (done) break;
-                if (l == 0) {          // into the strip above, at lane 63
-                    s -= 1;
-                    cb ^= 1;
-                    const int te = j - 1 + (kWave - 1);
-                    if ((te >> 4) >= qn && (te >> 4) < qn + kTbWin) {
-                        q0 = qn;
-                    } else {           // entered left of the prefetched window
-                        q0 = tb_q0(te);
-                        tb_prefetch(tbuf[cb], J, s, q0, lane);
-                    }
-                    qn = tb_q0(te);
-                    want_next = s > 0;
-                    break;
-                }
+                // next guess: the exit column of the lane above; the top lane's entry is fixed
+                const int prop = end ? 0 : nj;
+                int gn = __builtin_amdgcn_update_dpp(0, prop, 0x130 /* wave_shl:1 */, 0xF, 0xF, false);
+                gn = lane == R ? ce : gn;
+                changed = act && gn != g;
+                ++rounds;
+                if (__builtin_amdgcn_ballot_w64(changed) == 0) break;
+                g = gn;
             }
+            // the path covers lanes R down to the first lane (from the top) where it ends
+            const unsigned long long em = __builtin_amdgcn_ballot_w64(act && end);
+            const int E = em ? 63 - __builtin_clzll(em) : -1;
+            const int lo = E >= 0 ? E : 0;
+            if (act && lane >= lo) recs[nrec + (R - lane)] = (uint32_t)rec;
+            nrec += R - lo + 1;
+            if (E >= 0) {                      // the walk leaves the interior in this strip
+                const bool re = __builtin_amdgcn_readlane((int)run_end, E) != 0;
+                const int jE = __builtin_amdgcn_readlane(nj, E);
+                if (re) { i = s * kWave + E + 1; j = 0; }
+                else { i = s * kWave + E; j = jE; }
+                break;
+            }
+            ce = __builtin_amdgcn_readlane(nj, 0);
+            s -= 1;
+            R = kWave - 1;
+            cb ^= 1;
+            q0 = qn;
         }
     }
-    const int rem = nrec & 63;
-    if (rem && lane < rem) recs[nrec - rem + lane] = recbuf;
-    if (lane == 0) { *J.nrecs = nrec; J.end_ij[0] = i; J.end_ij[1] = j; }
+    if (lane == 0) { *J.nrecs = nrec; J.end_ij[0] = i; J.end_ij[1] = j; J.end_ij[2] = rounds; }
 }
 
 // Export: strip-major anti-diagonal planes -> row-major (n+1) x (m+1) int32
