@@ -293,7 +293,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         const int n = (int)ph[p].n, m = (int)ph[p].m;
         PairDev& d = job.pd[p];
         d.n = n; d.m = m;
-        d.strips = ceil_div(n, kWave);
+        d.strips = ceil_div(n, kStripRows);
         d.bands = ceil_div(d.strips, W);
         const int T = m + kWave;   // steps per strip (lane 63 pushes column m at step m + 63)
         d.t16 = ceil_div(T, 16);
@@ -305,8 +305,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         strips += d.strips;
         c1o[p] = chars_bytes; chars_bytes += align_up(n, 64);
         c2o[p] = chars_bytes; chars_bytes += align_up(m, 64);
-        po[p] = plane_elems; plane_elems += (size_t)d.strips * d.t4 * kWave * 4;
-        co[p] = code_elems; code_elems += (size_t)d.strips * d.t16 * kWave;
+        po[p] = plane_elems; plane_elems += (size_t)d.strips * d.t4 * kGroupInts;
+        co[p] = code_elems; code_elems += (size_t)d.strips * d.t16 * kStripRows;
         fo[p] = feed_recs; feed_recs += (size_t)std::max(d.bands - 1, 0) * d.feed_stride;
         gofs[p] = prog_elems; prog_elems += (size_t)std::max(d.bands - 1, 0);
     }

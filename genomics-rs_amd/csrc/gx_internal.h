@@ -1,18 +1,20 @@
 // gx_internal.h -- structures shared by the HIP kernels and the C++ host code.
 //
 // Device data layout (DESIGN.md "HBM layout"):
-//   A pair (s1: n rows, s2: m columns) is cut into STRIPS of 64 interior rows
-//   (strip k = rows 64k+1 .. 64k+64, lane l = row 64k+l+1).  One wave sweeps a
-//   strip along the anti-diagonal skew: at step t lane l computes column
-//   j = t - l + 1, so a strip takes T = m + 63 steps.  WAVES_PER_BAND strips
-//   form a BAND, processed by one workgroup (one wave per strip + one I/O wave).
+//   A pair (s1: n rows, s2: m columns) is cut into STRIPS of 128 interior rows
+//   (strip k = rows 128k+1 .. 128k+128; lane l owns rows 128k+2l+1 and
+//   128k+2l+2, "row-in-lane" h = 0, 1).  One wave sweeps a strip along the
+//   anti-diagonal skew: at step t lane l computes column j = t - l + 1 for both
+//   its rows, so a strip takes T = m + 64 steps.  kBandWaves strips form a
+//   BAND, processed by one workgroup (one wave per strip + one I/O wave).
 //
 //   Score planes (int32, one each for insert/delete/sub score):
-//       plane[strip][t/4][lane][t%4]        (16 B per lane per 4 steps)
-//   so each wave stores 1 KiB contiguous per plane every 4 steps.
+//       plane[strip][t/4][h][lane][t%4]     (16 B per lane per row per 4 steps)
+//   so each wave stores 1 KiB contiguous per plane and row every 4 steps.
 //   Traceback direction codes (2 bit/cell), two bit-planes per word:
-//       codes[strip][t/16][lane]  (uint32; for k = t%16 bit 31-k = "delete beats
-//       insert and sub", bit 15-k = "insert beats sub"; decode D ? 2 : I ? 1 : 0)
+//       codes[strip][t/16][row-in-strip]  (row-in-strip = 2l + h; uint32; for
+//       k = t%16 bit 31-k = "delete beats insert and sub", bit 15-k = "insert
+//       beats sub"; decode D ? 2 : I ? 1 : 0)
 #pragma once
 #include <stdint.h>
 
@@ -23,6 +25,11 @@ constexpr int kNeg = -(1 << 30);   // int32 stand-in for negative_inf (algo.rs:1
 constexpr int kRing = 256;         // LDS ring records per strip boundary (power of two)
 constexpr int kSub = 16;           // steps per flow-control sub-block (multiple of 16)
 constexpr int kIoChunk = 16;       // columns per I/O-wave transfer
+constexpr int kRowsPerLane = 2;    // a lane owns rows 2l+1, 2l+2 of its strip
+constexpr int kStripRows = kWave * kRowsPerLane;   // 128 rows per strip
+// Plane layout (ints): plane[strip][t/4][row-in-lane][lane][t%4]; one 4-step
+// group of one row is 1 KiB contiguous per wave.
+constexpr int kGroupInts = kRowsPerLane * kWave * 4;
 // Compute waves per band (workgroup = kBandWaves compute waves + 1 I/O wave).
 #ifndef GX_BAND_WAVES
 #define GX_BAND_WAVES 7

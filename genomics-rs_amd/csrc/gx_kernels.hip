@@ -116,18 +116,23 @@ __device__ __forceinline__ void gstore4_at(int32_t* base, uint32_t byte_off, int
 #define GX_FILL_MIN_WAVES 4
 #endif
 
-// Per-lane DP state of row i = 64*strip + lane + 1 (the cell left of the one
-// being computed, i.e. (i, j-1) in the reference's "top" naming, algo.rs:225).
+// DP state of one row (the cell left of the one being computed, i.e. (i, j-1)
+// in the reference's "top" naming, algo.rs:225).  A lane owns two rows of its
+// strip: A = 128*strip + 2*lane + 1 and B = A + 1 (kRowsPerLane).
+struct RowState {
+    int I, SD, Dd, SM, SMtl;   // insert, max(sub, delete), delete-successor, score_max, SM(i-1, j-1)
+    int L, Ltl;                // LCS field (TRACK only)
+    int best, bstep, bl;       // first strict max of the row (TRACK only)
+    int lbest, lstep;          // last max of the row (LOCAL only)
+    uint32_t cI, cD;           // traceback code bit-planes (16 steps each)
+};
 struct LaneState {
-    int I, SD, Dd, SM, c2c, SMtl;   // insert, max(sub, delete), delete-successor, score_max, s2[j-1], SM(i-1, j-1)
-    int L, Ltl;                     // LCS field (TRACK only)
-    int best, bstep, bl;            // first strict max of the row (TRACK only)
-    int lbest, lstep;               // last max of the row (LOCAL only)
-    uint32_t cI, cD;                // traceback code bit-planes (16 steps each)
+    RowState a, b;
+    int c2c;                   // s2[j-1] of the lane's current column
 };
 
-// Lane 63 pushes its cell (the strip's bottom row) into the LDS ring of the
-// wave below, under a lane-63 exec mask (no branch, no register tuple).
+// Lane 63 pushes its row-B cell (the strip's bottom row) into the LDS ring of
+// the wave below, under a lane-63 exec mask (no branch, no register tuple).
 // Record = {dd, sm, c2, l}; without TRACK the l word is not written.  Compute
 // waves run with all 64 lanes active, so exec is restored to -1, not saved.
 // U = step within the 16-step sub-block (the ring slot's constant offset).
@@ -140,8 +145,8 @@ __device__ __forceinline__ void push63(uint32_t base, const LaneState& st, unsig
             "ds_write2_b32 %1, %4, %5 offset0:%8 offset1:%9\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(base), "v"(st.Dd), "v"(st.SM), "v"(st.c2c), "v"(st.L), "i"(4 * U), "i"(4 * U + 1),
-              "i"(4 * U + 2), "i"(4 * U + 3));
+            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L), "i"(4 * U),
+              "i"(4 * U + 1), "i"(4 * U + 2), "i"(4 * U + 3));
     else
         asm volatile(
             "s_mov_b64 exec, %0\n\t"
@@ -149,7 +154,7 @@ __device__ __forceinline__ void push63(uint32_t base, const LaneState& st, unsig
             "ds_write_b32 %1, %4 offset:%7\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(base), "v"(st.Dd), "v"(st.SM), "v"(st.c2c), "i"(4 * U), "i"(4 * U + 1),
+            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "i"(4 * U), "i"(4 * U + 1),
               "i"(16 * U + 8));
 }
 
@@ -167,7 +172,7 @@ __device__ __forceinline__ void push63_pub(uint32_t base, const LaneState& st, u
             "ds_write_b32 %6, %7\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(base), "v"(st.Dd), "v"(st.SM), "v"(st.c2c), "v"(st.L), "v"(cnt_addr), "v"(cnt),
+            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L), "v"(cnt_addr), "v"(cnt),
               "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2), "i"(4 * U + 3)
             : "memory");
     else
@@ -178,7 +183,7 @@ __device__ __forceinline__ void push63_pub(uint32_t base, const LaneState& st, u
             "ds_write_b32 %5, %6\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(base), "v"(st.Dd), "v"(st.SM), "v"(st.c2c), "v"(cnt_addr), "v"(cnt), "i"(4 * U),
+            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(cnt_addr), "v"(cnt), "i"(4 * U),
               "i"(4 * U + 1), "i"(16 * U + 8)
             : "memory");
 }
@@ -199,7 +204,7 @@ __device__ __forceinline__ void push63_rt(uint32_t addr, const LaneState& st, un
             "ds_write2_b32 %1, %4, %5 offset0:2 offset1:3\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(addr), "v"(st.Dd), "v"(st.SM), "v"(st.c2c), "v"(st.L));
+            : "s"(m63), "v"(addr), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L));
     else
         asm volatile(
             "s_mov_b64 exec, %0\n\t"
@@ -207,7 +212,7 @@ __device__ __forceinline__ void push63_rt(uint32_t addr, const LaneState& st, un
             "ds_write_b32 %1, %4 offset:8\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(addr), "v"(st.Dd), "v"(st.SM), "v"(st.c2c));
+            : "s"(m63), "v"(addr), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c));
 }
 
 // One lane stores an LDS counter (exec = lane 0 only, no branch).
@@ -221,34 +226,27 @@ __device__ __forceinline__ void lds_store_lane0(lds_int* p, int v) {
         : "memory");
 }
 
-// One anti-diagonal step of a compute wave (algo.rs:222-268 for every lane's
-// cell).  MASKED: some lanes are outside columns 1..m this step (ramp-up /
-// ramp-down of the skew); their state is left unchanged.
+// One cell of the Gotoh recurrence (algo.rs:222-268) for the row in `st`,
+// given the cell above (dd_in = its delete-successor = D(i, j), sm_in =
+// score_max(i-1, j), l_in = max_matches(i-1, j)) and s2[j-1].  act = false
+// leaves the row unchanged (ramp lanes outside columns 1..m).
 template <bool LOCAL, bool MASKED, bool CODES, bool TRACK>
-__device__ __forceinline__ void dp_step(LaneState& st, const Rec& r, const int t, const int lane, const int m,
-                                        const int c1v, const Scores32& sc, int& oI, int& oD, int& oS, int& oL) {
-    // row above (i-1, j): lane 0 from the ring record, others from lane-1 (wave_shr:1)
-    const int dd_in = shr1(r.dd, st.Dd);   // == D(i, j): the delete score of the new cell
-    const int sm_in = shr1(r.sm, st.SM);   // score_max(i-1, j)
-    const int c2 = shr1(r.c2, st.c2c);     // s2[j-1]
+__device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm_in, const int l_in, const int c2,
+                                     const int c1v, const bool act, const int t, const Scores32& sc, int& oI,
+                                     int& oD, int& oS, int& oL) {
     // algo.rs:231-236  insert_score = top.score_max(g, h+g, h+g)
     const int In = LOCAL ? max3i(st.I + sc.g, st.SD + sc.hg, 0) : max(st.I + sc.g, st.SD + sc.hg);
     const bool mt = c2 == c1v;             // sequence.rs:113-114
     // algo.rs:245-248  sub_score = s_(mis)match + top_left.score_max(0,0,0)
     const int Sn = st.SMtl + (mt ? sc.sm : sc.smm);
-    const int Dn = dd_in;                  // algo.rs:238-243 (computed by the lane above)
+    const int Dn = dd_in;                  // algo.rs:238-243 (computed by the row above)
     const int IS = max(In, Sn);
     const int SMn = max(IS, Dn);           // cell.score_max(0,0,0); >= floor since In >= floor
     const int SDn = max(Sn, Dn);
     // delete-successor, i.e. D(i+1, j) = this.score_max(hg, g, hg) (algo.rs:238-243)
     const int Ddn = LOCAL ? max3i(IS + sc.hg, Dn + sc.g, 0) : max(IS + sc.hg, Dn + sc.g);
-    int Ln = 0, l_in = 0;
-    if (TRACK) {
-        l_in = shr1(r.l, st.L);            // max_matches(i-1, j)
-        Ln = max3i(st.L, l_in, st.Ltl + (mt ? 1 : 0));   // algo.rs:250-255
-    }
-    bool act = true;
-    if (MASKED) act = (unsigned)(t - lane) < (unsigned)m;
+    int Ln = 0;
+    if (TRACK) Ln = max3i(st.L, l_in, st.Ltl + (mt ? 1 : 0));   // algo.rs:250-255
     if (MASKED) {
         st.I = act ? In : st.I; st.SD = act ? SDn : st.SD; st.Dd = act ? Ddn : st.Dd; st.SM = act ? SMn : st.SM;
         if (TRACK) st.L = act ? Ln : st.L;
@@ -256,7 +254,7 @@ __device__ __forceinline__ void dp_step(LaneState& st, const Rec& r, const int t
         st.I = In; st.SD = SDn; st.Dd = Ddn; st.SM = SMn;
         if (TRACK) st.L = Ln;
     }
-    st.SMtl = sm_in; st.c2c = c2;
+    st.SMtl = sm_in;
     if (TRACK) {
         st.Ltl = l_in;
         // algo.rs:258-262: first strict maximum in row-major order
@@ -274,10 +272,30 @@ __device__ __forceinline__ void dp_step(LaneState& st, const Rec& r, const int t
         // The bit is the sign of a difference (|values| < 2^29 under the host's
         // range guard), shifted in with v_alignbit: no compare masks, which the
         // compiler would otherwise park in SGPR pairs across the sub-block.
-        st.cD = __builtin_amdgcn_alignbit(st.cD, (uint32_t)(IS - Dn), 31);   // Dn > IS
-        st.cI = __builtin_amdgcn_alignbit(st.cI, (uint32_t)(Sn - In), 31);   // In > Sn
+        // (volatile asm: otherwise LLVM sinks the chain to the store at the end of
+        // the sub-block and keeps 16 steps of IS/Dn/Sn/In alive -> VGPR spills)
+        asm volatile("v_alignbit_b32 %0, %0, %1, 31" : "+v"(st.cD) : "v"((uint32_t)(IS - Dn)));   // Dn > IS
+        asm volatile("v_alignbit_b32 %0, %0, %1, 31" : "+v"(st.cI) : "v"((uint32_t)(Sn - In)));   // In > Sn
     }
     oI = In; oD = Dn; oS = Sn; oL = Ln;
+}
+
+// One anti-diagonal step of a compute wave: both rows of every lane at
+// column j = t - lane + 1.  Row A's cell above comes from row B of lane-1
+// (wave_shr:1; lane 0 from the ring record r), row B's from row A.
+template <bool LOCAL, bool MASKED, bool CODES, bool TRACK>
+__device__ __forceinline__ void dp_step(LaneState& st, const Rec& r, const int t, const int lane, const int m,
+                                        const int c1a, const int c1b, const Scores32& sc, int (&oI)[2],
+                                        int (&oD)[2], int (&oS)[2], int (&oL)[2]) {
+    const int dd_in = shr1(r.dd, st.b.Dd);
+    const int sm_in = shr1(r.sm, st.b.SM);
+    const int c2 = shr1(r.c2, st.c2c);
+    const int l_in = TRACK ? shr1(r.l, st.b.L) : 0;
+    const bool act = MASKED ? (unsigned)(t - lane) < (unsigned)m : true;
+    cell<LOCAL, MASKED, CODES, TRACK>(st.a, dd_in, sm_in, l_in, c2, c1a, act, t, sc, oI[0], oD[0], oS[0], oL[0]);
+    cell<LOCAL, MASKED, CODES, TRACK>(st.b, st.a.Dd, st.a.SM, st.a.L, c2, c1b, act, t, sc, oI[1], oD[1], oS[1],
+                                      oL[1]);
+    st.c2c = c2;
 }
 
 // The ring pointers are deliberately NOT __restrict__: another wave writes the
@@ -297,7 +315,7 @@ struct WaveCtx {
     lds_int* wcnt_in;
     lds_int* wcnt_out;
     int* status;
-    int m, lane, c1v;
+    int m, lane, c1a, c1b;
     unsigned tr_win;
 };
 
@@ -316,29 +334,34 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
     const int seen_v = *w.wcnt_in;                            // consumed only at the end of the group
     asm volatile("" ::: "memory");
     read4(nxt, w.ring_in + ring_slot(t + 5));
-    int bI[4], bD[4], bS[4], bL[4];
+    int bI[4][2], bD[4][2], bS[4][2], bL[4][2];
     // lane 63 holds column t+U-63 before step U: push it (m63 = 0 when there is
     // no consumer); the last push of the group also publishes the counter
     push63<4 * G4 + 0, TRACK>(out_base, st, m63);
-    dp_step<LOCAL, false, CODES, TRACK>(st, cur[0], t + 0, w.lane, w.m, w.c1v, sc, bI[0], bD[0], bS[0], bL[0]);
+    dp_step<LOCAL, false, CODES, TRACK>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
     push63<4 * G4 + 1, TRACK>(out_base, st, m63);
-    dp_step<LOCAL, false, CODES, TRACK>(st, cur[1], t + 1, w.lane, w.m, w.c1v, sc, bI[1], bD[1], bS[1], bL[1]);
+    dp_step<LOCAL, false, CODES, TRACK>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
     push63<4 * G4 + 2, TRACK>(out_base, st, m63);
-    dp_step<LOCAL, false, CODES, TRACK>(st, cur[2], t + 2, w.lane, w.m, w.c1v, sc, bI[2], bD[2], bS[2], bL[2]);
+    dp_step<LOCAL, false, CODES, TRACK>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
     push63_pub<4 * G4 + 3, TRACK>(out_base, st, m63, lds_addr((const void*)w.wcnt_out), t + 3 - (kWave - 1) + 1);
-    dp_step<LOCAL, false, CODES, TRACK>(st, cur[3], t + 3, w.lane, w.m, w.c1v, sc, bI[3], bD[3], bS[3], bL[3]);
+    dp_step<LOCAL, false, CODES, TRACK>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, sc, bI[3], bD[3], bS[3], bL[3]);
     if (PLANES) {
-        // 16 B per lane, 1 KiB per wave: base (uniform) + lane*16 B + G4 KiB immediate
-        const uint32_t o = (uint32_t)w.lane * 16u + G4 * kWave * 16;
-        gstore4_at(w.pI + sb_off, o, make_int4(bI[0], bI[1], bI[2], bI[3]));
-        gstore4_at(w.pD + sb_off, o, make_int4(bD[0], bD[1], bD[2], bD[3]));
-        gstore4_at(w.pS + sb_off, o, make_int4(bS[0], bS[1], bS[2], bS[3]));
-        if (LCSP) gstore4_at(w.pL + sb_off, o, make_int4(bL[0], bL[1], bL[2], bL[3]));
+        // per row: 16 B per lane, 1 KiB per wave; base (uniform) + lane*16 B + immediate
+#pragma unroll
+        for (int h = 0; h < kRowsPerLane; ++h) {
+            const uint32_t o = (uint32_t)w.lane * 16u + (uint32_t)(G4 * kGroupInts + h * kWave * 4) * 4u;
+            gstore4_at(w.pI + sb_off, o, make_int4(bI[0][h], bI[1][h], bI[2][h], bI[3][h]));
+            gstore4_at(w.pD + sb_off, o, make_int4(bD[0][h], bD[1][h], bD[2][h], bD[3][h]));
+            gstore4_at(w.pS + sb_off, o, make_int4(bS[0][h], bS[1][h], bS[2][h], bS[3][h]));
+            if (LCSP) gstore4_at(w.pL + sb_off, o, make_int4(bL[0][h], bL[1][h], bL[2][h], bL[3][h]));
+        }
     }
     if (__builtin_amdgcn_readfirstlane(seen_v) < need) {      // producer was behind: wait, re-read
         w.tr_win += wait_ge(w.wcnt_in, need, w.status);
         read4(nxt, w.ring_in + ring_slot(t + 5));
     }
+    // keep groups apart: interleaving two groups' outputs overflows the VGPR budget
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // Ramp-up / ramp-down sub-block (some lanes outside columns 1..m): a rolled
@@ -347,7 +370,7 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
 // of the next sub-block.
 template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP>
 __device__ __forceinline__ void ramp_block(LaneState& st, Rec (&nxt)[4], WaveCtx& w, const Scores32& sc, const int t0,
-                                        const bool has_consumer, const size_t sb_off) {
+                                           const bool has_consumer, const size_t sb_off) {
     const int m = w.m;
     w.tr_win += wait_ge(w.wcnt_in, min(t0 + kSub, m) + 1, w.status);
 #pragma unroll 1
@@ -359,14 +382,17 @@ __device__ __forceinline__ void ramp_block(LaneState& st, Rec (&nxt)[4], WaveCtx
         const int col = t - (kWave - 1);
         const unsigned long long mk = lane63_mask(has_consumer && col >= 0 && col <= m);
         push63_rt<TRACK>(lds_addr(w.ring_out + ring_slot(col)), st, mk);
-        int oI, oD, oS, oL;
-        dp_step<LOCAL, true, CODES, TRACK>(st, r, t, w.lane, m, w.c1v, sc, oI, oD, oS, oL);
+        int oI[2], oD[2], oS[2], oL[2];
+        dp_step<LOCAL, true, CODES, TRACK>(st, r, t, w.lane, m, w.c1a, w.c1b, sc, oI, oD, oS, oL);
         if (PLANES) {
-            const size_t o = sb_off + (size_t)w.lane * 4 + (u >> 2) * (kWave * 4) + (u & 3);
-            ((gint*)w.pI)[o] = oI;
-            ((gint*)w.pD)[o] = oD;
-            ((gint*)w.pS)[o] = oS;
-            if (LCSP) ((gint*)w.pL)[o] = oL;
+#pragma unroll
+            for (int h = 0; h < kRowsPerLane; ++h) {
+                const size_t o = sb_off + (size_t)(u >> 2) * kGroupInts + h * kWave * 4 + (size_t)w.lane * 4 + (u & 3);
+                ((gint*)w.pI)[o] = oI[h];
+                ((gint*)w.pD)[o] = oD[h];
+                ((gint*)w.pS)[o] = oS[h];
+                if (LCSP) ((gint*)w.pL)[o] = oL[h];
+            }
         }
     }
     const int last_col = min(t0 + kSub - 1 - (kWave - 1), m);
@@ -384,45 +410,54 @@ __device__ __forceinline__ void sub_block(LaneState& st, Rec (&nxt)[4], WaveCtx&
     group4<LOCAL, PLANES, CODES, TRACK, LCSP, 3>(st, nxt, w, sc, t0, out_base, m63, sb_off);
 }
 
+__device__ __forceinline__ void init_row(RowState& rs, const int i, const bool row_ok, const Scores32& sc) {
+    // cell (i, 0): algo.rs:204-211
+    const int D0 = sc.h + i * sc.g;
+    rs.I = kNeg;
+    rs.SD = D0;                                   // max(sub=neg_inf, delete)
+    rs.SM = max(D0, sc.floor_);
+    rs.Dd = max3i(kNeg + sc.hg, D0 + sc.g, sc.floor_);
+    rs.L = 0; rs.Ltl = 0;
+    rs.SMtl = 0;
+    rs.best = row_ok ? INT_MIN : INT_MAX; rs.bstep = 0; rs.bl = 0;
+    rs.lbest = row_ok ? INT_MIN : INT_MAX; rs.lstep = 0;
+    rs.cI = 0; rs.cD = 0;
+}
+
 template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP>
 __device__ void compute_wave(const PairDev& P, const int s, const int lane, const Scores32& sc, const Rec* ring_in,
                              Rec* ring_out, lds_int* wcnt_in, lds_int* rcnt_in, lds_int* wcnt_out, lds_int* rcnt_out,
                              const bool has_consumer, StripRes* sres, PairRes* pres, int* status) {
     static_assert(kSub == 16, "16-step sub-blocks (code words, ring alignment)");
+    static_assert(kRowsPerLane == 2, "two rows per lane");
     const int n = P.n, m = P.m;
-    const int i = s * kWave + lane + 1;
-    const bool row_ok = i <= n;
+    const int ia = s * kStripRows + kRowsPerLane * lane + 1;   // row A; row B = ia + 1
+    const bool ok_a = ia <= n, ok_b = ia + 1 <= n;
     WaveCtx w;
     {
-        const size_t strip_planes = (size_t)s * P.t4 * kWave * 4;   // ints per plane per strip
+        const size_t strip_planes = (size_t)s * P.t4 * kGroupInts;   // ints per plane per strip
         w.pI = PLANES ? P.pI + strip_planes : nullptr;
         w.pD = PLANES ? P.pD + strip_planes : nullptr;
         w.pS = PLANES ? P.pS + strip_planes : nullptr;
         w.pL = LCSP ? P.pL + strip_planes : nullptr;
-        w.codes = CODES ? P.codes + (size_t)s * P.t16 * kWave : nullptr;
+        w.codes = CODES ? P.codes + (size_t)s * P.t16 * kWave * kRowsPerLane : nullptr;
     }
     w.ring_in = ring_in; w.ring_out = ring_out; w.wcnt_in = wcnt_in; w.wcnt_out = wcnt_out; w.status = status;
     w.m = m; w.lane = lane;
-    w.c1v = row_ok ? (int)P.c1[i - 1] : 0x1FF;   // 0x1FF never equals a byte
+    w.c1a = ok_a ? (int)P.c1[ia - 1] : 0x1FF;   // 0x1FF never equals a byte
+    w.c1b = ok_b ? (int)P.c1[ia] : 0x1FF;
     w.tr_win = 0;
     StripTrace* const trace = P.trace;
     const int strip_base = P.strip_base;
 
     LaneState st;
-    // cell (i, 0): algo.rs:204-211
-    const int D0 = sc.h + i * sc.g;
-    st.I = kNeg;
-    st.SD = D0;                                   // max(sub=neg_inf, delete)
-    st.SM = max(D0, sc.floor_);
-    st.Dd = max3i(kNeg + sc.hg, D0 + sc.g, sc.floor_);
-    st.L = 0; st.Ltl = 0;
+    init_row(st.a, ia, ok_a, sc);
+    init_row(st.b, ia + 1, ok_b, sc);
     st.c2c = 0;
-    st.best = row_ok ? INT_MIN : INT_MAX; st.bstep = 0; st.bl = 0;
-    st.lbest = row_ok ? INT_MIN : INT_MAX; st.lstep = 0;
-    st.cI = 0; st.cD = 0;
+    st.b.SMtl = st.a.SM;                          // (A, 0) is row B's top-left for column 1
 
     if (has_consumer) {
-        if (lane == kWave - 1) ring_out[ring_slot(0)] = Rec{st.Dd, st.SM, 0, st.L};
+        if (lane == kWave - 1) ring_out[ring_slot(0)] = Rec{st.b.Dd, st.b.SM, 0, st.b.L};
         lds_wait();
         if (lane == 0) *wcnt_out = 1;
     }
@@ -430,14 +465,15 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     long long tr_start = 0, tr_first = 0;
     unsigned tr_wout = 0;
     if (tracing) tr_start = __builtin_amdgcn_s_memrealtime();
-    // column 0 of the row above seeds the top-left of column 1; columns 1..4
-    // feed the first step group
+    // column 0 of the row above seeds row A's top-left of column 1; columns
+    // 1..4 feed the first step group
     w.tr_win += wait_ge(wcnt_in, min(4, m) + 1, status);
     Rec nxt[4];
     {
         const Rec r0 = ring_in[ring_slot(0)];
-        st.SMtl = r0.sm;
-        st.Ltl = r0.l;
+        // lane 0: (row above the strip, 0); other lanes: row B of lane-1 at column 0
+        st.a.SMtl = shr1(r0.sm, st.b.SM);
+        st.a.Ltl = 0;
         read4(nxt, ring_in + ring_slot(1));
     }
     if (tracing) tr_first = __builtin_amdgcn_s_memrealtime();
@@ -446,7 +482,7 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     for (int t0 = 0; t0 < T; t0 += kSub) {
         const int last_col = min(t0 + kSub - 1 - (kWave - 1), m);   // last column pushed here
         if (has_consumer && last_col >= kRing) tr_wout += wait_ge(rcnt_out, last_col - kRing + 1, status);
-        const size_t sb_off = (size_t)(t0 >> 2) * kWave * 4;          // this sub-block's plane offset (ints)
+        const size_t sb_off = (size_t)(t0 >> 2) * kGroupInts;         // this sub-block's plane offset (ints)
         const bool full = (t0 >= kWave) && (t0 + kSub - 1 <= m - 1) && !rolled_only;
         if (full) {
             const unsigned long long m63 = lane63_mask(has_consumer);
@@ -456,35 +492,50 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         } else {
             ramp_block<LOCAL, PLANES, CODES, TRACK, LCSP>(st, nxt, w, sc, t0, has_consumer, sb_off);
         }
-        if (CODES) gstore1(w.codes + (size_t)(t0 >> 4) * kWave + lane, (st.cD << 16) | (st.cI & 0xFFFFu));
+        if (CODES) {
+            // codes[strip][t/16][lane][row-in-lane]: 8 B per lane
+            typedef unsigned v2u __attribute__((ext_vector_type(2)));
+            typedef __attribute__((address_space(1))) v2u gv2u;
+            const v2u cw = {(st.a.cD << 16) | (st.a.cI & 0xFFFFu), (st.b.cD << 16) | (st.b.cI & 0xFFFFu)};
+            *(gv2u*)(w.codes + ((size_t)(t0 >> 4) * kWave + lane) * kRowsPerLane) = cw;
+        }
         // every ring read up to column t0+20 (incl. the next group's) was issued before this store
         lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
     }
 
     // ---- strip reduction of the max trackers ----
     if (TRACK || LOCAL) {
-        const int best = (TRACK && row_ok) ? st.best : INT_MIN;
-        const int lbest = (LOCAL && row_ok) ? st.lbest : INT_MIN;
+        // per lane: first max -> row A wins ties (earlier row); last max -> row B wins ties
+        const int ba = (TRACK && ok_a) ? st.a.best : INT_MIN, bb = (TRACK && ok_b) ? st.b.best : INT_MIN;
+        const bool fa = ba >= bb;
+        const int best = fa ? ba : bb;
+        const int bstep = fa ? st.a.bstep : st.b.bstep, bl = fa ? st.a.bl : st.b.bl, bh = fa ? 0 : 1;
+        const int la = (LOCAL && ok_a) ? st.a.lbest : INT_MIN, lb2 = (LOCAL && ok_b) ? st.b.lbest : INT_MIN;
+        const bool lbb = lb2 >= la && ok_b;
+        const int lbest = lbb ? lb2 : la;
+        const int lstep = lbb ? st.b.lstep : st.a.lstep, lh = lbb ? 1 : 0;
+        const bool any_ok = ok_a;
         int mx = best, lmx = lbest;
         for (int off = 32; off > 0; off >>= 1) {
             mx = max(mx, __shfl_xor(mx, off));
             lmx = max(lmx, __shfl_xor(lmx, off));
         }
-        const unsigned long long fmask = __ballot(row_ok && best == mx);
-        const unsigned long long lmask = __ballot(row_ok && lbest == lmx);
-        const int fl = fmask ? (__ffsll((long long)fmask) - 1) : 0;           // lowest row
-        const int ll = lmask ? (63 - __clzll((long long)lmask)) : 0;          // highest row
-        const int f_step = __shfl(st.bstep, fl), f_l = __shfl(st.bl, fl);
-        const int l_step = __shfl(st.lstep, ll);
+        const unsigned long long fmask = __ballot(any_ok && best == mx);
+        const unsigned long long lmask = __ballot(any_ok && lbest == lmx);
+        const int fl = fmask ? (__ffsll((long long)fmask) - 1) : 0;           // lowest lane
+        const int ll = lmask ? (63 - __clzll((long long)lmask)) : 0;          // highest lane
+        const int f_step = __shfl(bstep, fl), f_l = __shfl(bl, fl), f_h = __shfl(bh, fl);
+        const int l_step = __shfl(lstep, ll), l_h = __shfl(lh, ll);
         if (lane == 0) {
             StripRes r;
-            r.best = mx; r.bi = s * kWave + fl + 1; r.bj = f_step - fl + 1; r.bl = f_l;
-            r.lbest = lmx; r.li = s * kWave + ll + 1; r.lj = l_step - ll + 1; r.valid = 1;
+            r.best = mx; r.bi = s * kStripRows + kRowsPerLane * fl + f_h + 1; r.bj = f_step - fl + 1; r.bl = f_l;
+            r.lbest = lmx; r.li = s * kStripRows + kRowsPerLane * ll + l_h + 1; r.lj = l_step - ll + 1; r.valid = 1;
             sres[strip_base + s] = r;
         }
     }
     // cell (n, m) for the global-mode start (algo.rs:308, 331)
-    if (row_ok && i == n) pres->end_SM = st.SM;
+    if (ok_a && ia == n) pres->end_SM = st.a.SM;
+    if (ok_b && ia + 1 == n) pres->end_SM = st.b.SM;
     if (tracing && lane == 0) {
         StripTrace tr;
         tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
@@ -630,22 +681,22 @@ __global__ void finalize_kernel(const PairDev* __restrict__ pairs, const StripRe
 // Row view of the walk: on row i the path is a run of insert moves (j-1)
 // that ends at the nearest cell to the left whose code is not "insert",
 // followed by one sub (i-1, j-1) or delete (i-1, j) move.  The cells of one
-// row are consecutive steps of one lane's code words, so a row is a bit-scan
-// of the "not insert" mask D | ~I.  Output: one record per row,
-// (run << 2) | kind, kind 0 = sub, 2 = delete, 1 = the run reached column 0.
+// row are consecutive steps of its code words, so a row is a bit-scan of the
+// "not insert" mask D | ~I.  Output: one record per row, (run << 2) | kind,
+// kind 0 = sub, 2 = delete, 1 = the run reached column 0.
 //
-// Lane-parallel fixed point, one wave per pair and one strip (64 rows) at a
-// time: lane k guesses the column at which the path enters its row (first
-// guess: the diagonal from the strip's entry), every lane scans its own row
-// at once, and each lane's next guess becomes the exit column of the lane
-// above (DPP wave_shl:1).  The top lane's entry is known, so after round r the
-// top r lanes are exact; in practice paths started from wrong columns merge
-// with the true path within a few rows, so the iteration reaches the fixed
-// point -- which IS the sequential walk -- in far fewer than 64 rounds.
-// The strip's code window (kTbWin words = 512 steps of every lane) is read
-// from LDS, filled by LDS-DMA (global_load_lds) while the previous strip was
-// walked; words below the window are read from HBM.
+// Lane-parallel fixed point, one wave per pair and 64 rows (half a fill
+// strip) at a time: lane k guesses the column at which the path enters its
+// row (first guess: the diagonal from the block's entry), every lane scans
+// its own row at once, and each lane's next guess becomes the exit column of
+// the lane above (DPP wave_shl:1).  The top lane's entry is known, so after
+// round r the top r lanes are exact; the iteration stops at the fixed point,
+// which IS the sequential walk.  The block's code window (kTbWin words = 512
+// steps of each of its 64 rows) is read from LDS, filled by LDS-DMA
+// (global_load_lds) while the previous block was walked; words below the
+// window are read from HBM.
 constexpr int kTbWin = 32;
+constexpr int kTbRows = 64;   // rows per walked block (half a fill strip)
 
 __device__ __forceinline__ int tb_q0(int t) {
     return __builtin_amdgcn_readfirstlane(max((t >> 4) - (kTbWin - 1), 0));
@@ -656,13 +707,19 @@ typedef __attribute__((address_space(3))) void lvoid;
 typedef __attribute__((address_space(3))) const uint32_t lu32;
 typedef __attribute__((address_space(1))) const uint32_t gcu32;
 
-// async: words q0 .. q0+kTbWin-1 of strip s, all lanes -> buf[k][lane]
-__device__ __forceinline__ void tb_prefetch(uint32_t* buf, const TbDev& J, int s, int q0, int lane) {
-    const uint32_t* base = J.codes + ((size_t)s * J.t16 + q0) * kWave + lane;
+// Code word of row-in-strip rho, word q of strip s (codes[strip][q][rho]).
+__device__ __forceinline__ size_t tb_word(const TbDev& J, int s, int q, int rho) {
+    return ((size_t)s * J.t16 + q) * kStripRows + rho;
+}
+
+// async: words q0 .. q0+kTbWin-1 of block vb (rows 64*vb .. +63), lane = row -> buf[k][lane]
+__device__ __forceinline__ void tb_prefetch(uint32_t* buf, const TbDev& J, int vb, int q0, int lane) {
+    const int s = vb >> 1, rho = ((vb & 1) << 6) + lane;
 #pragma unroll
     for (int k = 0; k < kTbWin; ++k)
         if (q0 + k < J.t16)
-            __builtin_amdgcn_global_load_lds((gcvoid*)(base + (size_t)k * kWave), (lvoid*)(buf + k * kWave), 4, 0, 0);
+            __builtin_amdgcn_global_load_lds((gcvoid*)(J.codes + tb_word(J, s, q0 + k, rho)),
+                                             (lvoid*)(buf + k * kWave), 4, 0, 0);
 }
 
 __global__ __launch_bounds__(64) void traceback_kernel(const TbDev* __restrict__ jobs) {
@@ -674,19 +731,22 @@ __global__ __launch_bounds__(64) void traceback_kernel(const TbDev* __restrict__
     guint* const recs = (guint*)J.recs;
     gcu32* const codes = (gcu32*)J.codes;
     if (i >= 1 && j >= 1) {
-        int s = __builtin_amdgcn_readfirstlane((i - 1) >> 6);
-        int R = __builtin_amdgcn_readfirstlane((i - 1) & 63);   // path's top lane in this strip
-        int ce = __builtin_amdgcn_readfirstlane(j);              // its entry column
+        int vb = __builtin_amdgcn_readfirstlane((i - 1) / kTbRows);   // walked block (64 rows)
+        int R = __builtin_amdgcn_readfirstlane((i - 1) % kTbRows);    // path's top lane in the block
+        int ce = __builtin_amdgcn_readfirstlane(j);                   // its entry column
         int cb = 0;
-        int q0 = tb_q0(ce - 1 + R);
-        tb_prefetch(tbuf[cb], J, s, q0, lane);
+        // step of row-in-strip rho at column j: t = j - 1 + rho/2
+        int q0 = tb_q0(ce - 1 + ((((vb & 1) << 6) + R) >> 1));
+        tb_prefetch(tbuf[cb], J, vb, q0, lane);
         for (;;) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this strip's window has landed
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this block's window has landed
             const lu32* win = (const lu32*)(uintptr_t)lds_addr(tbuf[cb]);
-            // the strip above is entered at lane 63, no further right than column ce
-            const int qn = tb_q0(ce - 1 + (kWave - 1));
-            if (s > 0) tb_prefetch(tbuf[cb ^ 1], J, s - 1, qn, lane);
-            const size_t strip_w = (size_t)s * J.t16;
+            // the block above is entered at its lane 63, no further right than column ce
+            const int qn = vb > 0 ? tb_q0(ce - 1 + ((((vb - 1) & 1) << 6) + kTbRows - 1) / 2) : 0;
+            if (vb > 0) tb_prefetch(tbuf[cb ^ 1], J, vb - 1, qn, lane);
+            const int s = vb >> 1;
+            const int rho = ((vb & 1) << 6) + lane;
+            const int lo_t = rho >> 1;         // step of column 1 on this row
             const bool act = lane <= R;
             int g = ce - (R - lane);           // diagonal guess of this row's entry column
             int rec = 0, nj = 0;
@@ -696,12 +756,12 @@ __global__ __launch_bounds__(64) void traceback_kernel(const TbDev* __restrict__
                 if (changed) {                 // re-scan only rows whose entry moved
                     end = true; run_end = false; nj = 0; rec = 0;
                     if (g >= 1) {
-                        const int t_in = g - 1 + lane;
+                        const int t_in = g - 1 + lo_t;
                         int t = t_in, tf = -1;
                         uint32_t w = 0;
-                        while (t >= lane) {
+                        while (t >= lo_t) {
                             const int q = t >> 4;
-                            w = q >= q0 ? win[(q - q0) * kWave + lane] : codes[(strip_w + q) * kWave + lane];
+                            w = q >= q0 ? win[(q - q0) * kWave + lane] : codes[tb_word(J, s, q, rho)];
                             // bit 15-k: "insert beats sub"; bit 31-k: "delete beats both" (step 16q + k)
                             const uint32_t nonI = ((w >> 16) | ~w) & ((0xFFFFu << (15 - (t & 15))) & 0xFFFFu);
                             if (nonI) {
@@ -710,14 +770,14 @@ __global__ __launch_bounds__(64) void traceback_kernel(const TbDev* __restrict__
                             }
                             t = (t & ~15) - 1;
                         }
-                        if (tf < lane) {       // (i, g..1) all insert: the walk leaves at (i, 0)
+                        if (tf < lo_t) {       // (i, g..1) all insert: the walk leaves at (i, 0)
                             rec = (g << 2) | 1;
                             run_end = true;
                         } else {
                             const bool del = (w >> (31 - (tf & 15))) & 1u;
                             rec = ((t_in - tf) << 2) | (del ? 2 : 0);
-                            nj = tf - lane + 1 - (del ? 0 : 1);
-                            end = nj < 1 || (s == 0 && lane == 0);   // next cell (i-1, nj) off the interior
+                            nj = tf - lo_t + 1 - (del ? 0 : 1);
+                            end = nj < 1 || (vb == 0 && lane == 0);   // next cell (i-1, nj) off the interior
                         }
                     }
                 }
@@ -736,16 +796,16 @@ __global__ __launch_bounds__(64) void traceback_kernel(const TbDev* __restrict__
             const int lo = E >= 0 ? E : 0;
             if (act && lane >= lo) recs[nrec + (R - lane)] = (uint32_t)rec;
             nrec += R - lo + 1;
-            if (E >= 0) {                      // the walk leaves the interior in this strip
+            if (E >= 0) {                      // the walk leaves the interior in this block
                 const bool re = __builtin_amdgcn_readlane((int)run_end, E) != 0;
                 const int jE = __builtin_amdgcn_readlane(nj, E);
-                if (re) { i = s * kWave + E + 1; j = 0; }
-                else { i = s * kWave + E; j = jE; }
+                if (re) { i = vb * kTbRows + E + 1; j = 0; }
+                else { i = vb * kTbRows + E; j = jE; }
                 break;
             }
             ce = __builtin_amdgcn_readlane(nj, 0);
-            s -= 1;
-            R = kWave - 1;
+            vb -= 1;
+            R = kTbRows - 1;
             cb ^= 1;
             q0 = qn;
         }
@@ -761,8 +821,9 @@ __global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __rest
     if (idx >= total) return;
     const int i = (int)(idx / m) + 1;
     const int j = (int)(idx % m) + 1;
-    const int s = (i - 1) >> 6, l = (i - 1) & 63, t = j - 1 + l;
-    const size_t o = (((size_t)s * t4 + (t >> 2)) * kWave + l) * 4 + (t & 3);
+    const int s = (i - 1) / kStripRows, rho = (i - 1) % kStripRows;
+    const int l = rho >> 1, h = rho & 1, t = j - 1 + l;
+    const size_t o = ((size_t)s * t4 + (t >> 2)) * kGroupInts + h * kWave * 4 + l * 4 + (t & 3);
     out[(size_t)i * (m + 1) + j] = plane[o];
 }
 
