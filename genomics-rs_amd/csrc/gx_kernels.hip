@@ -697,6 +697,7 @@ __global__ void finalize_kernel(const PairDev* __restrict__ pairs, const StripRe
 // window are read from HBM.
 constexpr int kTbWin = 32;
 constexpr int kTbRows = 64;   // rows per walked block (half a fill strip)
+constexpr int kTbBufs = 3;    // windows in flight: current + two prefetched blocks
 
 __device__ __forceinline__ int tb_q0(int t) {
     return __builtin_amdgcn_readfirstlane(max((t >> 4) - (kTbWin - 1), 0));
@@ -705,6 +706,7 @@ __device__ __forceinline__ int tb_q0(int t) {
 typedef __attribute__((address_space(1))) const void gcvoid;
 typedef __attribute__((address_space(3))) void lvoid;
 typedef __attribute__((address_space(3))) const uint32_t lu32;
+typedef __attribute__((address_space(3))) int lint;
 typedef __attribute__((address_space(1))) const uint32_t gcu32;
 
 // Code word of row-in-strip rho, word q of strip s (codes[strip][q][rho]).
@@ -715,79 +717,113 @@ __device__ __forceinline__ size_t tb_word(const TbDev& J, int s, int q, int rho)
 // async: words q0 .. q0+kTbWin-1 of block vb (rows 64*vb .. +63), lane = row -> buf[k][lane]
 __device__ __forceinline__ void tb_prefetch(uint32_t* buf, const TbDev& J, int vb, int q0, int lane) {
     const int s = vb >> 1, rho = ((vb & 1) << 6) + lane;
+    // always exactly kTbWin loads (clamped): the block loop's vmcnt accounting relies on it
 #pragma unroll
     for (int k = 0; k < kTbWin; ++k)
-        if (q0 + k < J.t16)
-            __builtin_amdgcn_global_load_lds((gcvoid*)(J.codes + tb_word(J, s, q0 + k, rho)),
-                                             (lvoid*)(buf + k * kWave), 4, 0, 0);
+        __builtin_amdgcn_global_load_lds((gcvoid*)(J.codes + tb_word(J, s, min(q0 + k, J.t16 - 1), rho)),
+                                         (lvoid*)(buf + k * kWave), 4, 0, 0);
+}
+
+// Window top (in code words) of block vb when it is entered at its lane 63 no
+// further right than column ce.
+__device__ __forceinline__ int tb_top_q0(int vb, int ce) {
+    return tb_q0(ce - 1 + ((((vb & 1) << 6) + kTbRows - 1) >> 1));
 }
 
 __global__ __launch_bounds__(64) void traceback_kernel(const TbDev* __restrict__ jobs) {
-    __shared__ uint32_t tbuf[2][kTbWin * kWave];
+    __shared__ uint32_t tbuf[kTbBufs][kTbWin * kWave];
+    __shared__ int tbl[kTbWin * kWave];   // nearest non-insert step below each word, (step << 1) | del
     const TbDev J = jobs[blockIdx.x];
     const int lane = threadIdx.x;
     int i = J.start_i, j = J.start_j;
     int nrec = 0, rounds = 0;
     guint* const recs = (guint*)J.recs;
     gcu32* const codes = (gcu32*)J.codes;
+    lint* const ltbl = (lint*)(uintptr_t)lds_addr(tbl);
     if (i >= 1 && j >= 1) {
         int vb = __builtin_amdgcn_readfirstlane((i - 1) / kTbRows);   // walked block (64 rows)
         int R = __builtin_amdgcn_readfirstlane((i - 1) % kTbRows);    // path's top lane in the block
         int ce = __builtin_amdgcn_readfirstlane(j);                   // its entry column
-        int cb = 0;
         // step of row-in-strip rho at column j: t = j - 1 + rho/2
-        int q0 = tb_q0(ce - 1 + ((((vb & 1) << 6) + R) >> 1));
-        tb_prefetch(tbuf[cb], J, vb, q0, lane);
+        // windows: current block (q_c, buffer b_c), the block above (q_1, b_1) and
+        // the one above that (q_2, b_2); blocks above are entered no further right
+        // than column ce
+        int b_c = 0, b_1 = 1, b_2 = 2;
+        int q_c = tb_q0(ce - 1 + ((((vb & 1) << 6) + R) >> 1)), q_1 = 0, q_2 = 0;
+        tb_prefetch(tbuf[b_c], J, vb, q_c, lane);
+        if (vb > 0) { q_1 = tb_top_q0(vb - 1, ce); tb_prefetch(tbuf[b_1], J, vb - 1, q_1, lane); }
         for (;;) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this block's window has landed
-            const lu32* win = (const lu32*)(uintptr_t)lds_addr(tbuf[cb]);
-            // the block above is entered at its lane 63, no further right than column ce
-            const int qn = vb > 0 ? tb_q0(ce - 1 + ((((vb - 1) & 1) << 6) + kTbRows - 1) / 2) : 0;
-            if (vb > 0) tb_prefetch(tbuf[cb ^ 1], J, vb - 1, qn, lane);
+            // this block's window has landed: VMEM ops complete in issue order, and
+            // at least one full younger prefetch (kTbWin loads) follows it unless
+            // this is the top block
+            if (vb > 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(kTbWin) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int q0 = q_c;
+            if (vb > 1) { q_2 = tb_top_q0(vb - 2, ce); tb_prefetch(tbuf[b_2], J, vb - 2, q_2, lane); }
+            const lu32* win = (const lu32*)(uintptr_t)lds_addr(tbuf[b_c]);
             const int s = vb >> 1;
             const int rho = ((vb & 1) << 6) + lane;
             const int lo_t = rho >> 1;         // step of column 1 on this row
+            // per lane: nearest non-insert step strictly below each window word,
+            // (step << 1) | delete-bit, -1 if none in the window (branch-free)
+            {
+                int run = -1;
+#pragma unroll 8
+                for (int x = 0; x < kTbWin; ++x) {
+                    ltbl[x * kWave + lane] = run;
+                    const uint32_t w = win[x * kWave + lane];
+                    const uint32_t m = ((w >> 16) | ~w) & 0xFFFFu;
+                    const int k = 15 - (int)__builtin_ctz(m | 0x10000u);
+                    const int cand = ((16 * (q0 + x) + k) << 1) | (int)((w >> ((31 - k) & 31)) & 1u);
+                    run = m ? cand : run;
+                }
+            }
             const bool act = lane <= R;
+            const bool top_row = vb == 0 && lane == 0;
             int g = ce - (R - lane);           // diagonal guess of this row's entry column
             int rec = 0, nj = 0;
             bool end = true, run_end = false;
-            bool changed = act;
             for (;;) {
-                if (changed) {                 // re-scan only rows whose entry moved
-                    end = true; run_end = false; nj = 0; rec = 0;
-                    if (g >= 1) {
-                        const int t_in = g - 1 + lo_t;
-                        int t = t_in, tf = -1;
-                        uint32_t w = 0;
+                // evaluate every lane's row from its current guess, branch-free:
+                // the word holding the entry step and the table entry below it
+                // are read together; the rare scan below the window is separate
+                const bool valid = act && g >= 1;
+                const int t_in = g - 1 + lo_t;
+                const int x = (t_in >> 4) - q0;
+                const int xc = min(max(x, 0), kTbWin - 1);
+                const uint32_t w = win[xc * kWave + lane];
+                const int tb = ltbl[xc * kWave + lane];
+                const uint32_t nonI = ((w >> 16) | ~w) & ((0xFFFFu << (15 - (t_in & 15))) & 0xFFFFu);
+                const int kw = 15 - (int)__builtin_ctz(nonI | 0x10000u);
+                int tf = nonI ? (t_in & ~15) + kw : (tb >> 1);
+                int del = nonI ? (int)((w >> ((31 - kw) & 31)) & 1u) : (tb & 1);
+                const bool need_scan = valid && (x < 0 || (!nonI && tb < 0 && 16 * q0 > lo_t));
+                if (__builtin_amdgcn_ballot_w64(need_scan)) {
+                    if (need_scan) {           // below the window: scan the HBM words
+                        int t = x < 0 ? t_in : 16 * q0 - 1;
+                        tf = -1; del = 0;
                         while (t >= lo_t) {
-                            const int q = t >> 4;
-                            w = q >= q0 ? win[(q - q0) * kWave + lane] : codes[tb_word(J, s, q, rho)];
-                            // bit 15-k: "insert beats sub"; bit 31-k: "delete beats both" (step 16q + k)
-                            const uint32_t nonI = ((w >> 16) | ~w) & ((0xFFFFu << (15 - (t & 15))) & 0xFFFFu);
-                            if (nonI) {
-                                tf = (t & ~15) + (15 - __builtin_ctz(nonI));
+                            const uint32_t wg = codes[tb_word(J, s, t >> 4, rho)];
+                            const uint32_t ng = ((wg >> 16) | ~wg) & ((0xFFFFu << (15 - (t & 15))) & 0xFFFFu);
+                            if (ng) {
+                                tf = (t & ~15) + (15 - __builtin_ctz(ng));
+                                del = (wg >> (31 - (tf & 15))) & 1u;
                                 break;
                             }
                             t = (t & ~15) - 1;
                         }
-                        if (tf < lo_t) {       // (i, g..1) all insert: the walk leaves at (i, 0)
-                            rec = (g << 2) | 1;
-                            run_end = true;
-                        } else {
-                            const bool del = (w >> (31 - (tf & 15))) & 1u;
-                            rec = ((t_in - tf) << 2) | (del ? 2 : 0);
-                            nj = tf - lo_t + 1 - (del ? 0 : 1);
-                            end = nj < 1 || (vb == 0 && lane == 0);   // next cell (i-1, nj) off the interior
-                        }
                     }
                 }
+                run_end = valid && tf < lo_t;  // (i, g..1) all insert: the walk leaves at (i, 0)
+                nj = tf - lo_t + del;          // del ? tf-lo_t+1 : tf-lo_t
+                end = !valid || run_end || nj < 1 || top_row;
+                rec = run_end ? ((g << 2) | 1) : (((t_in - tf) << 2) | (del << 1));
                 // next guess: the exit column of the lane above; the top lane's entry is fixed
                 const int prop = end ? 0 : nj;
                 int gn = __builtin_amdgcn_update_dpp(0, prop, 0x130 /* wave_shl:1 */, 0xF, 0xF, false);
                 gn = lane == R ? ce : gn;
-                changed = act && gn != g;
                 ++rounds;
-                if (__builtin_amdgcn_ballot_w64(changed) == 0) break;
+                if (__builtin_amdgcn_ballot_w64(act && gn != g) == 0) break;
                 g = gn;
             }
             // the path covers lanes R down to the first lane (from the top) where it ends
@@ -806,8 +842,11 @@ __global__ __launch_bounds__(64) void traceback_kernel(const TbDev* __restrict__
             ce = __builtin_amdgcn_readlane(nj, 0);
             vb -= 1;
             R = kTbRows - 1;
-            cb ^= 1;
-            q0 = qn;
+            {   // rotate the windows (the prefetched ones were sized for an entry no
+                // further right than the previous one: always true)
+                const int b = b_c; b_c = b_1; b_1 = b_2; b_2 = b;
+                q_c = q_1; q_1 = q_2;
+            }
         }
     }
     if (lane == 0) { *J.nrecs = nrec; J.end_ij[0] = i; J.end_ij[1] = j; J.end_ij[2] = rounds; }
