@@ -28,7 +28,7 @@ hipError_t launch_fill(bool local, bool planes, bool track, bool lcs, const Pair
                        hipStream_t st);
 hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d_sres, PairRes* d_pres,
                            hipStream_t st);
-hipError_t launch_traceback(const TbDev* d_jobs, int njobs, hipStream_t st);
+hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipStream_t st);
 hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, hipStream_t st);
 }  // namespace gx
 
@@ -252,7 +252,7 @@ struct PairHost {
 
 struct FillJob {
     // device buffers (owned by the job until released)
-    DevBuf chars, planes, codes, feed, progress, sres, pres, pairs, counter;
+    DevBuf chars, planes, codes, skel, feed, progress, sres, pres, pairs, counter;
     std::vector<PairDev> pd;
     std::vector<PairRes> res;
     int W = 4;
@@ -264,7 +264,7 @@ struct FillJob {
 static void job_release(gx_context* ctx, FillJob& j) {
     pool_put(ctx, j.chars); pool_put(ctx, j.planes); pool_put(ctx, j.codes); pool_put(ctx, j.feed);
     pool_put(ctx, j.progress); pool_put(ctx, j.sres); pool_put(ctx, j.pres); pool_put(ctx, j.pairs);
-    pool_put(ctx, j.counter);
+    pool_put(ctx, j.counter); pool_put(ctx, j.skel);
 }
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -286,8 +286,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     const size_t P = ph.size();
     job.pd.assign(P, PairDev{});
     // -- sizes
-    size_t chars_bytes = 0, plane_elems = 0, code_elems = 0, feed_recs = 0, prog_elems = 0;
-    std::vector<size_t> c1o(P), c2o(P), po(P), co(P), fo(P), gofs(P);
+    size_t chars_bytes = 0, plane_elems = 0, code_elems = 0, feed_recs = 0, prog_elems = 0, skel_elems = 0;
+    std::vector<size_t> c1o(P), c2o(P), po(P), co(P), fo(P), gofs(P), so(P);
     int bands = 0, strips = 0;
     for (size_t p = 0; p < P; ++p) {
         const int n = (int)ph[p].n, m = (int)ph[p].m;
@@ -301,12 +301,14 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         d.band_base = bands;
         d.strip_base = strips;
         d.feed_stride = (int)align_up((size_t)m + 1 + 64, 16);
+        d.skel_stride = (int)align_up((size_t)m + 1, 64);
         bands += d.bands;
         strips += d.strips;
         c1o[p] = chars_bytes; chars_bytes += align_up(n, 64);
         c2o[p] = chars_bytes; chars_bytes += align_up(m, 64);
         po[p] = plane_elems; plane_elems += (size_t)d.strips * d.t4 * kGroupInts;
         co[p] = code_elems; code_elems += (size_t)d.strips * d.t16 * kStripRows;
+        so[p] = skel_elems; skel_elems += (size_t)d.strips * d.skel_stride;
         fo[p] = feed_recs; feed_recs += (size_t)std::max(d.bands - 1, 0) * d.feed_stride;
         gofs[p] = prog_elems; prog_elems += (size_t)std::max(d.bands - 1, 0);
     }
@@ -319,6 +321,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     }
     if (planes && (rc = pool_get(ctx, plane_elems * sizeof(int32_t) * nplanes, &job.planes))) return rc;
     if (codes && (rc = pool_get(ctx, code_elems * sizeof(uint32_t), &job.codes))) return rc;
+    if ((rc = pool_get(ctx, std::max<size_t>(skel_elems, 1) * sizeof(int), &job.skel))) return rc;
     if ((rc = pool_get(ctx, std::max<size_t>(feed_recs, 1) * sizeof(Rec), &job.feed))) return rc;
     if ((rc = pool_get(ctx, std::max<size_t>(prog_elems, 1) * sizeof(int), &job.progress))) return rc;
     if ((rc = pool_get(ctx, std::max(strips, 1) * sizeof(StripRes), &job.sres))) return rc;
@@ -347,6 +350,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         d.pS = planes ? pl + 2 * plane_elems + po[p] : nullptr;
         d.pL = (planes && lcs) ? pl + 3 * plane_elems + po[p] : nullptr;
         d.codes = codes ? (uint32_t*)job.codes.p + co[p] : nullptr;
+        d.skel = (int*)job.skel.p + so[p];
         d.feed = (Rec*)job.feed.p + fo[p];
         d.progress = (int*)job.progress.p + gofs[p];
     }
@@ -512,65 +516,83 @@ struct TbOut {
     double ms = 0;
 };
 
-static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<std::pair<int, int>>& starts,
-                         TbOut& out) {
+struct TbStart {
+    int i, j;   // interior start cell, or 0 = nothing to walk
+    int E;      // its landing column (PairRes.end_E / lmax_E)
+};
+
+static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<TbStart>& starts, TbOut& out) {
     const size_t P = starts.size();
     std::vector<TbDev> jobs(P);
-    std::vector<size_t> mo(P);
-    size_t mtot = 0;   // records (uint32): at most one per row + the final run
+    std::vector<size_t> so(P);
+    size_t stot = 0;   // strips over all pairs
+    int max_strips = 1;
     for (size_t p = 0; p < P; ++p) {
-        mo[p] = mtot;
-        mtot += align_up((size_t)job.pd[p].n + 64, 64);
+        so[p] = stot;
+        stot += (size_t)job.pd[p].strips;
+        max_strips = std::max(max_strips, job.pd[p].strips);
     }
-    DevBuf moves, jb, cnt;
+    DevBuf recs, seg, jb, cnt;
     int rc;
-    if ((rc = pool_get(ctx, mtot * sizeof(uint32_t), &moves))) return rc;
-    if ((rc = pool_get(ctx, P * sizeof(TbDev), &jb))) { pool_put(ctx, moves); return rc; }
-    if ((rc = pool_get(ctx, P * 4 * sizeof(int), &cnt))) { pool_put(ctx, moves); pool_put(ctx, jb); return rc; }
+    auto cleanup = [&]() { pool_put(ctx, recs); pool_put(ctx, seg); pool_put(ctx, jb); pool_put(ctx, cnt); };
+    if ((rc = pool_get(ctx, std::max<size_t>(stot, 1) * kStripRows * sizeof(uint32_t), &recs)) ||
+        (rc = pool_get(ctx, std::max<size_t>(stot, 1) * 4 * sizeof(int), &seg)) ||
+        (rc = pool_get(ctx, P * sizeof(TbDev), &jb)) || (rc = pool_get(ctx, P * 4 * sizeof(int), &cnt))) {
+        cleanup();
+        return rc;
+    }
     for (size_t p = 0; p < P; ++p) {
         TbDev& t = jobs[p];
-        t.codes = job.pd[p].codes;
-        t.n = job.pd[p].n; t.m = job.pd[p].m; t.t16 = job.pd[p].t16;
-        t.start_i = starts[p].first; t.start_j = starts[p].second;
-        t.recs = (uint32_t*)moves.p + mo[p];
-        t.nrecs = (int*)cnt.p + 4 * p;
-        t.end_ij = (int*)cnt.p + 4 * p + 1;
+        const PairDev& d = job.pd[p];
+        t.codes = d.codes;
+        t.skel = d.skel;
+        t.skel_stride = d.skel_stride;
+        t.n = d.n; t.m = d.m; t.t16 = d.t16; t.strips = d.strips;
+        t.start_i = starts[p].i; t.start_j = starts[p].j; t.start_E = starts[p].E;
+        t.seg = (int*)seg.p + 4 * so[p];
+        t.recs = (uint32_t*)recs.p + so[p] * kStripRows;
+        t.end_ij = (int*)cnt.p + 4 * p;
     }
-    auto cleanup = [&]() { pool_put(ctx, moves); pool_put(ctx, jb); pool_put(ctx, cnt); };
     hipError_t e = hipMemcpyAsync(jb.p, jobs.data(), P * sizeof(TbDev), hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(seg.p, 0, std::max<size_t>(stot, 1) * 4 * sizeof(int), ctx->stream);
     if (e == hipSuccess) e = hipEventRecord(ctx->ev1, ctx->stream);
-    if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, ctx->stream);
+    if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, max_strips, ctx->stream);
     if (e == hipSuccess) e = hipEventRecord(ctx->ev2, ctx->stream);
-    std::vector<int> c(4 * P);
+    std::vector<int> c(4 * P), sg(4 * std::max<size_t>(stot, 1));
+    std::vector<uint32_t> hr(std::max<size_t>(stot, 1) * kStripRows);
     if (e == hipSuccess) e = hipMemcpyAsync(c.data(), cnt.p, 4 * P * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(sg.data(), seg.p, sg.size() * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(hr.data(), recs.p, hr.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                            ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    if (e != hipSuccess) { cleanup(); return fail(GX_EHIP, std::string("traceback: ") + hipGetErrorString(e)); }
+    cleanup();
+    if (e != hipSuccess) return fail(GX_EHIP, std::string("traceback: ") + hipGetErrorString(e));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, ctx->ev1, ctx->ev2);
     out.ms = ms;
     out.moves.resize(P);
     out.end_i.resize(P);
     out.end_j.resize(P);
-    // one D2H for all records
-    std::vector<uint32_t> hm(mtot);
-    e = hipMemcpyAsync(hm.data(), moves.p, mtot * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    cleanup();
-    if (e != hipSuccess) return fail(GX_EHIP, std::string("traceback copy: ") + hipGetErrorString(e));
     for (size_t p = 0; p < P; ++p) {
-        // expand the per-row records into per-move codes (0 sub, 1 insert, 2 delete)
-        const int k = c[4 * p];
+        // concatenate the strips' row records from the start strip upwards and
+        // expand them into per-move codes (0 sub, 1 insert, 2 delete)
         std::vector<uint8_t>& mv = out.moves[p];
         mv.clear();
-        for (int r = 0; r < k; ++r) {
-            const uint32_t rec = hm[mo[p] + r];
-            mv.insert(mv.end(), rec >> 2, (uint8_t)1);
-            if ((rec & 3u) != 1u) mv.push_back((uint8_t)(rec & 3u));
+        int nseg = 0;
+        for (int s = c[4 * p + 2]; s >= 0; --s) {
+            const int* g = &sg[4 * (so[p] + s)];
+            if (!g[3]) break;
+            ++nseg;
+            const uint32_t* r = &hr[(so[p] + s) * kStripRows];
+            for (int k = 0; k < g[2]; ++k) {
+                mv.insert(mv.end(), r[k] >> 2, (uint8_t)1);
+                if ((r[k] & 3u) != 1u) mv.push_back((uint8_t)(r[k] & 3u));
+            }
         }
-        out.end_i[p] = c[4 * p + 1];
-        out.end_j[p] = c[4 * p + 2];
+        out.end_i[p] = c[4 * p + 0];
+        out.end_j[p] = c[4 * p + 1];
         if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug") && p == 0)
-            fprintf(stderr, "[gx DEBUG] traceback pair 0: %d row records, %d fixed-point rounds\n", k, c[4 * p + 3]);
+            fprintf(stderr, "[gx DEBUG] traceback pair 0: %d strips on the path, %zu moves\n", nseg, mv.size());
     }
     return GX_OK;
 }
@@ -781,7 +803,7 @@ extern "C" int gx_retrace(gx_table* t, int is_local, gx_step* steps, size_t cap,
                                 (unsigned long long)sj);
         TbOut tb;
         if (si >= 1 && sj >= 1 && n >= 1 && m >= 1) {
-            rc = run_traceback(ctx, t->job, {{(int)si, (int)sj}}, tb);
+            rc = run_traceback(ctx, t->job, {TbStart{(int)si, (int)sj, is_local ? r.lmax_E : r.end_E}}, tb);
         } else {
             tb.moves.assign(1, {});
         }
@@ -842,7 +864,7 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
     FillJob job;
     std::vector<PairRes> res(P, PairRes{});
     TbOut tb;
-    std::vector<std::pair<int, int>> starts(idx.size());
+    std::vector<TbStart> starts(idx.size());
     std::vector<uint64_t> si(P), sj(P);
     std::vector<int64_t> score(P);
     int rc = GX_OK;
@@ -859,7 +881,9 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
     if (!idx.empty()) {
         for (size_t k = 0; k < idx.size(); ++k) {
             const size_t p = idx[k];
-            starts[k] = (si[p] >= 1 && sj[p] >= 1) ? std::make_pair((int)si[p], (int)sj[p]) : std::make_pair(0, 0);
+            starts[k] = (si[p] >= 1 && sj[p] >= 1)
+                            ? TbStart{(int)si[p], (int)sj[p], is_local ? res[p].lmax_E : res[p].end_E}
+                            : TbStart{0, 0, 0};
         }
         rc = run_traceback(ctx, job, starts, tb);
     }

@@ -57,13 +57,18 @@ struct __attribute__((aligned(16))) Rec {
 
 struct __attribute__((aligned(16))) StripRes {
     int best, bi, bj, bl;      // first max of score_max in row-major order + LCS there
-    int lbest, li, lj, valid;  // last max (local start search)
+    int lbest, li, lj, lE;     // last max (local start search) + its landing column
 };
 
+// Landing column E(i, j): the traceback path from cell (i, j) leaves its
+// strip through the strip's top boundary row 128s at column E (E >= 0), or
+// reaches column 0 inside the strip at local row -E (E < 0).  The fill
+// propagates it with the traceback codes; each strip's bottom row is stored
+// as the traceback skeleton.
 struct __attribute__((aligned(16))) PairRes {
     int max_val, max_i, max_j, mam;       // first max over interior (algo.rs:258-262, 279)
     int lmax_val, lmax_i, lmax_j, nstrips;// last max over interior (algo.rs:310-322)
-    int end_SM, pad0, pad1, pad2;         // score_max of cell (n, m)
+    int end_SM, end_E, lmax_E, pad2;      // score_max and E of cell (n, m); E of the last max
 };
 
 // Optional per-strip timeline (GX_TRACE_FILE): s_memrealtime ticks (100 MHz)
@@ -96,17 +101,21 @@ struct PairDev {
     Rec* feed;           // [bands-1][feed_stride] band-boundary rows
     int* progress;       // [bands-1] columns published per boundary
     StripTrace* trace;   // per strip, or nullptr
+    int* skel;           // [strips][skel_stride] landing column E of each strip's bottom row
     int feed_stride;
-    int pad;
+    int skel_stride;
 };
 
 struct TbDev {           // per-pair traceback job
     const uint32_t* codes;
-    int n, m, t16;
+    const int* skel;
+    int skel_stride;
+    int n, m, t16, strips;
     int start_i, start_j;  // interior start cell (1-based), or 0 = nothing to walk
-    uint32_t* recs;        // out: one record per row, (insert run << 2) | kind (gx_kernels.hip)
-    int* nrecs;            // out
-    int* end_ij;           // out: [2] position where the walk left the interior
+    int start_E;           // landing column of the start cell (PairRes.end_E / lmax_E)
+    int* seg;              // out: [strips][4] {entry_i, entry_j, records, active} per strip on the path
+    uint32_t* recs;        // out: [strips][kStripRows] one record per row, (insert run << 2) | kind
+    int* end_ij;           // out: [4] {i, j} where the walk leaves the interior, first strip, rounds
 };
 
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }

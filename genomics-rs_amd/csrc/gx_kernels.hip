@@ -123,8 +123,9 @@ struct RowState {
     int I, SD, Dd, SM, SMtl;   // insert, max(sub, delete), delete-successor, score_max, SM(i-1, j-1)
     int L, Ltl;                // LCS field (TRACK only)
     int best, bstep, bl;       // first strict max of the row (TRACK only)
-    int lbest, lstep;          // last max of the row (LOCAL only)
+    int lbest, lstep, lE;      // last max of the row (LOCAL only) and its landing column
     uint32_t cI, cD;           // traceback code bit-planes (16 steps each)
+    int E, Etl;                // landing column (gx_internal.h) of (i, j-1) and of (i-1, j-1)
 };
 struct LaneState {
     RowState a, b;
@@ -132,60 +133,77 @@ struct LaneState {
 };
 
 // Lane 63 pushes its row-B cell (the strip's bottom row) into the LDS ring of
-// the wave below, under a lane-63 exec mask (no branch, no register tuple).
-// Record = {dd, sm, c2, l}; without TRACK the l word is not written.  Compute
-// waves run with all 64 lanes active, so exec is restored to -1, not saved.
-// U = step within the 16-step sub-block (the ring slot's constant offset).
+// the wave below, under a lane-63 exec mask (no branch, no register tuple),
+// and in the same exec window stores the cell's landing column E into the
+// traceback skeleton (global, 4 B).  Record = {dd, sm, c2, l}; without TRACK
+// the l word is not written.  Compute waves run with all 64 lanes active, so
+// exec is restored to -1, not saved.  U = step within the 16-step sub-block
+// (constant LDS and global offsets); sk = skeleton address of the sub-block's
+// first pushed column.
 template <int U, bool TRACK>
-__device__ __forceinline__ void push63(uint32_t base, const LaneState& st, unsigned long long m63) {
+__device__ __forceinline__ void push63(uint32_t base, const LaneState& st, unsigned long long m63, const int* sk) {
     if (TRACK)
         asm volatile(
             "s_mov_b64 exec, %0\n\t"
-            "ds_write2_b32 %1, %2, %3 offset0:%6 offset1:%7\n\t"
-            "ds_write2_b32 %1, %4, %5 offset0:%8 offset1:%9\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%9 offset1:%10\n\t"
+            "ds_write2_b32 %1, %4, %5 offset0:%11 offset1:%12\n\t"
+            "global_store_dword %7, %6, %8 offset:%13\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L), "i"(4 * U),
-              "i"(4 * U + 1), "i"(4 * U + 2), "i"(4 * U + 3));
+            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L), "v"(st.b.E), "v"(0),
+              "s"(sk), "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2), "i"(4 * U + 3), "i"(4 * U)
+            : "memory");
     else
         asm volatile(
             "s_mov_b64 exec, %0\n\t"
-            "ds_write2_b32 %1, %2, %3 offset0:%5 offset1:%6\n\t"
-            "ds_write_b32 %1, %4 offset:%7\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%8 offset1:%9\n\t"
+            "ds_write_b32 %1, %4 offset:%10\n\t"
+            "global_store_dword %6, %5, %7 offset:%11\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "i"(4 * U), "i"(4 * U + 1),
-              "i"(16 * U + 8));
+            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.E), "v"(0), "s"(sk),
+              "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8), "i"(4 * U)
+            : "memory");
 }
 
 // The same push followed, in the same lane-63 window, by the store of the
 // ring's write counter: LDS executes one wave's DS operations in order, so a
 // consumer that sees the counter also sees every record pushed before it.
 template <int U, bool TRACK>
-__device__ __forceinline__ void push63_pub(uint32_t base, const LaneState& st, unsigned long long m63,
+__device__ __forceinline__ void push63_pub(uint32_t base, const LaneState& st, unsigned long long m63, const int* sk,
                                            uint32_t cnt_addr, int cnt) {
     if (TRACK)
         asm volatile(
             "s_mov_b64 exec, %0\n\t"
-            "ds_write2_b32 %1, %2, %3 offset0:%8 offset1:%9\n\t"
-            "ds_write2_b32 %1, %4, %5 offset0:%10 offset1:%11\n\t"
-            "ds_write_b32 %6, %7\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%11 offset1:%12\n\t"
+            "ds_write2_b32 %1, %4, %5 offset0:%13 offset1:%14\n\t"
+            "ds_write_b32 %9, %10\n\t"
+            "global_store_dword %7, %6, %8 offset:%15\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L), "v"(cnt_addr), "v"(cnt),
-              "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2), "i"(4 * U + 3)
+            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L), "v"(st.b.E), "v"(0),
+              "s"(sk), "v"(cnt_addr), "v"(cnt), "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2), "i"(4 * U + 3),
+              "i"(4 * U)
             : "memory");
     else
         asm volatile(
             "s_mov_b64 exec, %0\n\t"
-            "ds_write2_b32 %1, %2, %3 offset0:%7 offset1:%8\n\t"
-            "ds_write_b32 %1, %4 offset:%9\n\t"
-            "ds_write_b32 %5, %6\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%10 offset1:%11\n\t"
+            "ds_write_b32 %1, %4 offset:%12\n\t"
+            "ds_write_b32 %8, %9\n\t"
+            "global_store_dword %6, %5, %7 offset:%13\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(cnt_addr), "v"(cnt), "i"(4 * U),
-              "i"(4 * U + 1), "i"(16 * U + 8)
+            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.E), "v"(0), "s"(sk),
+              "v"(cnt_addr), "v"(cnt), "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8), "i"(4 * U)
             : "memory");
+}
+
+// A wave-uniform pointer forced into an SGPR pair (for "s" asm operands).
+__device__ __forceinline__ const int* uniform_ptr(const int* p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const int*)(uintptr_t)(((uint64_t)hi << 32) | lo);
 }
 
 // exec mask selecting lane 63 (or no lane), forced into an SGPR pair: the
@@ -194,25 +212,31 @@ __device__ __forceinline__ unsigned long long lane63_mask(bool on) {
     return (unsigned long long)__builtin_amdgcn_readfirstlane(on ? 0x80000000u : 0u) << 32;
 }
 
-// Ramp-path push with a runtime slot address.
+// Ramp-path push with a runtime slot address and skeleton byte offset.
 template <bool TRACK>
-__device__ __forceinline__ void push63_rt(uint32_t addr, const LaneState& st, unsigned long long m63) {
+__device__ __forceinline__ void push63_rt(uint32_t addr, const LaneState& st, unsigned long long m63, const int* sk,
+                                          uint32_t sk_off) {
     if (TRACK)
         asm volatile(
             "s_mov_b64 exec, %0\n\t"
             "ds_write2_b32 %1, %2, %3 offset1:1\n\t"
             "ds_write2_b32 %1, %4, %5 offset0:2 offset1:3\n\t"
+            "global_store_dword %7, %6, %8\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(addr), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L));
+            : "s"(m63), "v"(addr), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L), "v"(st.b.E), "v"(sk_off),
+              "s"(sk)
+            : "memory");
     else
         asm volatile(
             "s_mov_b64 exec, %0\n\t"
             "ds_write2_b32 %1, %2, %3 offset1:1\n\t"
             "ds_write_b32 %1, %4 offset:8\n\t"
+            "global_store_dword %6, %5, %7\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(addr), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c));
+            : "s"(m63), "v"(addr), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.E), "v"(sk_off), "s"(sk)
+            : "memory");
 }
 
 // One lane stores an LDS counter (exec = lane 0 only, no branch).
@@ -228,12 +252,13 @@ __device__ __forceinline__ void lds_store_lane0(lds_int* p, int v) {
 
 // One cell of the Gotoh recurrence (algo.rs:222-268) for the row in `st`,
 // given the cell above (dd_in = its delete-successor = D(i, j), sm_in =
-// score_max(i-1, j), l_in = max_matches(i-1, j)) and s2[j-1].  act = false
-// leaves the row unchanged (ramp lanes outside columns 1..m).
+// score_max(i-1, j), l_in = max_matches(i-1, j), e_up = its landing column)
+// and s2[j-1].  act = false leaves the row unchanged (ramp lanes outside
+// columns 1..m).
 template <bool LOCAL, bool MASKED, bool CODES, bool TRACK>
-__device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm_in, const int l_in, const int c2,
-                                     const int c1v, const bool act, const int t, const Scores32& sc, int& oI,
-                                     int& oD, int& oS, int& oL) {
+__device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm_in, const int l_in, const int e_up,
+                                     const int c2, const int c1v, const bool act, const int t, const Scores32& sc,
+                                     int& oI, int& oD, int& oS, int& oL) {
     // algo.rs:231-236  insert_score = top.score_max(g, h+g, h+g)
     const int In = LOCAL ? max3i(st.I + sc.g, st.SD + sc.hg, 0) : max(st.I + sc.g, st.SD + sc.hg);
     const bool mt = c2 == c1v;             // sequence.rs:113-114
@@ -247,14 +272,37 @@ __device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm
     const int Ddn = LOCAL ? max3i(IS + sc.hg, Dn + sc.g, 0) : max(IS + sc.hg, Dn + sc.g);
     int Ln = 0;
     if (TRACK) Ln = max3i(st.L, l_in, st.Ltl + (mt ? 1 : 0));   // algo.rs:250-255
+    int En = 0;
+    if (CODES) {
+        // retrace priority S > I > D against the cell max (algo.rs:351-400):
+        // code bit-planes "D beats both" / "I beats S" (decode D ? delete :
+        // I ? insert : sub) and the landing column of the path through this
+        // cell, taken from the predecessor the priority picks.  One asm block:
+        // each compare feeds its select and its code bit at once (no SGPR-pair
+        // masks kept alive, no chain sunk to the end of the sub-block).
+        asm volatile(
+            "v_cmp_gt_i32 vcc, %[in], %[sn]\n\t"
+            "v_cndmask_b32 %[en], %[etl], %[el], vcc\n\t"
+            "v_addc_co_u32 %[ci], vcc, %[ci], %[ci], vcc\n\t"
+            "v_cmp_gt_i32 vcc, %[dn], %[is]\n\t"
+            "v_cndmask_b32 %[en], %[en], %[eu], vcc\n\t"
+            "v_addc_co_u32 %[cd], vcc, %[cd], %[cd], vcc"
+            : [en] "=&v"(En), [ci] "+v"(st.cI), [cd] "+v"(st.cD)
+            : [in] "v"(In), [sn] "v"(Sn), [dn] "v"(Dn), [is] "v"(IS), [etl] "v"(st.Etl), [el] "v"(st.E),
+              [eu] "v"(e_up)
+            : "vcc");
+    }
     if (MASKED) {
         st.I = act ? In : st.I; st.SD = act ? SDn : st.SD; st.Dd = act ? Ddn : st.Dd; st.SM = act ? SMn : st.SM;
         if (TRACK) st.L = act ? Ln : st.L;
+        if (CODES) st.E = act ? En : st.E;
     } else {
         st.I = In; st.SD = SDn; st.Dd = Ddn; st.SM = SMn;
         if (TRACK) st.L = Ln;
+        if (CODES) st.E = En;
     }
     st.SMtl = sm_in;
+    if (CODES) st.Etl = e_up;
     if (TRACK) {
         st.Ltl = l_in;
         // algo.rs:258-262: first strict maximum in row-major order
@@ -264,25 +312,16 @@ __device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm
     if (LOCAL) {
         // algo.rs:310-322: max_by keeps the LAST maximum
         const bool nl = act && SMn >= st.lbest;
-        st.lbest = nl ? SMn : st.lbest; st.lstep = nl ? t : st.lstep;
-    }
-    if (CODES) {
-        // retrace priority S > I > D against the cell max (algo.rs:351-400), two
-        // bit-planes: D beats both / I beats S.  Decode: D ? delete : I ? insert : sub.
-        // The bit is the sign of a difference (|values| < 2^29 under the host's
-        // range guard), shifted in with v_alignbit: no compare masks, which the
-        // compiler would otherwise park in SGPR pairs across the sub-block.
-        // (volatile asm: otherwise LLVM sinks the chain to the store at the end of
-        // the sub-block and keeps 16 steps of IS/Dn/Sn/In alive -> VGPR spills)
-        asm volatile("v_alignbit_b32 %0, %0, %1, 31" : "+v"(st.cD) : "v"((uint32_t)(IS - Dn)));   // Dn > IS
-        asm volatile("v_alignbit_b32 %0, %0, %1, 31" : "+v"(st.cI) : "v"((uint32_t)(Sn - In)));   // In > Sn
+        st.lbest = nl ? SMn : st.lbest; st.lstep = nl ? t : st.lstep; st.lE = nl ? En : st.lE;
     }
     oI = In; oD = Dn; oS = Sn; oL = Ln;
 }
 
 // One anti-diagonal step of a compute wave: both rows of every lane at
 // column j = t - lane + 1.  Row A's cell above comes from row B of lane-1
-// (wave_shr:1; lane 0 from the ring record r), row B's from row A.
+// (wave_shr:1; lane 0 from the ring record r), row B's from row A.  Lane 0's
+// row A is the strip's top row: its "landing column" from above is its own
+// column j = t + 1 (a delete lands on (128s, j), a sub on (128s, j-1)).
 template <bool LOCAL, bool MASKED, bool CODES, bool TRACK>
 __device__ __forceinline__ void dp_step(LaneState& st, const Rec& r, const int t, const int lane, const int m,
                                         const int c1a, const int c1b, const Scores32& sc, int (&oI)[2],
@@ -291,10 +330,12 @@ __device__ __forceinline__ void dp_step(LaneState& st, const Rec& r, const int t
     const int sm_in = shr1(r.sm, st.b.SM);
     const int c2 = shr1(r.c2, st.c2c);
     const int l_in = TRACK ? shr1(r.l, st.b.L) : 0;
+    const int e_in = CODES ? shr1(t + 1, st.b.E) : 0;
     const bool act = MASKED ? (unsigned)(t - lane) < (unsigned)m : true;
-    cell<LOCAL, MASKED, CODES, TRACK>(st.a, dd_in, sm_in, l_in, c2, c1a, act, t, sc, oI[0], oD[0], oS[0], oL[0]);
-    cell<LOCAL, MASKED, CODES, TRACK>(st.b, st.a.Dd, st.a.SM, st.a.L, c2, c1b, act, t, sc, oI[1], oD[1], oS[1],
-                                      oL[1]);
+    cell<LOCAL, MASKED, CODES, TRACK>(st.a, dd_in, sm_in, l_in, e_in, c2, c1a, act, t, sc, oI[0], oD[0], oS[0],
+                                      oL[0]);
+    cell<LOCAL, MASKED, CODES, TRACK>(st.b, st.a.Dd, st.a.SM, st.a.L, st.a.E, c2, c1b, act, t, sc, oI[1], oD[1],
+                                      oS[1], oL[1]);
     st.c2c = c2;
 }
 
@@ -315,6 +356,7 @@ struct WaveCtx {
     lds_int* wcnt_in;
     lds_int* wcnt_out;
     int* status;
+    int* skel;                                              // skeleton row of this strip (bottom-row E)
     int m, lane, c1a, c1b;
     unsigned tr_win;
 };
@@ -337,13 +379,15 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
     int bI[4][2], bD[4][2], bS[4][2], bL[4][2];
     // lane 63 holds column t+U-63 before step U: push it (m63 = 0 when there is
     // no consumer); the last push of the group also publishes the counter
-    push63<4 * G4 + 0, TRACK>(out_base, st, m63);
+    const int* sk = uniform_ptr(w.skel + (t0 - (kWave - 1)));   // column of step t0's push
+    push63<4 * G4 + 0, TRACK>(out_base, st, m63, sk);
     dp_step<LOCAL, false, CODES, TRACK>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
-    push63<4 * G4 + 1, TRACK>(out_base, st, m63);
+    push63<4 * G4 + 1, TRACK>(out_base, st, m63, sk);
     dp_step<LOCAL, false, CODES, TRACK>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
-    push63<4 * G4 + 2, TRACK>(out_base, st, m63);
+    push63<4 * G4 + 2, TRACK>(out_base, st, m63, sk);
     dp_step<LOCAL, false, CODES, TRACK>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
-    push63_pub<4 * G4 + 3, TRACK>(out_base, st, m63, lds_addr((const void*)w.wcnt_out), t + 3 - (kWave - 1) + 1);
+    push63_pub<4 * G4 + 3, TRACK>(out_base, st, m63, sk, lds_addr((const void*)w.wcnt_out),
+                                  t + 3 - (kWave - 1) + 1);
     dp_step<LOCAL, false, CODES, TRACK>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, sc, bI[3], bD[3], bS[3], bL[3]);
     if (PLANES) {
         // per row: 16 B per lane, 1 KiB per wave; base (uniform) + lane*16 B + immediate
@@ -381,7 +425,7 @@ __device__ __forceinline__ void ramp_block(LaneState& st, Rec (&nxt)[4], WaveCtx
         // c - 256, which a lagging consumer may not have read yet
         const int col = t - (kWave - 1);
         const unsigned long long mk = lane63_mask(has_consumer && col >= 0 && col <= m);
-        push63_rt<TRACK>(lds_addr(w.ring_out + ring_slot(col)), st, mk);
+        push63_rt<TRACK>(lds_addr(w.ring_out + ring_slot(col)), st, mk, uniform_ptr(w.skel), (uint32_t)col * 4u);
         int oI[2], oD[2], oS[2], oL[2];
         dp_step<LOCAL, true, CODES, TRACK>(st, r, t, w.lane, m, w.c1a, w.c1b, sc, oI, oD, oS, oL);
         if (PLANES) {
@@ -443,6 +487,8 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         w.codes = CODES ? P.codes + (size_t)s * P.t16 * kWave * kRowsPerLane : nullptr;
     }
     w.ring_in = ring_in; w.ring_out = ring_out; w.wcnt_in = wcnt_in; w.wcnt_out = wcnt_out; w.status = status;
+    // skeleton row (only stored when there is a strip below); any valid address otherwise (exec = 0)
+    w.skel = has_consumer ? P.skel + (size_t)s * P.skel_stride : P.skel;
     w.m = m; w.lane = lane;
     w.c1a = ok_a ? (int)P.c1[ia - 1] : 0x1FF;   // 0x1FF never equals a byte
     w.c1b = ok_b ? (int)P.c1[ia] : 0x1FF;
@@ -455,6 +501,11 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     init_row(st.b, ia + 1, ok_b, sc);
     st.c2c = 0;
     st.b.SMtl = st.a.SM;                          // (A, 0) is row B's top-left for column 1
+    // landing columns of column 0: the path reaches column 0 at its own local row
+    st.a.E = -(kRowsPerLane * lane + 1);
+    st.b.E = -(kRowsPerLane * lane + 2);
+    st.b.Etl = st.a.E;
+    st.a.lE = 0; st.b.lE = 0;
 
     if (has_consumer) {
         if (lane == kWave - 1) ring_out[ring_slot(0)] = Rec{st.b.Dd, st.b.SM, 0, st.b.L};
@@ -473,6 +524,7 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         const Rec r0 = ring_in[ring_slot(0)];
         // lane 0: (row above the strip, 0); other lanes: row B of lane-1 at column 0
         st.a.SMtl = shr1(r0.sm, st.b.SM);
+        st.a.Etl = shr1(0, st.b.E);               // lane 0: (128s, 0) itself
         st.a.Ltl = 0;
         read4(nxt, ring_in + ring_slot(1));
     }
@@ -513,7 +565,7 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         const int la = (LOCAL && ok_a) ? st.a.lbest : INT_MIN, lb2 = (LOCAL && ok_b) ? st.b.lbest : INT_MIN;
         const bool lbb = lb2 >= la && ok_b;
         const int lbest = lbb ? lb2 : la;
-        const int lstep = lbb ? st.b.lstep : st.a.lstep, lh = lbb ? 1 : 0;
+        const int lstep = lbb ? st.b.lstep : st.a.lstep, lh = lbb ? 1 : 0, lE = lbb ? st.b.lE : st.a.lE;
         const bool any_ok = ok_a;
         int mx = best, lmx = lbest;
         for (int off = 32; off > 0; off >>= 1) {
@@ -525,17 +577,17 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         const int fl = fmask ? (__ffsll((long long)fmask) - 1) : 0;           // lowest lane
         const int ll = lmask ? (63 - __clzll((long long)lmask)) : 0;          // highest lane
         const int f_step = __shfl(bstep, fl), f_l = __shfl(bl, fl), f_h = __shfl(bh, fl);
-        const int l_step = __shfl(lstep, ll), l_h = __shfl(lh, ll);
+        const int l_step = __shfl(lstep, ll), l_h = __shfl(lh, ll), l_E = __shfl(lE, ll);
         if (lane == 0) {
             StripRes r;
             r.best = mx; r.bi = s * kStripRows + kRowsPerLane * fl + f_h + 1; r.bj = f_step - fl + 1; r.bl = f_l;
-            r.lbest = lmx; r.li = s * kStripRows + kRowsPerLane * ll + l_h + 1; r.lj = l_step - ll + 1; r.valid = 1;
+            r.lbest = lmx; r.li = s * kStripRows + kRowsPerLane * ll + l_h + 1; r.lj = l_step - ll + 1; r.lE = l_E;
             sres[strip_base + s] = r;
         }
     }
     // cell (n, m) for the global-mode start (algo.rs:308, 331)
-    if (ok_a && ia == n) pres->end_SM = st.a.SM;
-    if (ok_b && ia + 1 == n) pres->end_SM = st.b.SM;
+    if (ok_a && ia == n) { pres->end_SM = st.a.SM; pres->end_E = st.a.E; }
+    if (ok_b && ia + 1 == n) { pres->end_SM = st.b.SM; pres->end_E = st.b.E; }
     if (tracing && lane == 0) {
         StripTrace tr;
         tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
@@ -664,40 +716,42 @@ __global__ void finalize_kernel(const PairDev* __restrict__ pairs, const StripRe
     const int p = blockIdx.x;
     const PairDev& P = pairs[p];
     if (threadIdx.x != 0) return;
-    int best = INT_MIN, bi = 0, bj = 0, bl = 0, lbest = INT_MIN, li = 0, lj = 0;
+    int best = INT_MIN, bi = 0, bj = 0, bl = 0, lbest = INT_MIN, li = 0, lj = 0, lE = 0;
     for (int s = 0; s < P.strips; ++s) {
         const StripRes r = sres[P.strip_base + s];
         if (r.best > best) { best = r.best; bi = r.bi; bj = r.bj; bl = r.bl; }
-        if (r.lbest >= lbest) { lbest = r.lbest; li = r.li; lj = r.lj; }
+        if (r.lbest >= lbest) { lbest = r.lbest; li = r.li; lj = r.lj; lE = r.lE; }
     }
     PairRes& o = pres[p];
     o.max_val = best; o.max_i = bi; o.max_j = bj; o.mam = bl;
-    o.lmax_val = lbest; o.lmax_i = li; o.lmax_j = lj; o.nstrips = P.strips;
+    o.lmax_val = lbest; o.lmax_i = li; o.lmax_j = lj; o.nstrips = P.strips; o.lmax_E = lE;
 }
 
-// Traceback walk over the direction codes (algo.rs:339-422), interior cells
-// only; the host finishes the boundary part and labels the moves.
+// Traceback (algo.rs:339-422), interior cells only; the host finishes the
+// boundary part and labels the moves.
 //
-// Row view of the walk: on row i the path is a run of insert moves (j-1)
-// that ends at the nearest cell to the left whose code is not "insert",
-// followed by one sub (i-1, j-1) or delete (i-1, j) move.  The cells of one
-// row are consecutive steps of its code words, so a row is a bit-scan of the
-// "not insert" mask D | ~I.  Output: one record per row, (run << 2) | kind,
-// kind 0 = sub, 2 = delete, 1 = the run reached column 0.
-//
-// Lane-parallel fixed point, one wave per pair and 64 rows (half a fill
-// strip) at a time: lane k guesses the column at which the path enters its
-// row (first guess: the diagonal from the block's entry), every lane scans
-// its own row at once, and each lane's next guess becomes the exit column of
-// the lane above (DPP wave_shl:1).  The top lane's entry is known, so after
-// round r the top r lanes are exact; the iteration stops at the fixed point,
-// which IS the sequential walk.  The block's code window (kTbWin words = 512
-// steps of each of its 64 rows) is read from LDS, filled by LDS-DMA
-// (global_load_lds) while the previous block was walked; words below the
-// window are read from HBM.
+// 1. Skeleton chase (tb_chase_kernel, one lane per pair): the fill stored,
+//    for every strip's bottom row, the landing column E of the traceback path
+//    through each cell on the strip's top boundary (gx_internal.h).  Starting
+//    from E of the start cell, a chain of lookups gives the column at which
+//    the path enters every strip above -- about n/128 dependent loads.
+// 2. Strip walks (tb_strip_kernel, one wave per strip on the path, all in
+//    parallel): each walks its strip from its entry cell to its top boundary.
+//    Row view: on row i the path is a run of insert moves (j-1) ending at the
+//    nearest cell to the left whose code is not "insert", followed by one sub
+//    (i-1, j-1) or delete (i-1, j) move; the cells of a row are consecutive
+//    steps of its code words, so a row is a bit-scan of the "not insert" mask
+//    D | ~I.  One record per row, (run << 2) | kind (0 sub, 2 delete, 1 = the
+//    run reached column 0).  The 64 rows of a block are solved as a
+//    lane-parallel fixed point: lane k guesses its row's entry column (the
+//    diagonal from the block's entry), all lanes scan at once, and each lane's
+//    next guess is the exit column of the lane above (DPP wave_shl:1); the top
+//    lane's entry is known, so the iteration ends at the sequential walk.  A
+//    block's code window (kTbWin words per row) is read from LDS (LDS-DMA,
+//    the next block prefetched) with a per-lane "nearest non-insert below
+//    this word" table, so a round is two LDS reads and no loop.
 constexpr int kTbWin = 32;
-constexpr int kTbRows = 64;   // rows per walked block (half a fill strip)
-constexpr int kTbBufs = 3;    // windows in flight: current + two prefetched blocks
+constexpr int kTbRows = 64;   // rows per walked block (half a fill strip); lane = row
 
 __device__ __forceinline__ int tb_q0(int t) {
     return __builtin_amdgcn_readfirstlane(max((t >> 4) - (kTbWin - 1), 0));
@@ -708,6 +762,7 @@ typedef __attribute__((address_space(3))) void lvoid;
 typedef __attribute__((address_space(3))) const uint32_t lu32;
 typedef __attribute__((address_space(3))) int lint;
 typedef __attribute__((address_space(1))) const uint32_t gcu32;
+typedef __attribute__((address_space(1))) const int gcint;
 
 // Code word of row-in-strip rho, word q of strip s (codes[strip][q][rho]).
 __device__ __forceinline__ size_t tb_word(const TbDev& J, int s, int q, int rho) {
@@ -717,139 +772,134 @@ __device__ __forceinline__ size_t tb_word(const TbDev& J, int s, int q, int rho)
 // async: words q0 .. q0+kTbWin-1 of block vb (rows 64*vb .. +63), lane = row -> buf[k][lane]
 __device__ __forceinline__ void tb_prefetch(uint32_t* buf, const TbDev& J, int vb, int q0, int lane) {
     const int s = vb >> 1, rho = ((vb & 1) << 6) + lane;
-    // always exactly kTbWin loads (clamped): the block loop's vmcnt accounting relies on it
 #pragma unroll
     for (int k = 0; k < kTbWin; ++k)
         __builtin_amdgcn_global_load_lds((gcvoid*)(J.codes + tb_word(J, s, min(q0 + k, J.t16 - 1), rho)),
                                          (lvoid*)(buf + k * kWave), 4, 0, 0);
 }
 
-// Window top (in code words) of block vb when it is entered at its lane 63 no
-// further right than column ce.
-__device__ __forceinline__ int tb_top_q0(int vb, int ce) {
-    return tb_q0(ce - 1 + ((((vb & 1) << 6) + kTbRows - 1) >> 1));
-}
-
-__global__ __launch_bounds__(64) void traceback_kernel(const TbDev* __restrict__ jobs) {
-    __shared__ uint32_t tbuf[kTbBufs][kTbWin * kWave];
-    __shared__ int tbl[kTbWin * kWave];   // nearest non-insert step below each word, (step << 1) | del
+__global__ void tb_chase_kernel(const TbDev* __restrict__ jobs) {
     const TbDev J = jobs[blockIdx.x];
-    const int lane = threadIdx.x;
+    if (threadIdx.x != 0) return;
     int i = J.start_i, j = J.start_j;
-    int nrec = 0, rounds = 0;
-    guint* const recs = (guint*)J.recs;
-    gcu32* const codes = (gcu32*)J.codes;
-    lint* const ltbl = (lint*)(uintptr_t)lds_addr(tbl);
+    int first = -1;
     if (i >= 1 && j >= 1) {
-        int vb = __builtin_amdgcn_readfirstlane((i - 1) / kTbRows);   // walked block (64 rows)
-        int R = __builtin_amdgcn_readfirstlane((i - 1) % kTbRows);    // path's top lane in the block
-        int ce = __builtin_amdgcn_readfirstlane(j);                   // its entry column
-        // step of row-in-strip rho at column j: t = j - 1 + rho/2
-        // windows: current block (q_c, buffer b_c), the block above (q_1, b_1) and
-        // the one above that (q_2, b_2); blocks above are entered no further right
-        // than column ce
-        int b_c = 0, b_1 = 1, b_2 = 2;
-        int q_c = tb_q0(ce - 1 + ((((vb & 1) << 6) + R) >> 1)), q_1 = 0, q_2 = 0;
-        tb_prefetch(tbuf[b_c], J, vb, q_c, lane);
-        if (vb > 0) { q_1 = tb_top_q0(vb - 1, ce); tb_prefetch(tbuf[b_1], J, vb - 1, q_1, lane); }
+        int s = (i - 1) / kStripRows;
+        first = s;
+        J.seg[4 * s + 0] = i; J.seg[4 * s + 1] = j; J.seg[4 * s + 3] = 1;
+        int E = J.start_E;
         for (;;) {
-            // this block's window has landed: VMEM ops complete in issue order, and
-            // at least one full younger prefetch (kTbWin loads) follows it unless
-            // this is the top block
-            if (vb > 0) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(kTbWin) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const int q0 = q_c;
-            if (vb > 1) { q_2 = tb_top_q0(vb - 2, ce); tb_prefetch(tbuf[b_2], J, vb - 2, q_2, lane); }
-            const lu32* win = (const lu32*)(uintptr_t)lds_addr(tbuf[b_c]);
-            const int s = vb >> 1;
-            const int rho = ((vb & 1) << 6) + lane;
-            const int lo_t = rho >> 1;         // step of column 1 on this row
-            // per lane: nearest non-insert step strictly below each window word,
-            // (step << 1) | delete-bit, -1 if none in the window (branch-free)
-            {
-                int run = -1;
-#pragma unroll 8
-                for (int x = 0; x < kTbWin; ++x) {
-                    ltbl[x * kWave + lane] = run;
-                    const uint32_t w = win[x * kWave + lane];
-                    const uint32_t m = ((w >> 16) | ~w) & 0xFFFFu;
-                    const int k = 15 - (int)__builtin_ctz(m | 0x10000u);
-                    const int cand = ((16 * (q0 + x) + k) << 1) | (int)((w >> ((31 - k) & 31)) & 1u);
-                    run = m ? cand : run;
-                }
-            }
-            const bool act = lane <= R;
-            const bool top_row = vb == 0 && lane == 0;
-            int g = ce - (R - lane);           // diagonal guess of this row's entry column
-            int rec = 0, nj = 0;
-            bool end = true, run_end = false;
-            for (;;) {
-                // evaluate every lane's row from its current guess, branch-free:
-                // the word holding the entry step and the table entry below it
-                // are read together; the rare scan below the window is separate
-                const bool valid = act && g >= 1;
-                const int t_in = g - 1 + lo_t;
-                const int x = (t_in >> 4) - q0;
-                const int xc = min(max(x, 0), kTbWin - 1);
-                const uint32_t w = win[xc * kWave + lane];
-                const int tb = ltbl[xc * kWave + lane];
-                const uint32_t nonI = ((w >> 16) | ~w) & ((0xFFFFu << (15 - (t_in & 15))) & 0xFFFFu);
-                const int kw = 15 - (int)__builtin_ctz(nonI | 0x10000u);
-                int tf = nonI ? (t_in & ~15) + kw : (tb >> 1);
-                int del = nonI ? (int)((w >> ((31 - kw) & 31)) & 1u) : (tb & 1);
-                const bool need_scan = valid && (x < 0 || (!nonI && tb < 0 && 16 * q0 > lo_t));
-                if (__builtin_amdgcn_ballot_w64(need_scan)) {
-                    if (need_scan) {           // below the window: scan the HBM words
-                        int t = x < 0 ? t_in : 16 * q0 - 1;
-                        tf = -1; del = 0;
-                        while (t >= lo_t) {
-                            const uint32_t wg = codes[tb_word(J, s, t >> 4, rho)];
-                            const uint32_t ng = ((wg >> 16) | ~wg) & ((0xFFFFu << (15 - (t & 15))) & 0xFFFFu);
-                            if (ng) {
-                                tf = (t & ~15) + (15 - __builtin_ctz(ng));
-                                del = (wg >> (31 - (tf & 15))) & 1u;
-                                break;
-                            }
-                            t = (t & ~15) - 1;
-                        }
-                    }
-                }
-                run_end = valid && tf < lo_t;  // (i, g..1) all insert: the walk leaves at (i, 0)
-                nj = tf - lo_t + del;          // del ? tf-lo_t+1 : tf-lo_t
-                end = !valid || run_end || nj < 1 || top_row;
-                rec = run_end ? ((g << 2) | 1) : (((t_in - tf) << 2) | (del << 1));
-                // next guess: the exit column of the lane above; the top lane's entry is fixed
-                const int prop = end ? 0 : nj;
-                int gn = __builtin_amdgcn_update_dpp(0, prop, 0x130 /* wave_shl:1 */, 0xF, 0xF, false);
-                gn = lane == R ? ce : gn;
-                ++rounds;
-                if (__builtin_amdgcn_ballot_w64(act && gn != g) == 0) break;
-                g = gn;
-            }
-            // the path covers lanes R down to the first lane (from the top) where it ends
-            const unsigned long long em = __builtin_amdgcn_ballot_w64(act && end);
-            const int E = em ? 63 - __builtin_clzll(em) : -1;
-            const int lo = E >= 0 ? E : 0;
-            if (act && lane >= lo) recs[nrec + (R - lane)] = (uint32_t)rec;
-            nrec += R - lo + 1;
-            if (E >= 0) {                      // the walk leaves the interior in this block
-                const bool re = __builtin_amdgcn_readlane((int)run_end, E) != 0;
-                const int jE = __builtin_amdgcn_readlane(nj, E);
-                if (re) { i = vb * kTbRows + E + 1; j = 0; }
-                else { i = vb * kTbRows + E; j = jE; }
-                break;
-            }
-            ce = __builtin_amdgcn_readlane(nj, 0);
-            vb -= 1;
-            R = kTbRows - 1;
-            {   // rotate the windows (the prefetched ones were sized for an entry no
-                // further right than the previous one: always true)
-                const int b = b_c; b_c = b_1; b_1 = b_2; b_2 = b;
-                q_c = q_1; q_1 = q_2;
-            }
+            if (E < 0) { i = s * kStripRows - E; j = 0; break; }    // reaches (i, 0) at local row -E
+            if (s == 0 || E == 0) { i = s * kStripRows; j = E; break; }   // lands on row 0 / column 0
+            s -= 1;                                               // enters strip s at its bottom row
+            J.seg[4 * s + 0] = (s + 1) * kStripRows; J.seg[4 * s + 1] = E; J.seg[4 * s + 3] = 1;
+            E = ((gcint*)J.skel)[(size_t)s * J.skel_stride + E];
         }
     }
-    if (lane == 0) { *J.nrecs = nrec; J.end_ij[0] = i; J.end_ij[1] = j; J.end_ij[2] = rounds; }
+    J.end_ij[0] = i; J.end_ij[1] = j; J.end_ij[2] = first;
+}
+
+__global__ __launch_bounds__(64) void tb_strip_kernel(const TbDev* __restrict__ jobs) {
+    __shared__ uint32_t tbuf[2][kTbWin * kWave];
+    __shared__ int tbl[kTbWin * kWave];   // nearest non-insert step below each word, (step << 1) | del
+    const TbDev J = jobs[blockIdx.y];
+    const int ss = blockIdx.x;            // strip
+    if (ss >= J.strips) return;
+    const int active = __builtin_amdgcn_readfirstlane(((gcint*)J.seg)[4 * ss + 3]);
+    if (!active) return;
+    const int lane = threadIdx.x;
+    const int i0 = __builtin_amdgcn_readfirstlane(((gcint*)J.seg)[4 * ss + 0]);
+    const int j0 = __builtin_amdgcn_readfirstlane(((gcint*)J.seg)[4 * ss + 1]);
+    guint* const recs = (guint*)(J.recs + (size_t)ss * kStripRows);
+    gcu32* const codes = (gcu32*)J.codes;
+    lint* const ltbl = (lint*)(uintptr_t)lds_addr(tbl);
+    const int vb_top = 2 * ss;            // the strip's top block
+    int vb = (i0 - 1) / kTbRows;          // current block
+    int R = (i0 - 1) % kTbRows;           // the path's top lane in it
+    int ce = j0;                          // its entry column
+    int nrec = 0;
+    int cb = 0;
+    int q_c = tb_q0(ce - 1 + ((((vb & 1) << 6) + R) >> 1));
+    tb_prefetch(tbuf[cb], J, vb, q_c, lane);
+    for (;;) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         // this block's window has landed
+        // the block above (if in this strip) is entered at its lane 63, no further right than ce
+        const int q_n = vb > vb_top ? tb_q0(ce - 1 + ((((vb - 1) & 1) << 6) + kTbRows - 1) / 2) : 0;
+        if (vb > vb_top) tb_prefetch(tbuf[cb ^ 1], J, vb - 1, q_n, lane);
+        const int q0 = q_c;
+        const lu32* win = (const lu32*)(uintptr_t)lds_addr(tbuf[cb]);
+        const int rho = ((vb & 1) << 6) + lane;
+        const int lo_t = rho >> 1;        // step of column 1 on this row
+        {   // per lane: nearest non-insert step strictly below each window word (branch-free)
+            int run = -1;
+#pragma unroll 8
+            for (int x = 0; x < kTbWin; ++x) {
+                ltbl[x * kWave + lane] = run;
+                const uint32_t w = win[x * kWave + lane];
+                const uint32_t m = ((w >> 16) | ~w) & 0xFFFFu;
+                const int k = 15 - (int)__builtin_ctz(m | 0x10000u);
+                const int cand = ((16 * (q0 + x) + k) << 1) | (int)((w >> ((31 - k) & 31)) & 1u);
+                run = m ? cand : run;
+            }
+        }
+        const bool act = lane <= R;
+        const bool top_row = vb == vb_top && lane == 0;   // its move leaves the strip
+        int g = ce - (R - lane);          // diagonal guess of this row's entry column
+        int rec = 0, nj = 0;
+        bool end = true, run_end = false;
+        for (;;) {
+            const bool valid = act && g >= 1;
+            const int t_in = g - 1 + lo_t;
+            const int x = (t_in >> 4) - q0;
+            const int xc = min(max(x, 0), kTbWin - 1);
+            const uint32_t w = win[xc * kWave + lane];
+            const int tb = ltbl[xc * kWave + lane];
+            const uint32_t nonI = ((w >> 16) | ~w) & ((0xFFFFu << (15 - (t_in & 15))) & 0xFFFFu);
+            const int kw = 15 - (int)__builtin_ctz(nonI | 0x10000u);
+            int tf = nonI ? (t_in & ~15) + kw : (tb >> 1);
+            int del = nonI ? (int)((w >> ((31 - kw) & 31)) & 1u) : (tb & 1);
+            const bool need_scan = valid && (x < 0 || (!nonI && tb < 0 && 16 * q0 > lo_t));
+            if (__builtin_amdgcn_ballot_w64(need_scan)) {
+                if (need_scan) {          // below the window (rare): scan the HBM words
+                    int t = x < 0 ? t_in : 16 * q0 - 1;
+                    tf = -1; del = 0;
+                    while (t >= lo_t) {
+                        const uint32_t wg = codes[tb_word(J, ss, t >> 4, rho)];
+                        const uint32_t ng = ((wg >> 16) | ~wg) & ((0xFFFFu << (15 - (t & 15))) & 0xFFFFu);
+                        if (ng) {
+                            tf = (t & ~15) + (15 - __builtin_ctz(ng));
+                            del = (wg >> (31 - (tf & 15))) & 1u;
+                            break;
+                        }
+                        t = (t & ~15) - 1;
+                    }
+                }
+            }
+            run_end = valid && tf < lo_t;     // (i, g..1) all insert: the walk leaves at (i, 0)
+            nj = tf - lo_t + del;             // del ? tf-lo_t+1 : tf-lo_t
+            end = !valid || run_end || nj < 1 || top_row;
+            rec = run_end ? ((g << 2) | 1) : (((t_in - tf) << 2) | (del << 1));
+            // next guess: the exit column of the lane above; the top lane's entry is fixed
+            const int prop = end ? 0 : nj;
+            int gn = __builtin_amdgcn_update_dpp(0, prop, 0x130 /* wave_shl:1 */, 0xF, 0xF, false);
+            gn = lane == R ? ce : gn;
+            if (__builtin_amdgcn_ballot_w64(act && gn != g) == 0) break;
+            g = gn;
+        }
+        // the path covers lanes R down to the first lane (from the top) where it ends
+        const unsigned long long em = __builtin_amdgcn_ballot_w64(act && end);
+        const int E = em ? 63 - __builtin_clzll(em) : -1;
+        const int lo = E >= 0 ? E : 0;
+        if (act && lane >= lo) recs[nrec + (R - lane)] = (uint32_t)rec;
+        nrec += R - lo + 1;
+        if (E >= 0) break;                // the walk leaves the strip (or the interior) here
+        ce = __builtin_amdgcn_readlane(nj, 0);
+        vb -= 1;
+        R = kTbRows - 1;
+        cb ^= 1;
+        q_c = q_n;
+    }
+    if (lane == 0) ((gint*)J.seg)[4 * ss + 2] = nrec;
 }
 
 // Export: strip-major anti-diagonal planes -> row-major (n+1) x (m+1) int32
@@ -908,8 +958,11 @@ hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d
     return hipGetLastError();
 }
 
-hipError_t launch_traceback(const TbDev* d_jobs, int njobs, hipStream_t st) {
-    hipLaunchKernelGGL(traceback_kernel, dim3(njobs), dim3(64), 0, st, d_jobs);
+hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipStream_t st) {
+    hipLaunchKernelGGL(tb_chase_kernel, dim3(njobs), dim3(64), 0, st, d_jobs);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(tb_strip_kernel, dim3(max_strips, njobs), dim3(64), 0, st, d_jobs);
     return hipGetLastError();
 }
 
