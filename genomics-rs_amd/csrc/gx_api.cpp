@@ -17,6 +17,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/gx.h"
@@ -72,6 +73,19 @@ struct DevBuf {
     size_t cap = 0;
 };
 
+// Interior walk + labelling + boundary continuation (algo.rs:306-422).
+struct Walk {
+    std::vector<gx_step> steps;
+    gx_result res{};
+};
+
+// Device walk for a set of jobs; returns moves per job.
+struct TbOut {
+    std::vector<std::vector<uint8_t>> moves;
+    std::vector<int> end_i, end_j;
+    double ms = 0;
+};
+
 struct gx_context {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -82,6 +96,11 @@ struct gx_context {
     std::vector<std::vector<uint8_t>> st_s1, st_s2;
     DevBuf st_chars;
     std::vector<size_t> st_off1, st_off2;
+    // host buffers reused across calls (no fresh, page-faulting allocations per batch)
+    std::vector<Walk> walk_cache;
+    TbOut tb_cache;
+    std::vector<int> tb_c, tb_sg;
+    std::vector<uint32_t> tb_hr;
 };
 
 static int pool_get(gx_context* ctx, size_t bytes, DevBuf* out) {
@@ -422,11 +441,6 @@ struct gx_table {
 
 static int start_cell(const gx_table* t, const PairRes& r, uint64_t* si, uint64_t* sj, int64_t* score);
 
-// Interior walk + labelling + boundary continuation (algo.rs:306-422).
-struct Walk {
-    std::vector<gx_step> steps;
-    gx_result res{};
-};
 
 static bool tb_match(const uint8_t* s1, size_t n, const uint8_t* s2, size_t m, uint64_t i, uint64_t j) {
     // is_match(i, j, false) with unshifted indices: nth() past the end is None
@@ -509,12 +523,6 @@ static int label_walk(const HostScores& hs, int is_local, const uint8_t* s1, siz
     return GX_OK;
 }
 
-// Device walk for a set of jobs; returns moves per job.
-struct TbOut {
-    std::vector<std::vector<uint8_t>> moves;
-    std::vector<int> end_i, end_j;
-    double ms = 0;
-};
 
 struct TbStart {
     int i, j;   // interior start cell, or 0 = nothing to walk
@@ -558,8 +566,12 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     if (e == hipSuccess) e = hipEventRecord(ctx->ev1, ctx->stream);
     if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, max_strips, ctx->stream);
     if (e == hipSuccess) e = hipEventRecord(ctx->ev2, ctx->stream);
-    std::vector<int> c(4 * P), sg(4 * std::max<size_t>(stot, 1));
-    std::vector<uint32_t> hr(std::max<size_t>(stot, 1) * kStripRows);
+    std::vector<int>& c = ctx->tb_c;
+    std::vector<int>& sg = ctx->tb_sg;
+    std::vector<uint32_t>& hr = ctx->tb_hr;
+    c.resize(4 * P);
+    sg.resize(4 * std::max<size_t>(stot, 1));
+    hr.resize(std::max<size_t>(stot, 1) * kStripRows);
     if (e == hipSuccess) e = hipMemcpyAsync(c.data(), cnt.p, 4 * P * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(sg.data(), seg.p, sg.size() * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(hr.data(), recs.p, hr.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
@@ -863,7 +875,7 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
     }
     FillJob job;
     std::vector<PairRes> res(P, PairRes{});
-    TbOut tb;
+    TbOut& tb = ctx->tb_cache;
     std::vector<TbStart> starts(idx.size());
     std::vector<uint64_t> si(P), sj(P);
     std::vector<int64_t> score(P);
@@ -905,15 +917,35 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
                             "label %.3f ms\n", P, ms(c0, c1), fill_ms, ms(c1, c2), tb_ms, ms(c2, clk::now()));
         }
     } plog{c0, c1, c2, job.fill_ms, tb.ms, P};
-    walks.assign(P, Walk{});
+    walks.resize(P);   // keeps the step buffers of a reused vector
     std::vector<int> dev_of(P, -1);
     for (size_t k = 0; k < idx.size(); ++k) dev_of[idx[k]] = (int)k;
+    // label the walks (host, algo.rs:339-422), pairs in parallel
+    std::vector<int> prc(P, GX_OK);
+    std::vector<std::string> perr(P);
+    auto label_range = [&](size_t lo, size_t hi) {
+        for (size_t p = lo; p < hi; ++p) {
+            const uint8_t* mv = nullptr;
+            size_t nm = 0;
+            if (dev_of[p] >= 0) { mv = tb.moves[dev_of[p]].data(); nm = tb.moves[dev_of[p]].size(); }
+            prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], mv, nm, walks[p]);
+            if (prc[p]) perr[p] = g_err;   // g_err is thread-local
+        }
+    };
+    const size_t nthreads = std::min<size_t>({P, (size_t)std::max(1u, std::thread::hardware_concurrency()), 8});
+    if (nthreads <= 1) {
+        label_range(0, P);
+    } else {
+        std::vector<std::thread> th;
+        const size_t per = (P + nthreads - 1) / nthreads;
+        for (size_t w = 0; w < nthreads; ++w) {
+            const size_t lo = w * per, hi = std::min(P, lo + per);
+            if (lo < hi) th.emplace_back(label_range, lo, hi);
+        }
+        for (auto& t : th) t.join();
+    }
     for (size_t p = 0; p < P; ++p) {
-        const uint8_t* mv = nullptr;
-        size_t nm = 0;
-        if (dev_of[p] >= 0) { mv = tb.moves[dev_of[p]].data(); nm = tb.moves[dev_of[p]].size(); }
-        rc = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], mv, nm, walks[p]);
-        if (rc) return rc;
+        if (prc[p]) return fail(prc[p], perr[p]);
         Walk& w = walks[p];
         const bool interior = ph[p].n >= 1 && ph[p].m >= 1 && track;
         w.res.score = score[p];
@@ -1007,7 +1039,7 @@ extern "C" int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_lo
         ph[p] = PairHost{ctx->st_s1[p].data(), ctx->st_s2[p].data(), ctx->st_s1[p].size(), ctx->st_s2[p].size()};
         proc[p] = {ph[p].s1, ph[p].s2};
     }
-    std::vector<Walk> walks;
+    std::vector<Walk>& walks = ctx->walk_cache;
     double fms = 0;
     rc = batch_core(ctx, ph, proc, hs, sc, is_local, keep_planes != 0, (flags & GX_ALIGN_MAX_CELL) != 0, walks, &fms,
                     (const uint8_t*)ctx->st_chars.p, &ctx->st_off1, &ctx->st_off2);
