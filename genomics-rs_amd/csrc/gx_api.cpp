@@ -24,7 +24,7 @@
 #include "gx_internal.h"
 
 namespace gx {
-hipError_t launch_fill(bool local, bool planes, bool track, bool lcs, const PairDev* d_pairs, int npairs,
+hipError_t launch_fill(int W, bool local, bool planes, bool track, bool lcs, const PairDev* d_pairs, int npairs,
                        int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                        hipStream_t st);
 hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d_sres, PairRes* d_pres,
@@ -253,14 +253,28 @@ static int processed_chars(const uint8_t* s1, size_t n, const uint8_t* s2, size_
 // ---------------------------------------------------------------------------
 // fill orchestration
 
-static int fill_grid_cap() {
-    static int g = -1;
-    if (g < 0) {
-        const char* e = getenv("GX_FILL_GRID");
-        g = e ? atoi(e) : 1024;
-        if (g < 1) g = 1024;
+// Persistent fill workgroups: one per CU by default (bands beyond the grid
+// are taken from the queue as earlier bands finish; a band deep in a pair
+// starts late anyway, so it loses little, and no CU runs two bands' waves).
+static int fill_grid_cap(int device) {
+    if (const char* e = getenv("GX_FILL_GRID"); e && atoi(e) > 0) return atoi(e);
+    static int cus = -1;
+    if (cus < 0) {
+        int c = 0;
+        if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c < 1) c = 256;
+        cus = c;
     }
-    return g;
+    return cus;
+}
+
+// Band width: narrow bands while the whole job fits one band per CU with
+// them (a strip's own speed sets the time), wide bands otherwise.
+static int fill_band_waves(int total_strips, int grid_cap) {
+    if (const char* e = getenv("GX_BAND_WAVES")) {
+        const int w = atoi(e);
+        if (w == kBandWavesNarrow || w == kBandWavesWide) return w;
+    }
+    return total_strips <= kBandWavesNarrow * grid_cap ? kBandWavesNarrow : kBandWavesWide;
 }
 
 struct PairHost {
@@ -296,7 +310,9 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                     const std::vector<PairHost>& ph, const Scores32& sc, int is_local, bool planes, bool track,
                     bool lcs, FillJob& job, const uint8_t* chars_dev = nullptr,
                     const std::vector<size_t>* off1 = nullptr, const std::vector<size_t>* off2 = nullptr) {
-    const int W = kBandWaves;
+    int total_strips = 0;
+    for (const PairHost& h : ph) total_strips += ceil_div((int)h.n, kStripRows);
+    const int W = fill_band_waves(total_strips, fill_grid_cap(ctx->device));
     const bool codes = true;
     lcs = lcs && planes;
     track = track || lcs;
@@ -384,11 +400,11 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     HIPCHK(hipMemsetAsync(job.progress.p, 0, std::max<size_t>(prog_elems, 1) * sizeof(int), ctx->stream));
     HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, ctx->stream));
     HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), ctx->stream));
-    const int grid = std::min(bands, fill_grid_cap());
+    const int grid = std::min(bands, fill_grid_cap(ctx->device));
     const auto h_launch = std::chrono::steady_clock::now();
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     if (bands > 0)
-        HIPCHK(launch_fill(is_local != 0, planes, track, lcs, (const PairDev*)job.pairs.p, (int)P, bands,
+        HIPCHK(launch_fill(W, is_local != 0, planes, track, lcs, (const PairDev*)job.pairs.p, (int)P, bands,
                            (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, sc, grid, ctx->stream));
     HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));   // ev0..ev1 brackets the fill kernel alone
     if (bands > 0)
@@ -412,11 +428,12 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         HIPCHK(hipMemcpy(tr.data(), trace.p, tr.size() * sizeof(StripTrace), hipMemcpyDeviceToHost));
         pool_put(ctx, trace);
         if (FILE* f = fopen(trace_file, "w")) {
-            fprintf(f, "pair,strip,t_start,t_first,t_end,wait_in,wait_out,W,fill_ms\n");
+            fprintf(f, "pair,strip,band,t_start,t_first,t_end,wait_in,wait_out,W,fill_ms\n");
             for (size_t p = 0; p < P; ++p)
                 for (int s = 0; s < job.pd[p].strips; ++s) {
                     const StripTrace& t = tr[job.pd[p].strip_base + s];
-                    fprintf(f, "%zu,%d,%lld,%lld,%lld,%d,%d,%d,%.4f\n", p, s, t.t_start, t.t_first, t.t_end, t.wait_in,
+                    fprintf(f, "%zu,%d,%d,%lld,%lld,%lld,%d,%d,%d,%.4f\n", p, s, job.pd[p].band_base + s / W,
+                            t.t_start, t.t_first, t.t_end, t.wait_in,
                             t.wait_out, W, ms);
                 }
             fclose(f);

@@ -5,8 +5,9 @@
 //   (strip k = rows 128k+1 .. 128k+128; lane l owns rows 128k+2l+1 and
 //   128k+2l+2, "row-in-lane" h = 0, 1).  One wave sweeps a strip along the
 //   anti-diagonal skew: at step t lane l computes column j = t - l + 1 for both
-//   its rows, so a strip takes T = m + 64 steps.  kBandWaves strips form a
-//   BAND, processed by one workgroup (one wave per strip + one I/O wave).
+//   its rows, so a strip takes T = m + 64 steps.  W strips (W = kBandWavesWide
+//   or kBandWavesNarrow, chosen per launch) form a BAND, processed by one
+//   workgroup (one wave per strip + one I/O wave).
 //
 //   Score planes (int32, one each for insert/delete/sub score):
 //       plane[strip][t/4][h][lane][t%4]     (16 B per lane per row per 4 steps)
@@ -30,11 +31,12 @@ constexpr int kStripRows = kWave * kRowsPerLane;   // 128 rows per strip
 // Plane layout (ints): plane[strip][t/4][row-in-lane][lane][t%4]; one 4-step
 // group of one row is 1 KiB contiguous per wave.
 constexpr int kGroupInts = kRowsPerLane * kWave * 4;
-// Compute waves per band (workgroup = kBandWaves compute waves + 1 I/O wave).
-#ifndef GX_BAND_WAVES
-#define GX_BAND_WAVES 7
-#endif
-constexpr int kBandWaves = GX_BAND_WAVES;
+// Compute waves per band (workgroup = W compute waves + 1 I/O wave).  Wide
+// bands (8-wave workgroups, two compute waves per SIMD) for batches that
+// fill the chip; narrow bands (one compute wave per SIMD) when few strips
+// are in flight and a strip's own speed sets the time (a single pair).
+constexpr int kBandWavesWide = 7;
+constexpr int kBandWavesNarrow = 3;
 
 // Scores narrowed to int32 after the host range guard (DESIGN.md "Integer range").
 struct Scores32 {

@@ -111,9 +111,14 @@ __device__ __forceinline__ void gstore4_at(int32_t* base, uint32_t byte_off, int
 
 
 // Occupancy floor (waves per SIMD) that caps the fill kernel's VGPRs
-// (512 / 4 = 128): with 8-wave workgroups, two bands per CU.
+// (512 / 4 = 128): with 8-wave workgroups, two bands per CU.  The variants
+// that also track the maxima (first max + LCS, local mode) carry more state
+// per row and get 256 VGPRs at one band per CU instead of spilling.
 #ifndef GX_FILL_MIN_WAVES
 #define GX_FILL_MIN_WAVES 4
+#endif
+#ifndef GX_FILL_MIN_WAVES_TRACK
+#define GX_FILL_MIN_WAVES_TRACK 2
 #endif
 
 // DP state of one row (the cell left of the one being computed, i.e. (i, j-1)
@@ -210,33 +215,6 @@ __device__ __forceinline__ const int* uniform_ptr(const int* p) {
 // "s" asm operand of the pushes must not be given a VGPR.
 __device__ __forceinline__ unsigned long long lane63_mask(bool on) {
     return (unsigned long long)__builtin_amdgcn_readfirstlane(on ? 0x80000000u : 0u) << 32;
-}
-
-// Ramp-path push with a runtime slot address and skeleton byte offset.
-template <bool TRACK>
-__device__ __forceinline__ void push63_rt(uint32_t addr, const LaneState& st, unsigned long long m63, const int* sk,
-                                          uint32_t sk_off) {
-    if (TRACK)
-        asm volatile(
-            "s_mov_b64 exec, %0\n\t"
-            "ds_write2_b32 %1, %2, %3 offset1:1\n\t"
-            "ds_write2_b32 %1, %4, %5 offset0:2 offset1:3\n\t"
-            "global_store_dword %7, %6, %8\n\t"
-            "s_mov_b64 exec, -1"
-            :
-            : "s"(m63), "v"(addr), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L), "v"(st.b.E), "v"(sk_off),
-              "s"(sk)
-            : "memory");
-    else
-        asm volatile(
-            "s_mov_b64 exec, %0\n\t"
-            "ds_write2_b32 %1, %2, %3 offset1:1\n\t"
-            "ds_write_b32 %1, %4 offset:8\n\t"
-            "global_store_dword %6, %5, %7\n\t"
-            "s_mov_b64 exec, -1"
-            :
-            : "s"(m63), "v"(addr), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.E), "v"(sk_off), "s"(sk)
-            : "memory");
 }
 
 // One lane stores an LDS counter (exec = lane 0 only, no branch).
@@ -361,14 +339,17 @@ struct WaveCtx {
     unsigned tr_win;
 };
 
-// One 4-step group of a full sub-block.  `nxt` holds validated ring records
-// for these steps.  The producer's counter is observed and the next group's
+// One 4-step group of a sub-block.  `nxt` holds validated ring records for
+// these steps.  The producer's counter is observed and the next group's
 // records are read (in that LDS order) before computing, so the read latency
 // hides behind the group; if the observed counter did not cover them, they
-// are re-read after waiting.
-template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP, int G4>
+// are re-read after waiting.  MASKED (ramp-up / ramp-down sub-blocks, some
+// lanes outside columns 1..m): state updates are masked per lane and each
+// push per step (columns 0..m only: a push past m would land on the slot of
+// column c - 256, which a lagging consumer may not have read yet).
+template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP, bool MASKED, int G4>
 __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w, const Scores32& sc,
-                                       const int t0, const uint32_t out_base, const unsigned long long m63,
+                                       const int t0, const uint32_t out_base, const bool push_on,
                                        const size_t sb_off) {
     const int t = t0 + 4 * G4;
     Rec cur[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
@@ -377,18 +358,32 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
     asm volatile("" ::: "memory");
     read4(nxt, w.ring_in + ring_slot(t + 5));
     int bI[4][2], bD[4][2], bS[4][2], bL[4][2];
-    // lane 63 holds column t+U-63 before step U: push it (m63 = 0 when there is
-    // no consumer); the last push of the group also publishes the counter
+    // lane 63 holds column t+U-63 before step U: push it (mask 0 when there is
+    // no consumer); the last push of a full group also publishes the counter
     const int* sk = uniform_ptr(w.skel + (t0 - (kWave - 1)));   // column of step t0's push
-    push63<4 * G4 + 0, TRACK>(out_base, st, m63, sk);
-    dp_step<LOCAL, false, CODES, TRACK>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
-    push63<4 * G4 + 1, TRACK>(out_base, st, m63, sk);
-    dp_step<LOCAL, false, CODES, TRACK>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
-    push63<4 * G4 + 2, TRACK>(out_base, st, m63, sk);
-    dp_step<LOCAL, false, CODES, TRACK>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
-    push63_pub<4 * G4 + 3, TRACK>(out_base, st, m63, sk, lds_addr((const void*)w.wcnt_out),
-                                  t + 3 - (kWave - 1) + 1);
-    dp_step<LOCAL, false, CODES, TRACK>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, sc, bI[3], bD[3], bS[3], bL[3]);
+    const int col0 = t - (kWave - 1);
+    if (MASKED) {
+        push63<4 * G4 + 0, TRACK>(out_base, st, lane63_mask(push_on && col0 >= 0 && col0 <= w.m), sk);
+        dp_step<LOCAL, true, CODES, TRACK>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
+        push63<4 * G4 + 1, TRACK>(out_base, st, lane63_mask(push_on && col0 + 1 >= 0 && col0 + 1 <= w.m), sk);
+        dp_step<LOCAL, true, CODES, TRACK>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
+        push63<4 * G4 + 2, TRACK>(out_base, st, lane63_mask(push_on && col0 + 2 >= 0 && col0 + 2 <= w.m), sk);
+        dp_step<LOCAL, true, CODES, TRACK>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
+        push63<4 * G4 + 3, TRACK>(out_base, st, lane63_mask(push_on && col0 + 3 >= 0 && col0 + 3 <= w.m), sk);
+        // publish the pushes (same wave, DS operations in order)
+        if (push_on && col0 + 3 >= 0 && col0 <= w.m) lds_store_lane0(w.wcnt_out, min(col0 + 3, w.m) + 1);
+        dp_step<LOCAL, true, CODES, TRACK>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, sc, bI[3], bD[3], bS[3], bL[3]);
+    } else {
+        const unsigned long long m63 = lane63_mask(push_on);
+        push63<4 * G4 + 0, TRACK>(out_base, st, m63, sk);
+        dp_step<LOCAL, false, CODES, TRACK>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
+        push63<4 * G4 + 1, TRACK>(out_base, st, m63, sk);
+        dp_step<LOCAL, false, CODES, TRACK>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
+        push63<4 * G4 + 2, TRACK>(out_base, st, m63, sk);
+        dp_step<LOCAL, false, CODES, TRACK>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
+        push63_pub<4 * G4 + 3, TRACK>(out_base, st, m63, sk, lds_addr((const void*)w.wcnt_out), col0 + 3 + 1);
+        dp_step<LOCAL, false, CODES, TRACK>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, sc, bI[3], bD[3], bS[3], bL[3]);
+    }
     if (PLANES) {
         // per row: 16 B per lane, 1 KiB per wave; base (uniform) + lane*16 B + immediate
 #pragma unroll
@@ -408,50 +403,15 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// Ramp-up / ramp-down sub-block (some lanes outside columns 1..m): a rolled
-// loop that waits for the whole sub-block's input first and masks the state
-// updates and the pushes.  At the end `nxt` is re-primed with the first group
-// of the next sub-block.
-template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP>
-__device__ __forceinline__ void ramp_block(LaneState& st, Rec (&nxt)[4], WaveCtx& w, const Scores32& sc, const int t0,
-                                           const bool has_consumer, const size_t sb_off) {
-    const int m = w.m;
-    w.tr_win += wait_ge(w.wcnt_in, min(t0 + kSub, m) + 1, w.status);
-#pragma unroll 1
-    for (int u = 0; u < kSub; ++u) {
-        const int t = t0 + u;
-        const Rec r = w.ring_in[ring_slot(t + 1)];
-        // push only columns 0..m: a push past m would land on the slot of column
-        // c - 256, which a lagging consumer may not have read yet
-        const int col = t - (kWave - 1);
-        const unsigned long long mk = lane63_mask(has_consumer && col >= 0 && col <= m);
-        push63_rt<TRACK>(lds_addr(w.ring_out + ring_slot(col)), st, mk, uniform_ptr(w.skel), (uint32_t)col * 4u);
-        int oI[2], oD[2], oS[2], oL[2];
-        dp_step<LOCAL, true, CODES, TRACK>(st, r, t, w.lane, m, w.c1a, w.c1b, sc, oI, oD, oS, oL);
-        if (PLANES) {
-#pragma unroll
-            for (int h = 0; h < kRowsPerLane; ++h) {
-                const size_t o = sb_off + (size_t)(u >> 2) * kGroupInts + h * kWave * 4 + (size_t)w.lane * 4 + (u & 3);
-                ((gint*)w.pI)[o] = oI[h];
-                ((gint*)w.pD)[o] = oD[h];
-                ((gint*)w.pS)[o] = oS[h];
-                if (LCSP) ((gint*)w.pL)[o] = oL[h];
-            }
-        }
-    }
-    const int last_col = min(t0 + kSub - 1 - (kWave - 1), m);
-    if (has_consumer && last_col >= 0) lds_store_lane0(w.wcnt_out, last_col + 1);
-    w.tr_win += wait_ge(w.wcnt_in, min(t0 + kSub + 4, m) + 1, w.status);
-    read4(nxt, w.ring_in + ring_slot(t0 + kSub + 1));
-}
-
-template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP>
+// One 16-step sub-block: four groups.  MASKED for the ramp-up (t0 < 64) and
+// ramp-down (columns past m) sub-blocks.
+template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP, bool MASKED>
 __device__ __forceinline__ void sub_block(LaneState& st, Rec (&nxt)[4], WaveCtx& w, const Scores32& sc, const int t0,
-                                          const uint32_t out_base, const unsigned long long m63, const size_t sb_off) {
-    group4<LOCAL, PLANES, CODES, TRACK, LCSP, 0>(st, nxt, w, sc, t0, out_base, m63, sb_off);
-    group4<LOCAL, PLANES, CODES, TRACK, LCSP, 1>(st, nxt, w, sc, t0, out_base, m63, sb_off);
-    group4<LOCAL, PLANES, CODES, TRACK, LCSP, 2>(st, nxt, w, sc, t0, out_base, m63, sb_off);
-    group4<LOCAL, PLANES, CODES, TRACK, LCSP, 3>(st, nxt, w, sc, t0, out_base, m63, sb_off);
+                                          const uint32_t out_base, const bool push_on, const size_t sb_off) {
+    group4<LOCAL, PLANES, CODES, TRACK, LCSP, MASKED, 0>(st, nxt, w, sc, t0, out_base, push_on, sb_off);
+    group4<LOCAL, PLANES, CODES, TRACK, LCSP, MASKED, 1>(st, nxt, w, sc, t0, out_base, push_on, sb_off);
+    group4<LOCAL, PLANES, CODES, TRACK, LCSP, MASKED, 2>(st, nxt, w, sc, t0, out_base, push_on, sb_off);
+    group4<LOCAL, PLANES, CODES, TRACK, LCSP, MASKED, 3>(st, nxt, w, sc, t0, out_base, push_on, sb_off);
 }
 
 __device__ __forceinline__ void init_row(RowState& rs, const int i, const bool row_ok, const Scores32& sc) {
@@ -536,14 +496,11 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         if (has_consumer && last_col >= kRing) tr_wout += wait_ge(rcnt_out, last_col - kRing + 1, status);
         const size_t sb_off = (size_t)(t0 >> 2) * kGroupInts;         // this sub-block's plane offset (ints)
         const bool full = (t0 >= kWave) && (t0 + kSub - 1 <= m - 1) && !rolled_only;
-        if (full) {
-            const unsigned long long m63 = lane63_mask(has_consumer);
-            sub_block<LOCAL, PLANES, CODES, TRACK, LCSP>(st, nxt, w, sc, t0,
-                                                         lds_addr(ring_out + ring_slot(t0 - (kWave - 1))), m63,
-                                                         sb_off);
-        } else {
-            ramp_block<LOCAL, PLANES, CODES, TRACK, LCSP>(st, nxt, w, sc, t0, has_consumer, sb_off);
-        }
+        const uint32_t out_base = lds_addr(ring_out + ring_slot(t0 - (kWave - 1)));
+        if (full)
+            sub_block<LOCAL, PLANES, CODES, TRACK, LCSP, false>(st, nxt, w, sc, t0, out_base, has_consumer, sb_off);
+        else
+            sub_block<LOCAL, PLANES, CODES, TRACK, LCSP, true>(st, nxt, w, sc, t0, out_base, has_consumer, sb_off);
         if (CODES) {
             // codes[strip][t/16][lane][row-in-lane]: 8 B per lane
             typedef unsigned v2u __attribute__((ext_vector_type(2)));
@@ -592,7 +549,7 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         StripTrace tr;
         tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
         tr.wait_in = (int)w.tr_win; tr.wait_out = (int)tr_wout;
-        tr.band = s / kBandWaves; tr.wave = s % kBandWaves; tr.pad0 = 0; tr.pad1 = 0;
+        tr.band = 0; tr.wave = 0; tr.pad0 = 0; tr.pad1 = 0;   // the host knows W
         trace[s] = tr;
     }
 }
@@ -669,7 +626,7 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
 }
 
 template <int W, bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP>
-__global__ __launch_bounds__((W + 1) * kWave, GX_FILL_MIN_WAVES) void fill_kernel(
+__global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAVES_TRACK : GX_FILL_MIN_WAVES) void fill_kernel(
     const PairDev* __restrict__ pairs, const int npairs, const int total_bands, int* band_counter, StripRes* sres,
     PairRes* pres, const Scores32 sc) {
     __shared__ Rec rings[W + 1][kRing];
@@ -921,10 +878,9 @@ __global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __rest
 // ---- explicit launch wrappers (C++ linkage, used by gx_api.cpp) ----
 namespace gx {
 
-template <bool LOCAL, bool PLANES, bool TRACK, bool LCSP>
+template <int W, bool LOCAL, bool PLANES, bool TRACK, bool LCSP>
 static hipError_t launch_fill_t(const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
                                 StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
-    constexpr int W = kBandWaves;
     hipLaunchKernelGGL((fill_kernel<W, LOCAL, PLANES, true, TRACK, LCSP>), dim3(grid), dim3((W + 1) * kWave), 0, st,
                        d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc);
     return hipGetLastError();
@@ -932,12 +888,16 @@ static hipError_t launch_fill_t(const PairDev* d_pairs, int npairs, int total_ba
 
 // Variants: mode (global/local) x planes x {no max tracking, first max + LCS
 // field, first max + LCS plane}.  Traceback codes are always produced.
-hipError_t launch_fill(bool local, bool planes, bool track, bool lcs, const PairDev* d_pairs, int npairs,
+hipError_t launch_fill(int W, bool local, bool planes, bool track, bool lcs, const PairDev* d_pairs, int npairs,
                        int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                        hipStream_t st) {
-#define GX_FILL_CASE(LO, PL, TR, LC)                                                                  \
-    if (local == LO && planes == PL && track == TR && lcs == LC)                                      \
-        return launch_fill_t<LO, PL, TR, LC>(d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc, grid, st);
+#define GX_FILL_CASE(LO, PL, TR, LC)                                                                        \
+    if (local == LO && planes == PL && track == TR && lcs == LC)                                            \
+        return W == kBandWavesNarrow                                                                        \
+                   ? launch_fill_t<kBandWavesNarrow, LO, PL, TR, LC>(d_pairs, npairs, total_bands, d_counter, \
+                                                                     d_sres, d_pres, sc, grid, st)          \
+                   : launch_fill_t<kBandWavesWide, LO, PL, TR, LC>(d_pairs, npairs, total_bands, d_counter,   \
+                                                                   d_sres, d_pres, sc, grid, st);
     GX_FILL_CASE(false, false, false, false)
     GX_FILL_CASE(false, false, true, false)
     GX_FILL_CASE(false, true, false, false)

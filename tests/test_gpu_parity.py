@@ -1,10 +1,12 @@
 """GPU parity: the HIP path (through the C ABI) vs the CPU oracle, bit-exact.
 
 Covers the reference's own golden vectors (tests/test_alignment.rs), the
-committed oracle fixtures, seeded random pairs around the 64-row strip and
-256-row band edges, exported score planes and full AlignmentCell tables,
+committed oracle fixtures, seeded random pairs around the 128-row strip and
+band edges, exported score planes and full AlignmentCell tables,
 reverse_sequences, batched pairs, and the large pairs of BASELINE configs 2
-and 3 through digests.
+and 3 through digests.  Every test runs under each fill launch shape: narrow
+(3-strip) and wide (7-strip) bands, and wide bands on a 2-workgroup grid
+(bands wait in the queue for a workgroup, hand-offs cross launch order).
 """
 import hashlib
 import json
@@ -17,6 +19,16 @@ import pytest
 from conftest import COMPARISON, CONFIG_SCORES, FASTA, GOLDEN, TEST_SCORES, read_fasta_records
 
 pytestmark = pytest.mark.gpu
+
+LAUNCH_SHAPES = {"narrow": {"GX_BAND_WAVES": "3"}, "wide": {"GX_BAND_WAVES": "7"},
+                 "wide_grid2": {"GX_BAND_WAVES": "7", "GX_FILL_GRID": "2"}}
+
+
+@pytest.fixture(autouse=True, params=sorted(LAUNCH_SHAPES))
+def launch_shape(request, monkeypatch):
+    for k, v in LAUNCH_SHAPES[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
 
 NAMES = ["Match", "Mismatch", "Insert", "Delete", "OpenInsert", "OpenDelete"]
 

@@ -1,0 +1,33 @@
+# GPU box: interleaved A/B timing of libraries (GX_LIB) over "P|flags" cases,
+# R rounds, to separate a change from the box's run-to-run drift.
+#   gpurun -- 'bash tools/gpu_ab.sh "libA libB" "1| 8|" 3'
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+O=gpurun_out/ab
+rm -rf "$O" && mkdir -p "$O"
+R=${3:-3}
+for r in $(seq 1 "$R"); do
+  for C in $2; do
+    for L in $1; do
+      P=${C%%|*}; F=${C#*|}
+      GX_LIB=$L timeout -k 10 300 python bench.py --pairs-per-gpu $P --steps 4 --warmup 1 --no-cpu-baseline $F \
+          > "$O/b.json" 2>> "$O/err.log" || { echo BENCH_FAIL $L $C; tail -20 "$O/err.log"; exit 1; }
+      python3 - "$L" "$C" >> "$O/ab.tsv" <<'PY'
+import json, sys
+d = json.loads(open("gpurun_out/ab/b.json").read().strip().splitlines()[-1])
+print(sys.argv[1].split("/")[-1], sys.argv[2], d["roofline"]["fill_ms_avg"], d["ms_per_step"], sep="\t")
+PY
+    done
+  done
+done
+python3 - <<'PY'
+import collections, statistics
+rows = [l.rstrip("\n").split("\t") for l in open("gpurun_out/ab/ab.tsv")]
+g = collections.defaultdict(list)
+for lib, case, f, s in rows:
+    g[(case, lib)].append((float(f), float(s)))
+for (case, lib), v in sorted(g.items()):
+    fs = [x for x, _ in v]; ss = [y for _, y in v]
+    print(f"{case:12s} {lib:18s} fill min {min(fs):7.3f} med {statistics.median(fs):7.3f}  step med {statistics.median(ss):7.3f}")
+PY
