@@ -267,14 +267,20 @@ static int fill_grid_cap(int device) {
     return cus;
 }
 
-// Band width: narrow bands while the whole job fits one band per CU with
-// them (a strip's own speed sets the time), wide bands otherwise.
-static int fill_band_waves(int total_strips, int grid_cap) {
+// Band width: the narrowest instantiated width whose bands fit the grid
+// (one band per workgroup, all strips in flight from the start), else the
+// widest.  GX_BAND_WAVES forces a width (if instantiated for the variant).
+template <size_t N>
+static int pick_width(const int (&ws)[N], int total_strips, int grid_cap) {
     if (const char* e = getenv("GX_BAND_WAVES")) {
         const int w = atoi(e);
-        if (w == kBandWavesNarrow || w == kBandWavesWide) return w;
+        for (int x : ws) if (x == w) return w;
     }
-    return total_strips <= kBandWavesNarrow * grid_cap ? kBandWavesNarrow : kBandWavesWide;
+    for (int x : ws) if (ceil_div(total_strips, x) <= grid_cap) return x;
+    return ws[N - 1];
+}
+static int fill_band_waves(bool track, int total_strips, int grid_cap) {
+    return track ? pick_width(kFillWidthsTrack, total_strips, grid_cap) : pick_width(kFillWidths, total_strips, grid_cap);
 }
 
 struct PairHost {
@@ -312,10 +318,10 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                     const std::vector<size_t>* off1 = nullptr, const std::vector<size_t>* off2 = nullptr) {
     int total_strips = 0;
     for (const PairHost& h : ph) total_strips += ceil_div((int)h.n, kStripRows);
-    const int W = fill_band_waves(total_strips, fill_grid_cap(ctx->device));
     const bool codes = true;
     lcs = lcs && planes;
     track = track || lcs;
+    const int W = fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device));
     job.W = W;
     job.planes_on = planes; job.lcs_on = lcs; job.track_on = track;
     const size_t P = ph.size();
@@ -428,12 +434,12 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         HIPCHK(hipMemcpy(tr.data(), trace.p, tr.size() * sizeof(StripTrace), hipMemcpyDeviceToHost));
         pool_put(ctx, trace);
         if (FILE* f = fopen(trace_file, "w")) {
-            fprintf(f, "pair,strip,band,t_start,t_first,t_end,wait_in,wait_out,W,fill_ms\n");
+            fprintf(f, "pair,strip,band,t_start,t_first,t_end,clk,wait_in,wait_out,W,fill_ms\n");
             for (size_t p = 0; p < P; ++p)
                 for (int s = 0; s < job.pd[p].strips; ++s) {
                     const StripTrace& t = tr[job.pd[p].strip_base + s];
-                    fprintf(f, "%zu,%d,%d,%lld,%lld,%lld,%d,%d,%d,%.4f\n", p, s, job.pd[p].band_base + s / W,
-                            t.t_start, t.t_first, t.t_end, t.wait_in,
+                    fprintf(f, "%zu,%d,%d,%lld,%lld,%lld,%lld,%d,%d,%d,%.4f\n", p, s, job.pd[p].band_base + s / W,
+                            t.t_start, t.t_first, t.t_end, t.clk, t.wait_in,
                             t.wait_out, W, ms);
                 }
             fclose(f);

@@ -5,9 +5,9 @@
 //   (strip k = rows 128k+1 .. 128k+128; lane l owns rows 128k+2l+1 and
 //   128k+2l+2, "row-in-lane" h = 0, 1).  One wave sweeps a strip along the
 //   anti-diagonal skew: at step t lane l computes column j = t - l + 1 for both
-//   its rows, so a strip takes T = m + 64 steps.  W strips (W = kBandWavesWide
-//   or kBandWavesNarrow, chosen per launch) form a BAND, processed by one
-//   workgroup (one wave per strip + one I/O wave).
+//   its rows, so a strip takes T = m + 64 steps.  W strips (W from
+//   kFillWidths, chosen per launch) form a BAND, processed by one workgroup
+//   (one wave per strip + one I/O wave).
 //
 //   Score planes (int32, one each for insert/delete/sub score):
 //       plane[strip][t/4][h][lane][t%4]     (16 B per lane per row per 4 steps)
@@ -31,12 +31,15 @@ constexpr int kStripRows = kWave * kRowsPerLane;   // 128 rows per strip
 // Plane layout (ints): plane[strip][t/4][row-in-lane][lane][t%4]; one 4-step
 // group of one row is 1 KiB contiguous per wave.
 constexpr int kGroupInts = kRowsPerLane * kWave * 4;
-// Compute waves per band (workgroup = W compute waves + 1 I/O wave).  Wide
-// bands (8-wave workgroups, two compute waves per SIMD) for batches that
-// fill the chip; narrow bands (one compute wave per SIMD) when few strips
-// are in flight and a strip's own speed sets the time (a single pair).
-constexpr int kBandWavesWide = 7;
-constexpr int kBandWavesNarrow = 3;
+// Compute waves per band (workgroup = W compute waves + 1 I/O wave).  The
+// host picks the narrowest width whose bands fit one workgroup per CU (a
+// single pair: 3, one compute wave per SIMD, so a strip's own speed sets the
+// time; a batch: wider bands, all strips in flight from the start).  The
+// launcher instantiates these widths (must match GX_W_ALL / GX_W_TRACK in
+// gx_kernels.hip); the tracked and local variants carry more state per row
+// (256-VGPR builds) and stop at 8-wave workgroups.
+constexpr int kFillWidths[] = {3, 4, 6, 8, 11, 15};
+constexpr int kFillWidthsTrack[] = {3, 7};
 
 // Scores narrowed to int32 after the host range guard (DESIGN.md "Integer range").
 struct Scores32 {
@@ -81,7 +84,7 @@ struct __attribute__((aligned(16))) StripTrace {
     long long t_end;     // strip done
     int wait_in;         // spin iterations waiting for the row above
     int wait_out;        // spin iterations waiting for ring space below
-    int band, wave;
+    long long clk;       // shader-clock ticks (s_memtime) from t_first to t_end
     int pad0, pad1;
 };
 

@@ -114,6 +114,9 @@ __device__ __forceinline__ void gstore4_at(int32_t* base, uint32_t byte_off, int
 // (512 / 4 = 128): with 8-wave workgroups, two bands per CU.  The variants
 // that also track the maxima (first max + LCS, local mode) carry more state
 // per row and get 256 VGPRs at one band per CU instead of spilling.
+#ifndef GX_CODE_VCC
+#define GX_CODE_VCC 0
+#endif
 #ifndef GX_FILL_MIN_WAVES
 #define GX_FILL_MIN_WAVES 4
 #endif
@@ -258,6 +261,7 @@ __device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm
         // cell, taken from the predecessor the priority picks.  One asm block:
         // each compare feeds its select and its code bit at once (no SGPR-pair
         // masks kept alive, no chain sunk to the end of the sub-block).
+#if GX_CODE_VCC
         asm volatile(
             "v_cmp_gt_i32 vcc, %[in], %[sn]\n\t"
             "v_cndmask_b32 %[en], %[etl], %[el], vcc\n\t"
@@ -269,6 +273,22 @@ __device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm
             : [in] "v"(In), [sn] "v"(Sn), [dn] "v"(Dn), [is] "v"(IS), [etl] "v"(st.Etl), [el] "v"(st.E),
               [eu] "v"(e_up)
             : "vcc");
+#else
+        // the two compares write their own SGPR pairs, so the selects and the
+        // code-bit shifts of the two compares overlap (no serial VCC chain)
+        unsigned long long m1, m2, k1, k2;
+        asm volatile(
+            "v_cmp_gt_i32 %[m1], %[in], %[sn]\n\t"
+            "v_cmp_gt_i32 %[m2], %[dn], %[is]\n\t"
+            "v_cndmask_b32 %[en], %[etl], %[el], %[m1]\n\t"
+            "v_addc_co_u32 %[ci], %[k1], %[ci], %[ci], %[m1]\n\t"
+            "v_addc_co_u32 %[cd], %[k2], %[cd], %[cd], %[m2]\n\t"
+            "v_cndmask_b32 %[en], %[en], %[eu], %[m2]"
+            : [en] "=&v"(En), [ci] "+v"(st.cI), [cd] "+v"(st.cD), [m1] "=&s"(m1), [m2] "=&s"(m2),
+              [k1] "=&s"(k1), [k2] "=&s"(k2)
+            : [in] "v"(In), [sn] "v"(Sn), [dn] "v"(Dn), [is] "v"(IS), [etl] "v"(st.Etl), [el] "v"(st.E),
+              [eu] "v"(e_up));
+#endif
     }
     if (MASKED) {
         st.I = act ? In : st.I; st.SD = act ? SDn : st.SD; st.Dd = act ? Ddn : st.Dd; st.SM = act ? SMn : st.SM;
@@ -473,7 +493,7 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         if (lane == 0) *wcnt_out = 1;
     }
     const bool tracing = trace != nullptr;
-    long long tr_start = 0, tr_first = 0;
+    long long tr_start = 0, tr_first = 0, clk_first = 0;
     unsigned tr_wout = 0;
     if (tracing) tr_start = __builtin_amdgcn_s_memrealtime();
     // column 0 of the row above seeds row A's top-left of column 1; columns
@@ -488,7 +508,7 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         st.a.Ltl = 0;
         read4(nxt, ring_in + ring_slot(1));
     }
-    if (tracing) tr_first = __builtin_amdgcn_s_memrealtime();
+    if (tracing) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
     const int T = m + kWave;                          // lane 63 pushes column m at step m + 63
     const bool rolled_only = (sc.dbg & 1) != 0;
     for (int t0 = 0; t0 < T; t0 += kSub) {
@@ -549,7 +569,7 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         StripTrace tr;
         tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
         tr.wait_in = (int)w.tr_win; tr.wait_out = (int)tr_wout;
-        tr.band = 0; tr.wave = 0; tr.pad0 = 0; tr.pad1 = 0;   // the host knows W
+        tr.clk = __builtin_amdgcn_s_memtime() - clk_first; tr.pad0 = 0; tr.pad1 = 0;
         trace[s] = tr;
     }
 }
@@ -886,28 +906,41 @@ static hipError_t launch_fill_t(const PairDev* d_pairs, int npairs, int total_ba
     return hipGetLastError();
 }
 
+// Launch with the band width W from the variant's width list (gx_internal.h).
+template <bool LO, bool PL, bool TR, bool LC, int W0, int... Ws>
+static hipError_t launch_fill_w(int W, const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
+                                StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
+    if (W == W0)
+        return launch_fill_t<W0, LO, PL, TR, LC>(d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc, grid, st);
+    if constexpr (sizeof...(Ws) > 0)
+        return launch_fill_w<LO, PL, TR, LC, Ws...>(W, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc,
+                                                    grid, st);
+    return hipErrorInvalidValue;
+}
+
 // Variants: mode (global/local) x planes x {no max tracking, first max + LCS
-// field, first max + LCS plane}.  Traceback codes are always produced.
+// field, first max + LCS plane}.  Traceback codes are always produced.  The
+// untracked global variants (the batch path) come in every width of kFillWidths,
+// the tracked and local ones (256-VGPR builds) in kFillWidthsTrack.
 hipError_t launch_fill(int W, bool local, bool planes, bool track, bool lcs, const PairDev* d_pairs, int npairs,
                        int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                        hipStream_t st) {
-#define GX_FILL_CASE(LO, PL, TR, LC)                                                                        \
-    if (local == LO && planes == PL && track == TR && lcs == LC)                                            \
-        return W == kBandWavesNarrow                                                                        \
-                   ? launch_fill_t<kBandWavesNarrow, LO, PL, TR, LC>(d_pairs, npairs, total_bands, d_counter, \
-                                                                     d_sres, d_pres, sc, grid, st)          \
-                   : launch_fill_t<kBandWavesWide, LO, PL, TR, LC>(d_pairs, npairs, total_bands, d_counter,   \
-                                                                   d_sres, d_pres, sc, grid, st);
-    GX_FILL_CASE(false, false, false, false)
-    GX_FILL_CASE(false, false, true, false)
-    GX_FILL_CASE(false, true, false, false)
-    GX_FILL_CASE(false, true, true, false)
-    GX_FILL_CASE(false, true, true, true)
-    GX_FILL_CASE(true, false, false, false)
-    GX_FILL_CASE(true, false, true, false)
-    GX_FILL_CASE(true, true, false, false)
-    GX_FILL_CASE(true, true, true, false)
-    GX_FILL_CASE(true, true, true, true)
+#define GX_FILL_CASE(LO, PL, TR, LC, ...)                                                                \
+    if (local == LO && planes == PL && track == TR && lcs == LC)                                         \
+        return launch_fill_w<LO, PL, TR, LC, __VA_ARGS__>(W, d_pairs, npairs, total_bands, d_counter, d_sres, \
+                                                          d_pres, sc, grid, st);
+#define GX_W_ALL 3, 4, 6, 8, 11, 15
+#define GX_W_TRACK 3, 7
+    GX_FILL_CASE(false, false, false, false, GX_W_ALL)
+    GX_FILL_CASE(false, false, true, false, GX_W_TRACK)
+    GX_FILL_CASE(false, true, false, false, GX_W_ALL)
+    GX_FILL_CASE(false, true, true, false, GX_W_TRACK)
+    GX_FILL_CASE(false, true, true, true, GX_W_TRACK)
+    GX_FILL_CASE(true, false, false, false, GX_W_TRACK)
+    GX_FILL_CASE(true, false, true, false, GX_W_TRACK)
+    GX_FILL_CASE(true, true, false, false, GX_W_TRACK)
+    GX_FILL_CASE(true, true, true, false, GX_W_TRACK)
+    GX_FILL_CASE(true, true, true, true, GX_W_TRACK)
 #undef GX_FILL_CASE
     return hipErrorInvalidValue;
 }

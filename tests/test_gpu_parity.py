@@ -4,9 +4,10 @@ Covers the reference's own golden vectors (tests/test_alignment.rs), the
 committed oracle fixtures, seeded random pairs around the 128-row strip and
 band edges, exported score planes and full AlignmentCell tables,
 reverse_sequences, batched pairs, and the large pairs of BASELINE configs 2
-and 3 through digests.  Every test runs under each fill launch shape: narrow
-(3-strip) and wide (7-strip) bands, and wide bands on a 2-workgroup grid
-(bands wait in the queue for a workgroup, hand-offs cross launch order).
+and 3 through digests.  Every test runs under each fill launch shape: the
+automatic band width, forced 7-strip (tracked variants) and 8-strip bands,
+and 15-strip bands on a 2-workgroup grid (bands wait in the queue for a
+workgroup, hand-offs cross launch order).
 """
 import hashlib
 import json
@@ -20,8 +21,8 @@ from conftest import COMPARISON, CONFIG_SCORES, FASTA, GOLDEN, TEST_SCORES, read
 
 pytestmark = pytest.mark.gpu
 
-LAUNCH_SHAPES = {"narrow": {"GX_BAND_WAVES": "3"}, "wide": {"GX_BAND_WAVES": "7"},
-                 "wide_grid2": {"GX_BAND_WAVES": "7", "GX_FILL_GRID": "2"}}
+LAUNCH_SHAPES = {"auto": {}, "w7": {"GX_BAND_WAVES": "7"}, "w8": {"GX_BAND_WAVES": "8"},
+                 "w15_grid2": {"GX_BAND_WAVES": "15", "GX_FILL_GRID": "2"}}
 
 
 @pytest.fixture(autouse=True, params=sorted(LAUNCH_SHAPES))

@@ -18,6 +18,9 @@ for f in [a for a in sys.argv[1:] if not a.startswith("--")]:
     print(f"  lag intra-band {sum(intra)/len(intra):.2f} us, inter-band {sum(inter)/len(inter):.2f} us")
     print(f"  strip compute {sum(durs)/len(durs):.0f} us avg (min {min(durs):.0f}, max {max(durs):.0f}) -> "
           f"{sum(durs)/len(durs)*1000/m_steps:.1f} ns/step")
+    if "clk" in rows[0]:
+        mhz = [int(r["clk"]) / max(us(r["t_end"]) - us(r["t_first"]), 1e-9) for r in rows]
+        print(f"  shader clock while computing: {sum(mhz)/len(mhz):.0f} MHz avg (min {min(mhz):.0f}, max {max(mhz):.0f})")
     print(f"  last strip of pair 0 starts {firsts[-1]:.0f} us; last end {max(us(r['t_end']) for r in rows):.0f} us")
 
     # timeline: active strips and implied plane-store bandwidth per 1 ms bin
