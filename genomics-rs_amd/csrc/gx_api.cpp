@@ -24,7 +24,7 @@
 #include "gx_internal.h"
 
 namespace gx {
-hipError_t launch_fill(int W, bool local, bool planes, bool track, bool lcs, const PairDev* d_pairs, int npairs,
+hipError_t launch_fill(int W, bool local, bool planes, bool track, bool lcs, bool tbl, const PairDev* d_pairs, int npairs,
                        int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                        hipStream_t st);
 hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d_sres, PairRes* d_pres,
@@ -73,6 +73,24 @@ struct DevBuf {
     size_t cap = 0;
 };
 
+// Distinct processed bytes of a job, while there are at most 4 (the fill's
+// small-alphabet score table, Scores32.sym); n = 5 means "more than 4".
+struct SmallAlpha {
+    int sym[4] = {-1, -1, -1, -1};
+    int n = 0;
+    void add(const uint8_t* p, size_t len) {
+        if (n > 4) return;
+        bool seen[256] = {};
+        for (int k = 0; k < n; ++k) seen[sym[k]] = true;
+        for (size_t i = 0; i < len; ++i) {
+            if (seen[p[i]]) continue;
+            if (n == 4) { n = 5; return; }
+            seen[p[i]] = true;
+            sym[n++] = p[i];
+        }
+    }
+};
+
 // Interior walk + labelling + boundary continuation (algo.rs:306-422).
 struct Walk {
     std::vector<gx_step> steps;
@@ -96,6 +114,7 @@ struct gx_context {
     std::vector<std::vector<uint8_t>> st_s1, st_s2;
     DevBuf st_chars;
     std::vector<size_t> st_off1, st_off2;
+    SmallAlpha st_alpha;
     // host buffers reused across calls (no fresh, page-faulting allocations per batch)
     std::vector<Walk> walk_cache;
     TbOut tb_cache;
@@ -212,6 +231,7 @@ static int check_scores(const gx_scores* s, size_t n, size_t m, HostScores* hs, 
     sc->floor_ = is_local ? 0 : kNeg;
     const char* dbg = getenv("GX_DEBUG_FLAGS");
     sc->dbg = dbg ? atoi(dbg) : 0;
+    for (int k = 0; k < 4; ++k) sc->sym[k] = -1;
     return GX_OK;
 }
 
@@ -315,13 +335,20 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc,
                     const std::vector<PairHost>& ph, const Scores32& sc, int is_local, bool planes, bool track,
                     bool lcs, FillJob& job, const uint8_t* chars_dev = nullptr,
-                    const std::vector<size_t>* off1 = nullptr, const std::vector<size_t>* off2 = nullptr) {
+                    const std::vector<size_t>* off1 = nullptr, const std::vector<size_t>* off2 = nullptr,
+                    const SmallAlpha* alpha = nullptr) {
     int total_strips = 0;
     for (const PairHost& h : ph) total_strips += ceil_div((int)h.n, kStripRows);
     const bool codes = true;
     lcs = lcs && planes;
     track = track || lcs;
     const int W = fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device));
+    // small-alphabet score table: untracked global fill, <= 4 symbols, scores in a signed byte
+    Scores32 scl = sc;
+    const bool tbl = alpha && alpha->n <= 4 && !track && !is_local && sc.sm >= -128 && sc.sm <= 127 &&
+                     sc.smm >= -128 && sc.smm <= 127 && !getenv("GX_NO_SCORE_TABLE");
+    if (tbl)
+        for (int k = 0; k < 4; ++k) scl.sym[k] = alpha->sym[k];
     job.W = W;
     job.planes_on = planes; job.lcs_on = lcs; job.track_on = track;
     const size_t P = ph.size();
@@ -410,8 +437,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     const auto h_launch = std::chrono::steady_clock::now();
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     if (bands > 0)
-        HIPCHK(launch_fill(W, is_local != 0, planes, track, lcs, (const PairDev*)job.pairs.p, (int)P, bands,
-                           (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, sc, grid, ctx->stream));
+        HIPCHK(launch_fill(W, is_local != 0, planes, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
+                           (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, ctx->stream));
     HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));   // ev0..ev1 brackets the fill kernel alone
     if (bands > 0)
         HIPCHK(launch_finalize((const PairDev*)job.pairs.p, (int)P, (const StripRes*)job.sres.p,
@@ -434,13 +461,16 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         HIPCHK(hipMemcpy(tr.data(), trace.p, tr.size() * sizeof(StripTrace), hipMemcpyDeviceToHost));
         pool_put(ctx, trace);
         if (FILE* f = fopen(trace_file, "w")) {
-            fprintf(f, "pair,strip,band,t_start,t_first,t_end,clk,wait_in,wait_out,W,fill_ms\n");
+            fprintf(f, "pair,strip,band,t_start,t_first,t_end,clk,wait_in,wait_out,W,fill_ms");
+            for (int q = 0; q < kTraceQ; ++q) fprintf(f, ",q%d", q + 1);
+            fprintf(f, "\n");
             for (size_t p = 0; p < P; ++p)
                 for (int s = 0; s < job.pd[p].strips; ++s) {
                     const StripTrace& t = tr[job.pd[p].strip_base + s];
-                    fprintf(f, "%zu,%d,%d,%lld,%lld,%lld,%lld,%d,%d,%d,%.4f\n", p, s, job.pd[p].band_base + s / W,
-                            t.t_start, t.t_first, t.t_end, t.clk, t.wait_in,
-                            t.wait_out, W, ms);
+                    fprintf(f, "%zu,%d,%d,%lld,%lld,%lld,%lld,%d,%d,%d,%.4f", p, s, job.pd[p].band_base + s / W,
+                            t.t_start, t.t_first, t.t_end, t.clk, t.wait_in, t.wait_out, W, ms);
+                    for (int q = 0; q < kTraceQ; ++q) fprintf(f, ",%lld", t.t_q[q]);
+                    fprintf(f, "\n");
                 }
             fclose(f);
         }
@@ -883,7 +913,7 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
                       const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc, const HostScores& hs,
                       const Scores32& sc, int is_local, bool planes, bool track, std::vector<Walk>& walks,
                       double* fill_ms, const uint8_t* chars_dev = nullptr, const std::vector<size_t>* off1 = nullptr,
-                      const std::vector<size_t>* off2 = nullptr) {
+                      const std::vector<size_t>* off2 = nullptr, const SmallAlpha* staged_alpha = nullptr) {
     const size_t P = ph.size();
     // pairs with an interior go to the device
     std::vector<size_t> idx;
@@ -906,8 +936,15 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
     using clk = std::chrono::steady_clock;
     const auto c0 = clk::now();
     if (!idx.empty()) {
+        SmallAlpha alpha;
+        if (staged_alpha) alpha = *staged_alpha;
+        else
+            for (size_t k = 0; k < dproc.size() && alpha.n <= 4; ++k) {
+                alpha.add(dproc[k].first, dph[k].n);
+                alpha.add(dproc[k].second, dph[k].m);
+            }
         rc = run_fill(ctx, dproc, dph, sc, is_local, planes, track, false, job, chars_dev, chars_dev ? &o1 : nullptr,
-                      chars_dev ? &o2 : nullptr);
+                      chars_dev ? &o2 : nullptr, &alpha);
         if (rc) { job_release(ctx, job); return rc; }
         for (size_t k = 0; k < idx.size(); ++k) res[idx[k]] = job.res[k];
     }
@@ -1025,6 +1062,10 @@ extern "C" int gx_stage_pairs(gx_context* ctx, const uint8_t* const* s1, const s
     ctx->st_s2.assign(npairs, {});
     ctx->st_off1.assign(npairs, 0);
     ctx->st_off2.assign(npairs, 0);
+    ctx->st_alpha = SmallAlpha{};
+    for (size_t p = 0; p < npairs; ++p) {
+        if (n[p] && m[p]) { ctx->st_alpha.add(s1[p], n[p]); ctx->st_alpha.add(s2[p], m[p]); }
+    }
     size_t tot = 0;
     for (size_t p = 0; p < npairs; ++p) {
         ctx->st_s1[p].assign(s1[p], s1[p] + n[p]);
@@ -1065,7 +1106,7 @@ extern "C" int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_lo
     std::vector<Walk>& walks = ctx->walk_cache;
     double fms = 0;
     rc = batch_core(ctx, ph, proc, hs, sc, is_local, keep_planes != 0, (flags & GX_ALIGN_MAX_CELL) != 0, walks, &fms,
-                    (const uint8_t*)ctx->st_chars.p, &ctx->st_off1, &ctx->st_off2);
+                    (const uint8_t*)ctx->st_chars.p, &ctx->st_off1, &ctx->st_off2, &ctx->st_alpha);
     if (rc) return rc;
     for (size_t p = 0; p < P; ++p) out[p] = walks[p].res;
     if (fill_ms_out) *fill_ms_out = fms;

@@ -50,6 +50,7 @@ struct Scores32 {
     int hg;      // h + g
     int floor_;  // local ? 0 : kNeg  (the 4th lane of score_max, algo.rs:103)
     int dbg;     // GX_DEBUG_FLAGS: bit0 = rolled (ramp) path only
+    int sym[4];  // small-alphabet launches: the job's distinct processed bytes (code k = sym[k])
 };
 
 // One inter-strip record: the bottom-row cell (r, j) of a strip, as needed by
@@ -78,6 +79,7 @@ struct __attribute__((aligned(16))) PairRes {
 
 // Optional per-strip timeline (GX_TRACE_FILE): s_memrealtime ticks (100 MHz)
 // and spin iterations, for the diagnostic runs behind DESIGN.md's numbers.
+constexpr int kTraceQ = 7;   // progress stamps per strip (at k/8 of the sweep)
 struct __attribute__((aligned(16))) StripTrace {
     long long t_start;   // wave starts the strip
     long long t_first;   // first input sub-block available
@@ -85,7 +87,7 @@ struct __attribute__((aligned(16))) StripTrace {
     int wait_in;         // spin iterations waiting for the row above
     int wait_out;        // spin iterations waiting for ring space below
     long long clk;       // shader-clock ticks (s_memtime) from t_first to t_end
-    int pad0, pad1;
+    long long t_q[kTraceQ];   // when the sweep passed k/8 of its steps (k = 1..7)
 };
 
 struct PairDev {

@@ -101,25 +101,22 @@ __device__ __forceinline__ void gstore4(int32_t* p, int4 v) {
     *(gv4i*)p = x;
 }
 __device__ __forceinline__ void gstore1(uint32_t* p, uint32_t v) { *(guint*)p = v; }
-// Uniform base + 32-bit per-lane byte offset: selects the saddr form
-// (global_store_dwordx4 voff, data, s[base] offset:imm), no 64-bit VALU math.
-typedef __attribute__((address_space(1))) char gchar;
-__device__ __forceinline__ void gstore4_at(int32_t* base, uint32_t byte_off, int4 v) {
+// Plane stores: one 16-B store per lane through a buffer descriptor of the
+// sub-block (uniform base, per-lane offset + immediate; the compiler places
+// the wait states for the SGPR operands).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t voff, int4 v) {
     v4i x = {v.x, v.y, v.z, v.w};
-    *(gv4i*)((gchar*)base + byte_off) = x;
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)voff, 0, 0);
 }
 
-
-// Occupancy floor (waves per SIMD) that caps the fill kernel's VGPRs
-// (512 / 4 = 128): with 8-wave workgroups, two bands per CU.  The variants
-// that also track the maxima (first max + LCS, local mode) carry more state
-// per row and get 256 VGPRs at one band per CU instead of spilling.
-#ifndef GX_CODE_VCC
-#define GX_CODE_VCC 0
-#endif
-#ifndef GX_FILL_MIN_WAVES
-#define GX_FILL_MIN_WAVES 4
-#endif
+// Occupancy floor (waves per SIMD), which sets the fill kernel's VGPR cap
+// (512 / floor, at most 256): one workgroup per CU, so the floor is the
+// workgroup's waves per SIMD.  The variants that also track the maxima
+// (first max + LCS, local mode) carry more state per row and get 256 VGPRs
+// (8-wave workgroups at most).
 #ifndef GX_FILL_MIN_WAVES_TRACK
 #define GX_FILL_MIN_WAVES_TRACK 2
 #endif
@@ -141,36 +138,34 @@ struct LaneState {
 };
 
 // Lane 63 pushes its row-B cell (the strip's bottom row) into the LDS ring of
-// the wave below, under a lane-63 exec mask (no branch, no register tuple),
-// and in the same exec window stores the cell's landing column E into the
-// traceback skeleton (global, 4 B).  Record = {dd, sm, c2, l}; without TRACK
-// the l word is not written.  Compute waves run with all 64 lanes active, so
-// exec is restored to -1, not saved.  U = step within the 16-step sub-block
-// (constant LDS and global offsets); sk = skeleton address of the sub-block's
-// first pushed column.
+// the wave below, under a lane-63 exec mask (no branch, no register tuple).
+// Record = {dd, sm, c2, l}; without TRACK the l word is not written.  Compute
+// waves run with all 64 lanes active, so exec is restored to -1, not saved.
+// U = step within the 16-step sub-block (constant LDS offsets).  No global
+// memory access in here: an SGPR address written by a VALU op (readfirstlane)
+// needs wait states before a VMEM instruction reads it, which the compiler
+// only inserts for the instructions it emits itself.
 template <int U, bool TRACK>
-__device__ __forceinline__ void push63(uint32_t base, const LaneState& st, unsigned long long m63, const int* sk) {
+__device__ __forceinline__ void push63(uint32_t base, const LaneState& st, unsigned long long m63) {
     if (TRACK)
         asm volatile(
             "s_mov_b64 exec, %0\n\t"
-            "ds_write2_b32 %1, %2, %3 offset0:%9 offset1:%10\n\t"
-            "ds_write2_b32 %1, %4, %5 offset0:%11 offset1:%12\n\t"
-            "global_store_dword %7, %6, %8 offset:%13\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%6 offset1:%7\n\t"
+            "ds_write2_b32 %1, %4, %5 offset0:%8 offset1:%9\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L), "v"(st.b.E), "v"(0),
-              "s"(sk), "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2), "i"(4 * U + 3), "i"(4 * U)
+            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L), "i"(4 * U),
+              "i"(4 * U + 1), "i"(4 * U + 2), "i"(4 * U + 3)
             : "memory");
     else
         asm volatile(
             "s_mov_b64 exec, %0\n\t"
-            "ds_write2_b32 %1, %2, %3 offset0:%8 offset1:%9\n\t"
-            "ds_write_b32 %1, %4 offset:%10\n\t"
-            "global_store_dword %6, %5, %7 offset:%11\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%5 offset1:%6\n\t"
+            "ds_write_b32 %1, %4 offset:%7\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.E), "v"(0), "s"(sk),
-              "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8), "i"(4 * U)
+            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "i"(4 * U), "i"(4 * U + 1),
+              "i"(16 * U + 8)
             : "memory");
 }
 
@@ -178,33 +173,43 @@ __device__ __forceinline__ void push63(uint32_t base, const LaneState& st, unsig
 // ring's write counter: LDS executes one wave's DS operations in order, so a
 // consumer that sees the counter also sees every record pushed before it.
 template <int U, bool TRACK>
-__device__ __forceinline__ void push63_pub(uint32_t base, const LaneState& st, unsigned long long m63, const int* sk,
+__device__ __forceinline__ void push63_pub(uint32_t base, const LaneState& st, unsigned long long m63,
                                            uint32_t cnt_addr, int cnt) {
     if (TRACK)
         asm volatile(
             "s_mov_b64 exec, %0\n\t"
-            "ds_write2_b32 %1, %2, %3 offset0:%11 offset1:%12\n\t"
-            "ds_write2_b32 %1, %4, %5 offset0:%13 offset1:%14\n\t"
-            "ds_write_b32 %9, %10\n\t"
-            "global_store_dword %7, %6, %8 offset:%15\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%8 offset1:%9\n\t"
+            "ds_write2_b32 %1, %4, %5 offset0:%10 offset1:%11\n\t"
+            "ds_write_b32 %6, %7\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L), "v"(st.b.E), "v"(0),
-              "s"(sk), "v"(cnt_addr), "v"(cnt), "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2), "i"(4 * U + 3),
-              "i"(4 * U)
+            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L), "v"(cnt_addr), "v"(cnt),
+              "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2), "i"(4 * U + 3)
             : "memory");
     else
         asm volatile(
             "s_mov_b64 exec, %0\n\t"
-            "ds_write2_b32 %1, %2, %3 offset0:%10 offset1:%11\n\t"
-            "ds_write_b32 %1, %4 offset:%12\n\t"
-            "ds_write_b32 %8, %9\n\t"
-            "global_store_dword %6, %5, %7 offset:%13\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%7 offset1:%8\n\t"
+            "ds_write_b32 %1, %4 offset:%9\n\t"
+            "ds_write_b32 %5, %6\n\t"
             "s_mov_b64 exec, -1"
             :
-            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.E), "v"(0), "s"(sk),
-              "v"(cnt_addr), "v"(cnt), "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8), "i"(4 * U)
+            : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(cnt_addr), "v"(cnt), "i"(4 * U),
+              "i"(4 * U + 1), "i"(16 * U + 8)
             : "memory");
+}
+
+// Skeleton stores of lane 63's landing columns through a buffer descriptor:
+// every lane issues them, the other lanes' offsets lie past the descriptor's
+// range (kSkelOff) and are dropped by the range check -- no exec switch.
+// Full groups store their four columns at once; ramp groups one per step.
+constexpr uint32_t kSkelOff = 0x40000000u;
+__device__ __forceinline__ void skel_store(__amdgpu_buffer_rsrc_t r, uint32_t voff, int E) {
+    __builtin_amdgcn_raw_buffer_store_b32(E, r, (int)voff, 0, 0);
+}
+__device__ __forceinline__ void skel_store4(__amdgpu_buffer_rsrc_t r, uint32_t voff, int e0, int e1, int e2, int e3) {
+    v4i x = {e0, e1, e2, e3};
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)voff, 0, 0);
 }
 
 // A wave-uniform pointer forced into an SGPR pair (for "s" asm operands).
@@ -231,20 +236,37 @@ __device__ __forceinline__ void lds_store_lane0(lds_int* p, int v) {
         : "memory");
 }
 
+// Small-alphabet scoring (TBL): the host maps the job's <= 4 distinct
+// processed bytes to codes 0..3 (Scores32.sym); a row's table holds
+// score(c1, sym[k]) as signed byte k.
+__device__ __forceinline__ int sym_code(int c, const Scores32& sc) {
+    return c == sc.sym[1] ? 1 : c == sc.sym[2] ? 2 : c == sc.sym[3] ? 3 : 0;
+}
+__device__ __forceinline__ int score_table(int c1, const Scores32& sc) {
+    int t = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t |= ((c1 == sc.sym[k] ? sc.sm : sc.smm) & 0xFF) << (8 * k);
+    return t;
+}
+
 // One cell of the Gotoh recurrence (algo.rs:222-268) for the row in `st`,
 // given the cell above (dd_in = its delete-successor = D(i, j), sm_in =
 // score_max(i-1, j), l_in = max_matches(i-1, j), e_up = its landing column)
 // and s2[j-1].  act = false leaves the row unchanged (ramp lanes outside
 // columns 1..m).
-template <bool LOCAL, bool MASKED, bool CODES, bool TRACK>
+template <bool LOCAL, bool MASKED, bool CODES, bool TRACK, bool TBL>
 __device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm_in, const int l_in, const int e_up,
                                      const int c2, const int c1v, const bool act, const int t, const Scores32& sc,
                                      int& oI, int& oD, int& oS, int& oL) {
     // algo.rs:231-236  insert_score = top.score_max(g, h+g, h+g)
     const int In = LOCAL ? max3i(st.I + sc.g, st.SD + sc.hg, 0) : max(st.I + sc.g, st.SD + sc.hg);
+    static_assert(!(TBL && TRACK), "the LCS field needs the match bit");
     const bool mt = c2 == c1v;             // sequence.rs:113-114
-    // algo.rs:245-248  sub_score = s_(mis)match + top_left.score_max(0,0,0)
-    const int Sn = st.SMtl + (mt ? sc.sm : sc.smm);
+    // algo.rs:245-248  sub_score = s_(mis)match + top_left.score_max(0,0,0);
+    // TBL: c1v is the row's packed score table (one signed byte per symbol
+    // code) and c2 the column's code * 8, so the score is one bit-field
+    // extract instead of a compare and a select
+    const int Sn = st.SMtl + (TBL ? __builtin_amdgcn_sbfe(c1v, c2, 8) : (mt ? sc.sm : sc.smm));
     const int Dn = dd_in;                  // algo.rs:238-243 (computed by the row above)
     const int IS = max(In, Sn);
     const int SMn = max(IS, Dn);           // cell.score_max(0,0,0); >= floor since In >= floor
@@ -261,19 +283,6 @@ __device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm
         // cell, taken from the predecessor the priority picks.  One asm block:
         // each compare feeds its select and its code bit at once (no SGPR-pair
         // masks kept alive, no chain sunk to the end of the sub-block).
-#if GX_CODE_VCC
-        asm volatile(
-            "v_cmp_gt_i32 vcc, %[in], %[sn]\n\t"
-            "v_cndmask_b32 %[en], %[etl], %[el], vcc\n\t"
-            "v_addc_co_u32 %[ci], vcc, %[ci], %[ci], vcc\n\t"
-            "v_cmp_gt_i32 vcc, %[dn], %[is]\n\t"
-            "v_cndmask_b32 %[en], %[en], %[eu], vcc\n\t"
-            "v_addc_co_u32 %[cd], vcc, %[cd], %[cd], vcc"
-            : [en] "=&v"(En), [ci] "+v"(st.cI), [cd] "+v"(st.cD)
-            : [in] "v"(In), [sn] "v"(Sn), [dn] "v"(Dn), [is] "v"(IS), [etl] "v"(st.Etl), [el] "v"(st.E),
-              [eu] "v"(e_up)
-            : "vcc");
-#else
         // the two compares write their own SGPR pairs, so the selects and the
         // code-bit shifts of the two compares overlap (no serial VCC chain)
         unsigned long long m1, m2, k1, k2;
@@ -288,7 +297,6 @@ __device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm
               [k1] "=&s"(k1), [k2] "=&s"(k2)
             : [in] "v"(In), [sn] "v"(Sn), [dn] "v"(Dn), [is] "v"(IS), [etl] "v"(st.Etl), [el] "v"(st.E),
               [eu] "v"(e_up));
-#endif
     }
     if (MASKED) {
         st.I = act ? In : st.I; st.SD = act ? SDn : st.SD; st.Dd = act ? Ddn : st.Dd; st.SM = act ? SMn : st.SM;
@@ -320,7 +328,7 @@ __device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm
 // (wave_shr:1; lane 0 from the ring record r), row B's from row A.  Lane 0's
 // row A is the strip's top row: its "landing column" from above is its own
 // column j = t + 1 (a delete lands on (128s, j), a sub on (128s, j-1)).
-template <bool LOCAL, bool MASKED, bool CODES, bool TRACK>
+template <bool LOCAL, bool MASKED, bool CODES, bool TRACK, bool TBL>
 __device__ __forceinline__ void dp_step(LaneState& st, const Rec& r, const int t, const int lane, const int m,
                                         const int c1a, const int c1b, const Scores32& sc, int (&oI)[2],
                                         int (&oD)[2], int (&oS)[2], int (&oL)[2]) {
@@ -330,9 +338,9 @@ __device__ __forceinline__ void dp_step(LaneState& st, const Rec& r, const int t
     const int l_in = TRACK ? shr1(r.l, st.b.L) : 0;
     const int e_in = CODES ? shr1(t + 1, st.b.E) : 0;
     const bool act = MASKED ? (unsigned)(t - lane) < (unsigned)m : true;
-    cell<LOCAL, MASKED, CODES, TRACK>(st.a, dd_in, sm_in, l_in, e_in, c2, c1a, act, t, sc, oI[0], oD[0], oS[0],
+    cell<LOCAL, MASKED, CODES, TRACK, TBL>(st.a, dd_in, sm_in, l_in, e_in, c2, c1a, act, t, sc, oI[0], oD[0], oS[0],
                                       oL[0]);
-    cell<LOCAL, MASKED, CODES, TRACK>(st.b, st.a.Dd, st.a.SM, st.a.L, st.a.E, c2, c1b, act, t, sc, oI[1], oD[1],
+    cell<LOCAL, MASKED, CODES, TRACK, TBL>(st.b, st.a.Dd, st.a.SM, st.a.L, st.a.E, c2, c1b, act, t, sc, oI[1], oD[1],
                                       oS[1], oL[1]);
     st.c2c = c2;
 }
@@ -354,10 +362,32 @@ struct WaveCtx {
     lds_int* wcnt_in;
     lds_int* wcnt_out;
     int* status;
-    int* skel;                                              // skeleton row of this strip (bottom-row E)
+    __amdgpu_buffer_rsrc_t skel_rsrc;                       // skeleton row of this strip (bottom-row E)
+    uint32_t skel_voff;                                     // lane 63: 0; other lanes: out of range
     int m, lane, c1a, c1b;
     unsigned tr_win;
 };
+
+// Plane stores of the previous 4-step group, issued one plane per step in
+// the next group (six 1-KiB stores at the end of a group stall the wave's
+// in-order issue; spread out they overlap the next group's arithmetic).
+// bytes = 0 (nothing pending) empties the descriptor's range.
+struct PendStore {
+    int4 I0, I1, D0, D1, S0, S1, L0, L1;   // rows A/B of each plane
+    size_t sb_off;                         // the group's sub-block (ints)
+    int bytes;
+};
+
+template <bool LCSP, int PLANE, int G4P>
+__device__ __forceinline__ void pend_store(const PendStore& pd, const WaveCtx& w) {
+    constexpr int kSubBytes = kSub / 4 * kGroupInts * 4;
+    (void)kSubBytes;
+    const uint32_t v0 = (uint32_t)w.lane * 16u + G4P * kGroupInts * 4, v1 = v0 + kWave * 16;
+    const int32_t* base = PLANE == 0 ? w.pI : PLANE == 1 ? w.pD : PLANE == 2 ? w.pS : w.pL;
+    const auto r = rsrc_of(base + pd.sb_off, pd.bytes);
+    bstore4(r, v0, PLANE == 0 ? pd.I0 : PLANE == 1 ? pd.D0 : PLANE == 2 ? pd.S0 : pd.L0);
+    bstore4(r, v1, PLANE == 0 ? pd.I1 : PLANE == 1 ? pd.D1 : PLANE == 2 ? pd.S1 : pd.L1);
+}
 
 // One 4-step group of a sub-block.  `nxt` holds validated ring records for
 // these steps.  The producer's counter is observed and the next group's
@@ -367,10 +397,11 @@ struct WaveCtx {
 // lanes outside columns 1..m): state updates are masked per lane and each
 // push per step (columns 0..m only: a push past m would land on the slot of
 // column c - 256, which a lagging consumer may not have read yet).
-template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP, bool MASKED, int G4>
+template <bool LOCAL, int PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL, bool MASKED, int G4>
 __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w, const Scores32& sc,
                                        const int t0, const uint32_t out_base, const bool push_on,
-                                       const size_t sb_off) {
+                                       const size_t sb_off, PendStore& pend) {
+    constexpr int G4P = (G4 + 3) & 3;   // the pending group's index in its sub-block
     const int t = t0 + 4 * G4;
     Rec cur[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
     const int need = min(t + 8, w.m) + 1;                     // columns of the next group: t+5 .. t+8
@@ -379,41 +410,84 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
     read4(nxt, w.ring_in + ring_slot(t + 5));
     int bI[4][2], bD[4][2], bS[4][2], bL[4][2];
     // lane 63 holds column t+U-63 before step U: push it (mask 0 when there is
-    // no consumer); the last push of a full group also publishes the counter
-    const int* sk = uniform_ptr(w.skel + (t0 - (kWave - 1)));   // column of step t0's push
+    // no consumer); the last push of a full group also publishes the counter.
+    // Skeleton: lane 63's landing column after step U (its column t+U-62).
     const int col0 = t - (kWave - 1);
     if (MASKED) {
-        push63<4 * G4 + 0, TRACK>(out_base, st, lane63_mask(push_on && col0 >= 0 && col0 <= w.m), sk);
-        dp_step<LOCAL, true, CODES, TRACK>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
-        push63<4 * G4 + 1, TRACK>(out_base, st, lane63_mask(push_on && col0 + 1 >= 0 && col0 + 1 <= w.m), sk);
-        dp_step<LOCAL, true, CODES, TRACK>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
-        push63<4 * G4 + 2, TRACK>(out_base, st, lane63_mask(push_on && col0 + 2 >= 0 && col0 + 2 <= w.m), sk);
-        dp_step<LOCAL, true, CODES, TRACK>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
-        push63<4 * G4 + 3, TRACK>(out_base, st, lane63_mask(push_on && col0 + 3 >= 0 && col0 + 3 <= w.m), sk);
+        // per step: column in 0..m, else the push is masked off and the skeleton offset out of range
+        auto sko = [&](int c) { return (c >= 0 && c <= w.m) ? w.skel_voff + 4u * (uint32_t)c : kSkelOff; };
+        push63<4 * G4 + 0, TRACK>(out_base, st, lane63_mask(push_on && col0 >= 0 && col0 <= w.m));
+        dp_step<LOCAL, true, CODES, TRACK, TBL>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
+        skel_store(w.skel_rsrc, sko(col0 + 1), st.b.E);   // lane 63's column after the step
+        if (PLANES == 2) pend_store<LCSP, 0, G4P>(pend, w);
+        push63<4 * G4 + 1, TRACK>(out_base, st, lane63_mask(push_on && col0 + 1 >= 0 && col0 + 1 <= w.m));
+        dp_step<LOCAL, true, CODES, TRACK, TBL>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
+        skel_store(w.skel_rsrc, sko(col0 + 2), st.b.E);   // lane 63's column after the step
+        if (PLANES == 2) pend_store<LCSP, 1, G4P>(pend, w);
+        push63<4 * G4 + 2, TRACK>(out_base, st, lane63_mask(push_on && col0 + 2 >= 0 && col0 + 2 <= w.m));
+        dp_step<LOCAL, true, CODES, TRACK, TBL>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
+        skel_store(w.skel_rsrc, sko(col0 + 3), st.b.E);   // lane 63's column after the step
+        if (PLANES == 2) pend_store<LCSP, 2, G4P>(pend, w);
+        if (PLANES == 2 && LCSP) pend_store<LCSP, 3, G4P>(pend, w);
+        push63<4 * G4 + 3, TRACK>(out_base, st, lane63_mask(push_on && col0 + 3 >= 0 && col0 + 3 <= w.m));
         // publish the pushes (same wave, DS operations in order)
         if (push_on && col0 + 3 >= 0 && col0 <= w.m) lds_store_lane0(w.wcnt_out, min(col0 + 3, w.m) + 1);
-        dp_step<LOCAL, true, CODES, TRACK>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, sc, bI[3], bD[3], bS[3], bL[3]);
+        dp_step<LOCAL, true, CODES, TRACK, TBL>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, sc, bI[3], bD[3], bS[3], bL[3]);
+        skel_store(w.skel_rsrc, sko(col0 + 4), st.b.E);   // lane 63's column after the step
     } else {
         const unsigned long long m63 = lane63_mask(push_on);
-        push63<4 * G4 + 0, TRACK>(out_base, st, m63, sk);
-        dp_step<LOCAL, false, CODES, TRACK>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
-        push63<4 * G4 + 1, TRACK>(out_base, st, m63, sk);
-        dp_step<LOCAL, false, CODES, TRACK>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
-        push63<4 * G4 + 2, TRACK>(out_base, st, m63, sk);
-        dp_step<LOCAL, false, CODES, TRACK>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
-        push63_pub<4 * G4 + 3, TRACK>(out_base, st, m63, sk, lds_addr((const void*)w.wcnt_out), col0 + 3 + 1);
-        dp_step<LOCAL, false, CODES, TRACK>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, sc, bI[3], bD[3], bS[3], bL[3]);
+        push63<4 * G4 + 0, TRACK>(out_base, st, m63);
+        dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
+        if (PLANES == 2) pend_store<LCSP, 0, G4P>(pend, w);
+        const int e0 = st.b.E;              // lane 63: column col0 + 1
+        push63<4 * G4 + 1, TRACK>(out_base, st, m63);
+        dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
+        if (PLANES == 2) pend_store<LCSP, 1, G4P>(pend, w);
+        const int e1 = st.b.E;
+        push63<4 * G4 + 2, TRACK>(out_base, st, m63);
+        dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
+        if (PLANES == 2) pend_store<LCSP, 2, G4P>(pend, w);
+        if (PLANES == 2 && LCSP) pend_store<LCSP, 3, G4P>(pend, w);
+        const int e2 = st.b.E;
+        push63_pub<4 * G4 + 3, TRACK>(out_base, st, m63, lds_addr((const void*)w.wcnt_out), col0 + 3 + 1);
+        dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, sc, bI[3], bD[3], bS[3], bL[3]);
+        // lane 63's landing columns of columns col0+1 .. col0+4 (full groups: all in 1..m), one store
+        skel_store4(w.skel_rsrc, w.skel_voff + 4u * (uint32_t)(col0 + 1), e0, e1, e2, st.b.E);
     }
-    if (PLANES) {
-        // per row: 16 B per lane, 1 KiB per wave; base (uniform) + lane*16 B + immediate
-#pragma unroll
-        for (int h = 0; h < kRowsPerLane; ++h) {
-            const uint32_t o = (uint32_t)w.lane * 16u + (uint32_t)(G4 * kGroupInts + h * kWave * 4) * 4u;
-            gstore4_at(w.pI + sb_off, o, make_int4(bI[0][h], bI[1][h], bI[2][h], bI[3][h]));
-            gstore4_at(w.pD + sb_off, o, make_int4(bD[0][h], bD[1][h], bD[2][h], bD[3][h]));
-            gstore4_at(w.pS + sb_off, o, make_int4(bS[0][h], bS[1][h], bS[2][h], bS[3][h]));
-            if (LCSP) gstore4_at(w.pL + sb_off, o, make_int4(bL[0][h], bL[1][h], bL[2][h], bL[3][h]));
+    if (PLANES == 1) {
+        // this group's cells, 16 B per lane per row and plane, stored now
+        // (the widest bands have no VGPRs to keep them for the next group)
+        constexpr int kSubBytes = kSub / 4 * kGroupInts * 4;      // one sub-block of one plane
+        constexpr uint32_t kG = G4 * kGroupInts * 4;              // this group within it
+        const uint32_t v0 = (uint32_t)w.lane * 16u + kG, v1 = v0 + kWave * 16;
+        const auto rI = rsrc_of(w.pI + sb_off, kSubBytes), rD = rsrc_of(w.pD + sb_off, kSubBytes),
+                   rS = rsrc_of(w.pS + sb_off, kSubBytes);
+        bstore4(rI, v0, make_int4(bI[0][0], bI[1][0], bI[2][0], bI[3][0]));
+        bstore4(rD, v0, make_int4(bD[0][0], bD[1][0], bD[2][0], bD[3][0]));
+        bstore4(rS, v0, make_int4(bS[0][0], bS[1][0], bS[2][0], bS[3][0]));
+        bstore4(rI, v1, make_int4(bI[0][1], bI[1][1], bI[2][1], bI[3][1]));
+        bstore4(rD, v1, make_int4(bD[0][1], bD[1][1], bD[2][1], bD[3][1]));
+        bstore4(rS, v1, make_int4(bS[0][1], bS[1][1], bS[2][1], bS[3][1]));
+        if (LCSP) {
+            const auto rL = rsrc_of(w.pL + sb_off, kSubBytes);
+            bstore4(rL, v0, make_int4(bL[0][0], bL[1][0], bL[2][0], bL[3][0]));
+            bstore4(rL, v1, make_int4(bL[0][1], bL[1][1], bL[2][1], bL[3][1]));
         }
+    }
+    if (PLANES == 2) {
+        // this group's cells: 16 B per lane per row and plane, stored during the next group
+        pend.I0 = make_int4(bI[0][0], bI[1][0], bI[2][0], bI[3][0]);
+        pend.I1 = make_int4(bI[0][1], bI[1][1], bI[2][1], bI[3][1]);
+        pend.D0 = make_int4(bD[0][0], bD[1][0], bD[2][0], bD[3][0]);
+        pend.D1 = make_int4(bD[0][1], bD[1][1], bD[2][1], bD[3][1]);
+        pend.S0 = make_int4(bS[0][0], bS[1][0], bS[2][0], bS[3][0]);
+        pend.S1 = make_int4(bS[0][1], bS[1][1], bS[2][1], bS[3][1]);
+        if (LCSP) {
+            pend.L0 = make_int4(bL[0][0], bL[1][0], bL[2][0], bL[3][0]);
+            pend.L1 = make_int4(bL[0][1], bL[1][1], bL[2][1], bL[3][1]);
+        }
+        pend.sb_off = sb_off;
+        pend.bytes = kSub / 4 * kGroupInts * 4;
     }
     if (__builtin_amdgcn_readfirstlane(seen_v) < need) {      // producer was behind: wait, re-read
         w.tr_win += wait_ge(w.wcnt_in, need, w.status);
@@ -425,13 +499,14 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
 
 // One 16-step sub-block: four groups.  MASKED for the ramp-up (t0 < 64) and
 // ramp-down (columns past m) sub-blocks.
-template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP, bool MASKED>
+template <bool LOCAL, int PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL, bool MASKED>
 __device__ __forceinline__ void sub_block(LaneState& st, Rec (&nxt)[4], WaveCtx& w, const Scores32& sc, const int t0,
-                                          const uint32_t out_base, const bool push_on, const size_t sb_off) {
-    group4<LOCAL, PLANES, CODES, TRACK, LCSP, MASKED, 0>(st, nxt, w, sc, t0, out_base, push_on, sb_off);
-    group4<LOCAL, PLANES, CODES, TRACK, LCSP, MASKED, 1>(st, nxt, w, sc, t0, out_base, push_on, sb_off);
-    group4<LOCAL, PLANES, CODES, TRACK, LCSP, MASKED, 2>(st, nxt, w, sc, t0, out_base, push_on, sb_off);
-    group4<LOCAL, PLANES, CODES, TRACK, LCSP, MASKED, 3>(st, nxt, w, sc, t0, out_base, push_on, sb_off);
+                                          const uint32_t out_base, const bool push_on, const size_t sb_off,
+                                          PendStore& pend) {
+    group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, MASKED, 0>(st, nxt, w, sc, t0, out_base, push_on, sb_off, pend);
+    group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, MASKED, 1>(st, nxt, w, sc, t0, out_base, push_on, sb_off, pend);
+    group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, MASKED, 2>(st, nxt, w, sc, t0, out_base, push_on, sb_off, pend);
+    group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, MASKED, 3>(st, nxt, w, sc, t0, out_base, push_on, sb_off, pend);
 }
 
 __device__ __forceinline__ void init_row(RowState& rs, const int i, const bool row_ok, const Scores32& sc) {
@@ -448,7 +523,7 @@ __device__ __forceinline__ void init_row(RowState& rs, const int i, const bool r
     rs.cI = 0; rs.cD = 0;
 }
 
-template <bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP>
+template <bool LOCAL, int PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL>
 __device__ void compute_wave(const PairDev& P, const int s, const int lane, const Scores32& sc, const Rec* ring_in,
                              Rec* ring_out, lds_int* wcnt_in, lds_int* rcnt_in, lds_int* wcnt_out, lds_int* rcnt_out,
                              const bool has_consumer, StripRes* sres, PairRes* pres, int* status) {
@@ -467,11 +542,13 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         w.codes = CODES ? P.codes + (size_t)s * P.t16 * kWave * kRowsPerLane : nullptr;
     }
     w.ring_in = ring_in; w.ring_out = ring_out; w.wcnt_in = wcnt_in; w.wcnt_out = wcnt_out; w.status = status;
-    // skeleton row (only stored when there is a strip below); any valid address otherwise (exec = 0)
-    w.skel = has_consumer ? P.skel + (size_t)s * P.skel_stride : P.skel;
+    // skeleton row (only stored when there is a strip below: otherwise an empty range)
+    w.skel_rsrc = rsrc_of(uniform_ptr(P.skel + (size_t)s * P.skel_stride), has_consumer ? 4 * (m + 1) : 0);
+    w.skel_voff = lane == kWave - 1 ? 0u : kSkelOff;
     w.m = m; w.lane = lane;
     w.c1a = ok_a ? (int)P.c1[ia - 1] : 0x1FF;   // 0x1FF never equals a byte
     w.c1b = ok_b ? (int)P.c1[ia] : 0x1FF;
+    if (TBL) { w.c1a = score_table(w.c1a, sc); w.c1b = score_table(w.c1b, sc); }
     w.tr_win = 0;
     StripTrace* const trace = P.trace;
     const int strip_base = P.strip_base;
@@ -495,6 +572,7 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     const bool tracing = trace != nullptr;
     long long tr_start = 0, tr_first = 0, clk_first = 0;
     unsigned tr_wout = 0;
+    long long tr_q[kTraceQ] = {};
     if (tracing) tr_start = __builtin_amdgcn_s_memrealtime();
     // column 0 of the row above seeds row A's top-left of column 1; columns
     // 1..4 feed the first step group
@@ -511,16 +589,24 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     if (tracing) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
     const int T = m + kWave;                          // lane 63 pushes column m at step m + 63
     const bool rolled_only = (sc.dbg & 1) != 0;
+    PendStore pend;
+    pend.sb_off = 0; pend.bytes = 0;   // nothing pending before the first group
     for (int t0 = 0; t0 < T; t0 += kSub) {
         const int last_col = min(t0 + kSub - 1 - (kWave - 1), m);   // last column pushed here
         if (has_consumer && last_col >= kRing) tr_wout += wait_ge(rcnt_out, last_col - kRing + 1, status);
+        if (tracing) {   // progress stamps at k/(kTraceQ+1) of the sweep
+            const int q = (int)((long long)t0 * (kTraceQ + 1) / T) - 1;
+            if (q >= 0 && q < kTraceQ && tr_q[q] == 0) tr_q[q] = __builtin_amdgcn_s_memrealtime();
+        }
         const size_t sb_off = (size_t)(t0 >> 2) * kGroupInts;         // this sub-block's plane offset (ints)
         const bool full = (t0 >= kWave) && (t0 + kSub - 1 <= m - 1) && !rolled_only;
         const uint32_t out_base = lds_addr(ring_out + ring_slot(t0 - (kWave - 1)));
         if (full)
-            sub_block<LOCAL, PLANES, CODES, TRACK, LCSP, false>(st, nxt, w, sc, t0, out_base, has_consumer, sb_off);
+            sub_block<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, false>(st, nxt, w, sc, t0, out_base, has_consumer, sb_off,
+                                                                     pend);
         else
-            sub_block<LOCAL, PLANES, CODES, TRACK, LCSP, true>(st, nxt, w, sc, t0, out_base, has_consumer, sb_off);
+            sub_block<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, true>(st, nxt, w, sc, t0, out_base, has_consumer, sb_off,
+                                                                    pend);
         if (CODES) {
             // codes[strip][t/16][lane][row-in-lane]: 8 B per lane
             typedef unsigned v2u __attribute__((ext_vector_type(2)));
@@ -530,6 +616,13 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         }
         // every ring read up to column t0+20 (incl. the next group's) was issued before this store
         lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
+    }
+
+    if (PLANES == 2) {   // the last group's planes (group 3 of the last sub-block)
+        pend_store<LCSP, 0, 3>(pend, w);
+        pend_store<LCSP, 1, 3>(pend, w);
+        pend_store<LCSP, 2, 3>(pend, w);
+        if (LCSP) pend_store<LCSP, 3, 3>(pend, w);
     }
 
     // ---- strip reduction of the max trackers ----
@@ -569,13 +662,15 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         StripTrace tr;
         tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
         tr.wait_in = (int)w.tr_win; tr.wait_out = (int)tr_wout;
-        tr.clk = __builtin_amdgcn_s_memtime() - clk_first; tr.pad0 = 0; tr.pad1 = 0;
+        tr.clk = __builtin_amdgcn_s_memtime() - clk_first;
+        for (int q = 0; q < kTraceQ; ++q) tr.t_q[q] = tr_q[q];
         trace[s] = tr;
     }
 }
 
 // I/O wave of a band: feeds ring 0 (row 0 analytic, or the previous band's
 // published bottom row) and drains ring W to HBM for the next band.
+template <bool TBL>
 __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Scores32& sc,
                         Rec* ring0, const Rec* ringW, lds_int* wcnt0, lds_int* rcnt0,
                         lds_int* wcntW, lds_int* rcntW, const bool do_out, int* status) {
@@ -606,7 +701,7 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
                             r.dd = max(I0 + sc.hg, sc.floor_);
                             r.sm = max(I0, sc.floor_);
                             r.l = 0;
-                            r.c2 = P.c2[j - 1];
+                            r.c2 = TBL ? sym_code(P.c2[j - 1], sc) * 8 : (int)P.c2[j - 1];
                         }
                     } else {
                         r = ld_rec_agent(feed_in + j);
@@ -645,8 +740,8 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
     }
 }
 
-template <int W, bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP>
-__global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAVES_TRACK : GX_FILL_MIN_WAVES) void fill_kernel(
+template <int W, bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL>
+__global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAVES_TRACK : (W + 1 + 3) / 4) void fill_kernel(
     const PairDev* __restrict__ pairs, const int npairs, const int total_bands, int* band_counter, StripRes* sres,
     PairRes* pres, const Scores32 sc) {
     __shared__ Rec rings[W + 1][kRing];
@@ -673,13 +768,15 @@ __global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAV
             if (s < P.strips) {
                 const bool last_in_band = wave == W - 1;
                 const bool has_consumer = last_in_band ? (lb + 1 < P.bands) : (s + 1 < P.strips);
-                compute_wave<LOCAL, PLANES, CODES, TRACK, LCSP>(
+                // plane stores pipelined one group late, except in 16-wave
+                // workgroups (128 VGPRs: no room for a group of pending cells)
+                compute_wave<LOCAL, PLANES ? ((W + 1) <= 12 ? 2 : 1) : 0, CODES, TRACK, LCSP, TBL>(
                     P, s, lane, sc, rings[wave], rings[wave + 1], (lds_int*)&wcnt[wave], (lds_int*)&rcnt[wave],
                     (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1], has_consumer, sres, pres + p,
                     band_counter + 1);
             }
         } else {
-            io_wave(P, lb, lane, sc, rings[0], rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0], (lds_int*)&wcnt[W],
+            io_wave<TBL>(P, lb, lane, sc, rings[0], rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0], (lds_int*)&wcnt[W],
                     (lds_int*)&rcnt[W], lb + 1 < P.bands, band_counter + 1);
         }
         __syncthreads();
@@ -898,49 +995,52 @@ __global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __rest
 // ---- explicit launch wrappers (C++ linkage, used by gx_api.cpp) ----
 namespace gx {
 
-template <int W, bool LOCAL, bool PLANES, bool TRACK, bool LCSP>
+template <int W, bool LOCAL, bool PLANES, bool TRACK, bool LCSP, bool TBL>
 static hipError_t launch_fill_t(const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
                                 StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
-    hipLaunchKernelGGL((fill_kernel<W, LOCAL, PLANES, true, TRACK, LCSP>), dim3(grid), dim3((W + 1) * kWave), 0, st,
+    hipLaunchKernelGGL((fill_kernel<W, LOCAL, PLANES, true, TRACK, LCSP, TBL>), dim3(grid), dim3((W + 1) * kWave), 0, st,
                        d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc);
     return hipGetLastError();
 }
 
 // Launch with the band width W from the variant's width list (gx_internal.h).
-template <bool LO, bool PL, bool TR, bool LC, int W0, int... Ws>
+template <bool LO, bool PL, bool TR, bool LC, bool TB, int W0, int... Ws>
 static hipError_t launch_fill_w(int W, const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
                                 StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
     if (W == W0)
-        return launch_fill_t<W0, LO, PL, TR, LC>(d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc, grid, st);
+        return launch_fill_t<W0, LO, PL, TR, LC, TB>(d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc, grid, st);
     if constexpr (sizeof...(Ws) > 0)
-        return launch_fill_w<LO, PL, TR, LC, Ws...>(W, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc,
+        return launch_fill_w<LO, PL, TR, LC, TB, Ws...>(W, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc,
                                                     grid, st);
     return hipErrorInvalidValue;
 }
 
 // Variants: mode (global/local) x planes x {no max tracking, first max + LCS
 // field, first max + LCS plane}.  Traceback codes are always produced.  The
-// untracked global variants (the batch path) come in every width of kFillWidths,
+// untracked global variants (the batch path) come in every width of kFillWidths
+// and with the small-alphabet score table (tbl) or the byte compare,
 // the tracked and local ones (256-VGPR builds) in kFillWidthsTrack.
-hipError_t launch_fill(int W, bool local, bool planes, bool track, bool lcs, const PairDev* d_pairs, int npairs,
-                       int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
-                       hipStream_t st) {
-#define GX_FILL_CASE(LO, PL, TR, LC, ...)                                                                \
-    if (local == LO && planes == PL && track == TR && lcs == LC)                                         \
-        return launch_fill_w<LO, PL, TR, LC, __VA_ARGS__>(W, d_pairs, npairs, total_bands, d_counter, d_sres, \
-                                                          d_pres, sc, grid, st);
+hipError_t launch_fill(int W, bool local, bool planes, bool track, bool lcs, bool tbl, const PairDev* d_pairs,
+                       int npairs, int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc,
+                       int grid, hipStream_t st) {
+#define GX_FILL_CASE(LO, PL, TR, LC, TB, ...)                                                                \
+    if (local == LO && planes == PL && track == TR && lcs == LC && tbl == TB)                                \
+        return launch_fill_w<LO, PL, TR, LC, TB, __VA_ARGS__>(W, d_pairs, npairs, total_bands, d_counter, d_sres, \
+                                                              d_pres, sc, grid, st);
 #define GX_W_ALL 3, 4, 6, 8, 11, 15
 #define GX_W_TRACK 3, 7
-    GX_FILL_CASE(false, false, false, false, GX_W_ALL)
-    GX_FILL_CASE(false, false, true, false, GX_W_TRACK)
-    GX_FILL_CASE(false, true, false, false, GX_W_ALL)
-    GX_FILL_CASE(false, true, true, false, GX_W_TRACK)
-    GX_FILL_CASE(false, true, true, true, GX_W_TRACK)
-    GX_FILL_CASE(true, false, false, false, GX_W_TRACK)
-    GX_FILL_CASE(true, false, true, false, GX_W_TRACK)
-    GX_FILL_CASE(true, true, false, false, GX_W_TRACK)
-    GX_FILL_CASE(true, true, true, false, GX_W_TRACK)
-    GX_FILL_CASE(true, true, true, true, GX_W_TRACK)
+    GX_FILL_CASE(false, false, false, false, false, GX_W_ALL)
+    GX_FILL_CASE(false, false, false, false, true, GX_W_ALL)
+    GX_FILL_CASE(false, false, true, false, false, GX_W_TRACK)
+    GX_FILL_CASE(false, true, false, false, false, GX_W_ALL)
+    GX_FILL_CASE(false, true, false, false, true, GX_W_ALL)
+    GX_FILL_CASE(false, true, true, false, false, GX_W_TRACK)
+    GX_FILL_CASE(false, true, true, true, false, GX_W_TRACK)
+    GX_FILL_CASE(true, false, false, false, false, GX_W_TRACK)
+    GX_FILL_CASE(true, false, true, false, false, GX_W_TRACK)
+    GX_FILL_CASE(true, true, false, false, false, GX_W_TRACK)
+    GX_FILL_CASE(true, true, true, false, false, GX_W_TRACK)
+    GX_FILL_CASE(true, true, true, true, false, GX_W_TRACK)
 #undef GX_FILL_CASE
     return hipErrorInvalidValue;
 }

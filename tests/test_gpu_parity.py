@@ -254,3 +254,22 @@ def test_staged_path_matches_oracle(gx, ctx, oracle):
                            (o.max_cell[0], o.max_cell[1], o.matches_at_max)
                 else:   # main.rs discards it: not tracked on the fused path
                     assert (r.max_cell_i, r.max_cell_j, r.matches_at_max) == (0, 0, 0)
+
+
+@pytest.mark.parametrize("alpha,scores", [(b"ACGT", CONFIG_SCORES), (b"AC", TEST_SCORES), (b"GT", (3, -1, -2, -4)),
+                                          (b"ACGTN", CONFIG_SCORES), (b"ACGT", (200, -2, -1, -5))],
+                         ids=["acgt", "ac", "gt", "five_symbols", "wide_scores"])
+def test_untracked_batch_score_table(gx, ctx, oracle, alpha, scores):
+    """The untracked global batch path: <= 4 symbols with byte-sized scores
+    take the packed score-table fill (one bit-field extract per cell), the
+    rest the byte compare; both bit-exact with the oracle."""
+    rng = random.Random(len(alpha) * 7 + scores[0])
+    pairs = [(bytes(rng.choice(alpha) for _ in range(n)), bytes(rng.choice(alpha) for _ in range(m)))
+             for n, m in [(1, 1), (5, 70), (128, 129), (300, 17), (257, 400)] + [(rng.randint(1, 300), rng.randint(1, 300))
+                                                                                 for _ in range(20)]]
+    out = gx.align_batch(pairs, sc(gx, scores), False, ctx=ctx, max_cell=False)
+    for (a, b), (steps, r) in zip(pairs, out):
+        o = oracle.align(a, b, scores)
+        assert steps_list(steps) == o.alignment(), (len(a), len(b))
+        assert (r.score, r.matches, r.mismatches, r.gap_extensions, r.opening_gaps) == \
+               (o.score, o.matches, o.mismatches, o.gap_extensions, o.opening_gaps)
