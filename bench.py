@@ -162,6 +162,8 @@ def main():
     ap.add_argument("--no-planes", action="store_true", help="score+traceback only (not the headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--single-pair-steps", type=int, default=5,
+                    help="also time BASELINE config 2's shape alone (one pair, latency), 1 GPU only; 0 = skip")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -246,6 +248,21 @@ def main():
         "fill_gcups_per_gpu": round(cells_rank / (avg_fill_ms * 1e-3) / 1e9, 3),
         "traceback_us_pair0": int(np.mean(tb_us)),
     }
+    if world == 1 and args.single_pair_steps > 0 and P > 1:
+        # one 30k x 30k pair per step (configs[1]'s shape): the latency view of the same kernel
+        one = gx.StagedPairs(pairs[:1], ctx=ctx)
+        one.run(scores, args.local, keep_planes)
+        f1 = []
+        t1 = time.perf_counter()
+        for _ in range(args.single_pair_steps):
+            _, fms = one.run(scores, args.local, keep_planes)
+            f1.append(fms)
+        e1 = time.perf_counter() - t1
+        c1 = len(pairs[0][0]) * len(pairs[0][1])
+        out["single_pair"] = {"gcups": round(c1 * args.single_pair_steps / e1 / 1e9, 3),
+                              "ms_per_step": round(e1 / args.single_pair_steps * 1e3, 3),
+                              "fill_ms_avg": round(float(np.mean(f1)), 3), "steps": args.single_pair_steps}
+        del one
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(pairs[0][0], pairs[0][1], args.cpu_seconds, args.local)
     if rank == 0:

@@ -97,11 +97,22 @@ struct Walk {
     gx_result res{};
 };
 
-// Device walk for a set of jobs; returns moves per job.
+// Device walk for a set of jobs: the per-strip row records in pinned host
+// memory (RecordsSrc replays one job's records as moves).
 struct TbOut {
-    std::vector<std::vector<uint8_t>> moves;
     std::vector<int> end_i, end_j;
+    std::vector<size_t> so;            // job -> its first strip in sg / hr
+    const int* c = nullptr;            // [4 * jobs] end i, end j, first strip
+    const int* sg = nullptr;           // [4 * strips] entry i, entry j, records, active
+    const uint32_t* hr = nullptr;      // [strips * kStripRows] records
     double ms = 0;
+};
+
+// Page-locked host buffer, grown on demand (device-to-host copies DMA
+// straight into it).
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
 };
 
 struct gx_context {
@@ -118,8 +129,7 @@ struct gx_context {
     // host buffers reused across calls (no fresh, page-faulting allocations per batch)
     std::vector<Walk> walk_cache;
     TbOut tb_cache;
-    std::vector<int> tb_c, tb_sg;
-    std::vector<uint32_t> tb_hr;
+    PinnedBuf tb_pin;
 };
 
 static int pool_get(gx_context* ctx, size_t bytes, DevBuf* out) {
@@ -189,6 +199,7 @@ extern "C" void gx_context_destroy(gx_context* ctx) {
     gx_context_trim(ctx);
     (void)hipSetDevice(ctx->device);
     if (ctx->st_chars.p) (void)hipFree(ctx->st_chars.p);
+    if (ctx->tb_pin.p) (void)hipHostFree(ctx->tb_pin.p);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->ev2) (void)hipEventDestroy(ctx->ev2);
@@ -502,40 +513,47 @@ static bool tb_match(const uint8_t* s1, size_t n, const uint8_t* s2, size_t m, u
     return a == b;
 }
 
+// Labels the walk (algo.rs:339-422).  The interior moves come from `src`,
+// which calls emit(code) per move (0 sub, 1 insert, 2 delete) while emit
+// returns true; the boundary part follows the reference loop.
+template <class Src>
 static int label_walk(const HostScores& hs, int is_local, const uint8_t* s1, size_t n, const uint8_t* s2, size_t m,
-                      uint64_t si, uint64_t sj, const uint8_t* moves, size_t nmoves, Walk& w) {
+                      uint64_t si, uint64_t sj, size_t nmoves_hint, Src&& src, Walk& w) {
     uint64_t i = si, j = sj;
     int last = GX_MATCH;
     gx_result& r = w.res;
-    r.matches = r.mismatches = r.gap_extensions = r.opening_gaps = 0;
+    uint64_t nmat = 0, nmis = 0, next = 0, nopen = 0;
     w.steps.clear();
-    w.steps.reserve(nmoves + (size_t)si + (size_t)sj + 2);
+    w.steps.reserve(nmoves_hint + (size_t)si + (size_t)sj + 2);
     bool done = false;
     // interior part, decided on the device
-    for (size_t k = 0; k < nmoves; ++k) {
+    src([&](uint8_t c) -> bool {
         gx_step st{};
         st.i = i; st.j = j;
-        const uint8_t c = moves[k];
         if (c == 0) {
             const bool mt = tb_match(s1, n, s2, m, i, j);
             st.choice = mt ? GX_MATCH : GX_MISMATCH;
-            if (mt) r.matches++; else r.mismatches++;
+            nmat += mt; nmis += !mt;
             last = st.choice;
             --i; --j;
         } else if (c == 1) {
-            if (last == GX_INSERT) { st.choice = GX_INSERT; r.gap_extensions++; }
-            else { st.choice = GX_OPEN_INSERT; r.opening_gaps++; }
+            const bool ext = last == GX_INSERT;
+            st.choice = ext ? GX_INSERT : GX_OPEN_INSERT;
+            next += ext; nopen += !ext;
             last = GX_INSERT;
             --j;
         } else {
-            if (last == GX_DELETE) { st.choice = GX_DELETE; r.gap_extensions++; }
-            else { st.choice = GX_OPEN_DELETE; r.opening_gaps++; }
+            const bool ext = last == GX_DELETE;
+            st.choice = ext ? GX_DELETE : GX_OPEN_DELETE;
+            next += ext; nopen += !ext;
             last = GX_DELETE;
             --i;
         }
         w.steps.push_back(st);
-        if (i == 0 && j == 0) { done = true; break; }
-    }
+        if (i == 0 && j == 0) { done = true; return false; }
+        return true;
+    });
+    r.matches = nmat; r.mismatches = nmis; r.gap_extensions = next; r.opening_gaps = nopen;
     // boundary part: the reference loop on analytic cells
     while (!done) {
         int64_t I, D, S;
@@ -619,48 +637,65 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     if (e == hipSuccess) e = hipEventRecord(ctx->ev1, ctx->stream);
     if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, max_strips, ctx->stream);
     if (e == hipSuccess) e = hipEventRecord(ctx->ev2, ctx->stream);
-    std::vector<int>& c = ctx->tb_c;
-    std::vector<int>& sg = ctx->tb_sg;
-    std::vector<uint32_t>& hr = ctx->tb_hr;
-    c.resize(4 * P);
-    sg.resize(4 * std::max<size_t>(stot, 1));
-    hr.resize(std::max<size_t>(stot, 1) * kStripRows);
-    if (e == hipSuccess) e = hipMemcpyAsync(c.data(), cnt.p, 4 * P * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(sg.data(), seg.p, sg.size() * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(hr.data(), recs.p, hr.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                            ctx->stream);
+    // one pinned host block: c | sg | hr
+    const size_t nc = 4 * P, nsg = 4 * std::max<size_t>(stot, 1), nhr = std::max<size_t>(stot, 1) * kStripRows;
+    const size_t bytes = (nc + nsg) * sizeof(int) + nhr * sizeof(uint32_t);
+    if (e == hipSuccess && ctx->tb_pin.cap < bytes) {
+        if (ctx->tb_pin.p) (void)hipHostFree(ctx->tb_pin.p);
+        ctx->tb_pin = PinnedBuf{};
+        e = hipHostMalloc(&ctx->tb_pin.p, bytes, hipHostMallocDefault);
+        if (e == hipSuccess) ctx->tb_pin.cap = bytes;
+    }
+    int* c = (int*)ctx->tb_pin.p;
+    int* sg = c + nc;
+    uint32_t* hr = (uint32_t*)(sg + nsg);
+    if (e == hipSuccess) e = hipMemcpyAsync(c, cnt.p, nc * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(sg, seg.p, nsg * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(hr, recs.p, nhr * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     cleanup();
     if (e != hipSuccess) return fail(GX_EHIP, std::string("traceback: ") + hipGetErrorString(e));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, ctx->ev1, ctx->ev2);
     out.ms = ms;
-    out.moves.resize(P);
+    out.c = c; out.sg = sg; out.hr = hr;
+    out.so = so;
     out.end_i.resize(P);
     out.end_j.resize(P);
     for (size_t p = 0; p < P; ++p) {
-        // concatenate the strips' row records from the start strip upwards and
-        // expand them into per-move codes (0 sub, 1 insert, 2 delete)
-        std::vector<uint8_t>& mv = out.moves[p];
-        mv.clear();
-        int nseg = 0;
-        for (int s = c[4 * p + 2]; s >= 0; --s) {
-            const int* g = &sg[4 * (so[p] + s)];
-            if (!g[3]) break;
-            ++nseg;
-            const uint32_t* r = &hr[(so[p] + s) * kStripRows];
-            for (int k = 0; k < g[2]; ++k) {
-                mv.insert(mv.end(), r[k] >> 2, (uint8_t)1);
-                if ((r[k] & 3u) != 1u) mv.push_back((uint8_t)(r[k] & 3u));
-            }
-        }
         out.end_i[p] = c[4 * p + 0];
         out.end_j[p] = c[4 * p + 1];
-        if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug") && p == 0)
-            fprintf(stderr, "[gx DEBUG] traceback pair 0: %d strips on the path, %zu moves\n", nseg, mv.size());
     }
     return GX_OK;
 }
+
+// Move source over a plain move array.
+struct MovesSrc {
+    const uint8_t* mv;
+    size_t n;
+    template <class E> void operator()(E&& emit) const {
+        for (size_t k = 0; k < n; ++k) if (!emit(mv[k])) return;
+    }
+};
+
+// Move source over job p's strip row records (run of inserts, then the
+// row's sub / delete move), from the start strip upwards.
+struct RecordsSrc {
+    const TbOut* tb;
+    size_t p;
+    template <class E> void operator()(E&& emit) const {
+        for (int s = tb->c[4 * p + 2]; s >= 0; --s) {
+            const int* g = &tb->sg[4 * (tb->so[p] + s)];
+            if (!g[3]) return;
+            const uint32_t* r = &tb->hr[(tb->so[p] + s) * kStripRows];
+            for (int k = 0; k < g[2]; ++k) {
+                for (uint32_t q = r[k] >> 2; q > 0; --q) if (!emit((uint8_t)1)) return;
+                if ((r[k] & 3u) != 1u && !emit((uint8_t)(r[k] & 3u))) return;
+            }
+        }
+    }
+};
+
 
 // Start cell + score (algo.rs:306-331).
 static int start_cell_common(const HostScores& hs, int is_local, size_t n, size_t m, const PairRes& r,
@@ -869,11 +904,11 @@ extern "C" int gx_retrace(gx_table* t, int is_local, gx_step* steps, size_t cap,
         TbOut tb;
         if (si >= 1 && sj >= 1 && n >= 1 && m >= 1) {
             rc = run_traceback(ctx, t->job, {TbStart{(int)si, (int)sj, is_local ? r.lmax_E : r.end_E}}, tb);
+            if (!rc) rc = label_walk(t->hs, is_local, t->s1.data(), n, t->s2.data(), m, si, sj, n + m,
+                                     RecordsSrc{&tb, 0}, w);
         } else {
-            tb.moves.assign(1, {});
+            rc = label_walk(t->hs, is_local, t->s1.data(), n, t->s2.data(), m, si, sj, 0, MovesSrc{nullptr, 0}, w);
         }
-        if (!rc) rc = label_walk(t->hs, is_local, t->s1.data(), n, t->s2.data(), m, si, sj, tb.moves[0].data(),
-                                 tb.moves[0].size(), w);
         const auto t1 = std::chrono::steady_clock::now();
         w.res.score = score;
         w.res.start_i = si; w.res.start_j = sj;
@@ -985,10 +1020,13 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
     std::vector<std::string> perr(P);
     auto label_range = [&](size_t lo, size_t hi) {
         for (size_t p = lo; p < hi; ++p) {
-            const uint8_t* mv = nullptr;
-            size_t nm = 0;
-            if (dev_of[p] >= 0) { mv = tb.moves[dev_of[p]].data(); nm = tb.moves[dev_of[p]].size(); }
-            prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], mv, nm, walks[p]);
+            // interior moves straight from the device's row records
+            if (dev_of[p] >= 0)
+                prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p],
+                                    ph[p].n + ph[p].m, RecordsSrc{&tb, (size_t)dev_of[p]}, walks[p]);
+            else
+                prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], 0,
+                                    MovesSrc{nullptr, 0}, walks[p]);
             if (prc[p]) perr[p] = g_err;   // g_err is thread-local
         }
     };
