@@ -101,6 +101,9 @@ __device__ __forceinline__ void gstore4(int32_t* p, int4 v) {
     *(gv4i*)p = x;
 }
 __device__ __forceinline__ void gstore1(uint32_t* p, uint32_t v) { *(guint*)p = v; }
+#ifndef GX_PLANE_AUX
+#define GX_PLANE_AUX 2   // nt: the planes are written once and never read back here
+#endif
 // Plane stores: one 16-B store per lane through a buffer descriptor of the
 // sub-block (uniform base, per-lane offset + immediate; the compiler places
 // the wait states for the SGPR operands).
@@ -108,8 +111,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, int byt
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
 }
 __device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t voff, int4 v) {
+#ifndef GX_DIAG_NO_PLANES
     v4i x = {v.x, v.y, v.z, v.w};
-    __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)voff, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)voff, 0, GX_PLANE_AUX);
+#endif
 }
 
 // Occupancy floor (waves per SIMD), which sets the fill kernel's VGPR cap
@@ -204,12 +209,17 @@ __device__ __forceinline__ void push63_pub(uint32_t base, const LaneState& st, u
 // range (kSkelOff) and are dropped by the range check -- no exec switch.
 // Full groups store their four columns at once; ramp groups one per step.
 constexpr uint32_t kSkelOff = 0x40000000u;
+// (GX_DIAG_* builds drop a kind of store, for timing only: tools/strip_pace.py)
 __device__ __forceinline__ void skel_store(__amdgpu_buffer_rsrc_t r, uint32_t voff, int E) {
+#ifndef GX_DIAG_NO_SKEL
     __builtin_amdgcn_raw_buffer_store_b32(E, r, (int)voff, 0, 0);
+#endif
 }
 __device__ __forceinline__ void skel_store4(__amdgpu_buffer_rsrc_t r, uint32_t voff, int e0, int e1, int e2, int e3) {
+#ifndef GX_DIAG_NO_SKEL
     v4i x = {e0, e1, e2, e3};
     __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)voff, 0, 0);
+#endif
 }
 
 // A wave-uniform pointer forced into an SGPR pair (for "s" asm operands).
@@ -612,7 +622,9 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
             typedef unsigned v2u __attribute__((ext_vector_type(2)));
             typedef __attribute__((address_space(1))) v2u gv2u;
             const v2u cw = {(st.a.cD << 16) | (st.a.cI & 0xFFFFu), (st.b.cD << 16) | (st.b.cI & 0xFFFFu)};
+#ifndef GX_DIAG_NO_CODES
             *(gv2u*)(w.codes + ((size_t)(t0 >> 4) * kWave + lane) * kRowsPerLane) = cw;
+#endif
         }
         // every ring read up to column t0+20 (incl. the next group's) was issued before this store
         lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
