@@ -156,7 +156,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs-per-gpu", type=int, default=int(os.environ.get("GX_BENCH_PAIRS", "8")))
+    ap.add_argument("--pairs-per-gpu", type=int, default=int(os.environ.get("GX_BENCH_PAIRS", "16")))
     ap.add_argument("--length", type=int, default=30000)
     ap.add_argument("--local", action="store_true", help="Smith-Waterman mode (default: global NW)")
     ap.add_argument("--no-planes", action="store_true", help="score+traceback only (not the headline)")

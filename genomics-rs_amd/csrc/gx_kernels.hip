@@ -2,21 +2,23 @@
 // fill of nlaha/genomics-rs (src/alignment/algo.rs:151-282) and the
 // per-cell-max traceback walk (algo.rs:339-422).
 //
-// Fill: one workgroup = one BAND of W strips (W compute waves) + 1 I/O wave.
-//   * lane l of a compute wave owns row i = 64*strip + l + 1 and sweeps the
-//     columns on the anti-diagonal skew (step t -> column t - l + 1);
+// Fill: one workgroup = one BAND of W 128-row strips (W compute waves) + 1 I/O
+// wave; persistent workgroups (one per CU) take bands from an atomic queue.
+//   * lane l of a compute wave owns rows 128*strip + 2l + 1 (A) and + 2 (B)
+//     and sweeps the columns on the anti-diagonal skew (step t -> column
+//     t - l + 1), row A then row B each step;
 //   * the row above arrives through a 64-lane DPP wave_shr:1 (lane l reads
-//     lane l-1's cell of the previous step); lane 0 takes it from an LDS ring
+//     lane l-1's row B of the previous step); lane 0 takes it from an LDS ring
 //     filled by the wave above (or by the I/O wave at a band boundary);
-//   * lane 63's cell is pushed into the LDS ring of the wave below;
-//   * the three int32 score planes are written 16 B/lane every 4 steps into
-//     the strip-major anti-diagonal layout (gx_internal.h) -- every store is a
-//     1 KiB contiguous wave store;
-//   * bands are taken from a global atomic queue in order, so the band a
-//     workgroup waits on is always held by a running workgroup (no residency
-//     assumption); band-to-band rows go through HBM with write-through (sc1)
-//     8-byte agent atomics and a per-boundary progress counter
-//     (cdna_hip_programming.md Guideline 16, "8-B agent atomics both sides").
+//   * lane 63's row-B cell is pushed into the LDS ring of the wave below;
+//   * the three int32 score planes are written 16 B/lane/row every 4 steps
+//     into the strip-major anti-diagonal layout (gx_internal.h) -- 1 KiB
+//     contiguous per store -- plus the traceback codes and the landing-column
+//     skeleton of the strip's bottom row;
+//   * bands are taken in order, so the band a workgroup waits on is always
+//     held by a running workgroup (no residency assumption); band-to-band
+//     rows go through HBM with write-through (sc1) 8-byte agent atomics and a
+//     per-boundary progress counter (cdna_hip_programming.md Guideline 16).
 // No MFMA: the recurrence is an integer max-plus, not a contraction.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
