@@ -389,7 +389,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         co[p] = code_elems; code_elems += (size_t)d.strips * d.t16 * kStripRows;
         so[p] = skel_elems; skel_elems += (size_t)d.strips * d.skel_stride;
         fo[p] = feed_recs; feed_recs += (size_t)std::max(d.bands - 1, 0) * d.feed_stride;
-        gofs[p] = prog_elems; prog_elems += (size_t)std::max(d.bands - 1, 0);
+        gofs[p] = prog_elems; prog_elems += (size_t)std::max(d.bands - 1, 0) * kProgStride;
     }
     job.total_bands = bands;
     job.total_strips = strips;

@@ -106,7 +106,7 @@ struct PairDev {
     int32_t* pL;         // optional LCS plane (full AlignmentCell export)
     uint32_t* codes;     // traceback codes (nullptr: none)
     Rec* feed;           // [bands-1][feed_stride] band-boundary rows
-    int* progress;       // [bands-1] columns published per boundary
+    int* progress;       // [bands-1][kProgStride] columns published per boundary (one per 256 B)
     StripTrace* trace;   // per strip, or nullptr
     int* skel;           // [strips][skel_stride] landing column E of each strip's bottom row
     int feed_stride;
@@ -124,6 +124,11 @@ struct TbDev {           // per-pair traceback job
     uint32_t* recs;        // out: [strips][kStripRows] one record per row, (insert run << 2) | kind
     int* end_ij;           // out: [4] {i, j} where the walk leaves the interior, first strip, rounds
 };
+
+// Band-boundary progress counters sit 256 B apart: every I/O wave polls its
+// own, and neighbouring counters in one cache line would put all of a
+// batch's polls on one L2 channel.
+constexpr int kProgStride = 64;
 
 inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
 

@@ -692,8 +692,8 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
     int in_next = 0, out_next = 0;
     const Rec* feed_in = lb > 0 ? P.feed + (size_t)(lb - 1) * P.feed_stride : nullptr;
     Rec* feed_out = do_out ? P.feed + (size_t)lb * P.feed_stride : nullptr;
-    const int* prog_in = lb > 0 ? P.progress + (lb - 1) : nullptr;
-    int* prog_out = do_out ? P.progress + lb : nullptr;
+    const int* prog_in = lb > 0 ? P.progress + (size_t)(lb - 1) * kProgStride : nullptr;
+    int* prog_out = do_out ? P.progress + (size_t)lb * kProgStride : nullptr;
     unsigned idle = 0;
     while (in_next <= m || (do_out && out_next <= m)) {
         bool moved = false;
