@@ -224,6 +224,34 @@ __device__ __forceinline__ void skel_store4(__amdgpu_buffer_rsrc_t r, uint32_t v
 #endif
 }
 
+constexpr int kPushScratch = 128;   // uint32 per wave: 64 lanes x 4 B + a sub-block's record offsets (252 B)
+// Full-group pushes without an exec switch: every lane writes, lane 63 to
+// the ring slot and the other lanes to their own scratch slots in LDS
+// (per-lane address vaddr, chosen once per sub-block), so the wave never
+// leaves full exec.  Same record layout as push63.
+template <int U, bool TRACK>
+__device__ __forceinline__ void push_all(uint32_t vaddr, const LaneState& st) {
+    if (TRACK)
+        asm volatile(
+            "ds_write2_b32 %0, %1, %2 offset0:%5 offset1:%6\n\t"
+            "ds_write2_b32 %0, %3, %4 offset0:%7 offset1:%8"
+            :
+            : "v"(vaddr), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "v"(st.b.L), "i"(4 * U), "i"(4 * U + 1),
+              "i"(4 * U + 2), "i"(4 * U + 3)
+            : "memory");
+    else
+        asm volatile(
+            "ds_write2_b32 %0, %1, %2 offset0:%4 offset1:%5\n\t"
+            "ds_write_b32 %0, %3 offset:%6"
+            :
+            : "v"(vaddr), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8)
+            : "memory");
+}
+// ... and the ring's write counter (lane 63: the counter; others: scratch)
+__device__ __forceinline__ void publish_all(uint32_t caddr, int cnt) {
+    asm volatile("ds_write_b32 %0, %1" : : "v"(caddr), "v"(cnt) : "memory");
+}
+
 // A wave-uniform pointer forced into an SGPR pair (for "s" asm operands).
 __device__ __forceinline__ const int* uniform_ptr(const int* p) {
     const uint64_t v = (uint64_t)(uintptr_t)p;
@@ -376,6 +404,8 @@ struct WaveCtx {
     int* status;
     __amdgpu_buffer_rsrc_t skel_rsrc;                       // skeleton row of this strip (bottom-row E)
     uint32_t skel_voff;                                     // lane 63: 0; other lanes: out of range
+    uint32_t scratch;                                       // this lane's LDS scratch slot (full-group pushes)
+    uint32_t cnt_addr;                                      // lane 63 with a consumer: the ring counter; else scratch
     int m, lane, c1a, c1b;
     unsigned tr_win;
 };
@@ -447,21 +477,23 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
         dp_step<LOCAL, true, CODES, TRACK, TBL>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, sc, bI[3], bD[3], bS[3], bL[3]);
         skel_store(w.skel_rsrc, sko(col0 + 4), st.b.E);   // lane 63's column after the step
     } else {
-        const unsigned long long m63 = lane63_mask(push_on);
-        push63<4 * G4 + 0, TRACK>(out_base, st, m63);
+        // lane 63 (with a consumer) pushes to the ring, the other lanes to scratch
+        const uint32_t pa = push_on && w.lane == kWave - 1 ? out_base : w.scratch;
+        push_all<4 * G4 + 0, TRACK>(pa, st);
         dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
         if (PLANES == 2) pend_store<LCSP, 0, G4P>(pend, w);
         const int e0 = st.b.E;              // lane 63: column col0 + 1
-        push63<4 * G4 + 1, TRACK>(out_base, st, m63);
+        push_all<4 * G4 + 1, TRACK>(pa, st);
         dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
         if (PLANES == 2) pend_store<LCSP, 1, G4P>(pend, w);
         const int e1 = st.b.E;
-        push63<4 * G4 + 2, TRACK>(out_base, st, m63);
+        push_all<4 * G4 + 2, TRACK>(pa, st);
         dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
         if (PLANES == 2) pend_store<LCSP, 2, G4P>(pend, w);
         if (PLANES == 2 && LCSP) pend_store<LCSP, 3, G4P>(pend, w);
         const int e2 = st.b.E;
-        push63_pub<4 * G4 + 3, TRACK>(out_base, st, m63, lds_addr((const void*)w.wcnt_out), col0 + 3 + 1);
+        push_all<4 * G4 + 3, TRACK>(pa, st);
+        publish_all(w.cnt_addr, col0 + 3 + 1);   // after the records: LDS runs one wave's DS ops in order
         dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, sc, bI[3], bD[3], bS[3], bL[3]);
         // lane 63's landing columns of columns col0+1 .. col0+4 (full groups: all in 1..m), one store
         skel_store4(w.skel_rsrc, w.skel_voff + 4u * (uint32_t)(col0 + 1), e0, e1, e2, st.b.E);
@@ -538,7 +570,8 @@ __device__ __forceinline__ void init_row(RowState& rs, const int i, const bool r
 template <bool LOCAL, int PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL>
 __device__ void compute_wave(const PairDev& P, const int s, const int lane, const Scores32& sc, const Rec* ring_in,
                              Rec* ring_out, lds_int* wcnt_in, lds_int* rcnt_in, lds_int* wcnt_out, lds_int* rcnt_out,
-                             const bool has_consumer, StripRes* sres, PairRes* pres, int* status) {
+                             const bool has_consumer, StripRes* sres, PairRes* pres, int* status,
+                             const uint32_t scratch_base) {
     static_assert(kSub == 16, "16-step sub-blocks (code words, ring alignment)");
     static_assert(kRowsPerLane == 2, "two rows per lane");
     const int n = P.n, m = P.m;
@@ -557,6 +590,9 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     // skeleton row (only stored when there is a strip below: otherwise an empty range)
     w.skel_rsrc = rsrc_of(uniform_ptr(P.skel + (size_t)s * P.skel_stride), has_consumer ? 4 * (m + 1) : 0);
     w.skel_voff = lane == kWave - 1 ? 0u : kSkelOff;
+    // scratch: 4-B lane stride (conflict-free), room for a sub-block's 16 record offsets
+    w.scratch = scratch_base + 4u * (uint32_t)lane;
+    w.cnt_addr = (has_consumer && lane == kWave - 1) ? lds_addr((const void*)wcnt_out) : w.scratch;
     w.m = m; w.lane = lane;
     w.c1a = ok_a ? (int)P.c1[ia - 1] : 0x1FF;   // 0x1FF never equals a byte
     w.c1b = ok_b ? (int)P.c1[ia] : 0x1FF;
@@ -682,6 +718,9 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     }
 }
 
+#ifndef GX_IO_SLEEP
+#define GX_IO_SLEEP 1
+#endif
 // I/O wave of a band: feeds ring 0 (row 0 analytic, or the previous band's
 // published bottom row) and drains ring W to HBM for the next band.
 template <bool TBL>
@@ -749,7 +788,7 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
             __hip_atomic_store((gint*)status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
         } else {
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(GX_IO_SLEEP);
         }
     }
 }
@@ -759,6 +798,7 @@ __global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAV
     const PairDev* __restrict__ pairs, const int npairs, const int total_bands, int* band_counter, StripRes* sres,
     PairRes* pres, const Scores32 sc) {
     __shared__ Rec rings[W + 1][kRing];
+    __shared__ uint32_t push_scratch[W][kPushScratch];   // lanes 0-62's writes of the full-group pushes
     __shared__ int wcnt[W + 1];
     __shared__ int rcnt[W + 1];
     __shared__ int band_sh;
@@ -787,7 +827,7 @@ __global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAV
                 compute_wave<LOCAL, PLANES ? ((W + 1) <= 12 ? 2 : 1) : 0, CODES, TRACK, LCSP, TBL>(
                     P, s, lane, sc, rings[wave], rings[wave + 1], (lds_int*)&wcnt[wave], (lds_int*)&rcnt[wave],
                     (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1], has_consumer, sres, pres + p,
-                    band_counter + 1);
+                    band_counter + 1, lds_addr(push_scratch[wave]));
             }
         } else {
             io_wave<TBL>(P, lb, lane, sc, rings[0], rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0], (lds_int*)&wcnt[W],
