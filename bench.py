@@ -130,6 +130,24 @@ def load_traffic(workload: str):
     return None, None
 
 
+def allvsall_share(gx, rank: int, world: int):
+    """BASELINE config 4: rank r's longest-processing-time share of the 45
+    pairs i<j of the comparison_data genomes (files in name order, the same
+    plan on every rank, so no scatter is needed for the bench; the product's
+    gxamd.all_vs_all broadcasts the sequences instead).  Returns (pairs, all
+    ranks' total cells)."""
+    cont = gx.SequenceContainer()
+    d = os.path.join(ROOT, "tests", "golden", "comparison_data")
+    for f in sorted(os.listdir(d)):
+        if f.endswith(".fasta"):
+            cont.from_fasta(os.path.join(d, f))
+    seqs = [x.sequence.encode() for x in cont.sequences]
+    pairs = gx.all_pairs(len(seqs), with_self=False)
+    w = [float(len(seqs[i])) * len(seqs[j]) for i, j in pairs]
+    mine = gx.lpt_partition(w, world)[rank]
+    return [(seqs[pairs[p][0]], seqs[pairs[p][1]]) for p in mine], int(sum(w))
+
+
 def rank_pairs(rank: int, pairs_per_rank: int, length: int):
     """Weak-scaling shard: rank r aligns synthetic pairs r*P .. r*P+P-1 (no
     data-path collective; every rank generates its own inputs)."""
@@ -145,10 +163,20 @@ def combine_over_ranks(dist, elapsed: float, rows, device: str):
     import torch
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    mine = torch.tensor(rows, dtype=torch.int64, device=device).reshape(-1, 3)
+    # ranks may hold different pair counts (all-vs-all LPT shares): pad to the
+    # largest share with a count column so that all_gather sees equal shapes
+    cnt = torch.tensor([len(rows)], dtype=torch.int64, device=device)
+    cap = cnt.clone()
+    dist.all_reduce(cap, op=dist.ReduceOp.MAX)
+    mine = torch.zeros((int(cap.item()), 3), dtype=torch.int64, device=device)
+    if rows:
+        mine[: len(rows)] = torch.tensor(rows, dtype=torch.int64, device=device).reshape(-1, 3)
     gathered = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+    counts = [torch.zeros_like(cnt) for _ in range(dist.get_world_size())]
     dist.all_gather(gathered, mine)
-    return float(t.item()), [[tuple(int(x) for x in r) for r in g.cpu().tolist()] for g in gathered]
+    dist.all_gather(counts, cnt)
+    return float(t.item()), [[tuple(int(x) for x in r) for r in g.cpu().tolist()[: int(c.item())]]
+                             for g, c in zip(gathered, counts)]
 
 
 def main():
@@ -162,6 +190,10 @@ def main():
     ap.add_argument("--no-planes", action="store_true", help="score+traceback only (not the headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["synthetic", "allvsall"], default="synthetic",
+                    help="allvsall: BASELINE config 4, the 45 pairs i<j of the 10 comparison_data genomes, "
+                         "LPT-sharded over the ranks (traceback-only fill unless --planes)")
+    ap.add_argument("--planes", action="store_true", help="allvsall: also write the score planes")
     ap.add_argument("--single-pair-steps", type=int, default=5,
                     help="also time BASELINE config 2's shape alone (one pair, latency), 1 GPU only; 0 = skip")
     args = ap.parse_args()
@@ -180,10 +212,16 @@ def main():
     import gxamd as gx
     ctx = gx.Context(local_rank)
     P, L = args.pairs_per_gpu, args.length
-    pairs = rank_pairs(rank, P, L)
+    if args.workload == "allvsall":
+        pairs, n_total = allvsall_share(gx, rank, world)
+        P = len(pairs)
+        keep_planes = args.planes
+        args.single_pair_steps = 0
+    else:
+        pairs = rank_pairs(rank, P, L)
+        keep_planes = not args.no_planes
     staged = gx.StagedPairs(pairs, ctx=ctx)             # inputs resident in HBM
     scores = gx.Scores(*SCORES)
-    keep_planes = not args.no_planes
     cells_rank = sum(len(a) * len(b) for a, b in pairs)
 
     def barrier():
@@ -214,11 +252,18 @@ def main():
     # max over ranks (time) and gather of per-pair results, over RCCL
     elapsed, _gathered = combine_over_ranks(dist, elapsed, [[r.score, r.n_steps, r.matches] for r in res], "cuda")
     total_cells = cells_rank * world
+    if args.workload == "allvsall":
+        total_cells = n_total
     ms_per_step = elapsed / args.steps * 1e3
     gcups = total_cells * args.steps / elapsed / 1e9
     avg_fill_ms = float(np.mean(fill_ms))
-    workload = f"synthetic {L}x{L} DNA pairs (SplitMix64), {P} per GPU, {'local SW' if args.local else 'global NW'}, " \
-               f"scores {SCORES}, {'score planes + traceback' if keep_planes else 'traceback only (no planes)'}"
+    mode_s = f"{'local SW' if args.local else 'global NW'}, scores {SCORES}, " \
+             f"{'score planes + traceback' if keep_planes else 'traceback only (no planes)'}"
+    if args.workload == "allvsall":
+        workload = f"all-vs-all of the 10 comparison_data genomes (45 pairs i<j, 29,644-30,123 nt), " \
+                   f"LPT-sharded over {world} GPU(s), {mode_s}"
+    else:
+        workload = f"synthetic {L}x{L} DNA pairs (SplitMix64), {P} per GPU, {mode_s}"
     fill_bytes = BYTES_PER_CELL * cells_rank
     achieved = fill_bytes / (avg_fill_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(workload)
@@ -232,11 +277,11 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.workload == "allvsall" else "weak",
         "vs_baseline": None,
         "dtype": "int32",
-        "data": "synthetic",
-        "config": {"workload": workload, "pairs_per_gpu": P, "seq_len": L,
+        "data": "comparison_data FASTA (real genomes)" if args.workload == "allvsall" else "synthetic",
+        "config": {"workload": workload, "pairs_per_gpu": P, "seq_len": L if args.workload == "synthetic" else None,
                    "cells_per_step": total_cells, "parallelism": f"pairs sharded over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if keep_planes else None,
                      "peak": PEAK_HBM_GBS, "unit": "GB/s",

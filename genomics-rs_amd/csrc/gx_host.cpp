@@ -368,3 +368,86 @@ extern "C" int gx_format_alignment(const uint8_t* s1, size_t n, const uint8_t* s
     memcpy(out, f.c_str(), f.size() + 1);
     return GX_OK;
 }
+
+// ---- display.rs:131-220  print_alignment_table / print_scores_table --------
+//
+// The reference prints these from inside retrace (algo.rs:438) with the table
+// it was handed; here the caller passes the three int64 score planes
+// (row-major (n+1)x(m+1), as gx_table_export_plane writes them) and the
+// alignment, and receives the text print_alignment_table writes to stdout.
+// Inputs with n >= 200 or m >= 2000 produce the empty string (the reference
+// warns "Sequence table too large to visualize" and prints nothing,
+// display.rs:139-144).  `color` selects the `colored` crate's ANSI styling
+// (it colours only when stdout is a terminal); 0 gives plain text.
+
+namespace {
+// Number of chars in a UTF-8 byte string (the reference indexes with chars().nth()).
+size_t utf8_chars(const uint8_t* s, size_t len) {
+    size_t c = 0;
+    for (size_t k = 0; k < len; ++k) c += (s[k] & 0xC0) != 0x80;
+    return c;
+}
+
+void scores_table(std::string& f, const int64_t* plane, size_t n, size_t m) {
+    // display.rs:183-219
+    f += ". \t";
+    for (size_t j = 0; j <= m; ++j) f += std::to_string(j) + "\t";
+    f += "\n";
+    for (size_t i = 0; i <= n; ++i) {
+        f += std::to_string(i) + "\t";
+        for (size_t j = 0; j <= m; ++j) {
+            const int64_t v = plane[i * (m + 1) + j];
+            f += v <= -9223372036854775700LL ? std::string("-inf") : std::to_string(v);
+            f += "\t";
+        }
+        f += "\n";
+    }
+}
+}  // namespace
+
+extern "C" int gx_format_table(const uint8_t* s1, size_t n, const uint8_t* s2, size_t m, const gx_step* steps,
+                               size_t n_steps, const int64_t* insert_plane, const int64_t* delete_plane,
+                               const int64_t* sub_plane, int color, char* out, size_t cap, size_t* needed) {
+    if ((!s1 && n) || (!s2 && m) || (!steps && n_steps)) return hfail(GX_EINVAL, "NULL argument");
+    const size_t W = 200;  // DISP_MAX_WIDTH (display.rs:7)
+    std::string f;
+    if (n < W && m < W * 10) {
+        if (!insert_plane || !delete_plane || !sub_plane) return hfail(GX_EINVAL, "NULL score plane");
+        // chars().nth(k).unwrap() for k < byte length panics on multi-byte text
+        if (utf8_chars(s1, n) != n || utf8_chars(s2, m) != m)
+            return hfail(GX_EPANIC, "called `Option::unwrap()` on a `None` value (display.rs:150)");
+        // path cells: .find(|(_, x, y)| x == i+1 && y == j+1) takes the first hit
+        std::vector<int8_t> mark((n + 1) * (m + 1), -1);
+        for (size_t k = n_steps; k-- > 0;) {
+            const gx_step& s = steps[k];
+            if (s.i <= n && s.j <= m) mark[s.i * (m + 1) + s.j] = (int8_t)s.choice;
+        }
+        static const char* glyph[6] = {"M", "X", "I", "D", "I", "D"};
+        // colored 3: fg green 32, red 31, blue 34, cyan 36; bold = style 1
+        static const char* style[6] = {"\x1b[32m", "\x1b[31m", "\x1b[34m", "\x1b[36m", "\x1b[1;34m", "\x1b[1;36m"};
+        f += "\nSequence Table (S1 columns, S2 rows):\n\n";
+        f += " ";
+        f.append((const char*)s2, m);
+        f += "\n";
+        for (size_t i = 0; i < n; ++i) {
+            f.push_back((char)s1[i]);
+            for (size_t j = 0; j < m; ++j) {
+                const int c = mark[(i + 1) * (m + 1) + (j + 1)];
+                if (c < 0 || c > 5) { f += "."; continue; }
+                if (color) f += std::string(style[c]) + glyph[c] + "\x1b[0m";
+                else f += glyph[c];
+            }
+            f += "\n";
+        }
+        f += "Delete Scores\n";
+        scores_table(f, delete_plane, n, m);
+        f += "Insert Scores\n";
+        scores_table(f, insert_plane, n, m);
+        f += "Sub Scores\n";
+        scores_table(f, sub_plane, n, m);
+    }
+    if (needed) *needed = f.size() + 1;
+    if (!out || cap < f.size() + 1) return hfail(GX_ECAP, "output buffer too small");
+    memcpy(out, f.c_str(), f.size() + 1);
+    return GX_OK;
+}

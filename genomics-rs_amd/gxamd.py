@@ -70,7 +70,7 @@ STEP_DTYPE = np.dtype([("choice", "u1"), ("pad", "u1", (7,)), ("i", "<u8"), ("j"
 EXPORTED = ["gx_last_error", "gx_version", "gx_context_create", "gx_context_destroy", "gx_context_trim",
             "gx_alignment_table", "gx_table_info", "gx_table_export", "gx_table_export_plane", "gx_retrace",
             "gx_table_free", "gx_align", "gx_align_batch", "gx_stage_pairs", "gx_run_staged", "gx_fasta_load",
-            "gx_config_load", "gx_format_alignment"]
+            "gx_config_load", "gx_format_alignment", "gx_format_table"]
 
 _lib = None
 
@@ -108,6 +108,7 @@ def lib():
     L.gx_fasta_load.argtypes = [ctypes.c_char_p, vp, sz, vp, vp, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.gx_config_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(CScores)]
     L.gx_format_alignment.argtypes = [vp, sz, vp, sz, vp, sz, ctypes.POINTER(CResult), vp, sz, ctypes.POINTER(sz)]
+    L.gx_format_table.argtypes = [vp, sz, vp, sz, vp, sz, vp, vp, vp, ctypes.c_int, vp, sz, ctypes.POINTER(sz)]
     _lib = L
     return L
 
@@ -362,15 +363,67 @@ def alignment_table(sequence_container: SequenceContainer, scores: Scores, is_lo
     return AlignmentTable(t, s1, s2, flags), int(mam.value)
 
 
+DISP_MAX_WIDTH = 200  # display.rs:7
+
+
+def _stdout_color() -> bool:
+    """The `colored` crate's decision: a terminal, unless NO_COLOR / CLICOLOR=0
+    (CLICOLOR_FORCE forces colour)."""
+    import sys
+    if os.environ.get("CLICOLOR_FORCE", "0") != "0":
+        return True
+    if os.environ.get("NO_COLOR") or os.environ.get("CLICOLOR") == "0":
+        return False
+    return sys.stdout.isatty()
+
+
+def format_alignment_table(aligned: "AlignedSequences", planes, color: bool = False) -> str:
+    """Text of print_alignment_table (display.rs:131-181) with its three
+    print_scores_table blocks (display.rs:183-220).  `planes` = (insert,
+    delete, sub) int64 row-major (n+1, m+1) arrays (AlignmentTable.plane);
+    "" when the table is too large to visualise (display.rs:139-144)."""
+    a = aligned.s1.sequence.encode()
+    b = aligned.s2.sequence.encode()
+    x, pa = _buf(a)
+    y, pb = _buf(b)
+    steps = aligned._steps if aligned._steps is not None else _steps_array(aligned.alignment)
+    small = len(a) < DISP_MAX_WIDTH and len(b) < DISP_MAX_WIDTH * 10
+    pl = [np.ascontiguousarray(p, dtype=np.int64) for p in planes] if small else [None, None, None]
+    ptrs = [p.ctypes.data if p is not None else None for p in pl]
+    need = ctypes.c_size_t(0)
+    L = lib()
+    L.gx_format_table(pa, len(a), pb, len(b), steps.ctypes.data, len(steps), *ptrs, int(color), None, 0,
+                      ctypes.byref(need))
+    out = ctypes.create_string_buffer(need.value)
+    _check(L.gx_format_table(pa, len(a), pb, len(b), steps.ctypes.data, len(steps), *ptrs, int(color), out,
+                             need.value, None))
+    return out.value.decode("utf-8")
+
+
+def print_alignment_table(aligned: "AlignedSequences", planes) -> None:
+    """print_alignment_table (display.rs:131-181) to stdout."""
+    import sys
+    sys.stdout.write(format_alignment_table(aligned, planes, _stdout_color()))
+
+
 def retrace(sequence_container: SequenceContainer, table: AlignmentTable, is_local: bool) -> AlignedSequences:
-    """retrace (algo.rs:287-441).  Consumes `table`."""
+    """retrace (algo.rs:287-441).  Consumes `table`.  Like the reference
+    (algo.rs:438) it ends by printing the sequence table for small inputs
+    (tables filled with GX_TABLE_PLANES; set GX_NO_TABLE_PRINT=1 to skip)."""
     a, b = _first_two(sequence_container)
     cap = len(table.s1) + len(table.s2) + 2
     steps = np.zeros(cap, STEP_DTYPE)
     r = CResult()
+    small = len(table.s1) < DISP_MAX_WIDTH and len(table.s2) < DISP_MAX_WIDTH * 10
+    planes = None
+    if small and (table.flags & GX_TABLE_PLANES) and not os.environ.get("GX_NO_TABLE_PRINT"):
+        planes = [table.plane(k) for k in range(3)]   # before the table is consumed
     ptr, table.ptr = table.ptr, None
     _check(lib().gx_retrace(ptr, int(is_local), steps.ctypes.data, cap, ctypes.byref(r)))
-    return _aligned(a, b, steps[: r.n_steps], r)
+    out = _aligned(a, b, steps[: r.n_steps], r)
+    if planes is not None:
+        print_alignment_table(out, planes)
+    return out
 
 
 def _aligned(a: Sequence, b: Sequence, steps: np.ndarray, r: CResult) -> AlignedSequences:
@@ -441,3 +494,120 @@ class StagedPairs:
         _check(lib().gx_run_staged(self.ctx.ptr, ctypes.byref(scores.c()), int(is_local), int(keep_planes),
                                    GX_ALIGN_MAX_CELL if max_cell else 0, res, ctypes.byref(fms)))
         return list(res), fms.value
+
+
+# ---------------------------------------------------------------------------
+# all-vs-all (BASELINE config 4)
+
+def lpt_partition(weights: Seq[float], parts: int) -> List[List[int]]:
+    """Longest-processing-time assignment of items (weight = n*m cells) to
+    `parts` GPUs; each bin sorted.  Deterministic, so every rank computes the
+    same plan without communicating."""
+    order = sorted(range(len(weights)), key=lambda k: (-weights[k], k))
+    bins: List[List[int]] = [[] for _ in range(parts)]
+    load = [0.0] * parts
+    for k in order:
+        b = min(range(parts), key=lambda x: (load[x], x))
+        bins[b].append(k)
+        load[b] += weights[k]
+    return [sorted(b) for b in bins]
+
+
+def all_pairs(k: int, with_self: bool = True) -> List[Tuple[int, int]]:
+    """(i, j) with i <= j (i < j without self pairs), in the reference compare
+    matrix's fill order: row j, column i (main.rs:253-264)."""
+    return [(i, j) for j in range(k) for i in range(j + 1) if i < j or with_self]
+
+
+PAIR_FIELDS = ("score", "matches", "mismatches", "gap_extensions", "opening_gaps", "n_steps")
+
+
+def _batch_stats(pairs, scores, is_local, ctx):
+    """Product aligner for one rank's share: one gx_align_batch launch."""
+    res = align_batch(pairs, scores, is_local, with_steps=False, ctx=ctx, max_cell=False)
+    return [[getattr(r, f) for f in PAIR_FIELDS] for _, r in res]
+
+
+def _pack(seqs: List[bytes]):
+    lens = np.array([len(s) for s in seqs], np.int64)
+    buf = np.frombuffer(b"".join(seqs), np.uint8) if lens.sum() else np.zeros(0, np.uint8)
+    return lens, buf
+
+
+def all_vs_all(sequence_container: SequenceContainer, scores: Scores, is_local: bool = False,
+               with_self: bool = True, ctx: Optional[Context] = None, dist=None, device: str = "cpu",
+               align_fn=None) -> dict:
+    """Align every pair (i <= j) of the container's sequences.
+
+    dist = None: one GPU (ctx), one batched launch.  dist = torch.distributed
+    (one process per GPU): rank 0's container is broadcast to every rank (the
+    scatter; ≈30 KB per genome), each rank aligns its longest-processing-time
+    share of the pairs, and the fixed-size per-pair records are all-gathered
+    (RCCL over xGMI for backend "nccl", `device` = "cuda"; gloo on CPU).  No
+    collective touches the DP data.  align_fn(pairs, scores, is_local) -> rows
+    replaces the GPU aligner (tests of the plumbing only).
+
+    Returns {"names", "lengths", "pairs", "records"}: records[p] = PAIR_FIELDS
+    of pairs[p]; matrix(...) renders the reference's TSV layout."""
+    align_fn = align_fn or (lambda prs, sc, loc: _batch_stats(prs, sc, loc, ctx or default_context()))
+    seqs = [s.sequence.encode() for s in sequence_container.sequences]
+    names = [s.name for s in sequence_container.sequences]
+    if dist is not None:
+        import torch
+        rank, world = dist.get_rank(), dist.get_world_size()
+        # scatter: broadcast the packed sequences from rank 0
+        meta = torch.zeros(2, dtype=torch.int64, device=device)
+        if rank == 0:
+            lens, buf = _pack(seqs)
+            meta[0], meta[1] = len(seqs), int(lens.sum())
+        dist.broadcast(meta, 0)
+        k, tot = int(meta[0]), int(meta[1])
+        tl = torch.zeros(k, dtype=torch.int64, device=device)
+        tb = torch.zeros(max(tot, 1), dtype=torch.uint8, device=device)
+        if rank == 0:
+            tl.copy_(torch.from_numpy(lens))
+            if tot:
+                tb[:tot].copy_(torch.from_numpy(buf.copy()))
+        dist.broadcast(tl, 0)
+        dist.broadcast(tb, 0)
+        lens = tl.cpu().numpy()
+        raw = tb.cpu().numpy().tobytes()
+        offs = np.concatenate([[0], np.cumsum(lens)])
+        seqs = [raw[int(offs[x]):int(offs[x + 1])] for x in range(k)]
+    else:
+        rank, world = 0, 1
+    pairs = all_pairs(len(seqs), with_self)
+    weights = [float(len(seqs[i])) * len(seqs[j]) for i, j in pairs]
+    mine = lpt_partition(weights, world)[rank]
+    rows = align_fn([(seqs[pairs[p][0]], seqs[pairs[p][1]]) for p in mine], scores, is_local) if mine else []
+    local = np.array([[p] + list(r) for p, r in zip(mine, rows)], np.int64).reshape(-1, 1 + len(PAIR_FIELDS))
+    if dist is not None:
+        import torch
+        # gather: fixed-size records, padded to the largest share
+        cap = max(len(b) for b in lpt_partition(weights, world))
+        t = torch.full((cap, local.shape[1]), -1, dtype=torch.int64, device=device)
+        if len(local):
+            t[: len(local)].copy_(torch.from_numpy(local))
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        local = np.concatenate([x.cpu().numpy() for x in parts])
+        local = local[local[:, 0] >= 0]
+    records: List[Optional[List[int]]] = [None] * len(pairs)
+    for row in local:
+        records[int(row[0])] = [int(x) for x in row[1:]]
+    if any(r is None for r in records):
+        raise GxError(1, "all_vs_all: missing pair records after gather")
+    return {"names": names, "lengths": [len(s) for s in seqs], "pairs": pairs, "records": records}
+
+
+def similarity_tsv(result: dict, field: str = "score", blank_header: bool = False) -> str:
+    """The reference compare writer's layout (main.rs:333-359): a header row of
+    sequence indices, then row r = "r\\t" + one value per column; cells (r, c)
+    with c <= r hold the pair's value, the rest 0 (never computed)."""
+    k = len(result["lengths"])
+    f = PAIR_FIELDS.index(field)
+    cell = {(j, i): rec[f] for (i, j), rec in zip(result["pairs"], result["records"])}
+    out = [(" \t" if blank_header else "\t") + "".join(f"{i}\t" for i in range(k)) + "\n"]
+    for r in range(k):
+        out.append(f"{r}\t" + "".join(f"{cell.get((r, c), 0)}\t" for c in range(k)) + "\n")
+    return "".join(out)

@@ -180,6 +180,18 @@ int gx_config_load(const char* path, gx_scores* out);
 int gx_format_alignment(const uint8_t* s1, size_t n, const uint8_t* s2, size_t m, const gx_step* steps,
                         size_t n_steps, const gx_result* res, char* out, size_t cap, size_t* needed);
 
+/* print_alignment_table + print_scores_table (display.rs:131-220), which the
+ * reference's retrace prints to stdout with the table it consumed
+ * (algo.rs:438).  Planes are int64 row-major (n+1)x(m+1), as
+ * gx_table_export_plane(.., colmajor = 0) writes them (export them before
+ * gx_retrace consumes the table).  Empty output when n >= 200 or m >= 2000
+ * (the reference only warns then).  color != 0: ANSI styles of the `colored`
+ * crate (the reference colours only when stdout is a terminal).  GX_EPANIC
+ * where the reference's chars().nth().unwrap() panics (non-ASCII input). */
+int gx_format_table(const uint8_t* s1, size_t n, const uint8_t* s2, size_t m, const gx_step* steps, size_t n_steps,
+                    const int64_t* insert_plane, const int64_t* delete_plane, const int64_t* sub_plane, int color,
+                    char* out, size_t cap, size_t* needed);
+
 #ifdef __cplusplus
 }
 #endif

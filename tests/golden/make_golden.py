@@ -93,11 +93,48 @@ def large_cases():
     return out
 
 
+def _allvsall_job(job):
+    i, j, a, b = job
+    r = o.align_lean(a, b, CONFIG, is_local=False)
+    assert r.status == 0
+    return {"i": i, "j": j, "n": len(a), "m": len(b), "score": r.score,
+            "stats": [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps],
+            "n_steps": int(len(r.choices)), "alignment_sha256": alignment_digest(r.choices, r.steps_i, r.steps_j)}
+
+
+def allvsall_cases(workers: int):
+    """BASELINE config 4: every pair i <= j of the comparison_data records (files
+    in name order), global NW under config.toml scores."""
+    from multiprocessing import Pool
+    cd = os.path.join(HERE, "comparison_data")
+    names, seqs = [], []
+    for f in sorted(os.listdir(cd)):
+        if f.endswith(".fasta"):
+            for name, seq in recs(os.path.join(cd, f)):
+                names.append(name.decode("utf-8") if isinstance(name, bytes) else name)
+                seqs.append(seq)
+    jobs = [(i, j, seqs[i], seqs[j]) for j in range(len(seqs)) for i in range(j + 1)]
+    jobs.sort(key=lambda x: -len(x[2]) * len(x[3]))
+    with Pool(workers) as pool:
+        out = pool.map(_allvsall_job, jobs, chunksize=1)
+    out.sort(key=lambda c: (c["j"], c["i"]))
+    return names, out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--large", action="store_true")
+    ap.add_argument("--allvsall", action="store_true")
+    ap.add_argument("--workers", type=int, default=7)
     args = ap.parse_args()
     o.build()
+    if args.allvsall:
+        names, cases = allvsall_cases(args.workers)
+        with open(os.path.join(HERE, "allvsall_digests.json"), "w") as f:
+            json.dump({"_source": "tests/golden/make_golden.py --allvsall (oracle_align_lean, global, "
+                                  "config.toml scores)", "names": names, "scores": list(CONFIG),
+                       "cases": cases}, f, indent=1)
+        return
     with open(os.path.join(HERE, "oracle_vectors.json"), "w") as f:
         json.dump({"_source": "tests/golden/make_golden.py (oracle restatement, pinned by "
                               "tests/test_alignment.rs vectors)", "cases": small_cases()}, f)

@@ -146,3 +146,52 @@ def test_display_matches_restatement(gx, oracle):
                                 c["stats"][0], c["stats"][1], c["stats"][2], c["stats"][3])
         want = _display_restatement(c["s1"], c["s2"], aln, c["score"], *c["stats"])
         assert str(a) == want, c["name"]
+
+
+def _table_restatement(s1, s2, alignment, planes, color):
+    """Python restatement of print_alignment_table + print_scores_table
+    (display.rs:131-220): the stdout text for one alignment."""
+    n, m = len(s1), len(s2)
+    if not (n < 200 and m < 2000):
+        return ""
+    glyph = {"Match": ("M", "\x1b[32m"), "Mismatch": ("X", "\x1b[31m"), "Insert": ("I", "\x1b[34m"),
+             "Delete": ("D", "\x1b[36m"), "OpenInsert": ("I", "\x1b[1;34m"), "OpenDelete": ("D", "\x1b[1;36m")}
+    out = ["\nSequence Table (S1 columns, S2 rows):\n\n", " " + s2 + "\n"]
+    for i in range(n):
+        row = s1[i]
+        for j in range(m):
+            hit = next((c for c, x, y in alignment if x == i + 1 and y == j + 1), None)
+            if hit is None:
+                row += "."
+            else:
+                g, st = glyph[hit]
+                row += f"{st}{g}\x1b[0m" if color else g
+        out.append(row + "\n")
+    for title, k in (("Delete Scores", 1), ("Insert Scores", 0), ("Sub Scores", 2)):
+        out.append(title + "\n")
+        out.append(". \t" + "".join(f"{j}\t" for j in range(m + 1)) + "\n")
+        for i in range(n + 1):
+            vals = ["-inf" if v <= -9223372036854775700 else str(int(v)) for v in planes[k][i]]
+            out.append(f"{i}\t" + "".join(v + "\t" for v in vals) + "\n")
+    return "".join(out)
+
+
+@pytest.mark.parametrize("is_local", [False, True])
+def test_alignment_table_print_matches_restatement(gx, oracle, is_local):
+    """print_alignment_table (display.rs:131-220, printed by retrace at
+    algo.rs:438): host formatter == restatement, on oracle planes (plain and
+    coloured), including the too-large cut-off."""
+    cases = [(b"BANANA", b"MISSISSIPPI"), (b"ACGGTTACGATTACA", b"ACGTTAGGATTTACGA"),
+             (b"ACGT" * 49 + b"AC", b"ACGA" * 40)]
+    for s1, s2 in cases:
+        o = oracle.align(s1, s2, (1, -2, -1, -5), is_local=is_local, want_planes=True)
+        aln = o.alignment()
+        a = gx.AlignedSequences(gx.Sequence("s1", s1.decode()), gx.Sequence("s2", s2.decode()),
+                                [(gx.AlignmentChoice[c], i, j) for c, i, j in aln], o.score,
+                                o.matches, o.mismatches, o.gap_extensions, o.opening_gaps)
+        planes = [o.planes[k] for k in range(3)]
+        for color in (False, True):
+            want = _table_restatement(s1.decode(), s2.decode(), aln, planes, color)
+            assert gx.format_alignment_table(a, planes, color) == want
+    big = gx.AlignedSequences(gx.Sequence("s1", "A" * 200), gx.Sequence("s2", "A"), [], 0, 0, 0, 0, 0)
+    assert gx.format_alignment_table(big, [None] * 3) == ""

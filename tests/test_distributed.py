@@ -71,3 +71,104 @@ def test_synthetic_inputs_follow_survey_seeds():
     x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & (2 ** 64 - 1)
     x ^= x >> 31
     assert s1[0] == b"ACGT"[x >> 62]
+
+
+# ---- all-vs-all (BASELINE config 4): broadcast scatter, LPT shares, gather ----
+
+def _fake_align(pairs, scores, is_local):
+    """Deterministic stand-in for the GPU aligner (plumbing test only)."""
+    return [[len(a) * 1000 + len(b), len(a), len(b), 0, 0, len(a) + len(b)] for a, b in pairs]
+
+
+def _avsa_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "genomics-rs_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    import gxamd as gx
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    seqs = [gx.Sequence(f"s{k}", "ACGT"[k % 4] * (50 + 37 * k)) for k in range(7)]
+    # only rank 0 holds the sequences: the others receive them through the broadcast
+    cont = gx.SequenceContainer(seqs if rank == 0 else [])
+    calls = []
+
+    def fn(pairs, scores, is_local):
+        calls.append(len(pairs))
+        return _fake_align(pairs, scores, is_local)
+
+    res = gx.all_vs_all(cont, gx.Scores(), dist=dist, device="cpu", align_fn=fn)
+    q.put((rank, res["pairs"], res["records"], res["lengths"], calls))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_all_vs_all_two_ranks_equals_single_process():
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "genomics-rs_amd"))
+    import gxamd as gx
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_avsa_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        out = sorted(q.get(timeout=180) for _ in range(2))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    seqs = [gx.Sequence(f"s{k}", "ACGT"[k % 4] * (50 + 37 * k)) for k in range(7)]
+    single = gx.all_vs_all(gx.SequenceContainer(seqs), gx.Scores(), align_fn=_fake_align)
+    assert len(single["pairs"]) == 28
+    for rank, pairs, records, lengths, calls in out:
+        assert pairs == single["pairs"] and records == single["records"]
+        assert lengths == [50 + 37 * k for k in range(7)]
+    # the two shares are disjoint and cover every pair; LPT balances n*m
+    shares = gx.lpt_partition([float(a * b) for a, b in
+                               ((single["lengths"][i], single["lengths"][j]) for i, j in single["pairs"])], 2)
+    assert sorted(shares[0] + shares[1]) == list(range(28))
+    assert [o[4] for o in out] == [[len(shares[0])], [len(shares[1])]]
+    loads = [sum(single["lengths"][single["pairs"][p][0]] * single["lengths"][single["pairs"][p][1]] for p in s)
+             for s in shares]
+    assert max(loads) / min(loads) < 1.1
+
+
+def test_similarity_tsv_layout():
+    sys.path.insert(0, os.path.join(ROOT, "genomics-rs_amd"))
+    import gxamd as gx
+    res = gx.all_vs_all(gx.SequenceContainer([gx.Sequence("a", "AC"), gx.Sequence("b", "ACG")]), gx.Scores(),
+                        align_fn=_fake_align)
+    # row r, column c filled for c <= r (main.rs:253-264, 343-359)
+    assert gx.similarity_tsv(res) == "\t0\t1\t\n0\t2002\t0\t\n1\t2003\t3003\t\n"
+    assert gx.similarity_tsv(res, "matches", blank_header=True) == " \t0\t1\t\n0\t2\t0\t\n1\t2\t3\t\n"
+
+
+def _ragged_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    import bench as b
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rows = [[rank, k, 7] for k in range(2 - rank)]     # rank 0: 2 pairs, rank 1: 1 pair
+    q.put((rank,) + tuple(b.combine_over_ranks(dist, 0.5, rows, "cpu")))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_combine_over_ranks_ragged_shares():
+    """All-vs-all LPT shares differ in size between ranks (45 pairs over 8 GPUs)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ragged_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        out = sorted(q.get(timeout=180) for _ in range(2))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for rank, t, gathered in out:
+        assert t == 0.5 and gathered == [[(0, 0, 7), (0, 1, 7)], [(1, 0, 7)]]
