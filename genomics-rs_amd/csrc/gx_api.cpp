@@ -1030,7 +1030,7 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
             if (prc[p]) perr[p] = g_err;   // g_err is thread-local
         }
     };
-    const size_t nthreads = std::min<size_t>({P, (size_t)std::max(1u, std::thread::hardware_concurrency()), 8});
+    const size_t nthreads = std::min<size_t>({P, (size_t)std::max(1u, std::thread::hardware_concurrency()), 16});
     if (nthreads <= 1) {
         label_range(0, P);
     } else {
