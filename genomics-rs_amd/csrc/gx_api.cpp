@@ -24,13 +24,13 @@
 #include "gx_internal.h"
 
 namespace gx {
-hipError_t launch_fill(int W, bool local, bool planes, bool track, bool lcs, bool tbl, const PairDev* d_pairs, int npairs,
+hipError_t launch_fill(int W, int lay, bool local, bool planes, bool track, bool lcs, bool tbl, const PairDev* d_pairs, int npairs,
                        int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                        hipStream_t st);
 hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d_sres, PairRes* d_pres,
                            hipStream_t st);
 hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipStream_t st);
-hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, hipStream_t st);
+hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, hipStream_t st);
 }  // namespace gx
 
 using namespace gx;
@@ -102,6 +102,7 @@ struct Walk {
 struct TbOut {
     std::vector<int> end_i, end_j;
     std::vector<size_t> so;            // job -> its first strip in sg / hr
+    int srows = kStripRows;            // rows per strip of the fill layout
     const int* c = nullptr;            // [4 * jobs] end i, end j, first strip
     const int* sg = nullptr;           // [4 * strips] entry i, entry j, records, active
     const uint32_t* hr = nullptr;      // [strips * kStripRows] records
@@ -320,12 +321,37 @@ struct PairHost {
     size_t n, m;
 };
 
+// Fill layout (gx_internal.h): 0 = anti-diagonal 128-row strips, 1 = column
+// step over 64-row strips (delete chain as a wave prefix max; a strip follows
+// the one above a few columns behind instead of 64+ steps).  GX_LAYOUT forces
+// one.  Layout 1 offsets the delete chain by up to 64 (|g| + |h|) inside the
+// scan, so it needs that much int32 headroom above the range guard's 2^28.
+//
+// Default: layout 1 while the job is latency-bound -- its 64-row strips fit
+// about two per SIMD (single pairs, a few 30k pairs: 1.45x on one 30k pair,
+// 1.07x on four); layout 0 for wide batches, which are HBM-bound and where
+// layout 0's 2-row lanes issue fewer instructions per cell (16 x 30k pairs:
+// 484 vs 429 GCUPS; 1024 x 1k pairs 246 vs 188; profiles/r01d_layouts.txt).
+static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int grid_cap) {
+    const long long span = 65LL * (std::llabs((long long)sc.g) + std::llabs((long long)sc.h));
+    size_t mmax = 0;
+    long long strips64 = 0;
+    for (const PairHost& h : ph) {
+        mmax = std::max(mmax, h.m);
+        strips64 += ceil_div((int)h.n, kStripRows1);
+    }
+    const bool cs_ok = span < (1LL << 29) && mmax < (1u << 24);
+    if (const char* e = getenv("GX_LAYOUT"); e && *e) return (atoi(e) == 1 && cs_ok) ? 1 : 0;
+    return (cs_ok && strips64 <= 8LL * grid_cap) ? 1 : 0;
+}
+
 struct FillJob {
     // device buffers (owned by the job until released)
     DevBuf chars, planes, codes, skel, feed, progress, sres, pres, pairs, counter;
     std::vector<PairDev> pd;
     std::vector<PairRes> res;
     int W = 4;
+    int lay = 0;   // 0: anti-diagonal 128-row strips, 1: column-step 64-row strips (gx_internal.h)
     int total_bands = 0, total_strips = 0;
     bool planes_on = false, lcs_on = false, track_on = false;
     double fill_ms = 0.0;
@@ -348,12 +374,15 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                     bool lcs, FillJob& job, const uint8_t* chars_dev = nullptr,
                     const std::vector<size_t>* off1 = nullptr, const std::vector<size_t>* off2 = nullptr,
                     const SmallAlpha* alpha = nullptr) {
+    const int lay = fill_layout(ph, sc, fill_grid_cap(ctx->device));
+    const int SR = strip_rows(lay);
     int total_strips = 0;
-    for (const PairHost& h : ph) total_strips += ceil_div((int)h.n, kStripRows);
+    for (const PairHost& h : ph) total_strips += ceil_div((int)h.n, SR);
     const bool codes = true;
     lcs = lcs && planes;
     track = track || lcs;
     const int W = fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device));
+    job.lay = lay;
     // small-alphabet score table: untracked global fill, <= 4 symbols, scores in a signed byte
     Scores32 scl = sc;
     const bool tbl = alpha && alpha->n <= 4 && !track && !is_local && sc.sm >= -128 && sc.sm <= 127 &&
@@ -372,9 +401,10 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         const int n = (int)ph[p].n, m = (int)ph[p].m;
         PairDev& d = job.pd[p];
         d.n = n; d.m = m;
-        d.strips = ceil_div(n, kStripRows);
+        d.strips = ceil_div(n, SR);
         d.bands = ceil_div(d.strips, W);
-        const int T = m + kWave;   // steps per strip (lane 63 pushes column m at step m + 63)
+        // steps per strip: layout 0, lane 63 pushes column m at step m + 63; layout 1, column m at step m - 1
+        const int T = lay ? m + 1 : m + kWave;
         d.t16 = ceil_div(T, 16);
         d.t4 = d.t16 * 4;
         d.band_base = bands;
@@ -385,8 +415,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         strips += d.strips;
         c1o[p] = chars_bytes; chars_bytes += align_up(n, 64);
         c2o[p] = chars_bytes; chars_bytes += align_up(m, 64);
-        po[p] = plane_elems; plane_elems += (size_t)d.strips * d.t4 * kGroupInts;
-        co[p] = code_elems; code_elems += (size_t)d.strips * d.t16 * kStripRows;
+        po[p] = plane_elems; plane_elems += (size_t)d.strips * d.t4 * (lay ? kGroupInts1 : kGroupInts);
+        co[p] = code_elems; code_elems += (size_t)d.strips * d.t16 * SR;
         so[p] = skel_elems; skel_elems += (size_t)d.strips * d.skel_stride;
         fo[p] = feed_recs; feed_recs += (size_t)std::max(d.bands - 1, 0) * d.feed_stride;
         gofs[p] = prog_elems; prog_elems += (size_t)std::max(d.bands - 1, 0) * kProgStride;
@@ -448,7 +478,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     const auto h_launch = std::chrono::steady_clock::now();
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     if (bands > 0)
-        HIPCHK(launch_fill(W, is_local != 0, planes, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
+        HIPCHK(launch_fill(W, lay, is_local != 0, planes, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
                            (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, ctx->stream));
     HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));   // ev0..ev1 brackets the fill kernel alone
     if (bands > 0)
@@ -614,7 +644,8 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     DevBuf recs, seg, jb, cnt;
     int rc;
     auto cleanup = [&]() { pool_put(ctx, recs); pool_put(ctx, seg); pool_put(ctx, jb); pool_put(ctx, cnt); };
-    if ((rc = pool_get(ctx, std::max<size_t>(stot, 1) * kStripRows * sizeof(uint32_t), &recs)) ||
+    const int SR = strip_rows(job.lay);
+    if ((rc = pool_get(ctx, std::max<size_t>(stot, 1) * SR * sizeof(uint32_t), &recs)) ||
         (rc = pool_get(ctx, std::max<size_t>(stot, 1) * 4 * sizeof(int), &seg)) ||
         (rc = pool_get(ctx, P * sizeof(TbDev), &jb)) || (rc = pool_get(ctx, P * 4 * sizeof(int), &cnt))) {
         cleanup();
@@ -629,7 +660,8 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
         t.n = d.n; t.m = d.m; t.t16 = d.t16; t.strips = d.strips;
         t.start_i = starts[p].i; t.start_j = starts[p].j; t.start_E = starts[p].E;
         t.seg = (int*)seg.p + 4 * so[p];
-        t.recs = (uint32_t*)recs.p + so[p] * kStripRows;
+        t.recs = (uint32_t*)recs.p + so[p] * SR;
+        t.srows = SR;
         t.end_ij = (int*)cnt.p + 4 * p;
     }
     hipError_t e = hipMemcpyAsync(jb.p, jobs.data(), P * sizeof(TbDev), hipMemcpyHostToDevice, ctx->stream);
@@ -638,7 +670,7 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, max_strips, ctx->stream);
     if (e == hipSuccess) e = hipEventRecord(ctx->ev2, ctx->stream);
     // one pinned host block: c | sg | hr
-    const size_t nc = 4 * P, nsg = 4 * std::max<size_t>(stot, 1), nhr = std::max<size_t>(stot, 1) * kStripRows;
+    const size_t nc = 4 * P, nsg = 4 * std::max<size_t>(stot, 1), nhr = std::max<size_t>(stot, 1) * SR;
     const size_t bytes = (nc + nsg) * sizeof(int) + nhr * sizeof(uint32_t);
     if (e == hipSuccess && ctx->tb_pin.cap < bytes) {
         if (ctx->tb_pin.p) (void)hipHostFree(ctx->tb_pin.p);
@@ -660,6 +692,7 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     out.ms = ms;
     out.c = c; out.sg = sg; out.hr = hr;
     out.so = so;
+    out.srows = SR;
     out.end_i.resize(P);
     out.end_j.resize(P);
     for (size_t p = 0; p < P; ++p) {
@@ -687,7 +720,7 @@ struct RecordsSrc {
         for (int s = tb->c[4 * p + 2]; s >= 0; --s) {
             const int* g = &tb->sg[4 * (tb->so[p] + s)];
             if (!g[3]) return;
-            const uint32_t* r = &tb->hr[(tb->so[p] + s) * kStripRows];
+            const uint32_t* r = &tb->hr[(tb->so[p] + s) * tb->srows];
             for (int k = 0; k < g[2]; ++k) {
                 for (uint32_t q = r[k] >> 2; q > 0; --q) if (!emit((uint8_t)1)) return;
                 if ((r[k] & 3u) != 1u && !emit((uint8_t)(r[k] & 3u))) return;
@@ -798,7 +831,7 @@ static int fetch_plane32(const gx_table* t, int which, std::vector<int32_t>& out
     DevBuf tmp;
     int rc = pool_get(ctx, out.size() * sizeof(int32_t), &tmp);
     if (rc) return rc;
-    hipError_t e = launch_export(src, (int32_t*)tmp.p, (int)n, (int)m, d.t4, ctx->stream);
+    hipError_t e = launch_export(src, (int32_t*)tmp.p, (int)n, (int)m, d.t4, t->job.lay, ctx->stream);
     if (e == hipSuccess)
         e = hipMemcpyAsync(out.data(), tmp.p, out.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);

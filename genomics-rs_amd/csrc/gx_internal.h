@@ -25,12 +25,21 @@ constexpr int kWave = 64;
 constexpr int kNeg = -(1 << 30);   // int32 stand-in for negative_inf (algo.rs:166)
 constexpr int kRing = 256;         // LDS ring records per strip boundary (power of two)
 constexpr int kSub = 16;           // steps per flow-control sub-block (multiple of 16)
-constexpr int kIoChunk = 16;       // columns per I/O-wave transfer
+constexpr int kIoChunk = 16;       // columns per I/O-wave transfer (layout 0)
+constexpr int kIoChunk1 = 4;       // columns per I/O-wave transfer (layout 1)
 constexpr int kRowsPerLane = 2;    // a lane owns rows 2l+1, 2l+2 of its strip
 constexpr int kStripRows = kWave * kRowsPerLane;   // 128 rows per strip
 // Plane layout (ints): plane[strip][t/4][row-in-lane][lane][t%4]; one 4-step
 // group of one row is 1 KiB contiguous per wave.
 constexpr int kGroupInts = kRowsPerLane * kWave * 4;
+// Column-step layout (layout 1): 64-row strips, lane l owns row 64s + l + 1,
+// step t = column t + 1 for every lane (no skew); planes
+// plane[strip][t/4][lane][t%4] (1 KiB per wave per plane every 4 columns),
+// codes[strip][t/16][lane].  The vertical delete chain is a prefix max over
+// the wave (gx_kernels.hip, compute_wave_cs).
+constexpr int kGroupInts1 = kWave * 4;
+constexpr int kStripRows1 = kWave;
+inline int strip_rows(int lay) { return lay ? kStripRows1 : kStripRows; }
 // Compute waves per band (workgroup = W compute waves + 1 I/O wave).  The
 // host picks the narrowest width whose bands fit one workgroup per CU (a
 // single pair: 3, one compute wave per SIMD, so a strip's own speed sets the
@@ -120,6 +129,7 @@ struct TbDev {           // per-pair traceback job
     int n, m, t16, strips;
     int start_i, start_j;  // interior start cell (1-based), or 0 = nothing to walk
     int start_E;           // landing column of the start cell (PairRes.end_E / lmax_E)
+    int srows;             // rows per strip: 128 (layout 0, anti-diagonal) or 64 (layout 1, column-step)
     int* seg;              // out: [strips][4] {entry_i, entry_j, records, active} per strip on the path
     uint32_t* recs;        // out: [strips][kStripRows] one record per row, (insert run << 2) | kind
     int* end_ij;           // out: [4] {i, j} where the walk leaves the interior, first strip, rounds

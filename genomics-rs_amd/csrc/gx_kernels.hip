@@ -718,29 +718,460 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     }
 }
 
+// ===========================================================================
+// Column-step fill (layout 1, gx_internal.h "colstep"): a strip is 64 rows,
+// lane l owns row i = 64 s + l + 1, and step t computes column j = t + 1 of
+// every row at once.  The insert (left) and sub (top-left) predecessors are
+// the lane's own previous column and lane l-1's previous column (DPP
+// wave_shr:1); the delete chain down the column,
+//     D(i, j) = max(IS(i-1, j) + h + g, D(i-1, j) + g [, 0])   (algo.rs:238-243)
+// is a max-plus linear recurrence along the lanes, solved as one inclusive
+// prefix max over the wave (6 DPP steps):
+//     D(l) = l*g + max_{k <= l} Z(k),  Z(0) = D(i0, j) (from the strip above),
+//     Z(k) = IS(k-1) + h + g - k*g  [local: max(.., -k*g)]   (k >= 1).
+// The landing column follows the same chain: a cell whose move is "delete"
+// takes E from the nearest lane above it whose move is not, found by a prefix
+// max over keys (lane << 25) | (E + 64).  No anti-diagonal skew: the strip
+// below consumes column j as soon as this strip has produced it, so strips
+// follow each other a few columns apart instead of 64 + steps.
+// ===========================================================================
+
+// in-place inclusive prefix max over the 64 lanes (lanes without a DPP source
+// keep their value: old = INT_MIN is the identity of max)
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int dpp_max(int x) {
+    return max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, CTRL, RM, BM, false));
+}
+__device__ __forceinline__ int scan_max64(int x) {
+    x = dpp_max<0x111, 0xF, 0xF>(x);   // row_shr:1
+    x = dpp_max<0x112, 0xF, 0xF>(x);   // row_shr:2
+    x = dpp_max<0x114, 0xF, 0xF>(x);   // row_shr:4
+    x = dpp_max<0x118, 0xF, 0xF>(x);   // row_shr:8
+    x = dpp_max<0x142, 0xA, 0xF>(x);   // row_bcast:15 -> rows 1, 3
+    x = dpp_max<0x143, 0xC, 0xF>(x);   // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+// Interleaved scans: independent chains side by side, so each DPP step's
+// latency (~14 cycles on a dependent chain, tools/dpp_probe.hip) is covered
+// by the other chain's step instead of wait states.
+template <int CTRL, int RM, int BM, int N>
+__device__ __forceinline__ void dpp_max_n(int (&x)[N]) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) x[q] = dpp_max<CTRL, RM, BM>(x[q]);
+}
+template <int N>
+__device__ __forceinline__ void scan_max64_n(int (&x)[N]) {
+    dpp_max_n<0x111, 0xF, 0xF>(x);
+    dpp_max_n<0x112, 0xF, 0xF>(x);
+    dpp_max_n<0x114, 0xF, 0xF>(x);
+    dpp_max_n<0x118, 0xF, 0xF>(x);
+    dpp_max_n<0x142, 0xA, 0xF>(x);
+    dpp_max_n<0x143, 0xC, 0xF>(x);
+}
+
+struct CsState {
+    int I, SD, SM;             // insert, max(sub, delete), score_max of (i, j-1)
+    int key;                   // landing-column key of (i, j-1), not yet scanned (see cs_step)
+    int L;                     // LCS field of (i, j-1) (TRACK)
+    int best, bstep, bl;       // first strict max of the row (TRACK)
+    int lbest, lstep, lE;      // last max of the row and its landing column (LOCAL)
+    uint32_t cI, cD;           // code bit-planes (16 steps)
+    int fin_sm, fin_E;         // score_max and E at column m (cell (n, m) if this lane holds row n)
+};
+struct CsConst {
+    int cY;      // h + g - (l+1) g
+    int cZ;      // -(l+1) g (local zero floor of the delete chain)
+    int lg;      // l g
+    int kl;      // lane << 25 (landing-column keys)
+    int c1;      // row char (or its packed score table, TBL)
+};
+
+// One column for all 64 rows, software-pipelined one column deep on the
+// landing column: step t computes the scores of column j = t + 1 and scans
+// the landing-column keys of column t (step t-1) in the same DPP sweep as the
+// delete chain of column j, returning E(., t) in `e_prev`.
+// r = ring record of column j (dd = D(i0, j), c2 = s2[j-1] or its code * 8,
+// l = LCS of (i0-1, j)); psm / pl = score_max / LCS of (i0-1, j-1).
+template <bool LOCAL, bool CODES, bool TRACK, bool TBL, bool TAIL>
+__device__ __forceinline__ void cs_step(CsState& st, const CsConst& k, const Rec& r, const int psm, const int pl,
+                                        const int t, const int m, const Scores32& sc, int& oI, int& oD, int& oS,
+                                        int& pdd, int& psm_out, int& pl_out, int& e_prev) {
+    const int j = t + 1;
+    const int smtl = shr1(psm, st.SM);                                  // SM(i-1, j-1)
+    const int In = LOCAL ? max3i(st.I + sc.g, st.SD + sc.hg, 0) : max(st.I + sc.g, st.SD + sc.hg);
+    const bool mt = r.c2 == k.c1;
+    const int Sn = smtl + (TBL ? __builtin_amdgcn_sbfe(k.c1, r.c2, 8) : (mt ? sc.sm : sc.smm));
+    const int IS = max(In, Sn);
+    int Y = IS + k.cY;
+    if (LOCAL) Y = max(Y, k.cZ);
+    int Ln = 0, Dn, Ek = 0;
+    if (TRACK) {
+        int x[3] = {shr1(r.dd, Y), st.key, max(st.L, shr1(pl, st.L) + (mt ? 1 : 0))};   // algo.rs:250-255
+        scan_max64_n(x);
+        Dn = x[0] + k.lg; Ek = x[1]; Ln = max(x[2], r.l);
+    } else if (CODES) {
+        int x[2] = {shr1(r.dd, Y), st.key};
+        scan_max64_n(x);
+        Dn = x[0] + k.lg; Ek = x[1];
+    } else {
+        int x[1] = {shr1(r.dd, Y)};
+        scan_max64_n(x);
+        Dn = x[0] + k.lg;
+    }
+    // E(i, t): no non-delete move above -> the path leaves at (i0-1, t)
+    const int Ep = Ek < 0 ? t : (Ek & 0x1FFFFFF) - 64;
+    e_prev = Ep;
+    const int SMn = max(IS, Dn);
+    const int SDn = max(Sn, Dn);
+    if (CODES) {
+        // D ? delete : I ? insert : sub (algo.rs:351-400).  One asm block: each
+        // compare feeds its code bit (v_addc shift-in) and its select, so no
+        // SGPR-pair mask stays alive (left to the compiler, a group's masks
+        // are kept and spilled to VGPR lanes).  key = delete ? -1 :
+        // (lane << 25) | (base + 64), base = E of the insert (own previous
+        // column) or sub (top-left) predecessor.
+        const int etl = shr1(t, Ep);                                    // lane 0: (i0-1, j-1) on the boundary
+        unsigned long long m1, m2, k1, k2;
+        asm volatile(
+            "v_cmp_gt_i32 %[m1], %[in], %[sn]\n\t"
+            "v_cmp_gt_i32 %[m2], %[dn], %[is]\n\t"
+            "v_cndmask_b32 %[key], %[etl], %[el], %[m1]\n\t"
+            "v_addc_co_u32 %[ci], %[k1], %[ci], %[ci], %[m1]\n\t"
+            "v_add3_u32 %[key], %[key], 64, %[kl]\n\t"
+            "v_addc_co_u32 %[cd], %[k2], %[cd], %[cd], %[m2]\n\t"
+            "v_cndmask_b32 %[key], %[key], -1, %[m2]"
+            : [key] "=&v"(st.key), [ci] "+v"(st.cI), [cd] "+v"(st.cD), [m1] "=&s"(m1), [m2] "=&s"(m2),
+              [k1] "=&s"(k1), [k2] "=&s"(k2)
+            : [in] "v"(In), [sn] "v"(Sn), [dn] "v"(Dn), [is] "v"(IS), [etl] "v"(etl), [el] "v"(Ep),
+              [kl] "v"(k.kl));
+    }
+    if (TRACK) {
+        const bool act = TAIL ? t < m : true;
+        const bool nb = act && SMn > st.best;
+        st.best = nb ? SMn : st.best; st.bstep = nb ? t : st.bstep; st.bl = nb ? Ln : st.bl;
+    }
+    if (LOCAL) {
+        // the last max of step t-1 (its landing column is known now)
+        const bool act = t >= 1 && (TAIL ? t <= m : true);
+        const bool nl = act && st.SM >= st.lbest;
+        st.lbest = nl ? st.SM : st.lbest; st.lstep = nl ? t - 1 : st.lstep; st.lE = nl ? Ep : st.lE;
+    }
+    if (TAIL && t == m - 1) st.fin_sm = SMn;
+    if (TAIL && t == m) st.fin_E = Ep;
+    pdd = LOCAL ? max3i(IS + sc.hg, Dn + sc.g, 0) : max(IS + sc.hg, Dn + sc.g);   // D(i+1, j)
+    psm_out = SMn;
+    pl_out = Ln;
+    st.I = In; st.SD = SDn; st.SM = SMn;
+    if (TRACK) st.L = Ln;
+    oI = In; oD = Dn; oS = Sn;
+}
+
+// record pushes with explicit values (all lanes write: lane 63 to the ring,
+// the others to scratch; or exec-masked to lane 63 in the tail)
+template <int U, bool TRACK>
+__device__ __forceinline__ void cs_push_all(uint32_t vaddr, int dd, int sm, int c2, int l) {
+    if (TRACK)
+        asm volatile(
+            "ds_write2_b32 %0, %1, %2 offset0:%5 offset1:%6\n\t"
+            "ds_write2_b32 %0, %3, %4 offset0:%7 offset1:%8"
+            :
+            : "v"(vaddr), "v"(dd), "v"(sm), "v"(c2), "v"(l), "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2),
+              "i"(4 * U + 3)
+            : "memory");
+    else
+        asm volatile(
+            "ds_write2_b32 %0, %1, %2 offset0:%4 offset1:%5\n\t"
+            "ds_write_b32 %0, %3 offset:%6"
+            :
+            : "v"(vaddr), "v"(dd), "v"(sm), "v"(c2), "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8)
+            : "memory");
+}
+template <int U, bool TRACK>
+__device__ __forceinline__ void cs_push63(uint32_t base, unsigned long long m63, int dd, int sm, int c2, int l) {
+    if (TRACK)
+        asm volatile(
+            "s_mov_b64 exec, %0\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%6 offset1:%7\n\t"
+            "ds_write2_b32 %1, %4, %5 offset0:%8 offset1:%9\n\t"
+            "s_mov_b64 exec, -1"
+            :
+            : "s"(m63), "v"(base), "v"(dd), "v"(sm), "v"(c2), "v"(l), "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2),
+              "i"(4 * U + 3)
+            : "memory");
+    else
+        asm volatile(
+            "s_mov_b64 exec, %0\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%5 offset1:%6\n\t"
+            "ds_write_b32 %1, %4 offset:%7\n\t"
+            "s_mov_b64 exec, -1"
+            :
+            : "s"(m63), "v"(base), "v"(dd), "v"(sm), "v"(c2), "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8)
+            : "memory");
+}
+
+struct CsPend {
+    int4 I, D, S, L;   // the previous group's cells (one row per lane)
+    size_t g_off;      // its group's plane offset (ints)
+    int bytes;         // 0: nothing pending
+};
+
+template <bool LCSP>
+__device__ __forceinline__ void cs_pend_store(const CsPend& pd, const WaveCtx& w, int plane) {
+    const uint32_t v = (uint32_t)w.lane * 16u;
+    const int32_t* base = plane == 0 ? w.pI : plane == 1 ? w.pD : plane == 2 ? w.pS : w.pL;
+    const auto rr = rsrc_of(base + pd.g_off, pd.bytes);
+    bstore4(rr, v, plane == 0 ? pd.I : plane == 1 ? pd.D : plane == 2 ? pd.S : pd.L);
+}
+
+// One 4-column group (columns t+1 .. t+4).  Same ring protocol as group4:
+// observe the producer's counter, speculatively read the next group's
+// records, compute, re-read after a wait if the counter did not cover them.
+template <bool LOCAL, int PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL, bool TAIL, int G4>
+__device__ __forceinline__ void cs_group4(CsState& st, const CsConst& kc, Rec (&nxt)[4], int& psm, int& pl,
+                                          WaveCtx& w, const Scores32& sc, const int t0, const uint32_t out_base,
+                                          const bool push_on, CsPend& pend) {
+    const int t = t0 + 4 * G4;
+    Rec cur[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
+    const int need = min(t + 8, w.m) + 1;
+    const int seen_v = *w.wcnt_in;
+    asm volatile("" ::: "memory");
+    read4(nxt, w.ring_in + ring_slot(t + 5));
+    int oI[4], oD[4], oS[4], oL[4], e[4];
+    const uint32_t pa = push_on && w.lane == kWave - 1 ? out_base : w.scratch;
+#pragma unroll
+    for (int U = 0; U < 4; ++U) {
+        int dd, sm, l;
+        cs_step<LOCAL, CODES, TRACK, TBL, TAIL>(st, kc, cur[U], psm, pl, t + U, w.m, sc, oI[U], oD[U], oS[U], dd, sm, l,
+                                                e[U]);
+        oL[U] = l;
+        psm = cur[U].sm;
+        pl = cur[U].l;
+        // lane 63's record of column t+U+1 for the strip below
+        if (!TAIL) {
+            if (U == 0) cs_push_all<4 * G4 + 0, TRACK>(pa, dd, sm, cur[U].c2, l);
+            if (U == 1) cs_push_all<4 * G4 + 1, TRACK>(pa, dd, sm, cur[U].c2, l);
+            if (U == 2) cs_push_all<4 * G4 + 2, TRACK>(pa, dd, sm, cur[U].c2, l);
+            if (U == 3) { cs_push_all<4 * G4 + 3, TRACK>(pa, dd, sm, cur[U].c2, l); publish_all(w.cnt_addr, t + 5); }
+        } else {
+            const unsigned long long mk = lane63_mask(push_on && t + U + 1 <= w.m);
+            if (U == 0) cs_push63<4 * G4 + 0, TRACK>(out_base, mk, dd, sm, cur[U].c2, l);
+            if (U == 1) cs_push63<4 * G4 + 1, TRACK>(out_base, mk, dd, sm, cur[U].c2, l);
+            if (U == 2) cs_push63<4 * G4 + 2, TRACK>(out_base, mk, dd, sm, cur[U].c2, l);
+            if (U == 3) cs_push63<4 * G4 + 3, TRACK>(out_base, mk, dd, sm, cur[U].c2, l);
+            if (U == 3 && push_on && t + 1 <= w.m) lds_store_lane0(w.wcnt_out, min(t + 4, w.m) + 1);
+        }
+        if (PLANES == 2 && !TAIL && (U < 3 || LCSP)) cs_pend_store<LCSP>(pend, w, U);   // the previous group's plane U
+    }
+    // lane 63's landing columns of columns t .. t+3 (the strip's bottom row: skeleton)
+    if (!TAIL) {
+        skel_store4(w.skel_rsrc, w.skel_voff + 4u * (uint32_t)t, e[0], e[1], e[2], e[3]);
+    } else {
+#pragma unroll
+        for (int U = 0; U < 4; ++U)
+            skel_store(w.skel_rsrc, t + U <= w.m ? w.skel_voff + 4u * (uint32_t)(t + U) : kSkelOff, e[U]);
+    }
+    const size_t g_off = (size_t)(t >> 2) * kGroupInts1;
+    if (PLANES == 1 || (PLANES == 2 && TAIL)) {
+        if (PLANES == 2) {   // flush the pending group first
+            cs_pend_store<LCSP>(pend, w, 0); cs_pend_store<LCSP>(pend, w, 1); cs_pend_store<LCSP>(pend, w, 2);
+            if (LCSP) cs_pend_store<LCSP>(pend, w, 3);
+            pend.bytes = 0;
+        }
+        const uint32_t v = (uint32_t)w.lane * 16u;
+        const auto rI = rsrc_of(w.pI + g_off, kGroupInts1 * 4), rD = rsrc_of(w.pD + g_off, kGroupInts1 * 4),
+                   rS = rsrc_of(w.pS + g_off, kGroupInts1 * 4);
+        bstore4(rI, v, make_int4(oI[0], oI[1], oI[2], oI[3]));
+        bstore4(rD, v, make_int4(oD[0], oD[1], oD[2], oD[3]));
+        bstore4(rS, v, make_int4(oS[0], oS[1], oS[2], oS[3]));
+        if (LCSP) bstore4(rsrc_of(w.pL + g_off, kGroupInts1 * 4), v, make_int4(oL[0], oL[1], oL[2], oL[3]));
+    } else if (PLANES == 2) {
+        pend.I = make_int4(oI[0], oI[1], oI[2], oI[3]);
+        pend.D = make_int4(oD[0], oD[1], oD[2], oD[3]);
+        pend.S = make_int4(oS[0], oS[1], oS[2], oS[3]);
+        if (LCSP) pend.L = make_int4(oL[0], oL[1], oL[2], oL[3]);
+        pend.g_off = g_off;
+        pend.bytes = kGroupInts1 * 4;
+    }
+    if (__builtin_amdgcn_readfirstlane(seen_v) < need) {
+        w.tr_win += wait_ge(w.wcnt_in, need, w.status);
+        read4(nxt, w.ring_in + ring_slot(t + 5));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool LOCAL, int PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL>
+__device__ void compute_wave_cs(const PairDev& P, const int s, const int lane, const Scores32& sc, const Rec* ring_in,
+                                Rec* ring_out, lds_int* wcnt_in, lds_int* rcnt_in, lds_int* wcnt_out,
+                                lds_int* rcnt_out, const bool has_consumer, StripRes* sres, PairRes* pres,
+                                int* status, const uint32_t scratch_base) {
+    static_assert(kSub == 16, "16-step sub-blocks (code words, ring alignment)");
+    const int n = P.n, m = P.m;
+    const int i = s * kWave + lane + 1;          // this lane's row
+    const bool ok = i <= n;
+    WaveCtx w;
+    {
+        const size_t strip_planes = (size_t)s * P.t4 * kGroupInts1;
+        w.pI = PLANES ? P.pI + strip_planes : nullptr;
+        w.pD = PLANES ? P.pD + strip_planes : nullptr;
+        w.pS = PLANES ? P.pS + strip_planes : nullptr;
+        w.pL = LCSP ? P.pL + strip_planes : nullptr;
+        w.codes = CODES ? P.codes + (size_t)s * P.t16 * kWave : nullptr;
+    }
+    w.ring_in = ring_in; w.ring_out = ring_out; w.wcnt_in = wcnt_in; w.wcnt_out = wcnt_out; w.status = status;
+    w.skel_rsrc = rsrc_of(uniform_ptr(P.skel + (size_t)s * P.skel_stride), has_consumer ? 4 * (m + 1) : 0);
+    w.skel_voff = lane == kWave - 1 ? 0u : kSkelOff;
+    w.scratch = scratch_base + 4u * (uint32_t)lane;
+    w.cnt_addr = (has_consumer && lane == kWave - 1) ? lds_addr((const void*)wcnt_out) : w.scratch;
+    w.m = m; w.lane = lane;
+    w.tr_win = 0;
+    CsConst kc;
+    kc.cY = sc.hg - (lane + 1) * sc.g;
+    kc.cZ = -(lane + 1) * sc.g;
+    kc.lg = lane * sc.g;
+    kc.kl = lane << 25;
+    kc.c1 = ok ? (int)P.c1[i - 1] : 0x1FF;
+    if (TBL) kc.c1 = score_table(kc.c1, sc);
+    StripTrace* const trace = P.trace;
+    const int strip_base = P.strip_base;
+
+    // column 0 (algo.rs:204-211): I = S = neg_inf, D = h + i g
+    CsState st;
+    {
+        RowState rs;
+        init_row(rs, i, ok, sc);
+        st.I = rs.I; st.SD = rs.SD; st.SM = rs.SM; st.L = 0;
+        st.best = rs.best; st.bstep = 0; st.bl = 0;
+        st.lbest = rs.lbest; st.lstep = 0; st.lE = 0;
+        st.cI = 0; st.cD = 0;
+        st.key = kc.kl | (63 - lane);             // column 0: E = -(lane + 1), no delete moves
+        st.fin_sm = 0; st.fin_E = 0;
+        if (has_consumer) {
+            if (lane == kWave - 1) ring_out[ring_slot(0)] = Rec{rs.Dd, rs.SM, 0, 0};
+            lds_wait();
+            if (lane == 0) *wcnt_out = 1;
+        }
+    }
+    const bool tracing = trace != nullptr;
+    long long tr_start = 0, tr_first = 0, clk_first = 0;
+    unsigned tr_wout = 0;
+    long long tr_q[kTraceQ] = {};
+    if (tracing) tr_start = __builtin_amdgcn_s_memrealtime();
+    w.tr_win += wait_ge(wcnt_in, min(4, m) + 1, status);
+    Rec nxt[4];
+    int psm, pl;
+    {
+        const Rec r0 = ring_in[ring_slot(0)];
+        psm = r0.sm;
+        pl = 0;
+        read4(nxt, ring_in + ring_slot(1));
+    }
+    if (tracing) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
+    CsPend pend;
+    pend.g_off = 0; pend.bytes = 0;
+    // steps 0 .. m: step t computes column t + 1 and finishes E of column t,
+    // so one step past the last column completes its landing columns
+    for (int t0 = 0; t0 <= m; t0 += kSub) {
+        const int last_col = min(t0 + kSub, m);   // last column pushed in this sub-block
+        if (has_consumer && last_col >= kRing) tr_wout += wait_ge(rcnt_out, last_col - kRing + 1, status);
+        if (tracing) {
+            const int q = (int)((long long)t0 * (kTraceQ + 1) / (m + 1)) - 1;
+            if (q >= 0 && q < kTraceQ && tr_q[q] == 0) tr_q[q] = __builtin_amdgcn_s_memrealtime();
+        }
+        const uint32_t out_base = lds_addr(ring_out + ring_slot(t0 + 1));
+        if (t0 + kSub < m) {   // step m - 1 (cell (., m)) and step m always run in a tail sub-block
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, false, 0>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, false, 1>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, false, 2>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, false, 3>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+        } else {
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, true, 0>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, true, 1>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, true, 2>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, true, 3>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+        }
+        if (CODES) {
+            // codes[strip][t/16][lane]
+#ifndef GX_DIAG_NO_CODES
+            gstore1(w.codes + (size_t)(t0 >> 4) * kWave + lane, (st.cD << 16) | (st.cI & 0xFFFFu));
+#endif
+        }
+        lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
+    }
+    if (PLANES == 2 && pend.bytes) {
+        cs_pend_store<LCSP>(pend, w, 0); cs_pend_store<LCSP>(pend, w, 1); cs_pend_store<LCSP>(pend, w, 2);
+        if (LCSP) cs_pend_store<LCSP>(pend, w, 3);
+    }
+    if (TRACK || LOCAL) {
+        const int best = (TRACK && ok) ? st.best : INT_MIN;
+        const int lbest = (LOCAL && ok) ? st.lbest : INT_MIN;
+        int mx = best, lmx = lbest;
+        for (int off = 32; off > 0; off >>= 1) {
+            mx = max(mx, __shfl_xor(mx, off));
+            lmx = max(lmx, __shfl_xor(lmx, off));
+        }
+        const unsigned long long fmask = __ballot(ok && best == mx);
+        const unsigned long long lmask = __ballot(ok && lbest == lmx);
+        const int fl = fmask ? (__ffsll((long long)fmask) - 1) : 0;
+        const int ll = lmask ? (63 - __clzll((long long)lmask)) : 0;
+        const int f_step = __shfl(st.bstep, fl), f_l = __shfl(st.bl, fl);
+        const int l_step = __shfl(st.lstep, ll), l_E = __shfl(st.lE, ll);
+        if (lane == 0) {
+            StripRes r;
+            r.best = mx; r.bi = s * kWave + fl + 1; r.bj = f_step + 1; r.bl = f_l;
+            r.lbest = lmx; r.li = s * kWave + ll + 1; r.lj = l_step + 1; r.lE = l_E;
+            sres[strip_base + s] = r;
+        }
+    }
+    if (ok && i == n) { pres->end_SM = st.fin_sm; pres->end_E = st.fin_E; }
+    if (tracing && lane == 0) {
+        StripTrace tr;
+        tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
+        tr.wait_in = (int)w.tr_win; tr.wait_out = (int)tr_wout;
+        tr.clk = __builtin_amdgcn_s_memtime() - clk_first;
+        for (int q = 0; q < kTraceQ; ++q) tr.t_q[q] = tr_q[q];
+        trace[s] = tr;
+    }
+}
+
 #ifndef GX_IO_SLEEP
 #define GX_IO_SLEEP 1
 #endif
 // I/O wave of a band: feeds ring 0 (row 0 analytic, or the previous band's
 // published bottom row) and drains ring W to HBM for the next band.
-template <bool TBL>
+// ADAPT (layout 1, whose strips run a few columns apart): the input side
+// moves every published column it can (up to 64 per pass) instead of fixed
+// chunks; the output side frees the ring as soon as it has read the records
+// and publishes a chunk's progress one pass later, after its stores have
+// drained, so a store round trip overlaps the next pass instead of stalling it.
+template <bool TBL, int CHUNK, bool ADAPT>
 __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Scores32& sc,
                         Rec* ring0, const Rec* ringW, lds_int* wcnt0, lds_int* rcnt0,
                         lds_int* wcntW, lds_int* rcntW, const bool do_out, int* status) {
     const int m = P.m;
     int in_next = 0, out_next = 0;
+    int pend_out = -1;   // ADAPT: columns stored to HBM, progress not yet published
     const Rec* feed_in = lb > 0 ? P.feed + (size_t)(lb - 1) * P.feed_stride : nullptr;
     Rec* feed_out = do_out ? P.feed + (size_t)lb * P.feed_stride : nullptr;
     const int* prog_in = lb > 0 ? P.progress + (size_t)(lb - 1) * kProgStride : nullptr;
     int* prog_out = do_out ? P.progress + (size_t)lb * kProgStride : nullptr;
     unsigned idle = 0;
-    while (in_next <= m || (do_out && out_next <= m)) {
+    while (in_next <= m || (do_out && (out_next <= m || pend_out >= 0))) {
         bool moved = false;
         if (in_next <= m) {
-            const int chunk = min(kIoChunk, m + 1 - in_next);
+            int chunk;
+            bool ok;
+            if (ADAPT) {
+                int lim = min(m + 1, *rcnt0 + kRing);
+                if (lb > 0) lim = min(lim, ld_agent(prog_in));
+                chunk = min(lim - in_next, kWave);
+                ok = chunk > 0;
+            } else {
+                chunk = min(CHUNK, m + 1 - in_next);
+                ok = in_next + chunk - 1 < *rcnt0 + kRing;
+                if (ok && lb > 0) ok = ld_agent(prog_in) > in_next + chunk - 1;
+            }
             const int last = in_next + chunk - 1;
-            bool ok = last < *rcnt0 + kRing;
-            if (ok && lb > 0) ok = ld_agent(prog_in) > last;
             if (ok) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 const int j = in_next + lane;
@@ -767,10 +1198,32 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
                 moved = true;
             }
         }
-        if (do_out && out_next <= m) {
+        if (ADAPT && do_out) {
+            if (pend_out >= 0) {   // the previous pass's stores: drained -> publish
+                vm_wait();
+                if (lane == 0) st_agent(prog_out, pend_out);
+                pend_out = -1;
+                moved = true;
+            }
+            if (out_next <= m) {
+                const int avail = *wcntW;
+                const int chunk = min(avail - out_next, kWave);
+                if (chunk >= CHUNK || (avail == m + 1 && chunk > 0)) {
+                    const int j = out_next + lane;
+                    Rec r{};
+                    if (lane < chunk) r = ringW[ring_slot(j)];
+                    lds_wait();
+                    if (lane == 0) *rcntW = out_next + chunk;   // ring slots free again
+                    if (lane < chunk) st_rec_agent(feed_out + j, r);
+                    out_next += chunk;
+                    pend_out = out_next;
+                    moved = true;
+                }
+            }
+        } else if (do_out && out_next <= m) {
             const int avail = *wcntW;
-            const int chunk = min(kIoChunk, avail - out_next);
-            if (chunk == kIoChunk || (avail == m + 1 && chunk > 0)) {
+            const int chunk = min(CHUNK, avail - out_next);
+            if (chunk == CHUNK || (avail == m + 1 && chunk > 0)) {
                 const int j = out_next + lane;
                 if (lane < chunk) st_rec_agent(feed_out + j, ringW[ring_slot(j)]);
                 vm_wait();
@@ -793,7 +1246,7 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
     }
 }
 
-template <int W, bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL>
+template <int W, bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL, int LAY>
 __global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAVES_TRACK : (W + 1 + 3) / 4) void fill_kernel(
     const PairDev* __restrict__ pairs, const int npairs, const int total_bands, int* band_counter, StripRes* sres,
     PairRes* pres, const Scores32 sc) {
@@ -824,13 +1277,21 @@ __global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAV
                 const bool has_consumer = last_in_band ? (lb + 1 < P.bands) : (s + 1 < P.strips);
                 // plane stores pipelined one group late, except in 16-wave
                 // workgroups (128 VGPRs: no room for a group of pending cells)
-                compute_wave<LOCAL, PLANES ? ((W + 1) <= 12 ? 2 : 1) : 0, CODES, TRACK, LCSP, TBL>(
-                    P, s, lane, sc, rings[wave], rings[wave + 1], (lds_int*)&wcnt[wave], (lds_int*)&rcnt[wave],
-                    (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1], has_consumer, sres, pres + p,
-                    band_counter + 1, lds_addr(push_scratch[wave]));
+                if (LAY == 0)
+                    compute_wave<LOCAL, PLANES ? ((W + 1) <= 12 ? 2 : 1) : 0, CODES, TRACK, LCSP, TBL>(
+                        P, s, lane, sc, rings[wave], rings[wave + 1], (lds_int*)&wcnt[wave], (lds_int*)&rcnt[wave],
+                        (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1], has_consumer, sres, pres + p,
+                        band_counter + 1, lds_addr(push_scratch[wave]));
+                else
+                    compute_wave_cs<LOCAL, PLANES ? ((W + 1) <= 12 ? 2 : 1) : 0, CODES, TRACK, LCSP, TBL>(
+                        P, s, lane, sc, rings[wave], rings[wave + 1], (lds_int*)&wcnt[wave], (lds_int*)&rcnt[wave],
+                        (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1], has_consumer, sres, pres + p,
+                        band_counter + 1, lds_addr(push_scratch[wave]));
             }
         } else {
-            io_wave<TBL>(P, lb, lane, sc, rings[0], rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0], (lds_int*)&wcnt[W],
+            // layout 1 strips run a few columns apart: hand band rows over in
+            // smaller chunks, so the next band does not wait for 16 columns
+            io_wave<TBL, LAY ? kIoChunk1 : kIoChunk, LAY == 1>(P, lb, lane, sc, rings[0], rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0], (lds_int*)&wcnt[W],
                     (lds_int*)&rcnt[W], lb + 1 < P.bands, band_counter + 1);
         }
         __syncthreads();
@@ -894,12 +1355,21 @@ typedef __attribute__((address_space(1))) const int gcint;
 
 // Code word of row-in-strip rho, word q of strip s (codes[strip][q][rho]).
 __device__ __forceinline__ size_t tb_word(const TbDev& J, int s, int q, int rho) {
-    return ((size_t)s * J.t16 + q) * kStripRows + rho;
+    return ((size_t)s * J.t16 + q) * J.srows + rho;
 }
+// Walked blocks are 64 rows: two per 128-row strip (layout 0), one per 64-row
+// strip (layout 1).  Row-in-strip of lane `lane` of block vb, and the step at
+// which that row computes column 1 (layout 0: the anti-diagonal skew rho/2;
+// layout 1: none).
+__device__ __forceinline__ int tb_rho(const TbDev& J, int vb, int lane) {
+    return J.srows == kStripRows ? ((vb & 1) << 6) + lane : lane;
+}
+__device__ __forceinline__ int tb_lot(const TbDev& J, int rho) { return J.srows == kStripRows ? rho >> 1 : 0; }
+__device__ __forceinline__ int tb_strip_of(const TbDev& J, int vb) { return J.srows == kStripRows ? vb >> 1 : vb; }
 
 // async: words q0 .. q0+kTbWin-1 of block vb (rows 64*vb .. +63), lane = row -> buf[k][lane]
 __device__ __forceinline__ void tb_prefetch(uint32_t* buf, const TbDev& J, int vb, int q0, int lane) {
-    const int s = vb >> 1, rho = ((vb & 1) << 6) + lane;
+    const int s = tb_strip_of(J, vb), rho = tb_rho(J, vb, lane);
 #pragma unroll
     for (int k = 0; k < kTbWin; ++k)
         __builtin_amdgcn_global_load_lds((gcvoid*)(J.codes + tb_word(J, s, min(q0 + k, J.t16 - 1), rho)),
@@ -912,15 +1382,16 @@ __global__ void tb_chase_kernel(const TbDev* __restrict__ jobs) {
     int i = J.start_i, j = J.start_j;
     int first = -1;
     if (i >= 1 && j >= 1) {
-        int s = (i - 1) / kStripRows;
+        const int SR = J.srows;
+        int s = (i - 1) / SR;
         first = s;
         J.seg[4 * s + 0] = i; J.seg[4 * s + 1] = j; J.seg[4 * s + 3] = 1;
         int E = J.start_E;
         for (;;) {
-            if (E < 0) { i = s * kStripRows - E; j = 0; break; }    // reaches (i, 0) at local row -E
-            if (s == 0 || E == 0) { i = s * kStripRows; j = E; break; }   // lands on row 0 / column 0
+            if (E < 0) { i = s * SR - E; j = 0; break; }          // reaches (i, 0) at local row -E
+            if (s == 0 || E == 0) { i = s * SR; j = E; break; }   // lands on row 0 / column 0
             s -= 1;                                               // enters strip s at its bottom row
-            J.seg[4 * s + 0] = (s + 1) * kStripRows; J.seg[4 * s + 1] = E; J.seg[4 * s + 3] = 1;
+            J.seg[4 * s + 0] = (s + 1) * SR; J.seg[4 * s + 1] = E; J.seg[4 * s + 3] = 1;
             E = ((gcint*)J.skel)[(size_t)s * J.skel_stride + E];
         }
     }
@@ -938,26 +1409,26 @@ __global__ __launch_bounds__(64) void tb_strip_kernel(const TbDev* __restrict__ 
     const int lane = threadIdx.x;
     const int i0 = __builtin_amdgcn_readfirstlane(((gcint*)J.seg)[4 * ss + 0]);
     const int j0 = __builtin_amdgcn_readfirstlane(((gcint*)J.seg)[4 * ss + 1]);
-    guint* const recs = (guint*)(J.recs + (size_t)ss * kStripRows);
+    guint* const recs = (guint*)(J.recs + (size_t)ss * J.srows);
     gcu32* const codes = (gcu32*)J.codes;
     lint* const ltbl = (lint*)(uintptr_t)lds_addr(tbl);
-    const int vb_top = 2 * ss;            // the strip's top block
+    const int vb_top = J.srows == kStripRows ? 2 * ss : ss;   // the strip's top block
     int vb = (i0 - 1) / kTbRows;          // current block
     int R = (i0 - 1) % kTbRows;           // the path's top lane in it
     int ce = j0;                          // its entry column
     int nrec = 0;
     int cb = 0;
-    int q_c = tb_q0(ce - 1 + ((((vb & 1) << 6) + R) >> 1));
+    int q_c = tb_q0(ce - 1 + tb_lot(J, tb_rho(J, vb, R)));
     tb_prefetch(tbuf[cb], J, vb, q_c, lane);
     for (;;) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");         // this block's window has landed
         // the block above (if in this strip) is entered at its lane 63, no further right than ce
-        const int q_n = vb > vb_top ? tb_q0(ce - 1 + ((((vb - 1) & 1) << 6) + kTbRows - 1) / 2) : 0;
+        const int q_n = vb > vb_top ? tb_q0(ce - 1 + tb_lot(J, tb_rho(J, vb - 1, kTbRows - 1))) : 0;
         if (vb > vb_top) tb_prefetch(tbuf[cb ^ 1], J, vb - 1, q_n, lane);
         const int q0 = q_c;
         const lu32* win = (const lu32*)(uintptr_t)lds_addr(tbuf[cb]);
-        const int rho = ((vb & 1) << 6) + lane;
-        const int lo_t = rho >> 1;        // step of column 1 on this row
+        const int rho = tb_rho(J, vb, lane);
+        const int lo_t = tb_lot(J, rho);  // step of column 1 on this row
         {   // per lane: nearest non-insert step strictly below each window word (branch-free)
             int run = -1;
 #pragma unroll 8
@@ -1032,15 +1503,22 @@ __global__ __launch_bounds__(64) void tb_strip_kernel(const TbDev* __restrict__ 
 
 // Export: strip-major anti-diagonal planes -> row-major (n+1) x (m+1) int32
 // (interior only; the host fills the boundary in int64).
-__global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __restrict__ out, int n, int m, int t4) {
+__global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __restrict__ out, int n, int m, int t4,
+                              int lay) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t total = (size_t)n * m;
     if (idx >= total) return;
     const int i = (int)(idx / m) + 1;
     const int j = (int)(idx % m) + 1;
-    const int s = (i - 1) / kStripRows, rho = (i - 1) % kStripRows;
-    const int l = rho >> 1, h = rho & 1, t = j - 1 + l;
-    const size_t o = ((size_t)s * t4 + (t >> 2)) * kGroupInts + h * kWave * 4 + l * 4 + (t & 3);
+    size_t o;
+    if (lay == 0) {
+        const int s = (i - 1) / kStripRows, rho = (i - 1) % kStripRows;
+        const int l = rho >> 1, h = rho & 1, t = j - 1 + l;
+        o = ((size_t)s * t4 + (t >> 2)) * kGroupInts + h * kWave * 4 + l * 4 + (t & 3);
+    } else {
+        const int s = (i - 1) / kStripRows1, l = (i - 1) % kStripRows1, t = j - 1;
+        o = ((size_t)s * t4 + (t >> 2)) * kGroupInts1 + l * 4 + (t & 3);
+    }
     out[(size_t)i * (m + 1) + j] = plane[o];
 }
 
@@ -1050,22 +1528,27 @@ __global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __rest
 namespace gx {
 
 template <int W, bool LOCAL, bool PLANES, bool TRACK, bool LCSP, bool TBL>
-static hipError_t launch_fill_t(const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
+static hipError_t launch_fill_t(int lay, const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
                                 StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
-    hipLaunchKernelGGL((fill_kernel<W, LOCAL, PLANES, true, TRACK, LCSP, TBL>), dim3(grid), dim3((W + 1) * kWave), 0, st,
-                       d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc);
+    if (lay == 0)
+        hipLaunchKernelGGL((fill_kernel<W, LOCAL, PLANES, true, TRACK, LCSP, TBL, 0>), dim3(grid), dim3((W + 1) * kWave),
+                           0, st, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc);
+    else
+        hipLaunchKernelGGL((fill_kernel<W, LOCAL, PLANES, true, TRACK, LCSP, TBL, 1>), dim3(grid), dim3((W + 1) * kWave),
+                           0, st, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc);
     return hipGetLastError();
 }
 
 // Launch with the band width W from the variant's width list (gx_internal.h).
 template <bool LO, bool PL, bool TR, bool LC, bool TB, int W0, int... Ws>
-static hipError_t launch_fill_w(int W, const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
+static hipError_t launch_fill_w(int W, int lay, const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
                                 StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
     if (W == W0)
-        return launch_fill_t<W0, LO, PL, TR, LC, TB>(d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc, grid, st);
+        return launch_fill_t<W0, LO, PL, TR, LC, TB>(lay, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc,
+                                                      grid, st);
     if constexpr (sizeof...(Ws) > 0)
-        return launch_fill_w<LO, PL, TR, LC, TB, Ws...>(W, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc,
-                                                    grid, st);
+        return launch_fill_w<LO, PL, TR, LC, TB, Ws...>(W, lay, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres,
+                                                        sc, grid, st);
     return hipErrorInvalidValue;
 }
 
@@ -1074,12 +1557,12 @@ static hipError_t launch_fill_w(int W, const PairDev* d_pairs, int npairs, int t
 // untracked global variants (the batch path) come in every width of kFillWidths
 // and with the small-alphabet score table (tbl) or the byte compare,
 // the tracked and local ones (256-VGPR builds) in kFillWidthsTrack.
-hipError_t launch_fill(int W, bool local, bool planes, bool track, bool lcs, bool tbl, const PairDev* d_pairs,
+hipError_t launch_fill(int W, int lay, bool local, bool planes, bool track, bool lcs, bool tbl, const PairDev* d_pairs,
                        int npairs, int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc,
                        int grid, hipStream_t st) {
 #define GX_FILL_CASE(LO, PL, TR, LC, TB, ...)                                                                \
     if (local == LO && planes == PL && track == TR && lcs == LC && tbl == TB)                                \
-        return launch_fill_w<LO, PL, TR, LC, TB, __VA_ARGS__>(W, d_pairs, npairs, total_bands, d_counter, d_sres, \
+        return launch_fill_w<LO, PL, TR, LC, TB, __VA_ARGS__>(W, lay, d_pairs, npairs, total_bands, d_counter, d_sres, \
                                                               d_pres, sc, grid, st);
 #define GX_W_ALL 3, 4, 6, 8, 11, 15
 #define GX_W_TRACK 3, 7
@@ -1113,12 +1596,12 @@ hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipS
     return hipGetLastError();
 }
 
-hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, hipStream_t st) {
+hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, hipStream_t st) {
     const size_t total = (size_t)n * m;
     if (total == 0) return hipSuccess;
     const int blk = 256;
     hipLaunchKernelGGL(export_kernel, dim3((unsigned)((total + blk - 1) / blk)), dim3(blk), 0, st, plane, out, n, m,
-                       t4);
+                       t4, lay);
     return hipGetLastError();
 }
 

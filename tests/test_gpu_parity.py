@@ -7,7 +7,9 @@ reverse_sequences, batched pairs, and the large pairs of BASELINE configs 2
 and 3 through digests.  Every test runs under each fill launch shape: the
 automatic band width, forced 7-strip (tracked variants) and 8-strip bands,
 and 15-strip bands on a 2-workgroup grid (bands wait in the queue for a
-workgroup, hand-offs cross launch order).
+workgroup, hand-offs cross launch order), for both fill layouts (0: the
+anti-diagonal sweep of 128-row strips; 1: the column step over 64-row
+strips) and the automatic layout choice.
 """
 import hashlib
 import json
@@ -21,8 +23,14 @@ from conftest import COMPARISON, CONFIG_SCORES, FASTA, GOLDEN, TEST_SCORES, read
 
 pytestmark = pytest.mark.gpu
 
-LAUNCH_SHAPES = {"auto": {}, "w7": {"GX_BAND_WAVES": "7"}, "w8": {"GX_BAND_WAVES": "8"},
-                 "w15_grid2": {"GX_BAND_WAVES": "15", "GX_FILL_GRID": "2"}}
+LAUNCH_SHAPES = {"auto": {},
+                 # layout 0: anti-diagonal fill over 128-row strips
+                 "lay0": {"GX_LAYOUT": "0"}, "w7": {"GX_LAYOUT": "0", "GX_BAND_WAVES": "7"},
+                 "w8": {"GX_LAYOUT": "0", "GX_BAND_WAVES": "8"},
+                 "w15_grid2": {"GX_LAYOUT": "0", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "2"},
+                 # layout 1: column-step fill over 64-row strips (gx_internal.h)
+                 "cs": {"GX_LAYOUT": "1"}, "cs_w7": {"GX_LAYOUT": "1", "GX_BAND_WAVES": "7"},
+                 "cs_w15_grid2": {"GX_LAYOUT": "1", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "2"}}
 
 
 @pytest.fixture(autouse=True, params=sorted(LAUNCH_SHAPES))

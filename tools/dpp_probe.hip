@@ -1,0 +1,56 @@
+// dpp_probe: cycles per wave64 prefix-max scan (6 DPP v_max steps), one wave
+// per SIMD: a single dependent chain vs two or three independent chains
+// interleaved (diagnostic for the column-step fill's per-column latency).
+//   hipcc --offload-arch=gfx950 -O3 -o var/dpp_probe tools/dpp_probe.hip
+#include <hip/hip_runtime.h>
+#include <climits>
+#include <cstdio>
+
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int dpp_max(int x) {
+    return max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, CTRL, RM, BM, false));
+}
+__device__ __forceinline__ int scan(int x) {
+    x = dpp_max<0x111, 0xF, 0xF>(x);
+    x = dpp_max<0x112, 0xF, 0xF>(x);
+    x = dpp_max<0x114, 0xF, 0xF>(x);
+    x = dpp_max<0x118, 0xF, 0xF>(x);
+    x = dpp_max<0x142, 0xA, 0xF>(x);
+    x = dpp_max<0x143, 0xC, 0xF>(x);
+    return x;
+}
+template <int K>
+__global__ void probe(int* out, long long* cyc, int iters) {
+    int x = threadIdx.x, y = threadIdx.x * 3, z = threadIdx.x * 5, u = threadIdx.x * 7;
+    const long long t0 = clock64();
+    for (int it = 0; it < iters; ++it) {
+        if (K == 0) { x = x + 1; x = max(x, y); }                       // plain dependent VALU pair
+        if (K >= 1) x = scan(x) + 1;
+        if (K >= 2) y = scan(y) + 1;
+        if (K >= 3) z = scan(z) + 1;
+        if (K >= 4) u = scan(u) + 1;
+    }
+    const long long t1 = clock64();
+    out[threadIdx.x] = x + y + z + u;
+    if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+int main() {
+    int* d; long long* c;
+    hipMalloc(&d, 256 * 4); hipMalloc(&c, 8);
+    const int iters = 100000;
+    for (int k = 0; k <= 4; ++k) {
+        for (int rep = 0; rep < 2; ++rep) {
+            if (k == 0) hipLaunchKernelGGL(probe<0>, dim3(1), dim3(64), 0, 0, d, c, iters);
+            if (k == 1) hipLaunchKernelGGL(probe<1>, dim3(1), dim3(64), 0, 0, d, c, iters);
+            if (k == 2) hipLaunchKernelGGL(probe<2>, dim3(1), dim3(64), 0, 0, d, c, iters);
+            if (k == 3) hipLaunchKernelGGL(probe<3>, dim3(1), dim3(64), 0, 0, d, c, iters);
+            if (k == 4) hipLaunchKernelGGL(probe<4>, dim3(1), dim3(64), 0, 0, d, c, iters);
+            hipDeviceSynchronize();
+        }
+        long long h = 0;
+        hipMemcpy(&h, c, 8, hipMemcpyDeviceToHost);
+        printf("chains %d: %.1f cycles per iteration (%.1f per scan)\n", k, (double)h / iters,
+               k ? (double)h / iters / k : 0.0);
+    }
+    return 0;
+}

@@ -7,7 +7,7 @@ O=gpurun_out/quick
 rm -rf "$O" && mkdir -p "$O"
 SEL=$1; shift
 if [ -n "$SEL" ]; then
-  timeout -k 10 600 python -u -m pytest $SEL -x -v --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1 \
+  eval "timeout -k 10 600 python -u -m pytest $SEL -x -v --timeout 300 --timeout-method thread" > "$O/tests.log" 2>&1 \
     || { echo TESTS_FAIL; tail -40 "$O/tests.log"; exit 1; }
   tail -3 "$O/tests.log"
 fi
