@@ -130,6 +130,19 @@ def load_traffic(workload: str):
     return None, None
 
 
+def fasta_pair(gx, which: str):
+    """BASELINE configs 2 and 3: the reference's own FASTA pairs (copied under
+    tests/golden), loaded with the from_fasta mirror."""
+    g = os.path.join(ROOT, "tests", "golden")
+    cont = gx.SequenceContainer()
+    if which == "covid":
+        cont.from_fasta(os.path.join(g, "comparison_data", "Covid_Wuhan.fasta"))
+        cont.from_fasta(os.path.join(g, "comparison_data", "Covid_USA-CA4.fasta"))
+    else:
+        cont.from_fasta(os.path.join(g, "fasta", "Human-Mouse-BRCA2-cds.fasta"))
+    return cont.sequences[0].sequence.encode(), cont.sequences[1].sequence.encode()
+
+
 def allvsall_share(gx, rank: int, world: int):
     """BASELINE config 4: rank r's longest-processing-time share of the 45
     pairs i<j of the comparison_data genomes (files in name order, the same
@@ -190,9 +203,11 @@ def main():
     ap.add_argument("--no-planes", action="store_true", help="score+traceback only (not the headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", choices=["synthetic", "allvsall"], default="synthetic",
+    ap.add_argument("--workload", choices=["synthetic", "allvsall", "covid", "brca2"], default="synthetic",
                     help="allvsall: BASELINE config 4, the 45 pairs i<j of the 10 comparison_data genomes, "
-                         "LPT-sharded over the ranks (traceback-only fill unless --planes)")
+                         "LPT-sharded over the ranks (traceback-only fill unless --planes); covid: config 2, "
+                         "Covid_Wuhan x Covid_USA-CA4 global; brca2: config 3, the Human x Mouse BRCA2 cds pair "
+                         "local (one copy per rank)")
     ap.add_argument("--planes", action="store_true", help="allvsall: also write the score planes")
     ap.add_argument("--single-pair-steps", type=int, default=5,
                     help="also time BASELINE config 2's shape alone (one pair, latency), 1 GPU only; 0 = skip")
@@ -216,6 +231,12 @@ def main():
         pairs, n_total = allvsall_share(gx, rank, world)
         P = len(pairs)
         keep_planes = args.planes
+        args.single_pair_steps = 0
+    elif args.workload in ("covid", "brca2"):
+        pairs = [fasta_pair(gx, args.workload)]
+        P = 1
+        args.local = args.workload == "brca2"
+        keep_planes = not args.no_planes
         args.single_pair_steps = 0
     else:
         pairs = rank_pairs(rank, P, L)
@@ -262,6 +283,10 @@ def main():
     if args.workload == "allvsall":
         workload = f"all-vs-all of the 10 comparison_data genomes (45 pairs i<j, 29,644-30,123 nt), " \
                    f"LPT-sharded over {world} GPU(s), {mode_s}"
+    elif args.workload == "covid":
+        workload = f"Covid_Wuhan x Covid_USA-CA4 ({len(pairs[0][0])}x{len(pairs[0][1])}), one pair per GPU, {mode_s}"
+    elif args.workload == "brca2":
+        workload = f"Human x Mouse BRCA2 cds ({len(pairs[0][0])}x{len(pairs[0][1])}), one pair per GPU, {mode_s}"
     else:
         workload = f"synthetic {L}x{L} DNA pairs (SplitMix64), {P} per GPU, {mode_s}"
     fill_bytes = BYTES_PER_CELL * cells_rank
@@ -280,7 +305,7 @@ def main():
         "scaling": "strong" if args.workload == "allvsall" else "weak",
         "vs_baseline": None,
         "dtype": "int32",
-        "data": "comparison_data FASTA (real genomes)" if args.workload == "allvsall" else "synthetic",
+        "data": "synthetic" if args.workload == "synthetic" else "reference FASTA data (tests/golden)",
         "config": {"workload": workload, "pairs_per_gpu": P, "seq_len": L if args.workload == "synthetic" else None,
                    "cells_per_step": total_cells, "parallelism": f"pairs sharded over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if keep_planes else None,
