@@ -311,8 +311,12 @@ static int pick_width(const int (&ws)[N], int total_strips, int grid_cap) {
     for (int x : ws) if (ceil_div(total_strips, x) <= grid_cap) return x;
     return ws[N - 1];
 }
-static int fill_band_waves(bool track, int total_strips, int grid_cap) {
-    return track ? pick_width(kFillWidthsTrack, total_strips, grid_cap) : pick_width(kFillWidths, total_strips, grid_cap);
+static int fill_band_waves(bool track, int total_strips, int grid_cap, int lay) {
+    // layout 1 starts at 4-strip bands: fewer HBM hand-offs for the same one
+    // compute wave per SIMD (the I/O wave shares a SIMD but mostly sleeps)
+    static constexpr int kWidths1[] = {4, 6, 8, 11, 15};
+    if (track) return pick_width(kFillWidthsTrack, total_strips, grid_cap);
+    return lay ? pick_width(kWidths1, total_strips, grid_cap) : pick_width(kFillWidths, total_strips, grid_cap);
 }
 
 struct PairHost {
@@ -340,7 +344,7 @@ static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int 
         mmax = std::max(mmax, h.m);
         strips64 += ceil_div((int)h.n, kStripRows1);
     }
-    const bool cs_ok = span < (1LL << 29) && mmax < (1u << 24);
+    const bool cs_ok = span < (1LL << 29) && mmax + 128 < (1u << 24);   // landing keys hold E + 64 in 24 bits
     if (const char* e = getenv("GX_LAYOUT"); e && *e) return (atoi(e) == 1 && cs_ok) ? 1 : 0;
     return (cs_ok && strips64 <= 8LL * grid_cap) ? 1 : 0;
 }
@@ -381,7 +385,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     const bool codes = true;
     lcs = lcs && planes;
     track = track || lcs;
-    const int W = fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device));
+    const int W = fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device), lay);
     job.lay = lay;
     // small-alphabet score table: untracked global fill, <= 4 symbols, scores in a signed byte
     Scores32 scl = sc;

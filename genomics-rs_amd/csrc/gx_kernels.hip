@@ -783,7 +783,8 @@ struct CsConst {
     int cY;      // h + g - (l+1) g
     int cZ;      // -(l+1) g (local zero floor of the delete chain)
     int lg;      // l g
-    int kl;      // lane << 25 (landing-column keys)
+    int kl;      // (lane + 1) << 24 (landing-column keys)
+    int lg1;     // (l+1) g
     int c1;      // row char (or its packed score table, TBL)
 };
 
@@ -805,22 +806,25 @@ __device__ __forceinline__ void cs_step(CsState& st, const CsConst& k, const Rec
     const int IS = max(In, Sn);
     int Y = IS + k.cY;
     if (LOCAL) Y = max(Y, k.cZ);
-    int Ln = 0, Dn, Ek = 0;
+    int Ln = 0, Dn, Ek = 0, Zs;
     if (TRACK) {
         int x[3] = {shr1(r.dd, Y), st.key, max(st.L, shr1(pl, st.L) + (mt ? 1 : 0))};   // algo.rs:250-255
         scan_max64_n(x);
-        Dn = x[0] + k.lg; Ek = x[1]; Ln = max(x[2], r.l);
+        Zs = x[0]; Ek = x[1]; Ln = max(x[2], r.l);
     } else if (CODES) {
         int x[2] = {shr1(r.dd, Y), st.key};
         scan_max64_n(x);
-        Dn = x[0] + k.lg; Ek = x[1];
+        Zs = x[0]; Ek = x[1];
     } else {
         int x[1] = {shr1(r.dd, Y)};
         scan_max64_n(x);
-        Dn = x[0] + k.lg;
+        Zs = x[0];
     }
-    // E(i, t): no non-delete move above -> the path leaves at (i0-1, t)
-    const int Ep = Ek < 0 ? t : (Ek & 0x1FFFFFF) - 64;
+    Dn = Zs + k.lg;
+    // E(i, t) + 64 (keys: ((lane+1) << 24) | (E + 64); a delete cell's key is
+    // (t + 64) with lane field 0, so a lane with no non-delete move above it
+    // reads the boundary column t -- the path leaves at (i0-1, t))
+    const int Ep = Ek & 0xFFFFFF;
     e_prev = Ep;
     const int SMn = max(IS, Dn);
     const int SDn = max(Sn, Dn);
@@ -831,20 +835,22 @@ __device__ __forceinline__ void cs_step(CsState& st, const CsConst& k, const Rec
         // are kept and spilled to VGPR lanes).  key = delete ? -1 :
         // (lane << 25) | (base + 64), base = E of the insert (own previous
         // column) or sub (top-left) predecessor.
-        const int etl = shr1(t, Ep);                                    // lane 0: (i0-1, j-1) on the boundary
+        const int etl = shr1(t + 64, Ep);                               // lane 0: (i0-1, j-1) on the boundary
+        const int dkey = t + 65;                                        // delete: boundary column j + 64 (a VGPR:
+                                                                        // VOP3 may read one SGPR, the mask)
         unsigned long long m1, m2, k1, k2;
         asm volatile(
             "v_cmp_gt_i32 %[m1], %[in], %[sn]\n\t"
             "v_cmp_gt_i32 %[m2], %[dn], %[is]\n\t"
             "v_cndmask_b32 %[key], %[etl], %[el], %[m1]\n\t"
             "v_addc_co_u32 %[ci], %[k1], %[ci], %[ci], %[m1]\n\t"
-            "v_add3_u32 %[key], %[key], 64, %[kl]\n\t"
+            "v_or_b32 %[key], %[key], %[kl]\n\t"
             "v_addc_co_u32 %[cd], %[k2], %[cd], %[cd], %[m2]\n\t"
-            "v_cndmask_b32 %[key], %[key], -1, %[m2]"
+            "v_cndmask_b32 %[key], %[key], %[dk], %[m2]"
             : [key] "=&v"(st.key), [ci] "+v"(st.cI), [cd] "+v"(st.cD), [m1] "=&s"(m1), [m2] "=&s"(m2),
               [k1] "=&s"(k1), [k2] "=&s"(k2)
             : [in] "v"(In), [sn] "v"(Sn), [dn] "v"(Dn), [is] "v"(IS), [etl] "v"(etl), [el] "v"(Ep),
-              [kl] "v"(k.kl));
+              [kl] "v"(k.kl), [dk] "v"(dkey));
     }
     if (TRACK) {
         const bool act = TAIL ? t < m : true;
@@ -859,7 +865,9 @@ __device__ __forceinline__ void cs_step(CsState& st, const CsConst& k, const Rec
     }
     if (TAIL && t == m - 1) st.fin_sm = SMn;
     if (TAIL && t == m) st.fin_E = Ep;
-    pdd = LOCAL ? max3i(IS + sc.hg, Dn + sc.g, 0) : max(IS + sc.hg, Dn + sc.g);   // D(i+1, j)
+    // D(i+1, j) = max(D + g, IS + h + g [, 0]) = (l+1) g + max(Zscan, Y): one step
+    // further down the same chain (lane 63's value is the record pushed below)
+    pdd = LOCAL ? max3i(IS + sc.hg, Dn + sc.g, 0) : max(Zs, Y) + k.lg1;
     psm_out = SMn;
     pl_out = Ln;
     st.I = In; st.SD = SDn; st.SM = SMn;
@@ -928,11 +936,12 @@ __device__ __forceinline__ void cs_pend_store(const CsPend& pd, const WaveCtx& w
 // observe the producer's counter, speculatively read the next group's
 // records, compute, re-read after a wait if the counter did not cover them.
 template <bool LOCAL, int PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL, bool TAIL, int G4>
-__device__ __forceinline__ void cs_group4(CsState& st, const CsConst& kc, Rec (&nxt)[4], int& psm, int& pl,
-                                          WaveCtx& w, const Scores32& sc, const int t0, const uint32_t out_base,
-                                          const bool push_on, CsPend& pend) {
+__device__ __forceinline__ void cs_group4(CsState& st, const CsConst& kc, Rec (&cur)[4], Rec (&nxt)[4], int& psm,
+                                          int& pl, WaveCtx& w, const Scores32& sc, const int t0,
+                                          const uint32_t out_base, const bool push_on, CsPend& pend) {
+    // cur: this group's validated records; nxt: filled with the next group's
+    // (the caller alternates the two buffers, so no records are copied)
     const int t = t0 + 4 * G4;
-    Rec cur[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
     const int need = min(t + 8, w.m) + 1;
     const int seen_v = *w.wcnt_in;
     asm volatile("" ::: "memory");
@@ -1029,7 +1038,8 @@ __device__ void compute_wave_cs(const PairDev& P, const int s, const int lane, c
     kc.cY = sc.hg - (lane + 1) * sc.g;
     kc.cZ = -(lane + 1) * sc.g;
     kc.lg = lane * sc.g;
-    kc.kl = lane << 25;
+    kc.lg1 = (lane + 1) * sc.g;
+    kc.kl = (lane + 1) << 24;
     kc.c1 = ok ? (int)P.c1[i - 1] : 0x1FF;
     if (TBL) kc.c1 = score_table(kc.c1, sc);
     StripTrace* const trace = P.trace;
@@ -1044,7 +1054,7 @@ __device__ void compute_wave_cs(const PairDev& P, const int s, const int lane, c
         st.best = rs.best; st.bstep = 0; st.bl = 0;
         st.lbest = rs.lbest; st.lstep = 0; st.lE = 0;
         st.cI = 0; st.cD = 0;
-        st.key = kc.kl | (63 - lane);             // column 0: E = -(lane + 1), no delete moves
+        st.key = kc.kl | (63 - lane);             // column 0: E = -(lane + 1) (+ 64), no delete moves
         st.fin_sm = 0; st.fin_E = 0;
         if (has_consumer) {
             if (lane == kWave - 1) ring_out[ring_slot(0)] = Rec{rs.Dd, rs.SM, 0, 0};
@@ -1058,13 +1068,13 @@ __device__ void compute_wave_cs(const PairDev& P, const int s, const int lane, c
     long long tr_q[kTraceQ] = {};
     if (tracing) tr_start = __builtin_amdgcn_s_memrealtime();
     w.tr_win += wait_ge(wcnt_in, min(4, m) + 1, status);
-    Rec nxt[4];
+    Rec ra[4], rb[4];   // records of the current / next group (alternating)
     int psm, pl;
     {
         const Rec r0 = ring_in[ring_slot(0)];
         psm = r0.sm;
         pl = 0;
-        read4(nxt, ring_in + ring_slot(1));
+        read4(ra, ring_in + ring_slot(1));
     }
     if (tracing) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
     CsPend pend;
@@ -1080,15 +1090,15 @@ __device__ void compute_wave_cs(const PairDev& P, const int s, const int lane, c
         }
         const uint32_t out_base = lds_addr(ring_out + ring_slot(t0 + 1));
         if (t0 + kSub < m) {   // step m - 1 (cell (., m)) and step m always run in a tail sub-block
-            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, false, 0>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
-            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, false, 1>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
-            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, false, 2>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
-            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, false, 3>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, false, 0>(st, kc, ra, rb, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, false, 1>(st, kc, rb, ra, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, false, 2>(st, kc, ra, rb, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, false, 3>(st, kc, rb, ra, psm, pl, w, sc, t0, out_base, has_consumer, pend);
         } else {
-            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, true, 0>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
-            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, true, 1>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
-            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, true, 2>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
-            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, true, 3>(st, kc, nxt, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, true, 0>(st, kc, ra, rb, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, true, 1>(st, kc, rb, ra, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, true, 2>(st, kc, ra, rb, psm, pl, w, sc, t0, out_base, has_consumer, pend);
+            cs_group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, true, 3>(st, kc, rb, ra, psm, pl, w, sc, t0, out_base, has_consumer, pend);
         }
         if (CODES) {
             // codes[strip][t/16][lane]
@@ -1119,11 +1129,11 @@ __device__ void compute_wave_cs(const PairDev& P, const int s, const int lane, c
         if (lane == 0) {
             StripRes r;
             r.best = mx; r.bi = s * kWave + fl + 1; r.bj = f_step + 1; r.bl = f_l;
-            r.lbest = lmx; r.li = s * kWave + ll + 1; r.lj = l_step + 1; r.lE = l_E;
+            r.lbest = lmx; r.li = s * kWave + ll + 1; r.lj = l_step + 1; r.lE = l_E - 64;
             sres[strip_base + s] = r;
         }
     }
-    if (ok && i == n) { pres->end_SM = st.fin_sm; pres->end_E = st.fin_E; }
+    if (ok && i == n) { pres->end_SM = st.fin_sm; pres->end_E = st.fin_E - 64; }
     if (tracing && lane == 0) {
         StripTrace tr;
         tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
@@ -1393,6 +1403,7 @@ __global__ void tb_chase_kernel(const TbDev* __restrict__ jobs) {
             s -= 1;                                               // enters strip s at its bottom row
             J.seg[4 * s + 0] = (s + 1) * SR; J.seg[4 * s + 1] = E; J.seg[4 * s + 3] = 1;
             E = ((gcint*)J.skel)[(size_t)s * J.skel_stride + E];
+            if (SR == kStripRows1) E -= 64;                        // layout 1 stores E + 64
         }
     }
     J.end_ij[0] = i; J.end_ij[1] = j; J.end_ij[2] = first;
