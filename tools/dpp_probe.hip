@@ -36,6 +36,10 @@ __global__ void probe(int* out, long long* cyc, int iters) {
     const int kl = (int)threadIdx.x << 25;
     const unsigned bits = 0x9E3779B9u * (threadIdx.x + 1);
     for (int it = 0; it < iters; ++it) {
+        if (K == 7) { x = __builtin_amdgcn_update_dpp(y, x, 0x138, 0xF, 0xF, false) + 1; continue; }   // wave_shr:1
+        if (K == 8) { x = __builtin_amdgcn_update_dpp(y, x, 0x111, 0xF, 0xF, false) + 1; continue; }   // row_shr:1
+        if (K == 9) { x = max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, 0x142, 0xA, 0xF, false)) + 1; continue; }  // row_bcast:15
+        if (K == 10) { x = (x ^ y) + 1; x = max(x, y) + 3; continue; }   // four dependent plain VALU
         if (K == 5 || K == 6) {
             const int ib = (bits >> (it & 31)) & 1, db = (bits >> ((it + 7) & 31)) & (threadIdx.x & 1);
             x = e_step(x, it, ib, db, kl);
@@ -56,7 +60,7 @@ int main() {
     int* d; long long* c;
     hipMalloc(&d, 256 * 4); hipMalloc(&c, 8);
     const int iters = 100000;
-    for (int k = 0; k <= 6; ++k) {
+    for (int k = 0; k <= 10; ++k) {
         for (int rep = 0; rep < 2; ++rep) {
             if (k == 0) hipLaunchKernelGGL(probe<0>, dim3(1), dim3(64), 0, 0, d, c, iters);
             if (k == 1) hipLaunchKernelGGL(probe<1>, dim3(1), dim3(64), 0, 0, d, c, iters);
@@ -65,6 +69,10 @@ int main() {
             if (k == 4) hipLaunchKernelGGL(probe<4>, dim3(1), dim3(64), 0, 0, d, c, iters);
             if (k == 5) hipLaunchKernelGGL(probe<5>, dim3(1), dim3(64), 0, 0, d, c, iters);
             if (k == 6) hipLaunchKernelGGL(probe<6>, dim3(1), dim3(64), 0, 0, d, c, iters);
+            if (k == 7) hipLaunchKernelGGL(probe<7>, dim3(1), dim3(64), 0, 0, d, c, iters);
+            if (k == 8) hipLaunchKernelGGL(probe<8>, dim3(1), dim3(64), 0, 0, d, c, iters);
+            if (k == 9) hipLaunchKernelGGL(probe<9>, dim3(1), dim3(64), 0, 0, d, c, iters);
+            if (k == 10) hipLaunchKernelGGL(probe<10>, dim3(1), dim3(64), 0, 0, d, c, iters);
             hipDeviceSynchronize();
         }
         long long h = 0;
@@ -72,8 +80,11 @@ int main() {
         if (k <= 4)
             printf("chains %d: %.1f cycles per iteration (%.1f per scan)\n", k, (double)h / iters,
                    k ? (double)h / iters / k : 0.0);
-        else
+        else if (k <= 6)
             printf("landing-column chain x%d: %.1f cycles per column\n", k - 4, (double)h / iters);
+        else
+            printf("probe %d (7 wave_shr mov+add, 8 row_shr mov+add, 9 bcast max+add, 10 4 plain): %.1f cycles\n", k,
+                   (double)h / iters);
     }
     return 0;
 }
