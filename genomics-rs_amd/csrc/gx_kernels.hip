@@ -408,6 +408,9 @@ struct WaveCtx {
     uint32_t cnt_addr;                                      // lane 63 with a consumer: the ring counter; else scratch
     int m, lane, c1a, c1b;
     unsigned tr_win;
+    // layout 1: one descriptor per plane covering the strip's whole plane; the
+    // group offset rides in the VGPR offset (no per-store descriptor SALU)
+    __amdgpu_buffer_rsrc_t rI, rD, rS, rL;
 };
 
 // Plane stores of the previous 4-step group, issued one plane per step in
@@ -920,16 +923,14 @@ __device__ __forceinline__ void cs_push63(uint32_t base, unsigned long long m63,
 
 struct CsPend {
     int4 I, D, S, L;   // the previous group's cells (one row per lane)
-    size_t g_off;      // its group's plane offset (ints)
-    int bytes;         // 0: nothing pending
+    uint32_t voff;     // this lane's byte offset in the strip plane; kNoStore: nothing pending
 };
+constexpr uint32_t kNoStore = 0xFFFFFFF0u;   // past every strip plane's range: the store is dropped
 
 template <bool LCSP>
 __device__ __forceinline__ void cs_pend_store(const CsPend& pd, const WaveCtx& w, int plane) {
-    const uint32_t v = (uint32_t)w.lane * 16u;
-    const int32_t* base = plane == 0 ? w.pI : plane == 1 ? w.pD : plane == 2 ? w.pS : w.pL;
-    const auto rr = rsrc_of(base + pd.g_off, pd.bytes);
-    bstore4(rr, v, plane == 0 ? pd.I : plane == 1 ? pd.D : plane == 2 ? pd.S : pd.L);
+    const auto rr = plane == 0 ? w.rI : plane == 1 ? w.rD : plane == 2 ? w.rS : w.rL;
+    bstore4(rr, pd.voff, plane == 0 ? pd.I : plane == 1 ? pd.D : plane == 2 ? pd.S : pd.L);
 }
 
 // One 4-column group (columns t+1 .. t+4).  Same ring protocol as group4:
@@ -985,22 +986,19 @@ __device__ __forceinline__ void cs_group4(CsState& st, const CsConst& kc, Rec (&
         if (PLANES == 2) {   // flush the pending group first
             cs_pend_store<LCSP>(pend, w, 0); cs_pend_store<LCSP>(pend, w, 1); cs_pend_store<LCSP>(pend, w, 2);
             if (LCSP) cs_pend_store<LCSP>(pend, w, 3);
-            pend.bytes = 0;
+            pend.voff = kNoStore;
         }
-        const uint32_t v = (uint32_t)w.lane * 16u;
-        const auto rI = rsrc_of(w.pI + g_off, kGroupInts1 * 4), rD = rsrc_of(w.pD + g_off, kGroupInts1 * 4),
-                   rS = rsrc_of(w.pS + g_off, kGroupInts1 * 4);
-        bstore4(rI, v, make_int4(oI[0], oI[1], oI[2], oI[3]));
-        bstore4(rD, v, make_int4(oD[0], oD[1], oD[2], oD[3]));
-        bstore4(rS, v, make_int4(oS[0], oS[1], oS[2], oS[3]));
-        if (LCSP) bstore4(rsrc_of(w.pL + g_off, kGroupInts1 * 4), v, make_int4(oL[0], oL[1], oL[2], oL[3]));
+        const uint32_t v = (uint32_t)w.lane * 16u + (uint32_t)g_off * 4u;
+        bstore4(w.rI, v, make_int4(oI[0], oI[1], oI[2], oI[3]));
+        bstore4(w.rD, v, make_int4(oD[0], oD[1], oD[2], oD[3]));
+        bstore4(w.rS, v, make_int4(oS[0], oS[1], oS[2], oS[3]));
+        if (LCSP) bstore4(w.rL, v, make_int4(oL[0], oL[1], oL[2], oL[3]));
     } else if (PLANES == 2) {
         pend.I = make_int4(oI[0], oI[1], oI[2], oI[3]);
         pend.D = make_int4(oD[0], oD[1], oD[2], oD[3]);
         pend.S = make_int4(oS[0], oS[1], oS[2], oS[3]);
         if (LCSP) pend.L = make_int4(oL[0], oL[1], oL[2], oL[3]);
-        pend.g_off = g_off;
-        pend.bytes = kGroupInts1 * 4;
+        pend.voff = (uint32_t)w.lane * 16u + (uint32_t)g_off * 4u;
     }
     if (__builtin_amdgcn_readfirstlane(seen_v) < need) {
         w.tr_win += wait_ge(w.wcnt_in, need, w.status);
@@ -1026,6 +1024,13 @@ __device__ void compute_wave_cs(const PairDev& P, const int s, const int lane, c
         w.pS = PLANES ? P.pS + strip_planes : nullptr;
         w.pL = LCSP ? P.pL + strip_planes : nullptr;
         w.codes = CODES ? P.codes + (size_t)s * P.t16 * kWave : nullptr;
+        const int pbytes = P.t4 * kGroupInts1 * 4;   // one strip's plane
+        if (PLANES) {
+            w.rI = rsrc_of(uniform_ptr(w.pI), pbytes);
+            w.rD = rsrc_of(uniform_ptr(w.pD), pbytes);
+            w.rS = rsrc_of(uniform_ptr(w.pS), pbytes);
+        }
+        if (LCSP) w.rL = rsrc_of(uniform_ptr(w.pL), pbytes);
     }
     w.ring_in = ring_in; w.ring_out = ring_out; w.wcnt_in = wcnt_in; w.wcnt_out = wcnt_out; w.status = status;
     w.skel_rsrc = rsrc_of(uniform_ptr(P.skel + (size_t)s * P.skel_stride), has_consumer ? 4 * (m + 1) : 0);
@@ -1078,7 +1083,7 @@ __device__ void compute_wave_cs(const PairDev& P, const int s, const int lane, c
     }
     if (tracing) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
     CsPend pend;
-    pend.g_off = 0; pend.bytes = 0;
+    pend.voff = kNoStore;   // nothing pending before the first group
     // steps 0 .. m: step t computes column t + 1 and finishes E of column t,
     // so one step past the last column completes its landing columns
     for (int t0 = 0; t0 <= m; t0 += kSub) {
@@ -1108,7 +1113,7 @@ __device__ void compute_wave_cs(const PairDev& P, const int s, const int lane, c
         }
         lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
     }
-    if (PLANES == 2 && pend.bytes) {
+    if (PLANES == 2 && pend.voff != kNoStore) {
         cs_pend_store<LCSP>(pend, w, 0); cs_pend_store<LCSP>(pend, w, 1); cs_pend_store<LCSP>(pend, w, 2);
         if (LCSP) cs_pend_store<LCSP>(pend, w, 3);
     }
