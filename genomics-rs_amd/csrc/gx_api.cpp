@@ -485,7 +485,9 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         HIPCHK(launch_fill(W, lay, is_local != 0, planes, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
                            (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, ctx->stream));
     HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));   // ev0..ev1 brackets the fill kernel alone
-    if (bands > 0)
+    // strip results exist only for the tracked and local fills (the untracked
+    // global fill writes end_SM / end_E itself): no reduction launch otherwise
+    if (bands > 0 && (track || is_local))
         HIPCHK(launch_finalize((const PairDev*)job.pairs.p, (int)P, (const StripRes*)job.sres.p,
                                (PairRes*)job.pres.p, ctx->stream));
     job.res.assign(P, PairRes{});

@@ -1315,20 +1315,47 @@ __global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAV
 
 // Per-pair reduction of the strip results (first max: lowest strip wins ties;
 // last max: highest strip wins ties).
+// One wave per pair: each lane scans strips lane, lane+64, ... in order, then
+// the wave combines (first max: lowest strip wins ties, i.e. the lowest lane
+// holding the max after the per-lane scans, whose strips are increasing; last
+// max: the highest strip holding it).
 __global__ void finalize_kernel(const PairDev* __restrict__ pairs, const StripRes* __restrict__ sres,
                                 PairRes* pres) {
     const int p = blockIdx.x;
     const PairDev& P = pairs[p];
-    if (threadIdx.x != 0) return;
-    int best = INT_MIN, bi = 0, bj = 0, bl = 0, lbest = INT_MIN, li = 0, lj = 0, lE = 0;
-    for (int s = 0; s < P.strips; ++s) {
+    const int lane = threadIdx.x;
+    int best = INT_MIN, bs = INT_MAX, lbest = INT_MIN, ls = -1;
+    for (int s = lane; s < P.strips; s += kWave) {
         const StripRes r = sres[P.strip_base + s];
-        if (r.best > best) { best = r.best; bi = r.bi; bj = r.bj; bl = r.bl; }
-        if (r.lbest >= lbest) { lbest = r.lbest; li = r.li; lj = r.lj; lE = r.lE; }
+        if (r.best > best) { best = r.best; bs = s; }
+        if (r.lbest >= lbest) { lbest = r.lbest; ls = s; }
     }
-    PairRes& o = pres[p];
-    o.max_val = best; o.max_i = bi; o.max_j = bj; o.mam = bl;
-    o.lmax_val = lbest; o.lmax_i = li; o.lmax_j = lj; o.nstrips = P.strips; o.lmax_E = lE;
+    int mx = best, lmx = lbest;
+    for (int off = 32; off > 0; off >>= 1) {
+        mx = max(mx, __shfl_xor(mx, off));
+        lmx = max(lmx, __shfl_xor(lmx, off));
+    }
+    int fs = best == mx ? bs : INT_MAX, lsel = lbest == lmx ? ls : -1;
+    for (int off = 32; off > 0; off >>= 1) {
+        fs = min(fs, __shfl_xor(fs, off));
+        lsel = max(lsel, __shfl_xor(lsel, off));
+    }
+    if (lane == 0) {
+        PairRes& o = pres[p];
+        o.max_val = mx; o.lmax_val = lmx; o.nstrips = P.strips;
+        if (fs != INT_MAX) {
+            const StripRes r = sres[P.strip_base + fs];
+            o.max_i = r.bi; o.max_j = r.bj; o.mam = r.bl;
+        } else {
+            o.max_i = 0; o.max_j = 0; o.mam = 0;
+        }
+        if (lsel >= 0) {
+            const StripRes r = sres[P.strip_base + lsel];
+            o.lmax_i = r.li; o.lmax_j = r.lj; o.lmax_E = r.lE;
+        } else {
+            o.lmax_i = 0; o.lmax_j = 0; o.lmax_E = 0;
+        }
+    }
 }
 
 // Traceback (algo.rs:339-422), interior cells only; the host finishes the
