@@ -387,9 +387,9 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     track = track || lcs;
     const int W = fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device), lay);
     job.lay = lay;
-    // small-alphabet score table: untracked global fill, <= 4 symbols, scores in a signed byte
+    // small-alphabet score table: untracked fill (global or local), <= 4 symbols, scores in a signed byte
     Scores32 scl = sc;
-    const bool tbl = alpha && alpha->n <= 4 && !track && !is_local && sc.sm >= -128 && sc.sm <= 127 &&
+    const bool tbl = alpha && alpha->n <= 4 && !track && sc.sm >= -128 && sc.sm <= 127 &&
                      sc.smm >= -128 && sc.smm <= 127 && !getenv("GX_NO_SCORE_TABLE");
     if (tbl)
         for (int k = 0; k < 4; ++k) scl.sym[k] = alpha->sym[k];

@@ -1617,8 +1617,10 @@ hipError_t launch_fill(int W, int lay, bool local, bool planes, bool track, bool
     GX_FILL_CASE(false, true, true, false, false, GX_W_TRACK)
     GX_FILL_CASE(false, true, true, true, false, GX_W_TRACK)
     GX_FILL_CASE(true, false, false, false, false, GX_W_TRACK)
+    GX_FILL_CASE(true, false, false, false, true, GX_W_TRACK)
     GX_FILL_CASE(true, false, true, false, false, GX_W_TRACK)
     GX_FILL_CASE(true, true, false, false, false, GX_W_TRACK)
+    GX_FILL_CASE(true, true, false, false, true, GX_W_TRACK)
     GX_FILL_CASE(true, true, true, false, false, GX_W_TRACK)
     GX_FILL_CASE(true, true, true, true, false, GX_W_TRACK)
 #undef GX_FILL_CASE

@@ -267,17 +267,18 @@ def test_staged_path_matches_oracle(gx, ctx, oracle):
 @pytest.mark.parametrize("alpha,scores", [(b"ACGT", CONFIG_SCORES), (b"AC", TEST_SCORES), (b"GT", (3, -1, -2, -4)),
                                           (b"ACGTN", CONFIG_SCORES), (b"ACGT", (200, -2, -1, -5))],
                          ids=["acgt", "ac", "gt", "five_symbols", "wide_scores"])
-def test_untracked_batch_score_table(gx, ctx, oracle, alpha, scores):
-    """The untracked global batch path: <= 4 symbols with byte-sized scores
-    take the packed score-table fill (one bit-field extract per cell), the
-    rest the byte compare; both bit-exact with the oracle."""
+@pytest.mark.parametrize("is_local", [False, True], ids=["global", "local"])
+def test_untracked_batch_score_table(gx, ctx, oracle, alpha, scores, is_local):
+    """The untracked batch path (global and local): <= 4 symbols with
+    byte-sized scores take the packed score-table fill (one bit-field extract
+    per cell), the rest the byte compare; both bit-exact with the oracle."""
     rng = random.Random(len(alpha) * 7 + scores[0])
     pairs = [(bytes(rng.choice(alpha) for _ in range(n)), bytes(rng.choice(alpha) for _ in range(m)))
              for n, m in [(1, 1), (5, 70), (128, 129), (300, 17), (257, 400)] + [(rng.randint(1, 300), rng.randint(1, 300))
                                                                                  for _ in range(20)]]
-    out = gx.align_batch(pairs, sc(gx, scores), False, ctx=ctx, max_cell=False)
+    out = gx.align_batch(pairs, sc(gx, scores), is_local, ctx=ctx, max_cell=False)
     for (a, b), (steps, r) in zip(pairs, out):
-        o = oracle.align(a, b, scores)
+        o = oracle.align(a, b, scores, is_local=is_local)
         assert steps_list(steps) == o.alignment(), (len(a), len(b))
         assert (r.score, r.matches, r.mismatches, r.gap_extensions, r.opening_gaps) == \
                (o.score, o.matches, o.mismatches, o.gap_extensions, o.opening_gaps)
