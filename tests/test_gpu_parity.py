@@ -282,3 +282,20 @@ def test_untracked_batch_score_table(gx, ctx, oracle, alpha, scores, is_local):
         assert steps_list(steps) == o.alignment(), (len(a), len(b))
         assert (r.score, r.matches, r.mismatches, r.gap_extensions, r.opening_gaps) == \
                (o.score, o.matches, o.mismatches, o.gap_extensions, o.opening_gaps)
+
+
+@pytest.mark.parametrize("scores", [(3, -2, -(1 << 22), -7), (1, -1, -(1 << 21), -(1 << 22)), (2, -3, -(1 << 23), -1)],
+                         ids=["g2^22", "h2^22", "g2^23"])
+def test_large_gap_scores_near_guard(gx, ctx, oracle, scores):
+    """Gap scores of 2^21-2^23 on short pairs: inside the host's exact-int32
+    guard, where the column-step scans offset the delete chain by up to
+    64 (|g| + |h|) (layout 1 takes them while 65 (|g| + |h|) < 2^29, layout 0
+    the rest); bit-exact with the oracle either way."""
+    rng = random.Random(scores[2] & 0xffff)
+    for _ in range(12):
+        n, m = rng.randint(1, 14), rng.randint(1, 14)   # (n+m+2)(|scores|) < 2^28
+        a = bytes(rng.choice(b"ACGT") for _ in range(n))
+        b = bytes(rng.choice(b"ACGT") for _ in range(m))
+        for loc in (False, True):
+            steps, r = gx.align_raw(a, b, sc(gx, scores), loc, ctx=ctx)
+            assert_same(steps, r, oracle.align(a, b, scores, is_local=loc), (n, m, scores, loc))
