@@ -11,7 +11,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -116,6 +119,62 @@ struct PinnedBuf {
     size_t cap = 0;
 };
 
+// Persistent host workers for the labelling of a batch's walks (spawning
+// threads per call cost ~0.5 ms per batch): items are taken from an atomic
+// counter by the workers and the calling thread.
+struct WorkPool {
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv, done_cv;
+    const std::function<void(size_t)>* fn = nullptr;
+    std::atomic<size_t> next{0};
+    size_t total = 0, busy = 0;
+    uint64_t gen = 0;
+    bool stop = false;
+
+    void worker() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv.wait(lk, [&] { return stop || gen != seen; });
+                if (stop) return;
+                seen = gen;
+            }
+            drain();
+            std::lock_guard<std::mutex> lk(m);
+            if (--busy == 0) done_cv.notify_all();
+        }
+    }
+    void drain() {
+        for (size_t i; (i = next.fetch_add(1)) < total;) (*fn)(i);
+    }
+    // f(i) for i in [0, n) on up to `workers` pool threads plus the caller
+    void run(size_t n, size_t workers, const std::function<void(size_t)>& f) {
+        while (th.size() < workers) th.emplace_back([this] { worker(); });
+        {
+            std::lock_guard<std::mutex> lk(m);
+            fn = &f;
+            total = n;
+            next = 0;
+            busy = th.size();
+            ++gen;
+        }
+        cv.notify_all();
+        drain();
+        std::unique_lock<std::mutex> lk(m);
+        done_cv.wait(lk, [&] { return busy == 0; });
+    }
+    ~WorkPool() {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& t : th) t.join();
+    }
+};
+
 struct gx_context {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -131,7 +190,22 @@ struct gx_context {
     std::vector<Walk> walk_cache;
     TbOut tb_cache;
     PinnedBuf tb_pin;
+    PinnedBuf io_pin;   // staging for the small per-launch descriptors and results (a pageable
+                        // copy goes through the runtime's staging and now and then stalls ms)
+    WorkPool workers;   // labelling threads (created on first use)
 };
+
+// ctx->io_pin grown to `bytes` (contents not kept); nullptr on failure.
+static void* io_pinned(gx_context* ctx, size_t bytes) {
+    if (ctx->io_pin.cap < bytes) {
+        if (ctx->io_pin.p) (void)hipHostFree(ctx->io_pin.p);
+        ctx->io_pin = PinnedBuf{};
+        const size_t cap = std::max<size_t>(bytes, 1 << 16);
+        if (hipHostMalloc(&ctx->io_pin.p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+        ctx->io_pin.cap = cap;
+    }
+    return ctx->io_pin.p;
+}
 
 static int pool_get(gx_context* ctx, size_t bytes, DevBuf* out) {
     bytes = std::max<size_t>(bytes, 256);
@@ -182,6 +256,23 @@ extern "C" int gx_context_create(int device, gx_context** out) {
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
     HIPCHK(hipEventCreate(&c->ev2));
+    // Exercise the copy paths once (device->pinned host of a few MB, host->
+    // device, memset): the runtime sets some of them up on first use, which
+    // otherwise stalled one later batch's traceback copies by ~8 ms.
+    {
+        const size_t wb = 16u << 20;
+        void* d = nullptr;
+        if (hipMalloc(&d, wb) == hipSuccess) {
+            if (void* h = io_pinned(c, wb)) {
+                (void)hipMemsetAsync(d, 0, wb, c->stream);
+                (void)hipMemcpyAsync(h, d, wb, hipMemcpyDeviceToHost, c->stream);
+                (void)hipMemcpyAsync(d, h, 4096, hipMemcpyHostToDevice, c->stream);
+                (void)hipMemcpyAsync(h, d, 4096, hipMemcpyDeviceToHost, c->stream);
+                (void)hipStreamSynchronize(c->stream);
+            }
+            (void)hipFree(d);
+        }
+    }
     *out = c;
     return GX_OK;
 }
@@ -201,6 +292,7 @@ extern "C" void gx_context_destroy(gx_context* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->st_chars.p) (void)hipFree(ctx->st_chars.p);
     if (ctx->tb_pin.p) (void)hipHostFree(ctx->tb_pin.p);
+    if (ctx->io_pin.p) (void)hipHostFree(ctx->io_pin.p);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->ev2) (void)hipEventDestroy(ctx->ev2);
@@ -474,7 +566,12 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         HIPCHK(hipMemsetAsync(trace.p, 0, (size_t)std::max(strips, 1) * sizeof(StripTrace), ctx->stream));
         for (size_t p = 0; p < P; ++p) job.pd[p].trace = (StripTrace*)trace.p + job.pd[p].strip_base;
     }
-    HIPCHK(hipMemcpyAsync(job.pairs.p, job.pd.data(), P * sizeof(PairDev), hipMemcpyHostToDevice, ctx->stream));
+    // descriptors in (and results out) through pinned staging, laid out [PairDev x P | PairRes x P | status]
+    const size_t pin_bytes = P * (sizeof(PairDev) + sizeof(PairRes)) + 2 * sizeof(int);
+    char* pin = (char*)io_pinned(ctx, pin_bytes);
+    if (!pin) return fail(GX_ENOMEM, "pinned staging buffer");
+    memcpy(pin, job.pd.data(), P * sizeof(PairDev));
+    HIPCHK(hipMemcpyAsync(job.pairs.p, pin, P * sizeof(PairDev), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemsetAsync(job.progress.p, 0, std::max<size_t>(prog_elems, 1) * sizeof(int), ctx->stream));
     HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, ctx->stream));
     HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), ctx->stream));
@@ -492,9 +589,13 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                                (PairRes*)job.pres.p, ctx->stream));
     job.res.assign(P, PairRes{});
     int status[2] = {0, 0};
-    HIPCHK(hipMemcpyAsync(job.res.data(), job.pres.p, P * sizeof(PairRes), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(status, job.counter.p, sizeof status, hipMemcpyDeviceToHost, ctx->stream));
+    PairRes* pin_res = (PairRes*)(pin + P * sizeof(PairDev));
+    int* pin_status = (int*)(pin + P * (sizeof(PairDev) + sizeof(PairRes)));
+    HIPCHK(hipMemcpyAsync(pin_res, job.pres.p, P * sizeof(PairRes), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(pin_status, job.counter.p, sizeof status, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    memcpy(job.res.data(), pin_res, P * sizeof(PairRes));
+    memcpy(status, pin_status, sizeof status);
     if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug"))
         fprintf(stderr, "[gx DEBUG] fill: launch..sync %.3f ms\n",
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h_launch).count());
@@ -670,7 +771,10 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
         t.srows = SR;
         t.end_ij = (int*)cnt.p + 4 * p;
     }
-    hipError_t e = hipMemcpyAsync(jb.p, jobs.data(), P * sizeof(TbDev), hipMemcpyHostToDevice, ctx->stream);
+    TbDev* pin_jobs = (TbDev*)io_pinned(ctx, P * sizeof(TbDev));
+    if (!pin_jobs) { cleanup(); return fail(GX_ENOMEM, "pinned staging buffer"); }
+    memcpy(pin_jobs, jobs.data(), P * sizeof(TbDev));
+    hipError_t e = hipMemcpyAsync(jb.p, pin_jobs, P * sizeof(TbDev), hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess) e = hipMemsetAsync(seg.p, 0, std::max<size_t>(stot, 1) * 4 * sizeof(int), ctx->stream);
     if (e == hipSuccess) e = hipEventRecord(ctx->ev1, ctx->stream);
     if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, max_strips, ctx->stream);
@@ -687,10 +791,20 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     int* c = (int*)ctx->tb_pin.p;
     int* sg = c + nc;
     uint32_t* hr = (uint32_t*)(sg + nsg);
+    using clk = std::chrono::steady_clock;
+    const auto q0 = clk::now();
     if (e == hipSuccess) e = hipMemcpyAsync(c, cnt.p, nc * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(sg, seg.p, nsg * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(hr, recs.p, nhr * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream);
+    const auto q1 = clk::now();
+    if (e == hipSuccess) e = hipEventSynchronize(ctx->ev2);
+    const auto q2 = clk::now();
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug"))
+        fprintf(stderr, "[gx DEBUG] traceback: D2H enqueue %.3f ms, kernels done +%.3f ms, copies done +%.3f ms\n",
+                std::chrono::duration<double, std::milli>(q1 - q0).count(),
+                std::chrono::duration<double, std::milli>(q2 - q1).count(),
+                std::chrono::duration<double, std::milli>(clk::now() - q2).count());
     cleanup();
     if (e != hipSuccess) return fail(GX_EHIP, std::string("traceback: ") + hipGetErrorString(e));
     float ms = 0;
@@ -1057,29 +1171,23 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
     // label the walks (host, algo.rs:339-422), pairs in parallel
     std::vector<int> prc(P, GX_OK);
     std::vector<std::string> perr(P);
-    auto label_range = [&](size_t lo, size_t hi) {
-        for (size_t p = lo; p < hi; ++p) {
-            // interior moves straight from the device's row records
-            if (dev_of[p] >= 0)
-                prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p],
-                                    ph[p].n + ph[p].m, RecordsSrc{&tb, (size_t)dev_of[p]}, walks[p]);
-            else
-                prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], 0,
-                                    MovesSrc{nullptr, 0}, walks[p]);
-            if (prc[p]) perr[p] = g_err;   // g_err is thread-local
-        }
+    const std::function<void(size_t)> label_one = [&](size_t p) {
+        // interior moves straight from the device's row records
+        if (dev_of[p] >= 0)
+            prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], ph[p].n + ph[p].m,
+                                RecordsSrc{&tb, (size_t)dev_of[p]}, walks[p]);
+        else
+            prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], 0,
+                                MovesSrc{nullptr, 0}, walks[p]);
+        if (prc[p]) perr[p] = g_err;   // g_err is thread-local
     };
-    const size_t nthreads = std::min<size_t>({P, (size_t)std::max(1u, std::thread::hardware_concurrency()), 16});
+    // the calling thread plus up to 11 pool workers (the box gives a process
+    // 16 CPUs; the HIP runtime's threads and the caller's keep the rest)
+    const size_t nthreads = std::min<size_t>({P, (size_t)std::max(1u, std::thread::hardware_concurrency()), 12});
     if (nthreads <= 1) {
-        label_range(0, P);
+        for (size_t p = 0; p < P; ++p) label_one(p);
     } else {
-        std::vector<std::thread> th;
-        const size_t per = (P + nthreads - 1) / nthreads;
-        for (size_t w = 0; w < nthreads; ++w) {
-            const size_t lo = w * per, hi = std::min(P, lo + per);
-            if (lo < hi) th.emplace_back(label_range, lo, hi);
-        }
-        for (auto& t : th) t.join();
+        ctx->workers.run(P, nthreads - 1, label_one);
     }
     for (size_t p = 0; p < P; ++p) {
         if (prc[p]) return fail(prc[p], perr[p]);

@@ -1,4 +1,5 @@
-"""Time StagedPairs.run calls (host wall) next to the library's GX_LOG=debug phase lines."""
+"""Time StagedPairs.run calls (host wall) next to the library's GX_LOG=debug phase lines.
+    python tools/time_staged.py [pairs] [length]"""
 import os
 import sys
 import time
@@ -10,10 +11,14 @@ import bench  # noqa: E402  (synthetic pairs)
 import gxamd as gx  # noqa: E402
 
 P = int(sys.argv[1]) if len(sys.argv) > 1 else 16
-pairs = [bench.synth_pair(p, 30000) for p in range(P)]
+L = int(sys.argv[2]) if len(sys.argv) > 2 else 30000
+pairs = [bench.synth_pair(p, L) for p in range(P)]
 st = gx.StagedPairs(pairs)
-for k in range(4):
+for k in range(5):
     t0 = time.perf_counter()
     res, fms = st.run(gx.Scores(*bench.SCORES), False, True)
     t1 = time.perf_counter()
-    print(f"call {k}: wall {1e3 * (t1 - t0):.3f} ms fill {fms:.3f} ms", file=sys.stderr, flush=True)
+    got = [(r.score, r.n_steps, r.matches) for r in res]
+    t2 = time.perf_counter()
+    print(f"call {k}: run {1e3 * (t1 - t0):.3f} ms (fill {fms:.3f}) + results {1e3 * (t2 - t1):.3f} ms",
+          file=sys.stderr, flush=True)
