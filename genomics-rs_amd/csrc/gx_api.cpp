@@ -193,7 +193,34 @@ struct gx_context {
     PinnedBuf io_pin;   // staging for the small per-launch descriptors and results (a pageable
                         // copy goes through the runtime's staging and now and then stalls ms)
     WorkPool workers;   // labelling threads (created on first use)
+    // pipelined multi-step batches (gx_run_staged_steps): two slots, so batch
+    // k's host labelling overlaps batch k+1's fill on the device
+    struct Slot {
+        PinnedBuf fpin, tjpin, tbpin;        // fill descriptors/results, traceback jobs, traceback records
+        hipEvent_t fb = nullptr, fe = nullptr, tb = nullptr, te = nullptr, fdone = nullptr, tdone = nullptr;
+        TbOut out;
+    } slots[2];
 };
+
+static void* pinned_grow(PinnedBuf& b, size_t bytes) {
+    if (b.cap < bytes) {
+        if (b.p) (void)hipHostFree(b.p);
+        b = PinnedBuf{};
+        const size_t cap = std::max<size_t>(bytes, 1 << 16);
+        if (hipHostMalloc(&b.p, cap, hipHostMallocDefault) != hipSuccess) return nullptr;
+        b.cap = cap;
+    }
+    return b.p;
+}
+
+static int slots_ready(gx_context* ctx) {
+    for (auto& s : ctx->slots) {
+        hipEvent_t* evs[] = {&s.fb, &s.fe, &s.tb, &s.te, &s.fdone, &s.tdone};
+        for (hipEvent_t* e : evs)
+            if (!*e && hipEventCreate(e) != hipSuccess) return GX_EHIP;
+    }
+    return GX_OK;
+}
 
 // ctx->io_pin grown to `bytes` (contents not kept); nullptr on failure.
 static void* io_pinned(gx_context* ctx, size_t bytes) {
@@ -293,6 +320,12 @@ extern "C" void gx_context_destroy(gx_context* ctx) {
     if (ctx->st_chars.p) (void)hipFree(ctx->st_chars.p);
     if (ctx->tb_pin.p) (void)hipHostFree(ctx->tb_pin.p);
     if (ctx->io_pin.p) (void)hipHostFree(ctx->io_pin.p);
+    for (auto& s : ctx->slots) {
+        for (PinnedBuf* b : {&s.fpin, &s.tjpin, &s.tbpin})
+            if (b->p) (void)hipHostFree(b->p);
+        for (hipEvent_t e : {s.fb, s.fe, s.tb, s.te, s.fdone, s.tdone})
+            if (e) (void)hipEventDestroy(e);
+    }
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->ev2) (void)hipEventDestroy(ctx->ev2);
@@ -448,6 +481,9 @@ struct FillJob {
     std::vector<PairRes> res;
     int W = 4;
     int lay = 0;   // 0: anti-diagonal 128-row strips, 1: column-step 64-row strips (gx_internal.h)
+    int slot = -1;                      // pipelined path: the context slot whose pinned staging / events it uses
+    PairRes* pin_res = nullptr;         // results in pinned staging (collected by fill_collect)
+    int* pin_status = nullptr;
     int total_bands = 0, total_strips = 0;
     bool planes_on = false, lcs_on = false, track_on = false;
     double fill_ms = 0.0;
@@ -469,7 +505,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                     const std::vector<PairHost>& ph, const Scores32& sc, int is_local, bool planes, bool track,
                     bool lcs, FillJob& job, const uint8_t* chars_dev = nullptr,
                     const std::vector<size_t>* off1 = nullptr, const std::vector<size_t>* off2 = nullptr,
-                    const SmallAlpha* alpha = nullptr) {
+                    const SmallAlpha* alpha = nullptr, int slot = -1, bool collect = true) {
     const int lay = fill_layout(ph, sc, fill_grid_cap(ctx->device));
     const int SR = strip_rows(lay);
     int total_strips = 0;
@@ -559,7 +595,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         d.feed = (Rec*)job.feed.p + fo[p];
         d.progress = (int*)job.progress.p + gofs[p];
     }
-    const char* trace_file = getenv("GX_TRACE_FILE");
+    const char* trace_file = slot < 0 ? getenv("GX_TRACE_FILE") : nullptr;
     DevBuf trace;
     if (trace_file && *trace_file) {
         if ((rc = pool_get(ctx, (size_t)std::max(strips, 1) * sizeof(StripTrace), &trace))) return rc;
@@ -568,7 +604,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     }
     // descriptors in (and results out) through pinned staging, laid out [PairDev x P | PairRes x P | status]
     const size_t pin_bytes = P * (sizeof(PairDev) + sizeof(PairRes)) + 2 * sizeof(int);
-    char* pin = (char*)io_pinned(ctx, pin_bytes);
+    char* pin = (char*)(slot >= 0 ? pinned_grow(ctx->slots[slot].fpin, pin_bytes) : io_pinned(ctx, pin_bytes));
     if (!pin) return fail(GX_ENOMEM, "pinned staging buffer");
     memcpy(pin, job.pd.data(), P * sizeof(PairDev));
     HIPCHK(hipMemcpyAsync(job.pairs.p, pin, P * sizeof(PairDev), hipMemcpyHostToDevice, ctx->stream));
@@ -577,11 +613,12 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), ctx->stream));
     const int grid = std::min(bands, fill_grid_cap(ctx->device));
     const auto h_launch = std::chrono::steady_clock::now();
-    HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+    hipEvent_t evb = slot >= 0 ? ctx->slots[slot].fb : ctx->ev0, eve = slot >= 0 ? ctx->slots[slot].fe : ctx->ev1;
+    HIPCHK(hipEventRecord(evb, ctx->stream));
     if (bands > 0)
         HIPCHK(launch_fill(W, lay, is_local != 0, planes, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
                            (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, ctx->stream));
-    HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));   // ev0..ev1 brackets the fill kernel alone
+    HIPCHK(hipEventRecord(eve, ctx->stream));   // evb..eve brackets the fill kernel alone
     // strip results exist only for the tracked and local fills (the untracked
     // global fill writes end_SM / end_E itself): no reduction launch otherwise
     if (bands > 0 && (track || is_local))
@@ -593,6 +630,13 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     int* pin_status = (int*)(pin + P * (sizeof(PairDev) + sizeof(PairRes)));
     HIPCHK(hipMemcpyAsync(pin_res, job.pres.p, P * sizeof(PairRes), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipMemcpyAsync(pin_status, job.counter.p, sizeof status, hipMemcpyDeviceToHost, ctx->stream));
+    job.pin_res = pin_res;
+    job.pin_status = pin_status;
+    job.slot = slot;
+    if (!collect) {   // pipelined: fill_collect() waits for the results later
+        HIPCHK(hipEventRecord(ctx->slots[slot].fdone, ctx->stream));
+        return GX_OK;
+    }
     HIPCHK(hipStreamSynchronize(ctx->stream));
     memcpy(job.res.data(), pin_res, P * sizeof(PairRes));
     memcpy(status, pin_status, sizeof status);
@@ -602,7 +646,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     if (status[1] != 0)
         return fail(GX_EHIP, "fill kernel: inter-wave wait timed out (status " + std::to_string(status[1]) + ")");
     float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    HIPCHK(hipEventElapsedTime(&ms, evb, eve));
     job.fill_ms = ms;
     if (trace.p) {
         std::vector<StripTrace> tr((size_t)strips);
@@ -623,6 +667,21 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
             fclose(f);
         }
     }
+    return GX_OK;
+}
+
+// Results of a fill enqueued with collect = false (pipelined path).
+static int fill_collect(gx_context* ctx, FillJob& job) {
+    auto& s = ctx->slots[job.slot];
+    HIPCHK(hipEventSynchronize(s.fdone));
+    const size_t P = job.pd.size();
+    job.res.assign(P, PairRes{});
+    memcpy(job.res.data(), job.pin_res, P * sizeof(PairRes));
+    if (job.pin_status[1] != 0)
+        return fail(GX_EHIP, "fill kernel: inter-wave wait timed out (status " + std::to_string(job.pin_status[1]) + ")");
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, s.fb, s.fe));
+    job.fill_ms = ms;
     return GX_OK;
 }
 
@@ -737,7 +796,8 @@ struct TbStart {
     int E;      // its landing column (PairRes.end_E / lmax_E)
 };
 
-static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<TbStart>& starts, TbOut& out) {
+static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<TbStart>& starts, TbOut& out,
+                         int slot = -1, bool collect = true) {
     const size_t P = starts.size();
     std::vector<TbDev> jobs(P);
     std::vector<size_t> so(P);
@@ -771,24 +831,22 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
         t.srows = SR;
         t.end_ij = (int*)cnt.p + 4 * p;
     }
-    TbDev* pin_jobs = (TbDev*)io_pinned(ctx, P * sizeof(TbDev));
+    TbDev* pin_jobs = (TbDev*)(slot >= 0 ? pinned_grow(ctx->slots[slot].tjpin, P * sizeof(TbDev))
+                                         : io_pinned(ctx, P * sizeof(TbDev)));
     if (!pin_jobs) { cleanup(); return fail(GX_ENOMEM, "pinned staging buffer"); }
     memcpy(pin_jobs, jobs.data(), P * sizeof(TbDev));
     hipError_t e = hipMemcpyAsync(jb.p, pin_jobs, P * sizeof(TbDev), hipMemcpyHostToDevice, ctx->stream);
     if (e == hipSuccess) e = hipMemsetAsync(seg.p, 0, std::max<size_t>(stot, 1) * 4 * sizeof(int), ctx->stream);
-    if (e == hipSuccess) e = hipEventRecord(ctx->ev1, ctx->stream);
+    hipEvent_t evb = slot >= 0 ? ctx->slots[slot].tb : ctx->ev1, eve = slot >= 0 ? ctx->slots[slot].te : ctx->ev2;
+    if (e == hipSuccess) e = hipEventRecord(evb, ctx->stream);
     if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, max_strips, ctx->stream);
-    if (e == hipSuccess) e = hipEventRecord(ctx->ev2, ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(eve, ctx->stream);
     // one pinned host block: c | sg | hr
     const size_t nc = 4 * P, nsg = 4 * std::max<size_t>(stot, 1), nhr = std::max<size_t>(stot, 1) * SR;
     const size_t bytes = (nc + nsg) * sizeof(int) + nhr * sizeof(uint32_t);
-    if (e == hipSuccess && ctx->tb_pin.cap < bytes) {
-        if (ctx->tb_pin.p) (void)hipHostFree(ctx->tb_pin.p);
-        ctx->tb_pin = PinnedBuf{};
-        e = hipHostMalloc(&ctx->tb_pin.p, bytes, hipHostMallocDefault);
-        if (e == hipSuccess) ctx->tb_pin.cap = bytes;
-    }
-    int* c = (int*)ctx->tb_pin.p;
+    PinnedBuf& recpin = slot >= 0 ? ctx->slots[slot].tbpin : ctx->tb_pin;
+    if (e == hipSuccess && !pinned_grow(recpin, bytes)) e = hipErrorOutOfMemory;
+    int* c = (int*)recpin.p;
     int* sg = c + nc;
     uint32_t* hr = (uint32_t*)(sg + nsg);
     using clk = std::chrono::steady_clock;
@@ -797,7 +855,16 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     if (e == hipSuccess) e = hipMemcpyAsync(sg, seg.p, nsg * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(hr, recs.p, nhr * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream);
     const auto q1 = clk::now();
-    if (e == hipSuccess) e = hipEventSynchronize(ctx->ev2);
+    out.c = c; out.sg = sg; out.hr = hr;
+    out.so = so;
+    out.srows = SR;
+    if (!collect) {   // pipelined: tb_collect() waits for the records later
+        if (e == hipSuccess) e = hipEventRecord(ctx->slots[slot].tdone, ctx->stream);
+        cleanup();    // the buffers' next users are later on the same stream
+        if (e != hipSuccess) return fail(GX_EHIP, std::string("traceback: ") + hipGetErrorString(e));
+        return GX_OK;
+    }
+    if (e == hipSuccess) e = hipEventSynchronize(eve);
     const auto q2 = clk::now();
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug"))
@@ -808,16 +875,29 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     cleanup();
     if (e != hipSuccess) return fail(GX_EHIP, std::string("traceback: ") + hipGetErrorString(e));
     float ms = 0;
-    (void)hipEventElapsedTime(&ms, ctx->ev1, ctx->ev2);
+    (void)hipEventElapsedTime(&ms, evb, eve);
     out.ms = ms;
-    out.c = c; out.sg = sg; out.hr = hr;
-    out.so = so;
-    out.srows = SR;
     out.end_i.resize(P);
     out.end_j.resize(P);
     for (size_t p = 0; p < P; ++p) {
         out.end_i[p] = c[4 * p + 0];
         out.end_j[p] = c[4 * p + 1];
+    }
+    return GX_OK;
+}
+
+// Records of a traceback enqueued with collect = false (pipelined path).
+static int tb_collect(gx_context* ctx, int slot, size_t P, TbOut& out) {
+    auto& s = ctx->slots[slot];
+    HIPCHK(hipEventSynchronize(s.tdone));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, s.tb, s.te);
+    out.ms = ms;
+    out.end_i.resize(P);
+    out.end_j.resize(P);
+    for (size_t p = 0; p < P; ++p) {
+        out.end_i[p] = out.c[4 * p + 0];
+        out.end_j[p] = out.c[4 * p + 1];
     }
     return GX_OK;
 }
@@ -1097,6 +1177,49 @@ extern "C" int gx_align(gx_context* ctx, const uint8_t* s1, size_t n, const uint
 // ---------------------------------------------------------------------------
 // batch of independent pairs (config 4 / 5)
 
+// Labels one batch's walks (host, algo.rs:339-422), pairs on the worker pool:
+// interior moves from the device's row records (dev_of[p] >= 0), then the
+// analytic boundary; fills walks[p].res.
+static int label_batch(gx_context* ctx, const std::vector<PairHost>& ph, const HostScores& hs, int is_local, bool track,
+                       const std::vector<int>& dev_of, const std::vector<uint64_t>& si,
+                       const std::vector<uint64_t>& sj, const std::vector<int64_t>& score,
+                       const std::vector<PairRes>& res, const TbOut& tb, double fill_ms, std::vector<Walk>& walks) {
+    const size_t P = ph.size();
+    walks.resize(P);   // keeps the step buffers of a reused vector
+    std::vector<int> prc(P, GX_OK);
+    std::vector<std::string> perr(P);
+    const std::function<void(size_t)> label_one = [&](size_t p) {
+        if (dev_of[p] >= 0)
+            prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], ph[p].n + ph[p].m,
+                                RecordsSrc{&tb, (size_t)dev_of[p]}, walks[p]);
+        else
+            prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], 0,
+                                MovesSrc{nullptr, 0}, walks[p]);
+        if (prc[p]) perr[p] = g_err;   // g_err is thread-local
+    };
+    // the calling thread plus up to 11 pool workers (the box gives a process
+    // 16 CPUs; the HIP runtime's threads and the caller's keep the rest)
+    const size_t nthreads = std::min<size_t>({P, (size_t)std::max(1u, std::thread::hardware_concurrency()), 12});
+    if (nthreads <= 1) {
+        for (size_t p = 0; p < P; ++p) label_one(p);
+    } else {
+        ctx->workers.run(P, nthreads - 1, label_one);
+    }
+    for (size_t p = 0; p < P; ++p) {
+        if (prc[p]) return fail(prc[p], perr[p]);
+        Walk& w = walks[p];
+        const bool interior = ph[p].n >= 1 && ph[p].m >= 1 && track;
+        w.res.score = score[p];
+        w.res.start_i = si[p]; w.res.start_j = sj[p];
+        w.res.max_cell_i = interior ? (uint64_t)res[p].max_i : 0;
+        w.res.max_cell_j = interior ? (uint64_t)res[p].max_j : 0;
+        w.res.matches_at_max = interior ? (uint64_t)res[p].mam : 0;
+        w.res.fill_us = (int64_t)(fill_ms * 1000.0);
+        w.res.retrace_us = (int64_t)(tb.ms * 1000.0);
+    }
+    return GX_OK;
+}
+
 static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
                       const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc, const HostScores& hs,
                       const Scores32& sc, int is_local, bool planes, bool track, std::vector<Walk>& walks,
@@ -1165,42 +1288,102 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
                             "label %.3f ms\n", P, ms(c0, c1), fill_ms, ms(c1, c2), tb_ms, ms(c2, clk::now()));
         }
     } plog{c0, c1, c2, job.fill_ms, tb.ms, P};
-    walks.resize(P);   // keeps the step buffers of a reused vector
     std::vector<int> dev_of(P, -1);
     for (size_t k = 0; k < idx.size(); ++k) dev_of[idx[k]] = (int)k;
-    // label the walks (host, algo.rs:339-422), pairs in parallel
-    std::vector<int> prc(P, GX_OK);
-    std::vector<std::string> perr(P);
-    const std::function<void(size_t)> label_one = [&](size_t p) {
-        // interior moves straight from the device's row records
-        if (dev_of[p] >= 0)
-            prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], ph[p].n + ph[p].m,
-                                RecordsSrc{&tb, (size_t)dev_of[p]}, walks[p]);
-        else
-            prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], 0,
-                                MovesSrc{nullptr, 0}, walks[p]);
-        if (prc[p]) perr[p] = g_err;   // g_err is thread-local
+    return label_batch(ctx, ph, hs, is_local, track, dev_of, si, sj, score, res, tb, job.fill_ms, walks);
+}
+
+
+// `nsteps` passes over the same batch (the staged benchmark path), pipelined
+// one batch deep: batch k+1's fill is queued behind batch k's traceback, so
+// the host labels batch k while the device fills batch k+1.  Device buffers
+// go back to the pool as soon as their last user is queued (everything runs on
+// one stream); pinned staging and events alternate between two slots.  Walks
+// and results are those of the last pass; *fill_ms is the mean fill time.
+static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
+                            const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc, const HostScores& hs,
+                            const Scores32& sc, int is_local, bool planes, bool track, int nsteps,
+                            std::vector<Walk>& walks, double* fill_ms, const uint8_t* chars_dev,
+                            const std::vector<size_t>* off1, const std::vector<size_t>* off2,
+                            const SmallAlpha* staged_alpha) {
+    const size_t P = ph.size();
+    std::vector<size_t> idx;
+    for (size_t p = 0; p < P; ++p) if (ph[p].n >= 1 && ph[p].m >= 1) idx.push_back(p);
+    if (nsteps <= 1 || idx.empty() || getenv("GX_TRACE_FILE")) {
+        double f = 0, fsum = 0;
+        for (int s = 0; s < std::max(nsteps, 1); ++s) {
+            const int rc = batch_core(ctx, ph, proc, hs, sc, is_local, planes, track, walks, &f, chars_dev, off1, off2,
+                                      staged_alpha);
+            if (rc) return rc;
+            fsum += f;
+        }
+        if (fill_ms) *fill_ms = fsum / std::max(nsteps, 1);
+        return GX_OK;
+    }
+    int rc = slots_ready(ctx);
+    if (rc) return fail(rc, "pipeline events");
+    std::vector<PairHost> dph;
+    std::vector<std::pair<const uint8_t*, const uint8_t*>> dproc;
+    std::vector<size_t> o1, o2;
+    for (size_t p : idx) {
+        dph.push_back(ph[p]);
+        dproc.push_back(proc[p]);
+        if (chars_dev) { o1.push_back((*off1)[p]); o2.push_back((*off2)[p]); }
+    }
+    SmallAlpha alpha;
+    if (staged_alpha) alpha = *staged_alpha;
+    else
+        for (size_t q = 0; q < dproc.size() && alpha.n <= 4; ++q) {
+            alpha.add(dproc[q].first, dph[q].n);
+            alpha.add(dproc[q].second, dph[q].m);
+        }
+    FillJob jobs[2];
+    std::vector<PairRes> res(P, PairRes{});
+    std::vector<TbStart> starts(idx.size());
+    std::vector<uint64_t> si(P), sj(P);
+    std::vector<int64_t> score(P);
+    std::vector<int> dev_of(P, -1);
+    for (size_t q = 0; q < idx.size(); ++q) dev_of[idx[q]] = (int)q;
+    double fsum = 0;
+    auto fill = [&](int s) {
+        return run_fill(ctx, dproc, dph, sc, is_local, planes, track, false, jobs[s], chars_dev,
+                        chars_dev ? &o1 : nullptr, chars_dev ? &o2 : nullptr, &alpha, s, false);
     };
-    // the calling thread plus up to 11 pool workers (the box gives a process
-    // 16 CPUs; the HIP runtime's threads and the caller's keep the rest)
-    const size_t nthreads = std::min<size_t>({P, (size_t)std::max(1u, std::thread::hardware_concurrency()), 12});
-    if (nthreads <= 1) {
-        for (size_t p = 0; p < P; ++p) label_one(p);
-    } else {
-        ctx->workers.run(P, nthreads - 1, label_one);
+    // results of slot s's fill -> start cells -> its traceback queued; the fill
+    // buffers return to the pool (their last user, the traceback, is queued)
+    auto trace = [&](int s) {
+        int r = fill_collect(ctx, jobs[s]);
+        if (r) return r;
+        fsum += jobs[s].fill_ms;
+        for (size_t q = 0; q < idx.size(); ++q) res[idx[q]] = jobs[s].res[q];
+        for (size_t p = 0; p < P; ++p)
+            start_cell_common(hs, is_local, ph[p].n, ph[p].m, res[p], &si[p], &sj[p], &score[p]);
+        for (size_t q = 0; q < idx.size(); ++q) {
+            const size_t p = idx[q];
+            starts[q] = (si[p] >= 1 && sj[p] >= 1)
+                            ? TbStart{(int)si[p], (int)sj[p], is_local ? res[p].lmax_E : res[p].end_E}
+                            : TbStart{0, 0, 0};
+        }
+        r = run_traceback(ctx, jobs[s], starts, ctx->slots[s].out, s, false);
+        job_release(ctx, jobs[s]);
+        return r;
+    };
+    if (!(rc = fill(0))) rc = trace(0);
+    for (int k = 0; k < nsteps && !rc; ++k) {
+        const int s = k & 1;
+        if (k + 1 < nsteps && (rc = fill(s ^ 1))) break;       // queued behind batch k's traceback
+        if ((rc = tb_collect(ctx, s, idx.size(), ctx->slots[s].out))) break;
+        if ((rc = label_batch(ctx, ph, hs, is_local, track, dev_of, si, sj, score, res, ctx->slots[s].out,
+                              jobs[s].fill_ms, walks)))
+            break;
+        if (k + 1 < nsteps && (rc = trace(s ^ 1))) break;
     }
-    for (size_t p = 0; p < P; ++p) {
-        if (prc[p]) return fail(prc[p], perr[p]);
-        Walk& w = walks[p];
-        const bool interior = ph[p].n >= 1 && ph[p].m >= 1 && track;
-        w.res.score = score[p];
-        w.res.start_i = si[p]; w.res.start_j = sj[p];
-        w.res.max_cell_i = interior ? (uint64_t)res[p].max_i : 0;
-        w.res.max_cell_j = interior ? (uint64_t)res[p].max_j : 0;
-        w.res.matches_at_max = interior ? (uint64_t)res[p].mam : 0;
-        w.res.fill_us = (int64_t)(job.fill_ms * 1000.0);
-        w.res.retrace_us = (int64_t)(tb.ms * 1000.0);
+    if (rc) {
+        (void)hipStreamSynchronize(ctx->stream);
+        for (auto& j : jobs) job_release(ctx, j);
+        return rc;
     }
+    if (fill_ms) *fill_ms = fsum / nsteps;
     return GX_OK;
 }
 
@@ -1270,8 +1453,8 @@ extern "C" int gx_stage_pairs(gx_context* ctx, const uint8_t* const* s1, const s
     return GX_OK;
 }
 
-extern "C" int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes,
-                             uint32_t flags, gx_result* out, double* fill_ms_out) {
+extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes,
+                                   uint32_t flags, int nsteps, gx_result* out, double* fill_ms_out) {
     if (!ctx || !out) return fail(GX_EINVAL, "NULL argument");
     std::lock_guard<std::mutex> lk(ctx->mu);
     HIPCHK(hipSetDevice(ctx->device));
@@ -1290,10 +1473,16 @@ extern "C" int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_lo
     }
     std::vector<Walk>& walks = ctx->walk_cache;
     double fms = 0;
-    rc = batch_core(ctx, ph, proc, hs, sc, is_local, keep_planes != 0, (flags & GX_ALIGN_MAX_CELL) != 0, walks, &fms,
-                    (const uint8_t*)ctx->st_chars.p, &ctx->st_off1, &ctx->st_off2, &ctx->st_alpha);
+    rc = batch_core_steps(ctx, ph, proc, hs, sc, is_local, keep_planes != 0, (flags & GX_ALIGN_MAX_CELL) != 0,
+                          std::max(nsteps, 1), walks, &fms, (const uint8_t*)ctx->st_chars.p, &ctx->st_off1,
+                          &ctx->st_off2, &ctx->st_alpha);
     if (rc) return rc;
     for (size_t p = 0; p < P; ++p) out[p] = walks[p].res;
     if (fill_ms_out) *fill_ms_out = fms;
     return GX_OK;
+}
+
+extern "C" int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes, uint32_t flags,
+                             gx_result* out, double* fill_ms_out) {
+    return gx_run_staged_steps(ctx, scores, is_local, keep_planes, flags, 1, out, fill_ms_out);
 }

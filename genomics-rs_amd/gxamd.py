@@ -69,7 +69,8 @@ STEP_DTYPE = np.dtype([("choice", "u1"), ("pad", "u1", (7,)), ("i", "<u8"), ("j"
 # exported symbols (include/gx.h) -- checked by tests/test_abi.py
 EXPORTED = ["gx_last_error", "gx_version", "gx_context_create", "gx_context_destroy", "gx_context_trim",
             "gx_alignment_table", "gx_table_info", "gx_table_export", "gx_table_export_plane", "gx_retrace",
-            "gx_table_free", "gx_align", "gx_align_batch", "gx_stage_pairs", "gx_run_staged", "gx_fasta_load",
+            "gx_table_free", "gx_align", "gx_align_batch", "gx_stage_pairs", "gx_run_staged", "gx_run_staged_steps",
+            "gx_fasta_load",
             "gx_config_load", "gx_format_alignment", "gx_format_table"]
 
 _lib = None
@@ -105,6 +106,8 @@ def lib():
     L.gx_stage_pairs.argtypes = [vp, vp, vp, vp, vp, sz]
     L.gx_run_staged.argtypes = [vp, ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int, ctypes.c_uint32, vp,
                                 ctypes.POINTER(ctypes.c_double)]
+    L.gx_run_staged_steps.argtypes = [vp, ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
+                                      ctypes.c_int, vp, ctypes.POINTER(ctypes.c_double)]
     L.gx_fasta_load.argtypes = [ctypes.c_char_p, vp, sz, vp, vp, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.gx_config_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(CScores)]
     L.gx_format_alignment.argtypes = [vp, sz, vp, sz, vp, sz, ctypes.POINTER(CResult), vp, sz, ctypes.POINTER(sz)]
@@ -488,11 +491,14 @@ class StagedPairs:
         m = (ctypes.c_size_t * self.P)(*[len(b) for _, b in pairs])
         _check(lib().gx_stage_pairs(self.ctx.ptr, s1p, n, s2p, m, self.P))
 
-    def run(self, scores: Scores, is_local: bool, keep_planes: bool = True, max_cell: bool = False):
+    def run(self, scores: Scores, is_local: bool, keep_planes: bool = True, max_cell: bool = False,
+            steps: int = 1):
+        """`steps` back-to-back passes (pipelined one pass deep when > 1) ->
+        (the last pass's results, mean fill ms)."""
         res = (CResult * self.P)()
         fms = ctypes.c_double(0)
-        _check(lib().gx_run_staged(self.ctx.ptr, ctypes.byref(scores.c()), int(is_local), int(keep_planes),
-                                   GX_ALIGN_MAX_CELL if max_cell else 0, res, ctypes.byref(fms)))
+        _check(lib().gx_run_staged_steps(self.ctx.ptr, ctypes.byref(scores.c()), int(is_local), int(keep_planes),
+                                         GX_ALIGN_MAX_CELL if max_cell else 0, int(steps), res, ctypes.byref(fms)))
         return list(res), fms.value
 
 

@@ -163,6 +163,11 @@ int gx_stage_pairs(gx_context* ctx, const uint8_t* const* s1, const size_t* n, c
                    const size_t* m, size_t npairs);
 int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes, uint32_t flags,
                   gx_result* out, double* fill_ms_out);
+/* nsteps back-to-back passes over the staged pairs, pipelined one pass deep
+ * (pass k's traceback labelling on the host overlaps pass k+1's fill on the
+ * device).  out = the last pass's results; *fill_ms_out = mean fill time. */
+int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes, uint32_t flags,
+                        int nsteps, gx_result* out, double* fill_ms_out);
 
 /* ---- sequence.rs / config.rs mirrors ----------------------------------- */
 /* from_fasta (sequence.rs:45-95) on a file: records are appended to the

@@ -249,19 +249,19 @@ def test_staged_path_matches_oracle(gx, ctx, oracle):
     pairs = [(bytes(rng.choice(b"ACGT") for _ in range(rng.randint(100, 700))),
               bytes(rng.choice(b"ACGT") for _ in range(rng.randint(100, 700)))) for _ in range(6)]
     st = gx.StagedPairs(pairs, ctx=ctx)
-    for keep in (True, False):
-        for track in (True, False):
-            res, fill_ms = st.run(sc(gx, CONFIG_SCORES), False, keep_planes=keep, max_cell=track)
-            assert fill_ms > 0
-            for (a, b), r in zip(pairs, res):
-                o = oracle.align(a, b, CONFIG_SCORES)
-                assert (r.score, r.n_steps, r.matches, r.mismatches, r.gap_extensions, r.opening_gaps) == \
-                       (o.score, len(o.choices), o.matches, o.mismatches, o.gap_extensions, o.opening_gaps)
-                if track:
-                    assert (r.max_cell_i, r.max_cell_j, r.matches_at_max) == \
-                           (o.max_cell[0], o.max_cell[1], o.matches_at_max)
-                else:   # main.rs discards it: not tracked on the fused path
-                    assert (r.max_cell_i, r.max_cell_j, r.matches_at_max) == (0, 0, 0)
+    for keep, track, steps in ((True, True, 1), (True, False, 1), (False, True, 1), (False, False, 1),
+                               (True, False, 3), (False, True, 4)):   # steps > 1: the pipelined passes
+        res, fill_ms = st.run(sc(gx, CONFIG_SCORES), False, keep_planes=keep, max_cell=track, steps=steps)
+        assert fill_ms > 0
+        for (a, b), r in zip(pairs, res):
+            o = oracle.align(a, b, CONFIG_SCORES)
+            assert (r.score, r.n_steps, r.matches, r.mismatches, r.gap_extensions, r.opening_gaps) == \
+                   (o.score, len(o.choices), o.matches, o.mismatches, o.gap_extensions, o.opening_gaps)
+            if track:
+                assert (r.max_cell_i, r.max_cell_j, r.matches_at_max) == \
+                       (o.max_cell[0], o.max_cell[1], o.matches_at_max)
+            else:   # main.rs discards it: not tracked on the fused path
+                assert (r.max_cell_i, r.max_cell_j, r.matches_at_max) == (0, 0, 0)
 
 
 @pytest.mark.parametrize("alpha,scores", [(b"ACGT", CONFIG_SCORES), (b"AC", TEST_SCORES), (b"GT", (3, -1, -2, -4)),
