@@ -7,7 +7,9 @@ DNA pairs (BASELINE.json metric), 1..8 GPUs, one process per GPU.
 
 A STEP is one pass of the hot path over one batch: for each of the P
 synthetic 30k x 30k pairs resident on this GPU, the full-table fill that
-writes the three int32 score planes (alignment_table, algo.rs:151-282) plus
+writes the three score planes (alignment_table, algo.rs:151-282; stored as
+exact per-cell byte differences when the scores allow it, gx_api.cpp
+d8_planes_ok, else int32) plus
 the traceback (retrace, algo.rs:287-441) down to the labelled alignment on
 the host.  Inputs are staged in HBM before the timed region; the K timed
 steps run as one pipelined call (step k's host labelling overlaps step k+1's
@@ -16,9 +18,14 @@ aligns its own pairs (weak scaling); RCCL (torch.distributed "nccl") carries
 only the barrier, the max-over-ranks time and the gather of per-pair
 results.  value = all ranks' cells / max-over-ranks time (GCUPS).
 
-roofline: the fill kernel, HBM-bound: 12 B of score-plane writes per cell
-(SURVEY.md 8(d)); achieved = 12 * cells / average fill-kernel time from HIP
-events on the kernel's own stream.  cpu_baseline: the reference-layout C
+P defaults to the pairs whose planes fill ~180 GB of HBM (64 x 30k with
+compact planes, 16 with int32 planes).
+
+roofline: the fill kernel's score-plane writes, B bytes per cell (3 compact,
+12 int32); achieved = B * cells / average fill-kernel time
+from HIP events on the kernel's own stream.  With compact planes the fill is
+issue-bound rather than HBM-bound: no_plane_fill times the same batch without
+plane stores (the kernel's compute ceiling) for comparison.  cpu_baseline: the reference-layout C
 restatement (oracle/, 48-B cells, column-major, i-outer/j-inner, one core)
 on the first R rows of the same synthetic pair.
 """
@@ -35,7 +42,7 @@ sys.path.insert(0, os.path.join(ROOT, "genomics-rs_amd"))
 
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MEASURED_HBM_GBS = 6290.0  # float4 copy ceiling (same source)
-BYTES_PER_CELL = 12        # one int32 write each of the insert/delete/sub planes
+PLANE_BUDGET = 180e9       # bytes of score planes per GPU the default batch is sized to (288 GB HBM)
 SCORES = (1, -2, -1, -5)   # config.toml:1-5
 
 
@@ -163,6 +170,12 @@ def allvsall_share(gx, rank: int, world: int):
     return [(seqs[pairs[p][0]], seqs[pairs[p][1]]) for p in mine], int(sum(w))
 
 
+def plane_desc(bytes_per_cell: int) -> str:
+    if bytes_per_cell == 3:
+        return "score planes (exact per-cell byte differences, 3 B/cell) + traceback"
+    return f"score planes (int32, {bytes_per_cell} B/cell) + traceback"
+
+
 def rank_pairs(rank: int, pairs_per_rank: int, length: int):
     """Weak-scaling shard: rank r aligns synthetic pairs r*P .. r*P+P-1 (no
     data-path collective; every rank generates its own inputs)."""
@@ -199,7 +212,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs-per-gpu", type=int, default=int(os.environ.get("GX_BENCH_PAIRS", "16")))
+    ap.add_argument("--pairs-per-gpu", type=int,
+                    default=int(os.environ["GX_BENCH_PAIRS"]) if "GX_BENCH_PAIRS" in os.environ else None,
+                    help="default: as many as fill ~180 GB with score planes (64 compact / 16 int32 at 30k)")
     ap.add_argument("--length", type=int, default=30000)
     ap.add_argument("--local", action="store_true", help="Smith-Waterman mode (default: global NW)")
     ap.add_argument("--no-planes", action="store_true", help="score+traceback only (not the headline)")
@@ -213,6 +228,8 @@ def main():
     ap.add_argument("--planes", action="store_true", help="allvsall: also write the score planes")
     ap.add_argument("--single-pair-steps", type=int, default=5,
                     help="also time BASELINE config 2's shape alone (one pair, latency), 1 GPU only; 0 = skip")
+    ap.add_argument("--no-plane-steps", type=int, default=2,
+                    help="also time the batch without plane stores (compute ceiling), 1 GPU only; 0 = skip")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -229,6 +246,10 @@ def main():
     import gxamd as gx
     ctx = gx.Context(local_rank)
     P, L = args.pairs_per_gpu, args.length
+    scores = gx.Scores(*SCORES)
+    if P is None:
+        pb = 0 if args.no_planes else gx.plane_bytes_per_cell(scores, args.local)
+        P = max(1, min(64, int(PLANE_BUDGET // (max(pb, 3) * L * (L + 64)))))
     if args.workload == "allvsall":
         pairs, n_total = allvsall_share(gx, rank, world)
         P = len(pairs)
@@ -244,7 +265,6 @@ def main():
         pairs = rank_pairs(rank, P, L)
         keep_planes = not args.no_planes
     staged = gx.StagedPairs(pairs, ctx=ctx)             # inputs resident in HBM
-    scores = gx.Scores(*SCORES)
     cells_rank = sum(len(a) * len(b) for a, b in pairs)
 
     def barrier():
@@ -272,6 +292,8 @@ def main():
         raise RuntimeError("non-deterministic result between steps")
     barrier()
     elapsed = time.perf_counter() - t0
+    finfo = ctx.fill_info()
+    bytes_per_cell = finfo["plane_bytes_per_cell"]
 
     # max over ranks (time) and gather of per-pair results, over RCCL
     elapsed, _gathered = combine_over_ranks(dist, elapsed, [[r.score, r.n_steps, r.matches] for r in res], "cuda")
@@ -282,7 +304,7 @@ def main():
     gcups = total_cells * args.steps / elapsed / 1e9
     avg_fill_ms = float(np.mean(fill_ms))
     mode_s = f"{'local SW' if args.local else 'global NW'}, scores {SCORES}, " \
-             f"{'score planes + traceback' if keep_planes else 'traceback only (no planes)'}"
+             f"{plane_desc(bytes_per_cell) if keep_planes else 'traceback only (no planes)'}"
     if args.workload == "allvsall":
         workload = f"all-vs-all of the 10 comparison_data genomes (45 pairs i<j, 29,644-30,123 nt), " \
                    f"LPT-sharded over {world} GPU(s), {mode_s}"
@@ -292,7 +314,7 @@ def main():
         workload = f"Human x Mouse BRCA2 cds ({len(pairs[0][0])}x{len(pairs[0][1])}), one pair per GPU, {mode_s}"
     else:
         workload = f"synthetic {L}x{L} DNA pairs (SplitMix64), {P} per GPU, {mode_s}"
-    fill_bytes = BYTES_PER_CELL * cells_rank
+    fill_bytes = bytes_per_cell * cells_rank
     achieved = fill_bytes / (avg_fill_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(workload)
 
@@ -317,10 +339,19 @@ def main():
                      "frac_of_measured_copy_ceiling": round(achieved / MEASURED_HBM_GBS, 4) if keep_planes else None,
                      "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "gx::fill_kernel", "fill_ms_avg": round(avg_fill_ms, 3),
+                     "algorithmic_bytes_per_cell": bytes_per_cell,
                      "algorithmic_bytes_per_launch": fill_bytes},
+        "fill_launch": finfo,
         "fill_gcups_per_gpu": round(cells_rank / (avg_fill_ms * 1e-3) / 1e9, 3),
         "traceback_us_pair0": int(np.mean(tb_us)),
     }
+    if world == 1 and keep_planes and args.no_plane_steps > 0:
+        # the same batch without plane stores: the fill's compute ceiling
+        staged.run(scores, args.local, False)
+        _, fms0 = staged.run(scores, args.local, False, steps=args.no_plane_steps)
+        out["no_plane_fill"] = {"fill_ms_avg": round(fms0, 3),
+                                "fill_gcups_per_gpu": round(cells_rank / (fms0 * 1e-3) / 1e9, 3),
+                                "planes_fill_frac": round(fms0 / avg_fill_ms, 4), "steps": args.no_plane_steps}
     if world == 1 and args.single_pair_steps > 0 and P > 1:
         # one 30k x 30k pair per step (configs[1]'s shape): the latency view of the same kernel
         one = gx.StagedPairs(pairs[:1], ctx=ctx)

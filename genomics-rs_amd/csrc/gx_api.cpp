@@ -27,13 +27,15 @@
 #include "gx_internal.h"
 
 namespace gx {
-hipError_t launch_fill(int W, int lay, bool local, bool planes, bool track, bool lcs, bool tbl, const PairDev* d_pairs, int npairs,
+hipError_t launch_fill(int W, int lay, bool local, int planes, bool track, bool lcs, bool tbl, const PairDev* d_pairs, int npairs,
                        int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                        hipStream_t st);
 hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d_sres, PairRes* d_pres,
                            hipStream_t st);
 hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipStream_t st);
 hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, hipStream_t st);
+hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, int n, int m, int t4, int h, int g,
+                            hipStream_t st);
 }  // namespace gx
 
 using namespace gx;
@@ -200,6 +202,7 @@ struct gx_context {
         hipEvent_t fb = nullptr, fe = nullptr, tb = nullptr, te = nullptr, fdone = nullptr, tdone = nullptr;
         TbOut out;
     } slots[2];
+    int last_lay = 0, last_W = 0, last_pbytes = 0;   // the last fill launch (gx_fill_info)
 };
 
 static void* pinned_grow(PinnedBuf& b, size_t bytes) {
@@ -425,16 +428,25 @@ static int fill_grid_cap(int device) {
 }
 
 // Band width: the narrowest instantiated width whose bands fit the grid
-// (one band per workgroup, all strips in flight from the start), else the
-// widest.  GX_BAND_WAVES forces a width (if instantiated for the variant).
+// (one band per workgroup, all strips in flight from the start) up to 8
+// strips; beyond that 8-strip bands that queue for workgroups.  Measured on
+// queued batches (profiles/r01i_widths.txt): 8 beats 11 and 15 everywhere
+// (45 Covid pairs 845 -> 969 GCUPS, 20 x 30k 433 -> 496, 64 x 16k 485 -> 524)
+// and ties 15 where 15 fits (16 x 30k).  GX_BAND_WAVES forces a width (if
+// instantiated for the variant).
 template <size_t N>
 static int pick_width(const int (&ws)[N], int total_strips, int grid_cap) {
     if (const char* e = getenv("GX_BAND_WAVES")) {
         const int w = atoi(e);
         for (int x : ws) if (x == w) return w;
     }
-    for (int x : ws) if (ceil_div(total_strips, x) <= grid_cap) return x;
-    return ws[N - 1];
+    int queued = ws[0];
+    for (int x : ws) {
+        if (x > 8) break;
+        if (ceil_div(total_strips, x) <= grid_cap) return x;
+        queued = x;
+    }
+    return queued;
 }
 static int fill_band_waves(bool track, int total_strips, int grid_cap, int lay) {
     // layout 1 starts at 4-strip bands: fewer HBM hand-offs for the same one
@@ -442,6 +454,26 @@ static int fill_band_waves(bool track, int total_strips, int grid_cap, int lay) 
     static constexpr int kWidths1[] = {4, 6, 8, 11, 15};
     if (track) return pick_width(kFillWidthsTrack, total_strips, grid_cap);
     return lay ? pick_width(kWidths1, total_strips, grid_cap) : pick_width(kFillWidths, total_strips, grid_cap);
+}
+
+// Compact score planes (layout 0, global, untracked: the batch path).  The
+// fill stores per cell one signed byte each of x_I = I(i,j) - I(i,j-1),
+// x_S = S(i,j) - I(i,j), x_D = D(i,j) - I(i,j) (gx_kernels.hip put_byte), 3 B
+// instead of 12.  With g, h <= 0, a = h + g, smax/smin the larger/smaller of
+// the match and mismatch scores and U = max(0, smax - a), every interior cell
+// satisfies (DESIGN.md section 4.2 has the derivation from algo.rs:231-248)
+//     a <= H(i,j) - H(i,j-1) <= U   (and the same down a column),
+//     H(i,j-1) + a <= I(i,j) <= H(i,j-1),   H(i-1,j) + a <= D(i,j) <= H(i-1,j),
+// so  x_I in [g, U - a],  x_S in [smin - U, smax - 2a],  x_D in [2a - U, U - 2a].
+// Compact planes are used when those ranges fit a signed byte (the default
+// scores give [-1, 13], [-9, 13], [-19, 19]); GX_PLANES32 forces int32 planes.
+static bool d8_planes_ok(const Scores32& sc, int is_local) {
+    if (is_local || sc.g > 0 || sc.h > 0 || getenv("GX_PLANES32")) return false;
+    const long long g = sc.g, a = (long long)sc.h + sc.g;
+    const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
+    const long long U = std::max(0LL, smax - a);
+    const long long lo = std::min({g, smin - U, 2 * a - U}), hi = std::max({U - a, smax - 2 * a, U - 2 * a});
+    return lo >= -128 && hi <= 127;
 }
 
 struct PairHost {
@@ -486,6 +518,7 @@ struct FillJob {
     int* pin_status = nullptr;
     int total_bands = 0, total_strips = 0;
     bool planes_on = false, lcs_on = false, track_on = false;
+    bool d8 = false;                    // compact byte planes (d8_planes_ok)
     double fill_ms = 0.0;
 };
 
@@ -523,6 +556,11 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         for (int k = 0; k < 4; ++k) scl.sym[k] = alpha->sym[k];
     job.W = W;
     job.planes_on = planes; job.lcs_on = lcs; job.track_on = track;
+    const bool d8 = planes && lay == 0 && !track && d8_planes_ok(sc, is_local);
+    job.d8 = d8;
+    const size_t plane_esz = d8 ? 1 : sizeof(int32_t);
+    ctx->last_lay = lay; ctx->last_W = W;
+    ctx->last_pbytes = planes ? (int)(plane_esz * 3) : 0;
     const size_t P = ph.size();
     job.pd.assign(P, PairDev{});
     // -- sizes
@@ -560,7 +598,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     if (!chars_dev) {
         if ((rc = pool_get(ctx, chars_bytes, &job.chars))) return rc;
     }
-    if (planes && (rc = pool_get(ctx, plane_elems * sizeof(int32_t) * nplanes, &job.planes))) return rc;
+    if (planes && (rc = pool_get(ctx, plane_elems * plane_esz * nplanes, &job.planes))) return rc;
     if (codes && (rc = pool_get(ctx, code_elems * sizeof(uint32_t), &job.codes))) return rc;
     if ((rc = pool_get(ctx, std::max<size_t>(skel_elems, 1) * sizeof(int), &job.skel))) return rc;
     if ((rc = pool_get(ctx, std::max<size_t>(feed_recs, 1) * sizeof(Rec), &job.feed))) return rc;
@@ -585,11 +623,12 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         PairDev& d = job.pd[p];
         d.c1 = cbase + (chars_dev ? (*off1)[p] : c1o[p]);
         d.c2 = cbase + (chars_dev ? (*off2)[p] : c2o[p]);
-        int32_t* pl = (int32_t*)job.planes.p;
-        d.pI = planes ? pl + po[p] : nullptr;
-        d.pD = planes ? pl + plane_elems + po[p] : nullptr;
-        d.pS = planes ? pl + 2 * plane_elems + po[p] : nullptr;
-        d.pL = (planes && lcs) ? pl + 3 * plane_elems + po[p] : nullptr;
+        uint8_t* pl = (uint8_t*)job.planes.p;
+        auto plane_at = [&](int k) { return (int32_t*)(pl + (k * plane_elems + po[p]) * plane_esz); };
+        d.pI = planes ? plane_at(0) : nullptr;
+        d.pD = planes ? plane_at(1) : nullptr;
+        d.pS = planes ? plane_at(2) : nullptr;
+        d.pL = (planes && lcs) ? plane_at(3) : nullptr;
         d.codes = codes ? (uint32_t*)job.codes.p + co[p] : nullptr;
         d.skel = (int*)job.skel.p + so[p];
         d.feed = (Rec*)job.feed.p + fo[p];
@@ -616,7 +655,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].fb : ctx->ev0, eve = slot >= 0 ? ctx->slots[slot].fe : ctx->ev1;
     HIPCHK(hipEventRecord(evb, ctx->stream));
     if (bands > 0)
-        HIPCHK(launch_fill(W, lay, is_local != 0, planes, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
+        HIPCHK(launch_fill(W, lay, is_local != 0, planes ? (d8 ? 2 : 1) : 0, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
                            (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, ctx->stream));
     HIPCHK(hipEventRecord(eve, ctx->stream));   // evb..eve brackets the fill kernel alone
     // strip results exist only for the tracked and local fills (the untracked
@@ -1031,7 +1070,12 @@ static int fetch_plane32(const gx_table* t, int which, std::vector<int32_t>& out
     DevBuf tmp;
     int rc = pool_get(ctx, out.size() * sizeof(int32_t), &tmp);
     if (rc) return rc;
-    hipError_t e = launch_export(src, (int32_t*)tmp.p, (int)n, (int)m, d.t4, t->job.lay, ctx->stream);
+    hipError_t e;
+    if (t->job.d8)   // compact planes: rebuilt from the insert plane's running sum (+ this plane's x)
+        e = launch_export_d8((const uint8_t*)d.pI, which == 0 ? nullptr : (const uint8_t*)src, (int32_t*)tmp.p,
+                             (int)n, (int)m, d.t4, t->sc.h, t->sc.g, ctx->stream);
+    else
+        e = launch_export(src, (int32_t*)tmp.p, (int)n, (int)m, d.t4, t->job.lay, ctx->stream);
     if (e == hipSuccess)
         e = hipMemcpyAsync(out.data(), tmp.p, out.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
@@ -1480,6 +1524,21 @@ extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int
     for (size_t p = 0; p < P; ++p) out[p] = walks[p].res;
     if (fill_ms_out) *fill_ms_out = fms;
     return GX_OK;
+}
+
+extern "C" int gx_fill_info(const gx_context* ctx, int* layout, int* band_waves, int* plane_bytes_per_cell) {
+    if (!ctx) return fail(GX_EINVAL, "context is NULL");
+    if (layout) *layout = ctx->last_lay;
+    if (band_waves) *band_waves = ctx->last_W;
+    if (plane_bytes_per_cell) *plane_bytes_per_cell = ctx->last_pbytes;
+    return GX_OK;
+}
+
+extern "C" int gx_plane_bytes_per_cell(const gx_scores* scores, int is_local) {
+    HostScores hs;
+    Scores32 sc;
+    if (check_scores(scores, 1, 1, &hs, &sc, is_local)) return -1;
+    return d8_planes_ok(sc, is_local) ? 3 : 12;
 }
 
 extern "C" int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes, uint32_t flags,

@@ -119,6 +119,35 @@ __device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 #endif
 }
 
+// Compact planes (plane mode 3, layout 0, global untracked launches whose
+// scores pass the host's range proof, gx_api.cpp d8_planes_ok): per cell one
+// signed byte each of
+//     x_I = I(i,j) - I(i,j-1),  x_S = S(i,j) - I(i,j),  x_D = D(i,j) - I(i,j)
+// in the int32 plane layout with bytes for ints (4 steps of a row = one dword
+// per lane).  The decoder (export_d8_kernel) rebuilds a row with one running
+// sum.  put_byte<K> writes (a - b) into byte K of acc in one VALU op (SDWA,
+// other bytes preserved; byte 0 clears the rest).
+template <int K>
+__device__ __forceinline__ void put_byte(uint32_t& acc, int a, int b) {
+    if constexpr (K == 0)
+        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD"
+            : "=v"(acc) : "v"(a), "v"(b));
+    else if constexpr (K == 1)
+        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+            : "+v"(acc) : "v"(a), "v"(b));
+    else if constexpr (K == 2)
+        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+            : "+v"(acc) : "v"(a), "v"(b));
+    else
+        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
+            : "+v"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t v) {
+#ifndef GX_DIAG_NO_PLANES
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, 0, GX_PLANE_AUX);
+#endif
+}
+
 // Occupancy floor (waves per SIMD), which sets the fill kernel's VGPR cap
 // (512 / floor, at most 256): one workgroup per CU, so the floor is the
 // workgroup's waves per SIMD.  The variants that also track the maxima
@@ -298,6 +327,7 @@ template <bool LOCAL, bool MASKED, bool CODES, bool TRACK, bool TBL>
 __device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm_in, const int l_in, const int e_up,
                                      const int c2, const int c1v, const bool act, const int t, const Scores32& sc,
                                      int& oI, int& oD, int& oS, int& oL) {
+    const int I_old = st.I;                // I(i, j-1): compact planes' x_I reference
     // algo.rs:231-236  insert_score = top.score_max(g, h+g, h+g)
     const int In = LOCAL ? max3i(st.I + sc.g, st.SD + sc.hg, 0) : max(st.I + sc.g, st.SD + sc.hg);
     static_assert(!(TBL && TRACK), "the LCS field needs the match bit");
@@ -360,7 +390,7 @@ __device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm
         const bool nl = act && SMn >= st.lbest;
         st.lbest = nl ? SMn : st.lbest; st.lstep = nl ? t : st.lstep; st.lE = nl ? En : st.lE;
     }
-    oI = In; oD = Dn; oS = Sn; oL = Ln;
+    oI = In; oD = Dn; oS = Sn; oL = TRACK ? Ln : I_old;   // untracked: oL carries I(i, j-1)
 }
 
 // One anti-diagonal step of a compute wave: both rows of every lane at
@@ -521,6 +551,26 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
             bstore4(rL, v1, make_int4(bL[0][1], bL[1][1], bL[2][1], bL[3][1]));
         }
     }
+    if (PLANES == 3) {
+        // compact planes: this group's 4 steps of a row are one dword per lane
+        // and plane (x_I, x_S, x_D above put_byte), stored now (256 B per wave)
+        uint32_t xI[2], xS[2], xD[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            put_byte<0>(xI[h], bI[0][h], bL[0][h]); put_byte<0>(xS[h], bS[0][h], bI[0][h]); put_byte<0>(xD[h], bD[0][h], bI[0][h]);
+            put_byte<1>(xI[h], bI[1][h], bL[1][h]); put_byte<1>(xS[h], bS[1][h], bI[1][h]); put_byte<1>(xD[h], bD[1][h], bI[1][h]);
+            put_byte<2>(xI[h], bI[2][h], bL[2][h]); put_byte<2>(xS[h], bS[2][h], bI[2][h]); put_byte<2>(xD[h], bD[2][h], bI[2][h]);
+            put_byte<3>(xI[h], bI[3][h], bL[3][h]); put_byte<3>(xS[h], bS[3][h], bI[3][h]); put_byte<3>(xD[h], bD[3][h], bI[3][h]);
+        }
+        constexpr int kSubBytes = kSub / 4 * kGroupInts;              // one sub-block of one byte plane
+        constexpr uint32_t kG = G4 * kGroupInts;
+        const uint32_t v0 = (uint32_t)w.lane * 4u + kG, v1 = v0 + kWave * 4;
+        const auto rI = rsrc_of((const uint8_t*)w.pI + sb_off, kSubBytes),
+                   rD = rsrc_of((const uint8_t*)w.pD + sb_off, kSubBytes),
+                   rS = rsrc_of((const uint8_t*)w.pS + sb_off, kSubBytes);
+        bstore1(rI, v0, xI[0]); bstore1(rS, v0, xS[0]); bstore1(rD, v0, xD[0]);
+        bstore1(rI, v1, xI[1]); bstore1(rS, v1, xS[1]); bstore1(rD, v1, xD[1]);
+    }
     if (PLANES == 2) {
         // this group's cells: 16 B per lane per row and plane, stored during the next group
         pend.I0 = make_int4(bI[0][0], bI[1][0], bI[2][0], bI[3][0]);
@@ -556,10 +606,14 @@ __device__ __forceinline__ void sub_block(LaneState& st, Rec (&nxt)[4], WaveCtx&
     group4<LOCAL, PLANES, CODES, TRACK, LCSP, TBL, MASKED, 3>(st, nxt, w, sc, t0, out_base, push_on, sb_off, pend);
 }
 
-__device__ __forceinline__ void init_row(RowState& rs, const int i, const bool row_ok, const Scores32& sc) {
+__device__ __forceinline__ void init_row(RowState& rs, const int i, const bool row_ok, const Scores32& sc,
+                                         const bool d8 = false) {
     // cell (i, 0): algo.rs:204-211
     const int D0 = sc.h + i * sc.g;
-    rs.I = kNeg;
+    // compact planes (global): I(i, 0) = negative_inf is replaced by D0 + h, which
+    // gives column 1 the same insert score, max(I + g, max(S, D) + h + g) =
+    // D0 + h + g, and x_I(i, 1) = g (the decoder's row base is D0 + h)
+    rs.I = d8 ? D0 + sc.h : kNeg;
     rs.SD = D0;                                   // max(sub=neg_inf, delete)
     rs.SM = max(D0, sc.floor_);
     rs.Dd = max3i(kNeg + sc.hg, D0 + sc.g, sc.floor_);
@@ -583,9 +637,11 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     WaveCtx w;
     {
         const size_t strip_planes = (size_t)s * P.t4 * kGroupInts;   // ints per plane per strip
-        w.pI = PLANES ? P.pI + strip_planes : nullptr;
-        w.pD = PLANES ? P.pD + strip_planes : nullptr;
-        w.pS = PLANES ? P.pS + strip_planes : nullptr;
+        // compact planes (mode 3): the same element offsets, in bytes
+        auto at = [&](int32_t* b) { return PLANES == 3 ? (int32_t*)((uint8_t*)b + strip_planes) : b + strip_planes; };
+        w.pI = PLANES ? at(P.pI) : nullptr;
+        w.pD = PLANES ? at(P.pD) : nullptr;
+        w.pS = PLANES ? at(P.pS) : nullptr;
         w.pL = LCSP ? P.pL + strip_planes : nullptr;
         w.codes = CODES ? P.codes + (size_t)s * P.t16 * kWave * kRowsPerLane : nullptr;
     }
@@ -605,8 +661,8 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     const int strip_base = P.strip_base;
 
     LaneState st;
-    init_row(st.a, ia, ok_a, sc);
-    init_row(st.b, ia + 1, ok_b, sc);
+    init_row(st.a, ia, ok_a, sc, PLANES == 3);
+    init_row(st.b, ia + 1, ok_b, sc, PLANES == 3);
     st.c2c = 0;
     st.b.SMtl = st.a.SM;                          // (A, 0) is row B's top-left for column 1
     // landing columns of column 0: the path reaches column 0 at its own local row
@@ -1261,7 +1317,8 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
     }
 }
 
-template <int W, bool LOCAL, bool PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL, int LAY>
+// PLANES: 0 none, 1 int32 planes, 2 compact byte planes (layout 0 only)
+template <int W, bool LOCAL, int PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL, int LAY>
 __global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAVES_TRACK : (W + 1 + 3) / 4) void fill_kernel(
     const PairDev* __restrict__ pairs, const int npairs, const int total_bands, int* band_counter, StripRes* sres,
     PairRes* pres, const Scores32 sc) {
@@ -1292,8 +1349,8 @@ __global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAV
                 const bool has_consumer = last_in_band ? (lb + 1 < P.bands) : (s + 1 < P.strips);
                 // plane stores pipelined one group late, except in 16-wave
                 // workgroups (128 VGPRs: no room for a group of pending cells)
-                if (LAY == 0)
-                    compute_wave<LOCAL, PLANES ? ((W + 1) <= 12 ? 2 : 1) : 0, CODES, TRACK, LCSP, TBL>(
+                if constexpr (LAY == 0)
+                    compute_wave<LOCAL, PLANES == 2 ? 3 : PLANES ? ((W + 1) <= 12 ? 2 : 1) : 0, CODES, TRACK, LCSP, TBL>(
                         P, s, lane, sc, rings[wave], rings[wave + 1], (lds_int*)&wcnt[wave], (lds_int*)&rcnt[wave],
                         (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1], has_consumer, sres, pres + p,
                         band_counter + 1, lds_addr(push_scratch[wave]));
@@ -1567,25 +1624,48 @@ __global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __rest
     out[(size_t)i * (m + 1) + j] = plane[o];
 }
 
+// Export of a compact (mode 3) plane: one thread per row rebuilds
+// I(i, j) = (D0 + h) + sum_{j' <= j} x_I(i, j') and, for the delete or sub
+// plane, adds that plane's x (gx_kernels.hip put_byte).  Global mode only.
+__global__ void export_d8_kernel(const uint8_t* __restrict__ pI, const uint8_t* __restrict__ px,
+                                 int32_t* __restrict__ out, int n, int m, int t4, int h, int g) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
+    if (i > n) return;
+    const int s = (i - 1) / kStripRows, rho = (i - 1) % kStripRows;
+    const int l = rho >> 1, hh = rho & 1;
+    const size_t row0 = (size_t)s * t4 * kGroupInts + hh * kWave * 4 + l * 4;
+    int I = h + i * g + h;
+    int32_t* o = out + (size_t)i * (m + 1);
+    for (int j = 1; j <= m; ++j) {
+        const int t = j - 1 + l;
+        const size_t off = row0 + (size_t)(t >> 2) * kGroupInts + (t & 3);
+        I += (int8_t)pI[off];
+        o[j] = px ? I + (int8_t)px[off] : I;
+    }
+}
+
 }  // namespace gx
 
 // ---- explicit launch wrappers (C++ linkage, used by gx_api.cpp) ----
 namespace gx {
 
-template <int W, bool LOCAL, bool PLANES, bool TRACK, bool LCSP, bool TBL>
+template <int W, bool LOCAL, int PLANES, bool TRACK, bool LCSP, bool TBL>
 static hipError_t launch_fill_t(int lay, const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
                                 StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
-    if (lay == 0)
+    if (lay == 0) {
         hipLaunchKernelGGL((fill_kernel<W, LOCAL, PLANES, true, TRACK, LCSP, TBL, 0>), dim3(grid), dim3((W + 1) * kWave),
                            0, st, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc);
-    else
-        hipLaunchKernelGGL((fill_kernel<W, LOCAL, PLANES, true, TRACK, LCSP, TBL, 1>), dim3(grid), dim3((W + 1) * kWave),
-                           0, st, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc);
+    } else {
+        if constexpr (PLANES == 2) return hipErrorInvalidValue;   // compact planes: layout 0 only
+        else
+            hipLaunchKernelGGL((fill_kernel<W, LOCAL, PLANES, true, TRACK, LCSP, TBL, 1>), dim3(grid),
+                               dim3((W + 1) * kWave), 0, st, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc);
+    }
     return hipGetLastError();
 }
 
 // Launch with the band width W from the variant's width list (gx_internal.h).
-template <bool LO, bool PL, bool TR, bool LC, bool TB, int W0, int... Ws>
+template <bool LO, int PL, bool TR, bool LC, bool TB, int W0, int... Ws>
 static hipError_t launch_fill_w(int W, int lay, const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
                                 StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
     if (W == W0)
@@ -1602,7 +1682,7 @@ static hipError_t launch_fill_w(int W, int lay, const PairDev* d_pairs, int npai
 // untracked global variants (the batch path) come in every width of kFillWidths
 // and with the small-alphabet score table (tbl) or the byte compare,
 // the tracked and local ones (256-VGPR builds) in kFillWidthsTrack.
-hipError_t launch_fill(int W, int lay, bool local, bool planes, bool track, bool lcs, bool tbl, const PairDev* d_pairs,
+hipError_t launch_fill(int W, int lay, bool local, int planes, bool track, bool lcs, bool tbl, const PairDev* d_pairs,
                        int npairs, int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc,
                        int grid, hipStream_t st) {
 #define GX_FILL_CASE(LO, PL, TR, LC, TB, ...)                                                                \
@@ -1611,20 +1691,22 @@ hipError_t launch_fill(int W, int lay, bool local, bool planes, bool track, bool
                                                               d_pres, sc, grid, st);
 #define GX_W_ALL 3, 4, 6, 8, 11, 15
 #define GX_W_TRACK 3, 7
-    GX_FILL_CASE(false, false, false, false, false, GX_W_ALL)
-    GX_FILL_CASE(false, false, false, false, true, GX_W_ALL)
-    GX_FILL_CASE(false, false, true, false, false, GX_W_TRACK)
-    GX_FILL_CASE(false, true, false, false, false, GX_W_ALL)
-    GX_FILL_CASE(false, true, false, false, true, GX_W_ALL)
-    GX_FILL_CASE(false, true, true, false, false, GX_W_TRACK)
-    GX_FILL_CASE(false, true, true, true, false, GX_W_TRACK)
-    GX_FILL_CASE(true, false, false, false, false, GX_W_TRACK)
-    GX_FILL_CASE(true, false, false, false, true, GX_W_TRACK)
-    GX_FILL_CASE(true, false, true, false, false, GX_W_TRACK)
-    GX_FILL_CASE(true, true, false, false, false, GX_W_TRACK)
-    GX_FILL_CASE(true, true, false, false, true, GX_W_TRACK)
-    GX_FILL_CASE(true, true, true, false, false, GX_W_TRACK)
-    GX_FILL_CASE(true, true, true, true, false, GX_W_TRACK)
+    GX_FILL_CASE(false, 0, false, false, false, GX_W_ALL)
+    GX_FILL_CASE(false, 0, false, false, true, GX_W_ALL)
+    GX_FILL_CASE(false, 0, true, false, false, GX_W_TRACK)
+    GX_FILL_CASE(false, 1, false, false, false, GX_W_ALL)
+    GX_FILL_CASE(false, 1, false, false, true, GX_W_ALL)
+    GX_FILL_CASE(false, 2, false, false, false, GX_W_ALL)   // compact planes (layout 0)
+    GX_FILL_CASE(false, 2, false, false, true, GX_W_ALL)
+    GX_FILL_CASE(false, 1, true, false, false, GX_W_TRACK)
+    GX_FILL_CASE(false, 1, true, true, false, GX_W_TRACK)
+    GX_FILL_CASE(true, 0, false, false, false, GX_W_TRACK)
+    GX_FILL_CASE(true, 0, false, false, true, GX_W_TRACK)
+    GX_FILL_CASE(true, 0, true, false, false, GX_W_TRACK)
+    GX_FILL_CASE(true, 1, false, false, false, GX_W_TRACK)
+    GX_FILL_CASE(true, 1, false, false, true, GX_W_TRACK)
+    GX_FILL_CASE(true, 1, true, false, false, GX_W_TRACK)
+    GX_FILL_CASE(true, 1, true, true, false, GX_W_TRACK)
 #undef GX_FILL_CASE
     return hipErrorInvalidValue;
 }
@@ -1640,6 +1722,13 @@ hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipS
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(tb_strip_kernel, dim3(max_strips, njobs), dim3(64), 0, st, d_jobs);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, int n, int m, int t4, int h, int g,
+                            hipStream_t st) {
+    if (n == 0 || m == 0) return hipSuccess;
+    hipLaunchKernelGGL(export_d8_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, pI, px, out, n, m, t4, h, g);
     return hipGetLastError();
 }
 

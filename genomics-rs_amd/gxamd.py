@@ -70,7 +70,7 @@ STEP_DTYPE = np.dtype([("choice", "u1"), ("pad", "u1", (7,)), ("i", "<u8"), ("j"
 EXPORTED = ["gx_last_error", "gx_version", "gx_context_create", "gx_context_destroy", "gx_context_trim",
             "gx_alignment_table", "gx_table_info", "gx_table_export", "gx_table_export_plane", "gx_retrace",
             "gx_table_free", "gx_align", "gx_align_batch", "gx_stage_pairs", "gx_run_staged", "gx_run_staged_steps",
-            "gx_fasta_load",
+            "gx_fill_info", "gx_plane_bytes_per_cell", "gx_fasta_load",
             "gx_config_load", "gx_format_alignment", "gx_format_table"]
 
 _lib = None
@@ -108,6 +108,8 @@ def lib():
                                 ctypes.POINTER(ctypes.c_double)]
     L.gx_run_staged_steps.argtypes = [vp, ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
                                       ctypes.c_int, vp, ctypes.POINTER(ctypes.c_double)]
+    L.gx_fill_info.argtypes = [vp] + [ctypes.POINTER(ctypes.c_int)] * 3
+    L.gx_plane_bytes_per_cell.argtypes = [ctypes.POINTER(CScores), ctypes.c_int]
     L.gx_fasta_load.argtypes = [ctypes.c_char_p, vp, sz, vp, vp, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.gx_config_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(CScores)]
     L.gx_format_alignment.argtypes = [vp, sz, vp, sz, vp, sz, ctypes.POINTER(CResult), vp, sz, ctypes.POINTER(sz)]
@@ -263,6 +265,15 @@ def _steps_array(alignment) -> np.ndarray:
     return arr
 
 
+def plane_bytes_per_cell(scores: "Scores", is_local: bool) -> int:
+    """Score-plane bytes per cell of a batch launch with these scores: 3
+    (compact byte differences) or 12 (int32 planes); gx_plane_bytes_per_cell."""
+    r = lib().gx_plane_bytes_per_cell(ctypes.byref(scores.c()), int(is_local))
+    if r < 0:
+        raise GxError(3, "invalid scores")
+    return r
+
+
 class Context:
     """One GPU: device-memory cache and stream (gx_context)."""
 
@@ -279,6 +290,12 @@ class Context:
 
     def trim(self):
         _check(lib().gx_context_trim(self.ptr))
+
+    def fill_info(self) -> dict:
+        """The last fill launch: layout, band width, score-plane bytes per cell (gx_fill_info)."""
+        v = [ctypes.c_int() for _ in range(3)]
+        _check(lib().gx_fill_info(self.ptr, *[ctypes.byref(x) for x in v]))
+        return {"layout": v[0].value, "band_waves": v[1].value, "plane_bytes_per_cell": v[2].value}
 
     def __del__(self):
         try:
@@ -352,8 +369,12 @@ def _first_two(sc: SequenceContainer) -> Tuple[Sequence, Sequence]:
 
 def alignment_table(sequence_container: SequenceContainer, scores: Scores, is_local: bool,
                     reverse_sequences: bool, flags: int = GX_TABLE_PLANES,
-                    ctx: Optional[Context] = None) -> Tuple[AlignmentTable, int]:
-    """alignment_table (algo.rs:151-282) on the GPU -> (table, matches_at_max)."""
+                    ctx: Optional[Context] = None, max_cell: bool = True) -> Tuple[AlignmentTable, int]:
+    """alignment_table (algo.rs:151-282) on the GPU -> (table, matches_at_max).
+
+    max_cell=False skips the running max cell and matches_at_max (returned as
+    0): the untracked fill, whose global score planes are kept in the compact
+    byte format (gx_api.cpp d8_planes_ok) when the table is built on layout 0."""
     a, b = _first_two(sequence_container)
     s1, s2 = a.sequence.encode(), b.sequence.encode()
     ctx = ctx or default_context()
@@ -362,7 +383,8 @@ def alignment_table(sequence_container: SequenceContainer, scores: Scores, is_lo
     t = ctypes.c_void_p()
     mam = ctypes.c_uint64()
     _check(lib().gx_alignment_table(ctx.ptr, px, len(s1), py, len(s2), ctypes.byref(scores.c()), int(is_local),
-                                    int(reverse_sequences), flags, ctypes.byref(t), ctypes.byref(mam)))
+                                    int(reverse_sequences), flags, ctypes.byref(t),
+                                    ctypes.byref(mam) if max_cell else None))
     return AlignmentTable(t, s1, s2, flags), int(mam.value)
 
 

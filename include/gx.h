@@ -168,6 +168,17 @@ int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_local, int ke
  * device).  out = the last pass's results; *fill_ms_out = mean fill time. */
 int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes, uint32_t flags,
                         int nsteps, gx_result* out, double* fill_ms_out);
+/* The last fill launch on ctx: its layout (0: anti-diagonal 128-row strips,
+ * 1: column step over 64-row strips), band width (strips per workgroup) and
+ * score-plane bytes written per cell (0: none, 12: int32 planes, 3: compact
+ * planes -- per-cell byte differences, decoded exactly by the exports).  No
+ * reference counterpart (measurement only). */
+int gx_fill_info(const gx_context* ctx, int* layout, int* band_waves, int* plane_bytes_per_cell);
+/* Score-plane bytes per cell a batch launch (layout 0, no max tracking)
+ * writes with these scores: 3 when the compact format's range proof holds
+ * (global mode, g, h <= 0, differences within a signed byte), else 12; -1 on
+ * invalid scores. */
+int gx_plane_bytes_per_cell(const gx_scores* scores, int is_local);
 
 /* ---- sequence.rs / config.rs mirrors ----------------------------------- */
 /* from_fasta (sequence.rs:45-95) on a file: records are appended to the

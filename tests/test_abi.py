@@ -195,3 +195,26 @@ def test_alignment_table_print_matches_restatement(gx, oracle, is_local):
             assert gx.format_alignment_table(a, planes, color) == want
     big = gx.AlignedSequences(gx.Sequence("s1", "A" * 200), gx.Sequence("s2", "A"), [], 0, 0, 0, 0, 0)
     assert gx.format_alignment_table(big, [None] * 3) == ""
+
+
+def _d8_rule(sm, smm, g, h, local):
+    """Independent restatement of the compact-plane range proof."""
+    if local or g > 0 or h > 0:
+        return 12
+    a = g + h
+    U = max(0, max(sm, smm) - a)
+    lo = min(g, min(sm, smm) - U, 2 * a - U)
+    hi = max(U - a, max(sm, smm) - 2 * a, U - 2 * a)
+    return 3 if lo >= -128 and hi <= 127 else 12
+
+
+@pytest.mark.parametrize("scores", [(1, -2, -1, -5), (1, -2, -2, -5), (2, -3, -2, -4), (5, -4, 0, -10),
+                                    (10, -10, -5, -20), (1, -1, 0, 0), (30, -30, -10, -40), (3, 1, -1, -2),
+                                    (40, -1, -1, -1), (20, -20, -10, -25), (1, -2, 1, -5)])
+@pytest.mark.parametrize("local", [False, True])
+def test_plane_bytes_per_cell(gx, scores, local, monkeypatch):
+    """Host-only: which score-plane format a batch launch picks (no GPU call)."""
+    monkeypatch.delenv("GX_PLANES32", raising=False)
+    assert gx.plane_bytes_per_cell(gx.Scores(*scores), local) == _d8_rule(*scores, local)
+    monkeypatch.setenv("GX_PLANES32", "1")
+    assert gx.plane_bytes_per_cell(gx.Scores(*scores), local) == 12
