@@ -173,7 +173,15 @@ struct WorkPool {
             stop = true;
         }
         cv.notify_all();
-        for (auto& t : th) t.join();
+        // a context destroyed during interpreter teardown may find its workers
+        // already gone: never let a failed join terminate the process
+        for (auto& t : th) {
+            try {
+                if (t.joinable()) t.join();
+            } catch (...) {
+                if (t.joinable()) t.detach();
+            }
+        }
     }
 };
 

@@ -153,6 +153,10 @@ __device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 // workgroup's waves per SIMD.  The variants that also track the maxima
 // (first max + LCS, local mode) carry more state per row and get 256 VGPRs
 // (8-wave workgroups at most).
+#ifndef GX_D8_PIPE
+#define GX_D8_PIPE 0   // 1: compact plane stores issued during the next group (9..12-wave
+                       // workgroups); measured 2 % slower than storing at the group end
+#endif
 #ifndef GX_FILL_MIN_WAVES_TRACK
 #define GX_FILL_MIN_WAVES_TRACK 2
 #endif
@@ -449,6 +453,7 @@ struct WaveCtx {
 // bytes = 0 (nothing pending) empties the descriptor's range.
 struct PendStore {
     int4 I0, I1, D0, D1, S0, S1, L0, L1;   // rows A/B of each plane
+    uint32_t xI0, xI1, xS0, xS1, xD0, xD1; // compact planes (mode 4): rows A/B, one dword each
     size_t sb_off;                         // the group's sub-block (ints)
     int bytes;
 };
@@ -462,6 +467,16 @@ __device__ __forceinline__ void pend_store(const PendStore& pd, const WaveCtx& w
     const auto r = rsrc_of(base + pd.sb_off, pd.bytes);
     bstore4(r, v0, PLANE == 0 ? pd.I0 : PLANE == 1 ? pd.D0 : PLANE == 2 ? pd.S0 : pd.L0);
     bstore4(r, v1, PLANE == 0 ? pd.I1 : PLANE == 1 ? pd.D1 : PLANE == 2 ? pd.S1 : pd.L1);
+}
+
+// Compact planes, pipelined (mode 4): the previous group's dwords of one plane.
+template <int PLANE, int G4P>
+__device__ __forceinline__ void pend_store_d8(const PendStore& pd, const WaveCtx& w) {
+    const uint32_t v0 = (uint32_t)w.lane * 4u + G4P * kGroupInts, v1 = v0 + kWave * 4;
+    const int32_t* base = PLANE == 0 ? w.pI : PLANE == 1 ? w.pS : w.pD;
+    const auto r = rsrc_of((const uint8_t*)base + pd.sb_off, pd.bytes);
+    bstore1(r, v0, PLANE == 0 ? pd.xI0 : PLANE == 1 ? pd.xS0 : pd.xD0);
+    bstore1(r, v1, PLANE == 0 ? pd.xI1 : PLANE == 1 ? pd.xS1 : pd.xD1);
 }
 
 // One 4-step group of a sub-block.  `nxt` holds validated ring records for
@@ -495,14 +510,17 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
         dp_step<LOCAL, true, CODES, TRACK, TBL>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
         skel_store(w.skel_rsrc, sko(col0 + 1), st.b.E);   // lane 63's column after the step
         if (PLANES == 2) pend_store<LCSP, 0, G4P>(pend, w);
+        if (PLANES == 4) pend_store_d8<0, G4P>(pend, w);
         push63<4 * G4 + 1, TRACK>(out_base, st, lane63_mask(push_on && col0 + 1 >= 0 && col0 + 1 <= w.m));
         dp_step<LOCAL, true, CODES, TRACK, TBL>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
         skel_store(w.skel_rsrc, sko(col0 + 2), st.b.E);   // lane 63's column after the step
         if (PLANES == 2) pend_store<LCSP, 1, G4P>(pend, w);
+        if (PLANES == 4) pend_store_d8<1, G4P>(pend, w);
         push63<4 * G4 + 2, TRACK>(out_base, st, lane63_mask(push_on && col0 + 2 >= 0 && col0 + 2 <= w.m));
         dp_step<LOCAL, true, CODES, TRACK, TBL>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
         skel_store(w.skel_rsrc, sko(col0 + 3), st.b.E);   // lane 63's column after the step
         if (PLANES == 2) pend_store<LCSP, 2, G4P>(pend, w);
+        if (PLANES == 4) pend_store_d8<2, G4P>(pend, w);
         if (PLANES == 2 && LCSP) pend_store<LCSP, 3, G4P>(pend, w);
         push63<4 * G4 + 3, TRACK>(out_base, st, lane63_mask(push_on && col0 + 3 >= 0 && col0 + 3 <= w.m));
         // publish the pushes (same wave, DS operations in order)
@@ -515,14 +533,17 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
         push_all<4 * G4 + 0, TRACK>(pa, st);
         dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
         if (PLANES == 2) pend_store<LCSP, 0, G4P>(pend, w);
+        if (PLANES == 4) pend_store_d8<0, G4P>(pend, w);
         const int e0 = st.b.E;              // lane 63: column col0 + 1
         push_all<4 * G4 + 1, TRACK>(pa, st);
         dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
         if (PLANES == 2) pend_store<LCSP, 1, G4P>(pend, w);
+        if (PLANES == 4) pend_store_d8<1, G4P>(pend, w);
         const int e1 = st.b.E;
         push_all<4 * G4 + 2, TRACK>(pa, st);
         dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
         if (PLANES == 2) pend_store<LCSP, 2, G4P>(pend, w);
+        if (PLANES == 4) pend_store_d8<2, G4P>(pend, w);
         if (PLANES == 2 && LCSP) pend_store<LCSP, 3, G4P>(pend, w);
         const int e2 = st.b.E;
         push_all<4 * G4 + 3, TRACK>(pa, st);
@@ -551,9 +572,10 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
             bstore4(rL, v1, make_int4(bL[0][1], bL[1][1], bL[2][1], bL[3][1]));
         }
     }
-    if (PLANES == 3) {
+    if (PLANES == 3 || PLANES == 4) {
         // compact planes: this group's 4 steps of a row are one dword per lane
-        // and plane (x_I, x_S, x_D above put_byte), stored now (256 B per wave)
+        // and plane (x_I, x_S, x_D above put_byte), 256 B per wave; mode 3
+        // stores them now, mode 4 during the next group
         uint32_t xI[2], xS[2], xD[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -568,8 +590,14 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
         const auto rI = rsrc_of((const uint8_t*)w.pI + sb_off, kSubBytes),
                    rD = rsrc_of((const uint8_t*)w.pD + sb_off, kSubBytes),
                    rS = rsrc_of((const uint8_t*)w.pS + sb_off, kSubBytes);
-        bstore1(rI, v0, xI[0]); bstore1(rS, v0, xS[0]); bstore1(rD, v0, xD[0]);
-        bstore1(rI, v1, xI[1]); bstore1(rS, v1, xS[1]); bstore1(rD, v1, xD[1]);
+        if (PLANES == 3) {
+            bstore1(rI, v0, xI[0]); bstore1(rS, v0, xS[0]); bstore1(rD, v0, xD[0]);
+            bstore1(rI, v1, xI[1]); bstore1(rS, v1, xS[1]); bstore1(rD, v1, xD[1]);
+        } else {
+            pend.xI0 = xI[0]; pend.xI1 = xI[1]; pend.xS0 = xS[0]; pend.xS1 = xS[1]; pend.xD0 = xD[0]; pend.xD1 = xD[1];
+            pend.sb_off = sb_off;
+            pend.bytes = kSubBytes;
+        }
     }
     if (PLANES == 2) {
         // this group's cells: 16 B per lane per row and plane, stored during the next group
@@ -638,7 +666,7 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     {
         const size_t strip_planes = (size_t)s * P.t4 * kGroupInts;   // ints per plane per strip
         // compact planes (mode 3): the same element offsets, in bytes
-        auto at = [&](int32_t* b) { return PLANES == 3 ? (int32_t*)((uint8_t*)b + strip_planes) : b + strip_planes; };
+        auto at = [&](int32_t* b) { return PLANES >= 3 ? (int32_t*)((uint8_t*)b + strip_planes) : b + strip_planes; };
         w.pI = PLANES ? at(P.pI) : nullptr;
         w.pD = PLANES ? at(P.pD) : nullptr;
         w.pS = PLANES ? at(P.pS) : nullptr;
@@ -661,8 +689,8 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     const int strip_base = P.strip_base;
 
     LaneState st;
-    init_row(st.a, ia, ok_a, sc, PLANES == 3);
-    init_row(st.b, ia + 1, ok_b, sc, PLANES == 3);
+    init_row(st.a, ia, ok_a, sc, PLANES >= 3);
+    init_row(st.b, ia + 1, ok_b, sc, PLANES >= 3);
     st.c2c = 0;
     st.b.SMtl = st.a.SM;                          // (A, 0) is row B's top-left for column 1
     // landing columns of column 0: the path reaches column 0 at its own local row
@@ -727,6 +755,11 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
     }
 
+    if (PLANES == 4) {   // the last group's compact planes
+        pend_store_d8<0, 3>(pend, w);
+        pend_store_d8<1, 3>(pend, w);
+        pend_store_d8<2, 3>(pend, w);
+    }
     if (PLANES == 2) {   // the last group's planes (group 3 of the last sub-block)
         pend_store<LCSP, 0, 3>(pend, w);
         pend_store<LCSP, 1, 3>(pend, w);
@@ -1317,7 +1350,9 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
     }
 }
 
-// PLANES: 0 none, 1 int32 planes, 2 compact byte planes (layout 0 only)
+// PLANES: 0 none, 1 int32 planes, 2 compact byte planes (layout 0 only).  compute_wave
+// plane modes: 0 none, 1/2 int32 stored now / during the next group, 3/4 compact
+// (byte) stored now / during the next group
 template <int W, bool LOCAL, int PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL, int LAY>
 __global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAVES_TRACK : (W + 1 + 3) / 4) void fill_kernel(
     const PairDev* __restrict__ pairs, const int npairs, const int total_bands, int* band_counter, StripRes* sres,
@@ -1350,7 +1385,7 @@ __global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAV
                 // plane stores pipelined one group late, except in 16-wave
                 // workgroups (128 VGPRs: no room for a group of pending cells)
                 if constexpr (LAY == 0)
-                    compute_wave<LOCAL, PLANES == 2 ? 3 : PLANES ? ((W + 1) <= 12 ? 2 : 1) : 0, CODES, TRACK, LCSP, TBL>(
+                    compute_wave<LOCAL, PLANES == 2 ? (GX_D8_PIPE && (W + 1) <= 12 ? 4 : 3) : PLANES ? ((W + 1) <= 12 ? 2 : 1) : 0, CODES, TRACK, LCSP, TBL>(
                         P, s, lane, sc, rings[wave], rings[wave + 1], (lds_int*)&wcnt[wave], (lds_int*)&rcnt[wave],
                         (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1], has_consumer, sres, pres + p,
                         band_counter + 1, lds_addr(push_scratch[wave]));
