@@ -139,6 +139,27 @@ def load_traffic(workload: str):
     return None, None
 
 
+def load_valu(workload: str):
+    """VALU issue profile of this workload's fill (profiles/valu_fill_*.json,
+    made by tools/gpu_valu.sh + tools/valu_summary.py): the compute-side
+    bound once the planes no longer saturate HBM."""
+    d = os.path.join(ROOT, "profiles")
+    for name in sorted(os.listdir(d), reverse=True) if os.path.isdir(d) else []:
+        if name.startswith("valu_fill") and name.endswith(".json"):
+            try:
+                with open(os.path.join(d, name)) as f:
+                    v = json.load(f)
+                for case in ("planes", "noplanes"):
+                    if v.get(case, {}).get("workload") == workload:
+                        c = v[case]
+                        return {"valu_insts_per_cell": c["valu_insts_per_cell"],
+                                "valu_issue_frac": c["valu_issue_frac"], "clock_ghz": c["clock_ghz"],
+                                "source": name}
+            except Exception:
+                continue
+    return None
+
+
 def fasta_pair(gx, which: str):
     """BASELINE configs 2 and 3: the reference's own FASTA pairs (copied under
     tests/golden), loaded with the from_fasta mirror."""
@@ -342,6 +363,7 @@ def main():
                      "algorithmic_bytes_per_cell": bytes_per_cell,
                      "algorithmic_bytes_per_launch": fill_bytes},
         "fill_launch": finfo,
+        "valu": load_valu(workload),
         "fill_gcups_per_gpu": round(cells_rank / (avg_fill_ms * 1e-3) / 1e9, 3),
         "traceback_us_pair0": int(np.mean(tb_us)),
     }

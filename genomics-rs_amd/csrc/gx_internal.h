@@ -23,7 +23,10 @@ namespace gx {
 
 constexpr int kWave = 64;
 constexpr int kNeg = -(1 << 30);   // int32 stand-in for negative_inf (algo.rs:166)
-constexpr int kRing = 256;         // LDS ring records per strip boundary (power of two)
+#ifndef GX_RING
+#define GX_RING 256
+#endif
+constexpr int kRing = GX_RING;     // LDS ring records per strip boundary (power of two)
 constexpr int kSub = 16;           // steps per flow-control sub-block (multiple of 16)
 constexpr int kIoChunk = 16;       // columns per I/O-wave transfer (layout 0)
 constexpr int kIoChunk1 = 4;       // columns per I/O-wave transfer (layout 1)
