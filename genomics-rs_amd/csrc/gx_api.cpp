@@ -35,7 +35,7 @@ hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d
 hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipStream_t st);
 hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, hipStream_t st);
 hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, int n, int m, int t4, int h, int g,
-                            hipStream_t st);
+                            int floor_, hipStream_t st);
 }  // namespace gx
 
 using namespace gx;
@@ -464,7 +464,7 @@ static int fill_band_waves(bool track, int total_strips, int grid_cap, int lay) 
     return lay ? pick_width(kWidths1, total_strips, grid_cap) : pick_width(kFillWidths, total_strips, grid_cap);
 }
 
-// Compact score planes (layout 0, global, untracked: the batch path).  The
+// Compact score planes (layout 0, untracked: the batch path).  The
 // fill stores per cell one signed byte each of x_I = I(i,j) - I(i,j-1),
 // x_S = S(i,j) - I(i,j), x_D = D(i,j) - I(i,j) (gx_kernels.hip put_byte), 3 B
 // instead of 12.  With g, h <= 0, a = h + g, smax/smin the larger/smaller of
@@ -473,10 +473,13 @@ static int fill_band_waves(bool track, int total_strips, int grid_cap, int lay) 
 //     a <= H(i,j) - H(i,j-1) <= U   (and the same down a column),
 //     H(i,j-1) + a <= I(i,j) <= H(i,j-1),   H(i-1,j) + a <= D(i,j) <= H(i-1,j),
 // so  x_I in [g, U - a],  x_S in [smin - U, smax - 2a],  x_D in [2a - U, U - 2a].
-// Compact planes are used when those ranges fit a signed byte (the default
-// scores give [-1, 13], [-9, 13], [-19, 19]); GX_PLANES32 forces int32 planes.
+// The same holds in local mode (the 0 floor of I, D and H keeps every
+// inequality; the row base is H(i, 0) + h = h).  Compact planes are used when
+// those ranges fit a signed byte (the default scores give [-1, 13], [-9, 13],
+// [-19, 19]); GX_PLANES32 forces int32 planes.
 static bool d8_planes_ok(const Scores32& sc, int is_local) {
-    if (is_local || sc.g > 0 || sc.h > 0 || getenv("GX_PLANES32")) return false;
+    (void)is_local;
+    if (sc.g > 0 || sc.h > 0 || getenv("GX_PLANES32")) return false;
     const long long g = sc.g, a = (long long)sc.h + sc.g;
     const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
     const long long U = std::max(0LL, smax - a);
@@ -1081,7 +1084,7 @@ static int fetch_plane32(const gx_table* t, int which, std::vector<int32_t>& out
     hipError_t e;
     if (t->job.d8)   // compact planes: rebuilt from the insert plane's running sum (+ this plane's x)
         e = launch_export_d8((const uint8_t*)d.pI, which == 0 ? nullptr : (const uint8_t*)src, (int32_t*)tmp.p,
-                             (int)n, (int)m, d.t4, t->sc.h, t->sc.g, ctx->stream);
+                             (int)n, (int)m, d.t4, t->sc.h, t->sc.g, t->sc.floor_, ctx->stream);
     else
         e = launch_export(src, (int32_t*)tmp.p, (int)n, (int)m, d.t4, t->job.lay, ctx->stream);
     if (e == hipSuccess)

@@ -638,10 +638,11 @@ __device__ __forceinline__ void init_row(RowState& rs, const int i, const bool r
                                          const bool d8 = false) {
     // cell (i, 0): algo.rs:204-211
     const int D0 = sc.h + i * sc.g;
-    // compact planes (global): I(i, 0) = negative_inf is replaced by D0 + h, which
-    // gives column 1 the same insert score, max(I + g, max(S, D) + h + g) =
-    // D0 + h + g, and x_I(i, 1) = g (the decoder's row base is D0 + h)
-    rs.I = d8 ? D0 + sc.h : kNeg;
+    // compact planes: I(i, 0) = negative_inf is replaced by H(i, 0) + h
+    // (H(i, 0) = max(D0, floor)), which gives column 1 the same insert score,
+    // max(I + g, max(S, D) + h + g [, 0]) = max(H(i, 0) + h + g [, 0]); the
+    // decoder's row base is the same H(i, 0) + h
+    rs.I = d8 ? max(D0, sc.floor_) + sc.h : kNeg;
     rs.SD = D0;                                   // max(sub=neg_inf, delete)
     rs.SM = max(D0, sc.floor_);
     rs.Dd = max3i(kNeg + sc.hg, D0 + sc.g, sc.floor_);
@@ -1661,15 +1662,15 @@ __global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __rest
 
 // Export of a compact (mode 3) plane: one thread per row rebuilds
 // I(i, j) = (D0 + h) + sum_{j' <= j} x_I(i, j') and, for the delete or sub
-// plane, adds that plane's x (gx_kernels.hip put_byte).  Global mode only.
+// plane, adds that plane's x (gx_kernels.hip put_byte).
 __global__ void export_d8_kernel(const uint8_t* __restrict__ pI, const uint8_t* __restrict__ px,
-                                 int32_t* __restrict__ out, int n, int m, int t4, int h, int g) {
+                                 int32_t* __restrict__ out, int n, int m, int t4, int h, int g, int floor_) {
     const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
     if (i > n) return;
     const int s = (i - 1) / kStripRows, rho = (i - 1) % kStripRows;
     const int l = rho >> 1, hh = rho & 1;
     const size_t row0 = (size_t)s * t4 * kGroupInts + hh * kWave * 4 + l * 4;
-    int I = h + i * g + h;
+    int I = max(h + i * g, floor_) + h;   // H(i, 0) + h, as the fill seeds it
     int32_t* o = out + (size_t)i * (m + 1);
     for (int j = 1; j <= m; ++j) {
         const int t = j - 1 + l;
@@ -1740,6 +1741,8 @@ hipError_t launch_fill(int W, int lay, bool local, int planes, bool track, bool 
     GX_FILL_CASE(true, 0, true, false, false, GX_W_TRACK)
     GX_FILL_CASE(true, 1, false, false, false, GX_W_TRACK)
     GX_FILL_CASE(true, 1, false, false, true, GX_W_TRACK)
+    GX_FILL_CASE(true, 2, false, false, false, GX_W_TRACK)   // compact planes, local (layout 0)
+    GX_FILL_CASE(true, 2, false, false, true, GX_W_TRACK)
     GX_FILL_CASE(true, 1, true, false, false, GX_W_TRACK)
     GX_FILL_CASE(true, 1, true, true, false, GX_W_TRACK)
 #undef GX_FILL_CASE
@@ -1761,9 +1764,10 @@ hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipS
 }
 
 hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, int n, int m, int t4, int h, int g,
-                            hipStream_t st) {
+                            int floor_, hipStream_t st) {
     if (n == 0 || m == 0) return hipSuccess;
-    hipLaunchKernelGGL(export_d8_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, pI, px, out, n, m, t4, h, g);
+    hipLaunchKernelGGL(export_d8_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, pI, px, out, n, m, t4, h, g,
+                       floor_);
     return hipGetLastError();
 }
 

@@ -373,7 +373,7 @@ def alignment_table(sequence_container: SequenceContainer, scores: Scores, is_lo
     """alignment_table (algo.rs:151-282) on the GPU -> (table, matches_at_max).
 
     max_cell=False skips the running max cell and matches_at_max (returned as
-    0): the untracked fill, whose global score planes are kept in the compact
+    0): the untracked fill, whose score planes are kept in the compact
     byte format (gx_api.cpp d8_planes_ok) when the table is built on layout 0."""
     a, b = _first_two(sequence_container)
     s1, s2 = a.sequence.encode(), b.sequence.encode()

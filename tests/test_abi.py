@@ -199,7 +199,7 @@ def test_alignment_table_print_matches_restatement(gx, oracle, is_local):
 
 def _d8_rule(sm, smm, g, h, local):
     """Independent restatement of the compact-plane range proof."""
-    if local or g > 0 or h > 0:
+    if g > 0 or h > 0:
         return 12
     a = g + h
     U = max(0, max(sm, smm) - a)

@@ -163,8 +163,9 @@ def test_exported_planes_and_cells(gx, ctx, oracle, n, m, is_local):
 
 @pytest.mark.parametrize("scores", [(1, -2, -1, -5), (1, -2, -2, -5), (2, -3, -2, -4), (5, -4, 0, -10),
                                     (10, -10, -5, -20), (1, -1, 0, 0), (30, -30, -10, -40), (3, 1, -1, -2)])
-def test_untracked_table_planes(gx, ctx, oracle, scores):
-    """Global tables built without the max-cell tracking: on layout 0 their
+@pytest.mark.parametrize("is_local", [False, True], ids=["global", "local"])
+def test_untracked_table_planes(gx, ctx, oracle, scores, is_local):
+    """Tables built without the max-cell tracking: on layout 0 their
     score planes are stored as per-cell byte differences when the scores pass
     the range proof (gx_api.cpp d8_planes_ok; (30, -30, -10, -40) does not and
     (3, 1, -1, -2) has g > 0, both keep int32 planes).  Every exported plane
@@ -175,13 +176,13 @@ def test_untracked_table_planes(gx, ctx, oracle, scores):
         for alpha in (b"ACGT", b"AC", b"A"):
             a = bytes(rng.choice(alpha) for _ in range(n))
             b = bytes(rng.choice(alpha) for _ in range(m))
-            o = oracle.align(a, b, scores, is_local=False, want_planes=True)
+            o = oracle.align(a, b, scores, is_local=is_local, want_planes=True)
             cont = gx.SequenceContainer([gx.Sequence("a", a.decode()), gx.Sequence("b", b.decode())])
-            table, mam = gx.alignment_table(cont, sc(gx, scores), False, False, ctx=ctx, max_cell=False)
+            table, mam = gx.alignment_table(cont, sc(gx, scores), is_local, False, ctx=ctx, max_cell=False)
             assert mam == 0
             for k in range(3):
                 assert np.array_equal(table.plane(k), o.planes[k]), (n, m, alpha, "plane", k)
-            aln = gx.retrace(cont, table, False)
+            aln = gx.retrace(cont, table, is_local)
             assert [(x[0].name, x[1], x[2]) for x in aln.alignment] == o.alignment(), (n, m, alpha)
             assert aln.score == o.score
 
