@@ -148,6 +148,19 @@ __device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 #endif
 }
 
+// Per-strip descriptor store: VGPR offset + SGPR soffset + immediate (a
+// group's offset inside the strip's plane), no descriptor SALU per group.
+__device__ __forceinline__ void bstore1_so(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff, uint32_t imm,
+                                           uint32_t v) {
+#ifndef GX_DIAG_NO_PLANES
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)(voff + imm), soff, GX_PLANE_AUX);
+#endif
+}
+#ifndef GX_D8_STRIPDESC
+#define GX_D8_STRIPDESC 0   // 1: compact planes through one descriptor per strip plane (measured
+                            // 0.8 % slower than one per sub-block, profiles/r01n_d8_desc_ab.txt)
+#endif
+
 // Occupancy floor (waves per SIMD), which sets the fill kernel's VGPR cap
 // (512 / floor, at most 256): one workgroup per CU, so the floor is the
 // workgroup's waves per SIMD.  The variants that also track the maxima
@@ -587,13 +600,22 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
         constexpr int kSubBytes = kSub / 4 * kGroupInts;              // one sub-block of one byte plane
         constexpr uint32_t kG = G4 * kGroupInts;
         const uint32_t v0 = (uint32_t)w.lane * 4u + kG, v1 = v0 + kWave * 4;
-        const auto rI = rsrc_of((const uint8_t*)w.pI + sb_off, kSubBytes),
-                   rD = rsrc_of((const uint8_t*)w.pD + sb_off, kSubBytes),
-                   rS = rsrc_of((const uint8_t*)w.pS + sb_off, kSubBytes);
-        if (PLANES == 3) {
+        if (PLANES == 3 && GX_D8_STRIPDESC) {
+            const int so = __builtin_amdgcn_readfirstlane((int)sb_off);
+            bstore1_so(w.rI, (uint32_t)w.lane * 4u, so, kG, xI[0]);
+            bstore1_so(w.rS, (uint32_t)w.lane * 4u, so, kG, xS[0]);
+            bstore1_so(w.rD, (uint32_t)w.lane * 4u, so, kG, xD[0]);
+            bstore1_so(w.rI, (uint32_t)w.lane * 4u, so, kG + kWave * 4, xI[1]);
+            bstore1_so(w.rS, (uint32_t)w.lane * 4u, so, kG + kWave * 4, xS[1]);
+            bstore1_so(w.rD, (uint32_t)w.lane * 4u, so, kG + kWave * 4, xD[1]);
+        } else if (PLANES == 3) {
+            const auto rI = rsrc_of((const uint8_t*)w.pI + sb_off, kSubBytes),
+                       rD = rsrc_of((const uint8_t*)w.pD + sb_off, kSubBytes),
+                       rS = rsrc_of((const uint8_t*)w.pS + sb_off, kSubBytes);
             bstore1(rI, v0, xI[0]); bstore1(rS, v0, xS[0]); bstore1(rD, v0, xD[0]);
             bstore1(rI, v1, xI[1]); bstore1(rS, v1, xS[1]); bstore1(rD, v1, xD[1]);
         } else {
+            (void)v0; (void)v1;
             pend.xI0 = xI[0]; pend.xI1 = xI[1]; pend.xS0 = xS[0]; pend.xS1 = xS[1]; pend.xD0 = xD[0]; pend.xD1 = xD[1];
             pend.sb_off = sb_off;
             pend.bytes = kSubBytes;
@@ -673,6 +695,14 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         w.pS = PLANES ? at(P.pS) : nullptr;
         w.pL = LCSP ? P.pL + strip_planes : nullptr;
         w.codes = CODES ? P.codes + (size_t)s * P.t16 * kWave * kRowsPerLane : nullptr;
+        if (PLANES == 3 && GX_D8_STRIPDESC) {
+            // compact planes: one descriptor per plane over the strip's whole
+            // plane, built once; a group's offset rides in soffset + imm
+            const int pbytes = P.t4 * kGroupInts;
+            w.rI = rsrc_of(uniform_ptr(w.pI), pbytes);
+            w.rD = rsrc_of(uniform_ptr(w.pD), pbytes);
+            w.rS = rsrc_of(uniform_ptr(w.pS), pbytes);
+        }
     }
     w.ring_in = ring_in; w.ring_out = ring_out; w.wcnt_in = wcnt_in; w.wcnt_out = wcnt_out; w.status = status;
     // skeleton row (only stored when there is a strip below: otherwise an empty range)
