@@ -616,7 +616,27 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     if ((rc = pool_get(ctx, std::max<size_t>(prog_elems, 1) * sizeof(int), &job.progress))) return rc;
     if ((rc = pool_get(ctx, std::max(strips, 1) * sizeof(StripRes), &job.sres))) return rc;
     if ((rc = pool_get(ctx, P * sizeof(PairRes), &job.pres))) return rc;
-    if ((rc = pool_get(ctx, P * sizeof(PairDev), &job.pairs))) return rc;
+    // band queue order, stored after the pair descriptors: band-major ("round"
+    // order: band 0 of every pair, then band 1, ...; a band's predecessor in its
+    // pair is always dequeued before it, so a waiting band is never waiting on
+    // an unstarted one) unless GX_BAND_ORDER=pair (all bands of pair 0 first)
+    std::vector<int> order;
+    order.reserve(2 * (size_t)bands);
+    {
+        const char* bo = getenv("GX_BAND_ORDER");
+        if (bo && !strcmp(bo, "pair")) {
+            for (size_t p = 0; p < P; ++p)
+                for (int lb = 0; lb < job.pd[p].bands; ++lb) { order.push_back((int)p); order.push_back(lb); }
+        } else {
+            int maxb = 0;
+            for (size_t p = 0; p < P; ++p) maxb = std::max(maxb, job.pd[p].bands);
+            for (int lb = 0; lb < maxb; ++lb)
+                for (size_t p = 0; p < P; ++p)
+                    if (lb < job.pd[p].bands) { order.push_back((int)p); order.push_back(lb); }
+        }
+    }
+    const size_t ord_bytes = align_up(order.size() * sizeof(int), 16);   // keeps the PairRes staging 16-B aligned
+    if ((rc = pool_get(ctx, P * sizeof(PairDev) + ord_bytes, &job.pairs))) return rc;
     if ((rc = pool_get(ctx, 64, &job.counter))) return rc;
     // -- chars upload
     const uint8_t* cbase = chars_dev;
@@ -653,11 +673,12 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         for (size_t p = 0; p < P; ++p) job.pd[p].trace = (StripTrace*)trace.p + job.pd[p].strip_base;
     }
     // descriptors in (and results out) through pinned staging, laid out [PairDev x P | PairRes x P | status]
-    const size_t pin_bytes = P * (sizeof(PairDev) + sizeof(PairRes)) + 2 * sizeof(int);
+    const size_t pin_bytes = P * (sizeof(PairDev) + sizeof(PairRes)) + ord_bytes + 2 * sizeof(int);
     char* pin = (char*)(slot >= 0 ? pinned_grow(ctx->slots[slot].fpin, pin_bytes) : io_pinned(ctx, pin_bytes));
     if (!pin) return fail(GX_ENOMEM, "pinned staging buffer");
     memcpy(pin, job.pd.data(), P * sizeof(PairDev));
-    HIPCHK(hipMemcpyAsync(job.pairs.p, pin, P * sizeof(PairDev), hipMemcpyHostToDevice, ctx->stream));
+    if (!order.empty()) memcpy(pin + P * sizeof(PairDev), order.data(), order.size() * sizeof(int));
+    HIPCHK(hipMemcpyAsync(job.pairs.p, pin, P * sizeof(PairDev) + ord_bytes, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemsetAsync(job.progress.p, 0, std::max<size_t>(prog_elems, 1) * sizeof(int), ctx->stream));
     HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, ctx->stream));
     HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), ctx->stream));
@@ -676,8 +697,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                                (PairRes*)job.pres.p, ctx->stream));
     job.res.assign(P, PairRes{});
     int status[2] = {0, 0};
-    PairRes* pin_res = (PairRes*)(pin + P * sizeof(PairDev));
-    int* pin_status = (int*)(pin + P * (sizeof(PairDev) + sizeof(PairRes)));
+    PairRes* pin_res = (PairRes*)(pin + P * sizeof(PairDev) + ord_bytes);
+    int* pin_status = (int*)(pin + P * (sizeof(PairDev) + sizeof(PairRes)) + ord_bytes);
     HIPCHK(hipMemcpyAsync(pin_res, job.pres.p, P * sizeof(PairRes), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipMemcpyAsync(pin_status, job.counter.p, sizeof status, hipMemcpyDeviceToHost, ctx->stream));
     job.pin_res = pin_res;

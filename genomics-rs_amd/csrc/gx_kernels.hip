@@ -1403,10 +1403,11 @@ __global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAV
         __syncthreads();
         const int b = __builtin_amdgcn_readfirstlane(band_sh);
         if (b >= total_bands) return;
-        int p = 0;
-        while (p + 1 < npairs && pairs[p + 1].band_base <= b) ++p;
+        // queue entry b -> (pair, band in pair): the host's order table after the descriptors
+        const int2 ob = reinterpret_cast<const int2*>(pairs + npairs)[b];
+        const int p = __builtin_amdgcn_readfirstlane(ob.x);
         const PairDev& P = pairs[p];
-        const int lb = b - P.band_base;
+        const int lb = __builtin_amdgcn_readfirstlane(ob.y);
         const int s0 = lb * W;
         if (wave < W) {
             const int s = s0 + wave;
