@@ -500,10 +500,11 @@ struct PairHost {
 // scan, so it needs that much int32 headroom above the range guard's 2^28.
 //
 // Default: layout 1 while the job is latency-bound -- its 64-row strips fit
-// about two per SIMD (single pairs, a few 30k pairs: 1.45x on one 30k pair,
-// 1.07x on four); layout 0 for wide batches, which are HBM-bound and where
-// layout 0's 2-row lanes issue fewer instructions per cell (16 x 30k pairs:
-// 484 vs 429 GCUPS; 1024 x 1k pairs 246 vs 188; profiles/r01d_layouts.txt).
+// about two per SIMD (one to three 30k pairs: 1.45x on one, 1.33x on two,
+// 1.06x on three); layout 0 from four 30k pairs on, where the band-major
+// queue keeps every CU busy and layout 0's 2-row lanes issue fewer
+// instructions per cell (four 30k pairs 7.7 vs 8.4 ms, eight 10.6 vs 15.9 ms;
+// profiles/r01o_round_sweep.txt, profiles/r01d_layouts.txt).
 static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int grid_cap) {
     const long long span = 65LL * (std::llabs((long long)sc.g) + std::llabs((long long)sc.h));
     size_t mmax = 0;
@@ -514,7 +515,7 @@ static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int 
     }
     const bool cs_ok = span < (1LL << 29) && mmax + 128 < (1u << 24);   // landing keys hold E + 64 in 24 bits
     if (const char* e = getenv("GX_LAYOUT"); e && *e) return (atoi(e) == 1 && cs_ok) ? 1 : 0;
-    return (cs_ok && strips64 <= 8LL * grid_cap) ? 1 : 0;
+    return (cs_ok && strips64 <= 6LL * grid_cap) ? 1 : 0;
 }
 
 struct FillJob {
