@@ -456,12 +456,22 @@ static int pick_width(const int (&ws)[N], int total_strips, int grid_cap) {
     }
     return queued;
 }
-static int fill_band_waves(bool track, int total_strips, int grid_cap, int lay) {
+// min_strips: the fewest strips of any pair in the launch.
+static int fill_band_waves(bool track, int total_strips, int grid_cap, int lay, int min_strips) {
     // layout 1 starts at 4-strip bands: fewer HBM hand-offs for the same one
     // compute wave per SIMD (the I/O wave shares a SIMD but mostly sleeps)
     static constexpr int kWidths1[] = {4, 6, 8, 11, 15};
     if (track) return pick_width(kFillWidthsTrack, total_strips, grid_cap);
-    return lay ? pick_width(kWidths1, total_strips, grid_cap) : pick_width(kFillWidths, total_strips, grid_cap);
+    if (lay) return pick_width(kWidths1, total_strips, grid_cap);
+    const int w = pick_width(kFillWidths, total_strips, grid_cap);
+    // Deep queues of long pairs: 15-strip bands (four compute waves per SIMD)
+    // once every pair spans >= 200 strips (25.6k rows) and the queue holds
+    // >= 2.5 rounds of them: 64 x 30k 50.9 -> 49.1 ms, 45 Covid pairs 32.3 ->
+    // 30.5; shallower queues (16 x 30k: 15.0 vs 22.5 ms, 12 x 64k) and shorter
+    // pairs (128 x 16k, 1024 x 4k) stay faster with 8 (profiles/r01o_round_sweep.txt)
+    if (w == 8 && !getenv("GX_BAND_WAVES") && min_strips >= 200 && 2 * ceil_div(total_strips, 15) >= 5 * grid_cap)
+        return 15;
+    return w;
 }
 
 // Compact score planes (layout 0, untracked: the batch path).  The
@@ -558,7 +568,9 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     const bool codes = true;
     lcs = lcs && planes;
     track = track || lcs;
-    const int W = fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device), lay);
+    int min_strips = INT_MAX;
+    for (const PairHost& h : ph) min_strips = std::min(min_strips, ceil_div((int)h.n, SR));
+    const int W = fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device), lay, min_strips);
     job.lay = lay;
     // small-alphabet score table: untracked fill (global or local), <= 4 symbols, scores in a signed byte
     Scores32 scl = sc;
