@@ -188,6 +188,7 @@ struct WorkPool {
 struct gx_context {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t cstream = nullptr;   // pipelined path: traceback record copies (D2H) off the fill stream
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     std::mutex mu;
     std::vector<DevBuf> free_list;
@@ -209,6 +210,7 @@ struct gx_context {
         PinnedBuf fpin, tjpin, tbpin;        // fill descriptors/results, traceback jobs, traceback records
         hipEvent_t fb = nullptr, fe = nullptr, tb = nullptr, te = nullptr, fdone = nullptr, tdone = nullptr;
         TbOut out;
+        DevBuf held[4];                      // traceback buffers the copy stream still reads (until tb_collect)
     } slots[2];
     int last_lay = 0, last_W = 0, last_pbytes = 0;   // the last fill launch (gx_fill_info)
 };
@@ -291,6 +293,7 @@ extern "C" int gx_context_create(int device, gx_context** out) {
     gx_context* c = new gx_context();
     c->device = device;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
     HIPCHK(hipEventCreate(&c->ev2));
@@ -341,6 +344,7 @@ extern "C" void gx_context_destroy(gx_context* ctx) {
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->ev2) (void)hipEventDestroy(ctx->ev2);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
     delete ctx;
 }
 
@@ -935,16 +939,22 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     uint32_t* hr = (uint32_t*)(sg + nsg);
     using clk = std::chrono::steady_clock;
     const auto q0 = clk::now();
-    if (e == hipSuccess) e = hipMemcpyAsync(c, cnt.p, nc * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(sg, seg.p, nsg * sizeof(int), hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(hr, recs.p, nhr * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream);
+    // pipelined: the record copies go on the copy stream after the traceback
+    // kernels, so the next fill (queued on the fill stream) starts as soon as
+    // the kernels end; the buffers stay held until tb_collect
+    hipStream_t cs = collect ? ctx->stream : ctx->cstream;
+    if (!collect && e == hipSuccess) e = hipStreamWaitEvent(cs, eve, 0);
+    if (e == hipSuccess) e = hipMemcpyAsync(c, cnt.p, nc * sizeof(int), hipMemcpyDeviceToHost, cs);
+    if (e == hipSuccess) e = hipMemcpyAsync(sg, seg.p, nsg * sizeof(int), hipMemcpyDeviceToHost, cs);
+    if (e == hipSuccess) e = hipMemcpyAsync(hr, recs.p, nhr * sizeof(uint32_t), hipMemcpyDeviceToHost, cs);
     const auto q1 = clk::now();
     out.c = c; out.sg = sg; out.hr = hr;
     out.so = so;
     out.srows = SR;
     if (!collect) {   // pipelined: tb_collect() waits for the records later
-        if (e == hipSuccess) e = hipEventRecord(ctx->slots[slot].tdone, ctx->stream);
-        cleanup();    // the buffers' next users are later on the same stream
+        if (e == hipSuccess) e = hipEventRecord(ctx->slots[slot].tdone, cs);
+        DevBuf* h = ctx->slots[slot].held;
+        h[0] = recs; h[1] = seg; h[2] = jb; h[3] = cnt;
         if (e != hipSuccess) return fail(GX_EHIP, std::string("traceback: ") + hipGetErrorString(e));
         return GX_OK;
     }
@@ -971,9 +981,14 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
 }
 
 // Records of a traceback enqueued with collect = false (pipelined path).
+static void release_held(gx_context* ctx, int slot) {
+    for (DevBuf& b : ctx->slots[slot].held) { pool_put(ctx, b); b = DevBuf{}; }
+}
+
 static int tb_collect(gx_context* ctx, int slot, size_t P, TbOut& out) {
     auto& s = ctx->slots[slot];
     HIPCHK(hipEventSynchronize(s.tdone));
+    release_held(ctx, slot);   // the copies that read them are done
     float ms = 0;
     (void)hipEventElapsedTime(&ms, s.tb, s.te);
     out.ms = ms;
@@ -1457,19 +1472,36 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
         job_release(ctx, jobs[s]);
         return r;
     };
+    using clk = std::chrono::steady_clock;
+    auto since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+    double t_fill = 0, t_tbwait = 0, t_label = 0, t_trace = 0;   // host time per phase (GX_LOG=debug)
+    const auto t_all = clk::now();
     if (!(rc = fill(0))) rc = trace(0);
     for (int k = 0; k < nsteps && !rc; ++k) {
         const int s = k & 1;
+        auto t = clk::now();
         if (k + 1 < nsteps && (rc = fill(s ^ 1))) break;       // queued behind batch k's traceback
+        t_fill += since(t); t = clk::now();
         if ((rc = tb_collect(ctx, s, idx.size(), ctx->slots[s].out))) break;
+        t_tbwait += since(t); t = clk::now();
         if ((rc = label_batch(ctx, ph, hs, is_local, track, dev_of, si, sj, score, res, ctx->slots[s].out,
                               jobs[s].fill_ms, walks)))
             break;
+        t_label += since(t); t = clk::now();
         if (k + 1 < nsteps && (rc = trace(s ^ 1))) break;
+        t_trace += since(t);
     }
+    if (const char* e = getenv("GX_LOG"); e && !strcmp(e, "debug"))
+        fprintf(stderr, "[gx DEBUG] pipelined %d steps P=%zu: %.3f ms/step; host per step: fill enqueue %.3f, "
+                        "traceback wait %.3f, label %.3f, fill wait + traceback enqueue %.3f ms\n",
+                nsteps, P, since(t_all) / nsteps, t_fill / nsteps, t_tbwait / nsteps, t_label / nsteps,
+                t_trace / nsteps);
     if (rc) {
         (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamSynchronize(ctx->cstream);
         for (auto& j : jobs) job_release(ctx, j);
+        release_held(ctx, 0);
+        release_held(ctx, 1);
         return rc;
     }
     if (fill_ms) *fill_ms = fsum / nsteps;

@@ -7,7 +7,8 @@ reverse_sequences, batched pairs, and the large pairs of BASELINE configs 2
 and 3 through digests.  Every test runs under each fill launch shape: the
 automatic band width, forced 7-strip (tracked variants) and 8-strip bands,
 and 15-strip bands on a 2-workgroup grid (bands wait in the queue for a
-workgroup, hand-offs cross launch order), for both fill layouts (0: the
+workgroup, hand-offs cross launch order), the pair-major band queue on a
+3-workgroup grid, for both fill layouts (0: the
 anti-diagonal sweep of 128-row strips; 1: the column step over 64-row
 strips) and the automatic layout choice.
 """
@@ -28,6 +29,8 @@ LAUNCH_SHAPES = {"auto": {},
                  "lay0": {"GX_LAYOUT": "0"}, "w7": {"GX_LAYOUT": "0", "GX_BAND_WAVES": "7"},
                  "w8": {"GX_LAYOUT": "0", "GX_BAND_WAVES": "8"},
                  "w15_grid2": {"GX_LAYOUT": "0", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "2"},
+                 # the pair-major band queue of earlier versions (the default is band-major)
+                 "pair_order": {"GX_LAYOUT": "0", "GX_BAND_ORDER": "pair", "GX_FILL_GRID": "3"},
                  # layout 1: column-step fill over 64-row strips (gx_internal.h)
                  "cs": {"GX_LAYOUT": "1"}, "cs_w7": {"GX_LAYOUT": "1", "GX_BAND_WAVES": "7"},
                  "cs_w15_grid2": {"GX_LAYOUT": "1", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "2"}}
