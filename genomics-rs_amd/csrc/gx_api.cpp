@@ -33,9 +33,10 @@ hipError_t launch_fill(int W, int lay, bool local, int planes, bool track, bool 
 hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d_sres, PairRes* d_pres,
                            hipStream_t st);
 hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipStream_t st);
-hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, hipStream_t st);
+hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, int gshift,
+                         hipStream_t st);
 hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, int n, int m, int t4, int h, int g,
-                            int floor_, hipStream_t st);
+                            int floor_, int gshift, hipStream_t st);
 }  // namespace gx
 
 using namespace gx;
@@ -383,6 +384,7 @@ static int check_scores(const gx_scores* s, size_t n, size_t m, HostScores* hs, 
     sc->floor_ = is_local ? 0 : kNeg;
     const char* dbg = getenv("GX_DEBUG_FLAGS");
     sc->dbg = dbg ? atoi(dbg) : 0;
+    sc->shift = 0;
     for (int k = 0; k < 4; ++k) sc->sym[k] = -1;
     return GX_OK;
 }
@@ -497,7 +499,8 @@ static bool d8_planes_ok(const Scores32& sc, int is_local) {
     const long long g = sc.g, a = (long long)sc.h + sc.g;
     const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
     const long long U = std::max(0LL, smax - a);
-    const long long lo = std::min({g, smin - U, 2 * a - U}), hi = std::max({U - a, smax - 2 * a, U - 2 * a});
+    // (the shifted fill, Scores32.shift, stores x_I - g: in [0, U - a - g])
+    const long long lo = std::min({g, smin - U, 2 * a - U}), hi = std::max({U - a - g, smax - 2 * a, U - 2 * a});
     return lo >= -128 && hi <= 127;
 }
 
@@ -545,8 +548,17 @@ struct FillJob {
     int total_bands = 0, total_strips = 0;
     bool planes_on = false, lcs_on = false, track_on = false;
     bool d8 = false;                    // compact byte planes (d8_planes_ok)
+    bool shift = false;                 // values kept as V - (i + j) g (Scores32.shift)
+    int g = 0;
     double fill_ms = 0.0;
 };
+
+// Shifted fills (Scores32.shift) report score_max(n, m) as H - (n + m) g.
+static void unshift_results(FillJob& j) {
+    if (!j.shift) return;
+    for (size_t p = 0; p < j.res.size() && p < j.pd.size(); ++p)
+        if (j.pd[p].n >= 1 && j.pd[p].m >= 1) j.res[p].end_SM += (j.pd[p].n + j.pd[p].m) * j.g;
+}
 
 static void job_release(gx_context* ctx, FillJob& j) {
     pool_put(ctx, j.chars); pool_put(ctx, j.planes); pool_put(ctx, j.codes); pool_put(ctx, j.feed);
@@ -576,10 +588,16 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     for (const PairHost& h : ph) min_strips = std::min(min_strips, ceil_div((int)h.n, SR));
     const int W = fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device), lay, min_strips);
     job.lay = lay;
-    // small-alphabet score table: untracked fill (global or local), <= 4 symbols, scores in a signed byte
+    // layout-0 untracked global fills keep every value as V - (i + j) g (one
+    // add less per recurrence, gx_kernels.hip cell); the sub scores carry -2g
     Scores32 scl = sc;
-    const bool tbl = alpha && alpha->n <= 4 && !track && sc.sm >= -128 && sc.sm <= 127 &&
-                     sc.smm >= -128 && sc.smm <= 127 && !getenv("GX_NO_SCORE_TABLE");
+    const bool shift = lay == 0 && !is_local && !track;
+    scl.shift = shift ? 1 : 0;
+    if (shift) { scl.sm = sc.sm - 2 * sc.g; scl.smm = sc.smm - 2 * sc.g; }
+    job.shift = shift; job.g = sc.g;
+    // small-alphabet score table: untracked fill (global or local), <= 4 symbols, scores in a signed byte
+    const bool tbl = alpha && alpha->n <= 4 && !track && scl.sm >= -128 && scl.sm <= 127 &&
+                     scl.smm >= -128 && scl.smm <= 127 && !getenv("GX_NO_SCORE_TABLE");
     if (tbl)
         for (int k = 0; k < 4; ++k) scl.sym[k] = alpha->sym[k];
     job.W = W;
@@ -727,6 +745,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     }
     HIPCHK(hipStreamSynchronize(ctx->stream));
     memcpy(job.res.data(), pin_res, P * sizeof(PairRes));
+    unshift_results(job);
     memcpy(status, pin_status, sizeof status);
     if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug"))
         fprintf(stderr, "[gx DEBUG] fill: launch..sync %.3f ms\n",
@@ -765,6 +784,7 @@ static int fill_collect(gx_context* ctx, FillJob& job) {
     const size_t P = job.pd.size();
     job.res.assign(P, PairRes{});
     memcpy(job.res.data(), job.pin_res, P * sizeof(PairRes));
+    unshift_results(job);
     if (job.pin_status[1] != 0)
         return fail(GX_EHIP, "fill kernel: inter-wave wait timed out (status " + std::to_string(job.pin_status[1]) + ")");
     float ms = 0.f;
@@ -1133,9 +1153,11 @@ static int fetch_plane32(const gx_table* t, int which, std::vector<int32_t>& out
     hipError_t e;
     if (t->job.d8)   // compact planes: rebuilt from the insert plane's running sum (+ this plane's x)
         e = launch_export_d8((const uint8_t*)d.pI, which == 0 ? nullptr : (const uint8_t*)src, (int32_t*)tmp.p,
-                             (int)n, (int)m, d.t4, t->sc.h, t->sc.g, t->sc.floor_, ctx->stream);
+                             (int)n, (int)m, d.t4, t->sc.h, t->sc.g, t->sc.floor_, t->job.shift ? t->sc.g : 0,
+                             ctx->stream);
     else
-        e = launch_export(src, (int32_t*)tmp.p, (int)n, (int)m, d.t4, t->job.lay, ctx->stream);
+        e = launch_export(src, (int32_t*)tmp.p, (int)n, (int)m, d.t4, t->job.lay, t->job.shift ? t->sc.g : 0,
+                          ctx->stream);
     if (e == hipSuccess)
         e = hipMemcpyAsync(out.data(), tmp.p, out.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);

@@ -62,6 +62,7 @@ struct Scores32 {
     int hg;      // h + g
     int floor_;  // local ? 0 : kNeg  (the 4th lane of score_max, algo.rs:103)
     int dbg;     // GX_DEBUG_FLAGS: bit0 = rolled (ramp) path only
+    int shift;   // layout-0 untracked global launches: values kept as V - (i + j) g (sm, smm hold s - 2g)
     int sym[4];  // small-alphabet launches: the job's distinct processed bytes (code k = sym[k])
 };
 

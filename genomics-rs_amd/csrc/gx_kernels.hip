@@ -346,7 +346,12 @@ __device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm
                                      int& oI, int& oD, int& oS, int& oL) {
     const int I_old = st.I;                // I(i, j-1): compact planes' x_I reference
     // algo.rs:231-236  insert_score = top.score_max(g, h+g, h+g)
-    const int In = LOCAL ? max3i(st.I + sc.g, st.SD + sc.hg, 0) : max(st.I + sc.g, st.SD + sc.hg);
+    // untracked global (layout 0): every value is kept as V - (i + j) g
+    // (Scores32.shift), so the insert and delete-successor recurrences lose
+    // their "+ g" (one add each) and the sub score's -2g rides in sm / smm
+    constexpr bool SHIFT = !LOCAL && !TRACK;
+    const int In = LOCAL ? max3i(st.I + sc.g, st.SD + sc.hg, 0)
+                         : SHIFT ? max(st.I, st.SD + sc.h) : max(st.I + sc.g, st.SD + sc.hg);
     static_assert(!(TBL && TRACK), "the LCS field needs the match bit");
     const bool mt = c2 == c1v;             // sequence.rs:113-114
     // algo.rs:245-248  sub_score = s_(mis)match + top_left.score_max(0,0,0);
@@ -359,7 +364,7 @@ __device__ __forceinline__ void cell(RowState& st, const int dd_in, const int sm
     const int SMn = max(IS, Dn);           // cell.score_max(0,0,0); >= floor since In >= floor
     const int SDn = max(Sn, Dn);
     // delete-successor, i.e. D(i+1, j) = this.score_max(hg, g, hg) (algo.rs:238-243)
-    const int Ddn = LOCAL ? max3i(IS + sc.hg, Dn + sc.g, 0) : max(IS + sc.hg, Dn + sc.g);
+    const int Ddn = LOCAL ? max3i(IS + sc.hg, Dn + sc.g, 0) : SHIFT ? max(IS + sc.h, Dn) : max(IS + sc.hg, Dn + sc.g);
     int Ln = 0;
     if (TRACK) Ln = max3i(st.L, l_in, st.Ltl + (mt ? 1 : 0));   // algo.rs:250-255
     int En = 0;
@@ -657,7 +662,7 @@ __device__ __forceinline__ void sub_block(LaneState& st, Rec (&nxt)[4], WaveCtx&
 }
 
 __device__ __forceinline__ void init_row(RowState& rs, const int i, const bool row_ok, const Scores32& sc,
-                                         const bool d8 = false) {
+                                         const bool d8 = false, const bool shift = false) {
     // cell (i, 0): algo.rs:204-211
     const int D0 = sc.h + i * sc.g;
     // compact planes: I(i, 0) = negative_inf is replaced by H(i, 0) + h
@@ -673,6 +678,9 @@ __device__ __forceinline__ void init_row(RowState& rs, const int i, const bool r
     rs.best = row_ok ? INT_MIN : INT_MAX; rs.bstep = 0; rs.bl = 0;
     rs.lbest = row_ok ? INT_MIN : INT_MAX; rs.lstep = 0;
     rs.cI = 0; rs.cD = 0;
+    if (shift) {   // V - (i + 0) g; the delete successor belongs to row i + 1
+        rs.I -= i * sc.g; rs.SD -= i * sc.g; rs.SM -= i * sc.g; rs.Dd -= (i + 1) * sc.g;
+    }
 }
 
 template <bool LOCAL, int PLANES, bool CODES, bool TRACK, bool LCSP, bool TBL>
@@ -720,8 +728,8 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     const int strip_base = P.strip_base;
 
     LaneState st;
-    init_row(st.a, ia, ok_a, sc, PLANES >= 3);
-    init_row(st.b, ia + 1, ok_b, sc, PLANES >= 3);
+    init_row(st.a, ia, ok_a, sc, PLANES >= 3, !LOCAL && !TRACK);
+    init_row(st.b, ia + 1, ok_b, sc, PLANES >= 3, !LOCAL && !TRACK);
     st.c2c = 0;
     st.b.SMtl = st.a.SM;                          // (A, 0) is row B's top-left for column 1
     // landing columns of column 0: the path reaches column 0 at its own local row
@@ -1319,6 +1327,7 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
                             const int I0 = sc.h + j * sc.g;
                             r.dd = max(I0 + sc.hg, sc.floor_);
                             r.sm = max(I0, sc.floor_);
+                            if (sc.shift) { r.dd -= (1 + j) * sc.g; r.sm -= j * sc.g; }
                             r.l = 0;
                             r.c2 = TBL ? sym_code(P.c2[j - 1], sc) * 8 : (int)P.c2[j - 1];
                         }
@@ -1673,7 +1682,7 @@ __global__ __launch_bounds__(64) void tb_strip_kernel(const TbDev* __restrict__ 
 // Export: strip-major anti-diagonal planes -> row-major (n+1) x (m+1) int32
 // (interior only; the host fills the boundary in int64).
 __global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __restrict__ out, int n, int m, int t4,
-                              int lay) {
+                              int lay, int gshift) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t total = (size_t)n * m;
     if (idx >= total) return;
@@ -1688,14 +1697,15 @@ __global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __rest
         const int s = (i - 1) / kStripRows1, l = (i - 1) % kStripRows1, t = j - 1;
         o = ((size_t)s * t4 + (t >> 2)) * kGroupInts1 + l * 4 + (t & 3);
     }
-    out[(size_t)i * (m + 1) + j] = plane[o];
+    out[(size_t)i * (m + 1) + j] = plane[o] + (i + j) * gshift;   // shifted fills: V - (i + j) g
 }
 
 // Export of a compact (mode 3) plane: one thread per row rebuilds
 // I(i, j) = (D0 + h) + sum_{j' <= j} x_I(i, j') and, for the delete or sub
 // plane, adds that plane's x (gx_kernels.hip put_byte).
 __global__ void export_d8_kernel(const uint8_t* __restrict__ pI, const uint8_t* __restrict__ px,
-                                 int32_t* __restrict__ out, int n, int m, int t4, int h, int g, int floor_) {
+                                 int32_t* __restrict__ out, int n, int m, int t4, int h, int g, int floor_,
+                                 int gshift) {
     const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
     if (i > n) return;
     const int s = (i - 1) / kStripRows, rho = (i - 1) % kStripRows;
@@ -1706,7 +1716,7 @@ __global__ void export_d8_kernel(const uint8_t* __restrict__ pI, const uint8_t* 
     for (int j = 1; j <= m; ++j) {
         const int t = j - 1 + l;
         const size_t off = row0 + (size_t)(t >> 2) * kGroupInts + (t & 3);
-        I += (int8_t)pI[off];
+        I += (int8_t)pI[off] + gshift;   // shifted fills store x_I - g
         o[j] = px ? I + (int8_t)px[off] : I;
     }
 }
@@ -1795,19 +1805,20 @@ hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipS
 }
 
 hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, int n, int m, int t4, int h, int g,
-                            int floor_, hipStream_t st) {
+                            int floor_, int gshift, hipStream_t st) {
     if (n == 0 || m == 0) return hipSuccess;
     hipLaunchKernelGGL(export_d8_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, pI, px, out, n, m, t4, h, g,
-                       floor_);
+                       floor_, gshift);
     return hipGetLastError();
 }
 
-hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, hipStream_t st) {
+hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, int gshift,
+                         hipStream_t st) {
     const size_t total = (size_t)n * m;
     if (total == 0) return hipSuccess;
     const int blk = 256;
     hipLaunchKernelGGL(export_kernel, dim3((unsigned)((total + blk - 1) / blk)), dim3(blk), 0, st, plane, out, n, m,
-                       t4, lay);
+                       t4, lay, gshift);
     return hipGetLastError();
 }
 
