@@ -18,8 +18,8 @@ aligns its own pairs (weak scaling); RCCL (torch.distributed "nccl") carries
 only the barrier, the max-over-ranks time and the gather of per-pair
 results.  value = all ranks' cells / max-over-ranks time (GCUPS).
 
-P defaults to the pairs whose planes fill ~180 GB of HBM (64 x 30k with
-compact planes, 16 with int32 planes).
+P defaults to the pairs whose planes fill ~220 GB of HBM, at most 80 (80 x 30k
+with compact planes, 20 with int32 planes).
 
 roofline: the fill kernel's score-plane writes, B bytes per cell (3 compact,
 12 int32); achieved = B * cells / average fill-kernel time
@@ -42,7 +42,8 @@ sys.path.insert(0, os.path.join(ROOT, "genomics-rs_amd"))
 
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MEASURED_HBM_GBS = 6290.0  # float4 copy ceiling (same source)
-PLANE_BUDGET = 180e9       # bytes of score planes per GPU the default batch is sized to (288 GB HBM)
+PLANE_BUDGET = 220e9       # bytes of score planes per GPU the default batch is sized to (288 GiB HBM)
+MAX_DEFAULT_PAIRS = 80     # 80 x 30k at 15-strip bands = 1,280 bands = 5 full rounds on 256 CUs
 SCORES = (1, -2, -1, -5)   # config.toml:1-5
 
 
@@ -235,7 +236,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs-per-gpu", type=int,
                     default=int(os.environ["GX_BENCH_PAIRS"]) if "GX_BENCH_PAIRS" in os.environ else None,
-                    help="default: as many as fill ~180 GB with score planes (64 compact / 16 int32 at 30k)")
+                    help="default: as many as fill ~220 GB with score planes (80 compact / 20 int32 at 30k)")
     ap.add_argument("--length", type=int, default=30000)
     ap.add_argument("--local", action="store_true", help="Smith-Waterman mode (default: global NW)")
     ap.add_argument("--no-planes", action="store_true", help="score+traceback only (not the headline)")
@@ -270,7 +271,7 @@ def main():
     scores = gx.Scores(*SCORES)
     if P is None:
         pb = 0 if args.no_planes else gx.plane_bytes_per_cell(scores, args.local)
-        P = max(1, min(64, int(PLANE_BUDGET // (max(pb, 3) * L * (L + 64)))))
+        P = max(1, min(MAX_DEFAULT_PAIRS, int(PLANE_BUDGET // (max(pb, 3) * L * (L + 64)))))
     if args.workload == "allvsall":
         pairs, n_total = allvsall_share(gx, rank, world)
         P = len(pairs)
