@@ -904,8 +904,11 @@ struct TbStart {
     int E;      // its landing column (PairRes.end_E / lmax_E)
 };
 
+// dev_end_E: take each start cell's landing column from the fill's device
+// results (global mode, start (n, m)), so the traceback can be queued right
+// behind the fill without waiting for its results on the host.
 static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<TbStart>& starts, TbOut& out,
-                         int slot = -1, bool collect = true) {
+                         int slot = -1, bool collect = true, bool dev_end_E = false) {
     const size_t P = starts.size();
     std::vector<TbDev> jobs(P);
     std::vector<size_t> so(P);
@@ -934,6 +937,7 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
         t.skel_stride = d.skel_stride;
         t.n = d.n; t.m = d.m; t.t16 = d.t16; t.strips = d.strips;
         t.start_i = starts[p].i; t.start_j = starts[p].j; t.start_E = starts[p].E;
+        t.start_E_dev = (dev_end_E && starts[p].i >= 1) ? &((const PairRes*)job.pres.p)[p].end_E : nullptr;
         t.seg = (int*)seg.p + 4 * so[p];
         t.recs = (uint32_t*)recs.p + so[p] * SR;
         t.srows = SR;
@@ -1498,6 +1502,53 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
     auto since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     double t_fill = 0, t_tbwait = 0, t_label = 0, t_trace = 0;   // host time per phase (GX_LOG=debug)
     const auto t_all = clk::now();
+    if (!is_local && !track) {
+        // global untracked: every start cell is (n, m) and its landing column
+        // is read on the device, so each step's traceback is queued right
+        // behind its fill; the fill results are collected on the host only
+        // for the labelling (no host round trip between fill and traceback)
+        for (size_t q = 0; q < idx.size(); ++q) starts[q] = TbStart{dph[q].n >= 1 && dph[q].m >= 1 ? (int)dph[q].n : 0,
+                                                                     (int)dph[q].m, 0};
+        auto trace_dev = [&](int s) {
+            int r = run_traceback(ctx, jobs[s], starts, ctx->slots[s].out, s, false, true);
+            job_release(ctx, jobs[s]);   // stream order: later users come after the traceback
+            return r;
+        };
+        auto results = [&](int s) {
+            int r = fill_collect(ctx, jobs[s]);
+            if (r) return r;
+            fsum += jobs[s].fill_ms;
+            for (size_t q = 0; q < idx.size(); ++q) res[idx[q]] = jobs[s].res[q];
+            for (size_t p = 0; p < P; ++p)
+                start_cell_common(hs, is_local, ph[p].n, ph[p].m, res[p], &si[p], &sj[p], &score[p]);
+            return GX_OK;
+        };
+        using clk = std::chrono::steady_clock;
+        const auto t_all = clk::now();
+        if (!(rc = fill(0))) rc = trace_dev(0);
+        for (int k = 0; k < nsteps && !rc; ++k) {
+            const int s = k & 1;
+            if (k + 1 < nsteps && ((rc = fill(s ^ 1)) || (rc = trace_dev(s ^ 1)))) break;
+            if ((rc = tb_collect(ctx, s, idx.size(), ctx->slots[s].out))) break;
+            if ((rc = results(s))) break;
+            if ((rc = label_batch(ctx, ph, hs, is_local, track, dev_of, si, sj, score, res, ctx->slots[s].out,
+                                  jobs[s].fill_ms, walks)))
+                break;
+        }
+        if (const char* e = getenv("GX_LOG"); e && !strcmp(e, "debug"))
+            fprintf(stderr, "[gx DEBUG] pipelined %d steps P=%zu (device traceback starts): %.3f ms/step\n", nsteps, P,
+                    std::chrono::duration<double, std::milli>(clk::now() - t_all).count() / nsteps);
+        if (rc) {
+            (void)hipStreamSynchronize(ctx->stream);
+            (void)hipStreamSynchronize(ctx->cstream);
+            for (auto& j : jobs) job_release(ctx, j);
+            release_held(ctx, 0);
+            release_held(ctx, 1);
+            return rc;
+        }
+        if (fill_ms) *fill_ms = fsum / nsteps;
+        return GX_OK;
+    }
     if (!(rc = fill(0))) rc = trace(0);
     for (int k = 0; k < nsteps && !rc; ++k) {
         const int s = k & 1;

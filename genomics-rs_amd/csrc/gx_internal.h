@@ -133,6 +133,7 @@ struct TbDev {           // per-pair traceback job
     int n, m, t16, strips;
     int start_i, start_j;  // interior start cell (1-based), or 0 = nothing to walk
     int start_E;           // landing column of the start cell (PairRes.end_E / lmax_E)
+    const int* start_E_dev;// or, when non-null, read on the device (the fill's PairRes.end_E: no host round trip)
     int srows;             // rows per strip: 128 (layout 0, anti-diagonal) or 64 (layout 1, column-step)
     int* seg;              // out: [strips][4] {entry_i, entry_j, records, active} per strip on the path
     uint32_t* recs;        // out: [strips][kStripRows] one record per row, (insert run << 2) | kind

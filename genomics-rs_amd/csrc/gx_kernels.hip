@@ -1563,7 +1563,7 @@ __global__ void tb_chase_kernel(const TbDev* __restrict__ jobs) {
         int s = (i - 1) / SR;
         first = s;
         J.seg[4 * s + 0] = i; J.seg[4 * s + 1] = j; J.seg[4 * s + 3] = 1;
-        int E = J.start_E;
+        int E = J.start_E_dev ? *J.start_E_dev : J.start_E;
         for (;;) {
             if (E < 0) { i = s * SR - E; j = 0; break; }          // reaches (i, 0) at local row -E
             if (s == 0 || E == 0) { i = s * SR; j = E; break; }   // lands on row 0 / column 0
