@@ -929,7 +929,6 @@ template <bool LOCAL, bool CODES, bool TRACK, bool TBL, bool TAIL>
 __device__ __forceinline__ void cs_step(CsState& st, const CsConst& k, const Rec& r, const int psm, const int pl,
                                         const int t, const int m, const Scores32& sc, int& oI, int& oD, int& oS,
                                         int& pdd, int& psm_out, int& pl_out, int& e_prev) {
-    const int j = t + 1;
     const int smtl = shr1(psm, st.SM);                                  // SM(i-1, j-1)
     const int In = LOCAL ? max3i(st.I + sc.g, st.SD + sc.hg, 0) : max(st.I + sc.g, st.SD + sc.hg);
     const bool mt = r.c2 == k.c1;
