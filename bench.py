@@ -229,6 +229,43 @@ def combine_over_ranks(dist, elapsed: float, rows, device: str):
                              for g, c in zip(gathered, counts)]
 
 
+def alignment_sha256(steps) -> str:
+    import hashlib
+    h = hashlib.sha256()
+    h.update(bytes(steps["choice"].astype(np.uint8)))
+    h.update(steps["i"].astype("<u8").tobytes())
+    h.update(steps["j"].astype("<u8").tobytes())
+    return h.hexdigest()
+
+
+def verify_against_golden(staged, scores, is_local, keep_planes, rank: int, P: int, L: int):
+    """Parity of the benchmarked launch itself: one more (untimed) pass of
+    the same staged batch with on-device plane checksums; every pair that has
+    an oracle digest (tests/golden/synthetic_L{L}.json: score, statistics,
+    alignment sha256, the three plane checksums) must match it bit for bit.
+    Raises on any difference.  Returns (pairs checked, source)."""
+    path = os.path.join(ROOT, "tests", "golden", f"synthetic_L{L}.json")
+    if is_local or not os.path.exists(path):
+        return 0, None
+    with open(path) as f:
+        golden = {c["k"]: c for c in json.load(f)["cases"]}
+    mine = {p: golden[rank * P + p] for p in range(P) if rank * P + p in golden}
+    if not mine:
+        return 0, os.path.relpath(path, ROOT)
+    res, _ = staged.run(scores, is_local, keep_planes, steps=1, plane_sums=keep_planes)
+    sums = staged.plane_sums() if keep_planes else None
+    for p, c in mine.items():
+        r = res[p]
+        got = (r.score, [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps], r.n_steps,
+               alignment_sha256(staged.steps(p)))
+        want = (c["score"], c["stats"], c["n_steps"], c["alignment_sha256"])
+        if got != want:
+            raise RuntimeError(f"parity: pair {rank * P + p} differs from the oracle digest: {got} != {want}")
+        if keep_planes and [int(x) for x in sums[0, p]] != [int(x) for x in c["plane_sums"]]:
+            raise RuntimeError(f"parity: pair {rank * P + p} score planes differ from the oracle's checksums")
+    return len(mine), os.path.relpath(path, ROOT)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -242,6 +279,7 @@ def main():
     ap.add_argument("--no-planes", action="store_true", help="score+traceback only (not the headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true", help="skip the parity pass against the oracle digests")
     ap.add_argument("--workload", choices=["synthetic", "allvsall", "covid", "brca2"], default="synthetic",
                     help="allvsall: BASELINE config 4, the 45 pairs i<j of the 10 comparison_data genomes, "
                          "LPT-sharded over the ranks (traceback-only fill unless --planes); covid: config 2, "
@@ -368,6 +406,17 @@ def main():
         "fill_gcups_per_gpu": round(cells_rank / (avg_fill_ms * 1e-3) / 1e9, 3),
         "traceback_us_pair0": int(np.mean(tb_us)),
     }
+    if args.workload == "synthetic" and not args.no_verify:
+        checked, src = verify_against_golden(staged, scores, args.local, keep_planes, rank, P, L)
+        if dist is not None:
+            import torch
+            t = torch.tensor([checked], dtype=torch.int64, device="cuda")
+            dist.all_reduce(t)
+            checked = int(t.item())
+        out["parity"] = {"pairs_checked": checked, "pairs_total": P * world, "bit_exact": True,
+                         "fields": "score, statistics, alignment sha256" + (", I/D/S plane checksums" if keep_planes
+                                                                            else ""),
+                         "source": src, "pass": "one extra untimed pass of the same staged launch"}
     if world == 1 and keep_planes and args.no_plane_steps > 0:
         # the same batch without plane stores: the fill's compute ceiling
         staged.run(scores, args.local, False)

@@ -33,10 +33,12 @@ hipError_t launch_fill(int W, int lay, bool local, int planes, bool track, bool 
 hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d_sres, PairRes* d_pres,
                            hipStream_t st);
 hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipStream_t st);
-hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, int gshift,
-                         hipStream_t st);
+hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, int gshift, int row0,
+                         int rows, hipStream_t st);
 hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, int n, int m, int t4, int h, int g,
-                            int floor_, int gshift, hipStream_t st);
+                            int floor_, int gshift, int row0, int rows, hipStream_t st);
+hipError_t launch_plane_sums(const PairDev* d_pairs, int npairs, int max_strips, int lay, int mode, int h, int g,
+                             int floor_, int gshift, unsigned long long* out, hipStream_t st);
 }  // namespace gx
 
 using namespace gx;
@@ -214,6 +216,10 @@ struct gx_context {
         DevBuf held[4];                      // traceback buffers the copy stream still reads (until tb_collect)
     } slots[2];
     int last_lay = 0, last_W = 0, last_pbytes = 0;   // the last fill launch (gx_fill_info)
+    // GX_STAGED_PLANE_SUMS: plane checksums of every pass of a staged run
+    DevBuf sums_dev;
+    unsigned long long* sums_dst = nullptr;          // where the next fill's checksums go (nullptr: off)
+    std::vector<uint64_t> sums_host;                 // [passes][staged pairs][3] of the last run
 };
 
 static void* pinned_grow(PinnedBuf& b, size_t bytes) {
@@ -280,8 +286,23 @@ static int pool_get(gx_context* ctx, size_t bytes, DevBuf* out) {
     out->cap = bytes;
     return GX_OK;
 }
+// GX_POOL_POISON=1 (debug): every buffer returned to the pool is filled with
+// 0xA5 bytes in stream order, so a later user that reads a buffer it did not
+// write (pool reuse or stream-order bugs) sees garbage instead of the previous
+// pass's identical data.
+static bool pool_poison() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("GX_POOL_POISON");
+        v = (e && *e && strcmp(e, "0")) ? 1 : 0;
+    }
+    return v == 1;
+}
 static void pool_put(gx_context* ctx, DevBuf& b) {
-    if (b.p) ctx->free_list.push_back(b);
+    if (b.p) {
+        if (pool_poison()) (void)hipMemsetAsync(b.p, 0xA5, b.cap, ctx->stream);
+        ctx->free_list.push_back(b);
+    }
     b = DevBuf{};
 }
 
@@ -333,6 +354,7 @@ extern "C" void gx_context_destroy(gx_context* ctx) {
     gx_context_trim(ctx);
     (void)hipSetDevice(ctx->device);
     if (ctx->st_chars.p) (void)hipFree(ctx->st_chars.p);
+    if (ctx->sums_dev.p) (void)hipFree(ctx->sums_dev.p);
     if (ctx->tb_pin.p) (void)hipHostFree(ctx->tb_pin.p);
     if (ctx->io_pin.p) (void)hipHostFree(ctx->io_pin.p);
     for (auto& s : ctx->slots) {
@@ -572,6 +594,8 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // at offsets off1/off2 (staged path); otherwise c1/c2 are uploaded.
 // track: first max cell + LCS field (alignment_table's max_cell and
 // matches_at_max, algo.rs:258-262, 279); lcs: also keep the LCS plane.
+static hipError_t enqueue_plane_sums(gx_context* ctx, const FillJob& job, const Scores32& sc, unsigned long long* out);
+
 static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc,
                     const std::vector<PairHost>& ph, const Scores32& sc, int is_local, bool planes, bool track,
                     bool lcs, FillJob& job, const uint8_t* chars_dev = nullptr,
@@ -725,6 +749,10 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         HIPCHK(launch_fill(W, lay, is_local != 0, planes ? (d8 ? 2 : 1) : 0, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
                            (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, ctx->stream));
     HIPCHK(hipEventRecord(eve, ctx->stream));   // evb..eve brackets the fill kernel alone
+    if (ctx->sums_dst && planes && bands > 0) {   // staged checksum run: this pass's plane sums
+        HIPCHK(enqueue_plane_sums(ctx, job, sc, ctx->sums_dst));
+        ctx->sums_dst += 3 * P;
+    }
     // strip results exist only for the tracked and local fills (the untracked
     // global fill writes end_SM / end_E itself): no reduction launch otherwise
     if (bands > 0 && (track || is_local))
@@ -1000,6 +1028,7 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     for (size_t p = 0; p < P; ++p) {
         out.end_i[p] = c[4 * p + 0];
         out.end_j[p] = c[4 * p + 1];
+        if (out.end_i[p] < 0) return fail(GX_EHIP, "traceback: landing column out of range (incomplete fill)");
     }
     return GX_OK;
 }
@@ -1021,6 +1050,7 @@ static int tb_collect(gx_context* ctx, int slot, size_t P, TbOut& out) {
     for (size_t p = 0; p < P; ++p) {
         out.end_i[p] = out.c[4 * p + 0];
         out.end_j[p] = out.c[4 * p + 1];
+        if (out.end_i[p] < 0) return fail(GX_EHIP, "traceback: landing column out of range (incomplete fill)");
     }
     return GX_OK;
 }
@@ -1142,11 +1172,12 @@ extern "C" int gx_table_info(const gx_table* t, uint64_t* n_rows, uint64_t* n_co
     return GX_OK;
 }
 
-// Interior of one plane as int32 row-major (n+1)x(m+1) (boundary slots undefined).
-static int fetch_plane32(const gx_table* t, int which, std::vector<int32_t>& out) {
+// Interior of rows row0 .. row0 + rows - 1 of one plane as int32, row-major
+// rows x (m+1) (slots of row 0 and column 0 undefined).
+static int fetch_rows32(const gx_table* t, int which, size_t row0, size_t rows, std::vector<int32_t>& out) {
     const size_t n = t->s1.size(), m = t->s2.size();
-    out.assign((n + 1) * (m + 1), 0);
-    if (n == 0 || m == 0) return GX_OK;
+    out.assign(rows * (m + 1), 0);
+    if (n == 0 || m == 0 || rows == 0) return GX_OK;
     const PairDev& d = t->job.pd[0];
     const int32_t* src = which == 0 ? d.pI : which == 1 ? d.pD : which == 2 ? d.pS : d.pL;
     if (!src) return fail(GX_EINVAL, "plane not kept: build the table with GX_TABLE_PLANES / GX_TABLE_MATCHES");
@@ -1158,15 +1189,45 @@ static int fetch_plane32(const gx_table* t, int which, std::vector<int32_t>& out
     if (t->job.d8)   // compact planes: rebuilt from the insert plane's running sum (+ this plane's x)
         e = launch_export_d8((const uint8_t*)d.pI, which == 0 ? nullptr : (const uint8_t*)src, (int32_t*)tmp.p,
                              (int)n, (int)m, d.t4, t->sc.h, t->sc.g, t->sc.floor_, t->job.shift ? t->sc.g : 0,
-                             ctx->stream);
+                             (int)row0, (int)rows, ctx->stream);
     else
         e = launch_export(src, (int32_t*)tmp.p, (int)n, (int)m, d.t4, t->job.lay, t->job.shift ? t->sc.g : 0,
-                          ctx->stream);
+                          (int)row0, (int)rows, ctx->stream);
     if (e == hipSuccess)
         e = hipMemcpyAsync(out.data(), tmp.p, out.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     pool_put(ctx, tmp);
     if (e != hipSuccess) return fail(GX_EHIP, std::string("export: ") + hipGetErrorString(e));
+    return GX_OK;
+}
+
+// Interior of one plane as int32 row-major (n+1)x(m+1) (boundary slots undefined).
+static int fetch_plane32(const gx_table* t, int which, std::vector<int32_t>& out) {
+    return fetch_rows32(t, which, 0, t->s1.size() + 1, out);
+}
+
+// Rows row0 .. row0 + rows - 1 of plane `which` as int64 into out (row-major
+// rows x (m+1), or column-major with leading dimension ld_rows when colmajor).
+static int export_rows(const gx_table* t, int which, size_t row0, size_t rows, int64_t* out, int colmajor,
+                       size_t ld_rows) {
+    const size_t m = t->s2.size();
+    std::vector<int32_t> p32;
+    int rc = fetch_rows32(t, which, row0, rows, p32);
+    if (rc) return rc;
+    for (size_t r = 0; r < rows; ++r) {
+        const size_t i = row0 + r;
+        for (size_t j = 0; j <= m; ++j) {
+            int64_t v;
+            if (i == 0 || j == 0) {
+                int64_t I, D, S;
+                boundary_cell(t->hs, i, j, &I, &D, &S);
+                v = which == 0 ? I : which == 1 ? D : S;
+            } else {
+                v = p32[r * (m + 1) + j];
+            }
+            out[colmajor ? r + j * ld_rows : r * (m + 1) + j] = v;
+        }
+    }
     return GX_OK;
 }
 
@@ -1177,21 +1238,49 @@ extern "C" int gx_table_export_plane(const gx_table* t, int which, int64_t* out,
     if (out_cells < (n + 1) * (m + 1)) return fail(GX_ECAP, "out too small");
     std::lock_guard<std::mutex> lk(t->ctx->mu);
     HIPCHK(hipSetDevice(t->ctx->device));
-    std::vector<int32_t> p32;
-    int rc = fetch_plane32(t, which, p32);
+    return export_rows(t, which, 0, n + 1, out, colmajor, n + 1);
+}
+
+extern "C" int gx_table_export_rows(const gx_table* t, int which, size_t row0, size_t rows, int64_t* out,
+                                    size_t out_cells) {
+    if (!t || (!out && rows)) return fail(GX_EINVAL, "NULL argument");
+    if (which < 0 || which > 2) return fail(GX_EINVAL, "which must be 0 (insert), 1 (delete) or 2 (sub)");
+    const size_t n = t->s1.size(), m = t->s2.size();
+    if (row0 > n + 1 || rows > n + 1 - row0) return fail(GX_EINVAL, "row range outside the table");
+    if (out_cells < rows * (m + 1)) return fail(GX_ECAP, "out too small");
+    if (rows == 0) return GX_OK;
+    std::lock_guard<std::mutex> lk(t->ctx->mu);
+    HIPCHK(hipSetDevice(t->ctx->device));
+    return export_rows(t, which, row0, rows, out, 0, rows);
+}
+
+// Plane checksums of job `job`'s pairs into the device buffer out[P][3].
+static hipError_t enqueue_plane_sums(gx_context* ctx, const FillJob& job, const Scores32& sc,
+                                     unsigned long long* out) {
+    int max_strips = 0;
+    for (const PairDev& d : job.pd) max_strips = std::max(max_strips, d.strips);
+    return launch_plane_sums((const PairDev*)job.pairs.p, (int)job.pd.size(), max_strips, job.lay, job.d8 ? 2 : 1,
+                             sc.h, sc.g, sc.floor_, job.shift ? sc.g : 0, out, ctx->stream);
+}
+
+extern "C" int gx_table_plane_sums(const gx_table* t, uint64_t* sums) {
+    if (!t || !sums) return fail(GX_EINVAL, "NULL argument");
+    const size_t n = t->s1.size(), m = t->s2.size();
+    sums[0] = sums[1] = sums[2] = 0;
+    if (n == 0 || m == 0) return GX_OK;
+    if (!t->job.pd[0].pI)
+        return fail(GX_EINVAL, "planes not kept: build the table with GX_TABLE_PLANES / GX_TABLE_MATCHES");
+    gx_context* ctx = t->ctx;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    DevBuf buf;
+    int rc = pool_get(ctx, 3 * sizeof(unsigned long long), &buf);
     if (rc) return rc;
-    for (size_t i = 0; i <= n; ++i)
-        for (size_t j = 0; j <= m; ++j) {
-            int64_t v;
-            if (i == 0 || j == 0) {
-                int64_t I, D, S;
-                boundary_cell(t->hs, i, j, &I, &D, &S);
-                v = which == 0 ? I : which == 1 ? D : S;
-            } else {
-                v = p32[i * (m + 1) + j];
-            }
-            out[colmajor ? i + j * (n + 1) : i * (m + 1) + j] = v;
-        }
+    hipError_t e = enqueue_plane_sums(ctx, t->job, t->sc, (unsigned long long*)buf.p);
+    if (e == hipSuccess) e = hipMemcpyAsync(sums, buf.p, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    pool_put(ctx, buf);
+    if (e != hipSuccess) return fail(GX_EHIP, std::string("plane sums: ") + hipGetErrorString(e));
     return GX_OK;
 }
 
@@ -1667,13 +1756,67 @@ extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int
     }
     std::vector<Walk>& walks = ctx->walk_cache;
     double fms = 0;
+    // GX_STAGED_PLANE_SUMS: every pass's fill is followed by the plane
+    // checksum kernel (stream order, before the planes return to the pool)
+    const bool want_sums = (flags & GX_STAGED_PLANE_SUMS) && keep_planes;
+    const int passes = std::max(nsteps, 1);
+    std::vector<size_t> idx;   // the pairs with an interior, in device-job order (batch_core's rule)
+    for (size_t p = 0; p < P; ++p) if (ph[p].n >= 1 && ph[p].m >= 1) idx.push_back(p);
+    ctx->sums_host.clear();
+    if (want_sums && !idx.empty()) {
+        const size_t bytes = (size_t)passes * idx.size() * 3 * sizeof(unsigned long long);
+        if (ctx->sums_dev.cap < bytes) {
+            if (ctx->sums_dev.p) (void)hipFree(ctx->sums_dev.p);
+            ctx->sums_dev = DevBuf{};
+            HIPCHK(hipMalloc(&ctx->sums_dev.p, bytes));
+            ctx->sums_dev.cap = bytes;
+        }
+        HIPCHK(hipMemsetAsync(ctx->sums_dev.p, 0, bytes, ctx->stream));
+        ctx->sums_dst = (unsigned long long*)ctx->sums_dev.p;
+    }
     rc = batch_core_steps(ctx, ph, proc, hs, sc, is_local, keep_planes != 0, (flags & GX_ALIGN_MAX_CELL) != 0,
-                          std::max(nsteps, 1), walks, &fms, (const uint8_t*)ctx->st_chars.p, &ctx->st_off1,
+                          passes, walks, &fms, (const uint8_t*)ctx->st_chars.p, &ctx->st_off1,
                           &ctx->st_off2, &ctx->st_alpha);
+    const size_t filled = ctx->sums_dst ? (size_t)(ctx->sums_dst - (unsigned long long*)ctx->sums_dev.p) : 0;
+    ctx->sums_dst = nullptr;
     if (rc) return rc;
+    if (want_sums) {
+        ctx->sums_host.assign((size_t)passes * P * 3, 0);
+        if (!idx.empty()) {
+            if (filled != (size_t)passes * idx.size() * 3)
+                return fail(GX_EHIP, "plane sums: " + std::to_string(filled / 3) + " pair records for " +
+                                         std::to_string(passes) + " passes of " + std::to_string(idx.size()));
+            std::vector<uint64_t> dev(filled);
+            HIPCHK(hipStreamSynchronize(ctx->stream));
+            HIPCHK(hipMemcpy(dev.data(), ctx->sums_dev.p, filled * sizeof(uint64_t), hipMemcpyDeviceToHost));
+            for (int k = 0; k < passes; ++k)
+                for (size_t q = 0; q < idx.size(); ++q)
+                    for (int c = 0; c < 3; ++c)
+                        ctx->sums_host[((size_t)k * P + idx[q]) * 3 + c] = dev[((size_t)k * idx.size() + q) * 3 + c];
+        }
+    }
     for (size_t p = 0; p < P; ++p) out[p] = walks[p].res;
     if (fill_ms_out) *fill_ms_out = fms;
     return GX_OK;
+}
+
+extern "C" int gx_staged_plane_sums(const gx_context* ctx, uint64_t* out, size_t cap, size_t* n_values) {
+    if (!ctx) return fail(GX_EINVAL, "context is NULL");
+    if (n_values) *n_values = ctx->sums_host.size();
+    if (!out) return GX_OK;
+    if (cap < ctx->sums_host.size()) return fail(GX_ECAP, "out too small");
+    std::copy(ctx->sums_host.begin(), ctx->sums_host.end(), out);
+    return GX_OK;
+}
+
+extern "C" int gx_staged_steps(const gx_context* ctx, size_t pair, gx_step* steps, size_t cap, size_t* n_steps) {
+    if (!ctx) return fail(GX_EINVAL, "context is NULL");
+    if (pair >= ctx->walk_cache.size() || pair >= ctx->st_s1.size())
+        return fail(GX_EINVAL, "no such staged pair in the last run");
+    const Walk& w = ctx->walk_cache[pair];
+    if (n_steps) *n_steps = w.steps.size();
+    if (!steps) return GX_OK;
+    return copy_steps(w, steps, cap);
 }
 
 extern "C" int gx_fill_info(const gx_context* ctx, int* layout, int* band_waves, int* plane_bytes_per_cell) {

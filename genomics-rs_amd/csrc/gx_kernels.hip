@@ -1564,6 +1564,9 @@ __global__ void tb_chase_kernel(const TbDev* __restrict__ jobs) {
         J.seg[4 * s + 0] = i; J.seg[4 * s + 1] = j; J.seg[4 * s + 3] = 1;
         int E = J.start_E_dev ? *J.start_E_dev : J.start_E;
         for (;;) {
+            // a landing column outside the strip's range (a fill that did not
+            // complete): report (-1, -1), the host returns GX_EHIP
+            if (E < -SR || E > J.m) { i = -1; j = -1; first = -1; break; }
             if (E < 0) { i = s * SR - E; j = 0; break; }          // reaches (i, 0) at local row -E
             if (s == 0 || E == 0) { i = s * SR; j = E; break; }   // lands on row 0 / column 0
             s -= 1;                                               // enters strip s at its bottom row
@@ -1678,15 +1681,102 @@ __global__ __launch_bounds__(64) void tb_strip_kernel(const TbDev* __restrict__ 
     if (lane == 0) ((gint*)J.seg)[4 * ss + 2] = nrec;
 }
 
-// Export: strip-major anti-diagonal planes -> row-major (n+1) x (m+1) int32
-// (interior only; the host fills the boundary in int64).
+// Plane checksums of every pair of a fill launch, decoded from the planes as
+// the exports decode them: for each of the I, D, S planes the sum over the
+// interior cells of value * (1 + i * 0x9E3779B1 + j * 0x85EBCA77) mod 2^64
+// (the oracle's plane_sums, oracle/gx_oracle.c oracle_align_lean).  One
+// thread per row, walking its row in step order (t = j - 1 + l on layout 0,
+// j - 1 on layout 1) so that a wave reads one contiguous group at a time;
+// the compact format keeps a running insert value along the row.  Wave sums
+// go to out[pair][3] with 64-bit atomic adds (order-independent mod 2^64).
+// mode: 1 = int32 planes, 2 = compact byte planes.
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+
+__global__ __launch_bounds__(64) void plane_sums_kernel(const PairDev* __restrict__ pairs, int lay, int mode, int h,
+                                                       int g, int floor_, int gshift,
+                                                       unsigned long long* __restrict__ out) {
+    const PairDev d = pairs[blockIdx.y];
+    const int lane = threadIdx.x;
+    const int SR = lay ? kStripRows1 : kStripRows;
+    const int s = blockIdx.x / (SR / kWave);            // strip (layout 0: two blocks of 64 rows per strip)
+    const int hh = lay ? 0 : (int)(blockIdx.x & 1);     // layout 0: row-in-lane of this block
+    if (s >= d.strips || !d.pI) return;
+    const int i = lay ? s * SR + lane + 1 : s * SR + 2 * lane + hh + 1;
+    const int l = lay ? 0 : lane;                       // step of column 1 on this row
+    const bool row_ok = i <= d.n;
+    unsigned long long sI = 0, sD = 0, sS = 0;
+    const unsigned long long wi = 1ull + (unsigned long long)i * 0x9E3779B1ull;
+    const size_t gints = lay ? kGroupInts1 : kGroupInts;
+    const size_t row0 = (size_t)s * d.t4 * gints + (lay ? (size_t)lane * 4 : (size_t)hh * kWave * 4 + (size_t)lane * 4);
+    if (mode == 2) {
+        const uint8_t* pI = (const uint8_t*)d.pI;
+        const uint8_t* pD = (const uint8_t*)d.pD;
+        const uint8_t* pS = (const uint8_t*)d.pS;
+        int I = max(h + i * g, floor_) + h;             // H(i, 0) + h, as the fill seeds it
+        for (int q = 0; q < d.t4; ++q) {
+            const size_t off = row0 + (size_t)q * gints;
+            const uint32_t wI = row_ok ? *(const uint32_t*)(pI + off) : 0u;
+            const uint32_t wD = row_ok ? *(const uint32_t*)(pD + off) : 0u;
+            const uint32_t wS = row_ok ? *(const uint32_t*)(pS + off) : 0u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int j = 4 * q + k - l + 1;
+                if (!row_ok || j < 1 || j > d.m) continue;
+                I += (int)(int8_t)(wI >> (8 * k)) + gshift;   // shifted fills store x_I - g
+                const long long vI = I, vD = I + (int)(int8_t)(wD >> (8 * k)), vS = I + (int)(int8_t)(wS >> (8 * k));
+                const unsigned long long w = wi + (unsigned long long)j * 0x85EBCA77ull;
+                sI += (unsigned long long)vI * w;
+                sD += (unsigned long long)vD * w;
+                sS += (unsigned long long)vS * w;
+            }
+        }
+    } else {
+        for (int q = 0; q < d.t4; ++q) {
+            const size_t off = row0 + (size_t)q * gints;
+            int4 a = make_int4(0, 0, 0, 0), b = a, c = a;
+            if (row_ok) {
+                a = *(const int4*)(d.pI + off);
+                b = *(const int4*)(d.pD + off);
+                c = *(const int4*)(d.pS + off);
+            }
+            const int va[4] = {a.x, a.y, a.z, a.w}, vb[4] = {b.x, b.y, b.z, b.w}, vc[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int j = 4 * q + k - l + 1;
+                if (!row_ok || j < 1 || j > d.m) continue;
+                const long long sh = (long long)(i + j) * gshift;   // shifted fills: V - (i + j) g
+                const unsigned long long w = wi + (unsigned long long)j * 0x85EBCA77ull;
+                sI += (unsigned long long)(va[k] + sh) * w;
+                sD += (unsigned long long)(vb[k] + sh) * w;
+                sS += (unsigned long long)(vc[k] + sh) * w;
+            }
+        }
+    }
+    sI = wave_sum_u64(sI);
+    sD = wave_sum_u64(sD);
+    sS = wave_sum_u64(sS);
+    if (lane == 0) {
+        atomicAdd(&out[3 * blockIdx.y + 0], sI);
+        atomicAdd(&out[3 * blockIdx.y + 1], sD);
+        atomicAdd(&out[3 * blockIdx.y + 2], sS);
+    }
+}
+
+// Export: strip-major anti-diagonal planes -> row-major int32 rows
+// row0 .. row0 + rows - 1 of the (n+1) x (m+1) table (interior only; the host
+// fills the boundary in int64).
 __global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __restrict__ out, int n, int m, int t4,
-                              int lay, int gshift) {
+                              int lay, int gshift, int row0, int rows) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t total = (size_t)n * m;
+    const size_t total = (size_t)rows * m;
     if (idx >= total) return;
-    const int i = (int)(idx / m) + 1;
+    const int i = (int)(idx / m) + row0;
     const int j = (int)(idx % m) + 1;
+    if (i < 1 || i > n) return;
     size_t o;
     if (lay == 0) {
         const int s = (i - 1) / kStripRows, rho = (i - 1) % kStripRows;
@@ -1696,25 +1786,27 @@ __global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __rest
         const int s = (i - 1) / kStripRows1, l = (i - 1) % kStripRows1, t = j - 1;
         o = ((size_t)s * t4 + (t >> 2)) * kGroupInts1 + l * 4 + (t & 3);
     }
-    out[(size_t)i * (m + 1) + j] = plane[o] + (i + j) * gshift;   // shifted fills: V - (i + j) g
+    out[(size_t)(i - row0) * (m + 1) + j] = plane[o] + (i + j) * gshift;   // shifted fills: V - (i + j) g
 }
 
 // Export of a compact (mode 3) plane: one thread per row rebuilds
 // I(i, j) = (D0 + h) + sum_{j' <= j} x_I(i, j') and, for the delete or sub
-// plane, adds that plane's x (gx_kernels.hip put_byte).
+// plane, adds that plane's x (gx_kernels.hip put_byte).  Rows row0 ..
+// row0 + rows - 1 (each at least 1).
 __global__ void export_d8_kernel(const uint8_t* __restrict__ pI, const uint8_t* __restrict__ px,
                                  int32_t* __restrict__ out, int n, int m, int t4, int h, int g, int floor_,
-                                 int gshift) {
-    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
-    if (i > n) return;
+                                 int gshift, int row0, int rows) {
+    const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int i = r + row0;
+    if (r >= rows || i < 1 || i > n) return;
     const int s = (i - 1) / kStripRows, rho = (i - 1) % kStripRows;
     const int l = rho >> 1, hh = rho & 1;
-    const size_t row0 = (size_t)s * t4 * kGroupInts + hh * kWave * 4 + l * 4;
+    const size_t rowoff = (size_t)s * t4 * kGroupInts + hh * kWave * 4 + l * 4;
     int I = max(h + i * g, floor_) + h;   // H(i, 0) + h, as the fill seeds it
-    int32_t* o = out + (size_t)i * (m + 1);
+    int32_t* o = out + (size_t)r * (m + 1);
     for (int j = 1; j <= m; ++j) {
         const int t = j - 1 + l;
-        const size_t off = row0 + (size_t)(t >> 2) * kGroupInts + (t & 3);
+        const size_t off = rowoff + (size_t)(t >> 2) * kGroupInts + (t & 3);
         I += (int8_t)pI[off] + gshift;   // shifted fills store x_I - g
         o[j] = px ? I + (int8_t)px[off] : I;
     }
@@ -1804,20 +1896,33 @@ hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipS
 }
 
 hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, int n, int m, int t4, int h, int g,
-                            int floor_, int gshift, hipStream_t st) {
-    if (n == 0 || m == 0) return hipSuccess;
-    hipLaunchKernelGGL(export_d8_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, pI, px, out, n, m, t4, h, g,
-                       floor_, gshift);
+                            int floor_, int gshift, int row0, int rows, hipStream_t st) {
+    if (n == 0 || m == 0 || rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(export_d8_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, pI, px, out, n, m, t4, h,
+                       g, floor_, gshift, row0, rows);
     return hipGetLastError();
 }
 
-hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, int gshift,
-                         hipStream_t st) {
-    const size_t total = (size_t)n * m;
-    if (total == 0) return hipSuccess;
+hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, int gshift, int row0,
+                         int rows, hipStream_t st) {
+    const size_t total = (size_t)rows * m;
+    if (total == 0 || rows <= 0) return hipSuccess;
     const int blk = 256;
     hipLaunchKernelGGL(export_kernel, dim3((unsigned)((total + blk - 1) / blk)), dim3(blk), 0, st, plane, out, n, m,
-                       t4, lay, gshift);
+                       t4, lay, gshift, row0, rows);
+    return hipGetLastError();
+}
+
+// Plane checksums of the npairs pairs of a launch (descriptors on the device)
+// into out[npairs][3] (zeroed here); max_strips = the most strips of any pair.
+hipError_t launch_plane_sums(const PairDev* d_pairs, int npairs, int max_strips, int lay, int mode, int h, int g,
+                             int floor_, int gshift, unsigned long long* out, hipStream_t st) {
+    if (npairs <= 0 || max_strips <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(out, 0, (size_t)npairs * 3 * sizeof(unsigned long long), st);
+    if (e != hipSuccess) return e;
+    const int blocks = max_strips * (lay ? 1 : kStripRows / kWave);
+    hipLaunchKernelGGL(plane_sums_kernel, dim3((unsigned)blocks, (unsigned)npairs), dim3(64), 0, st, d_pairs, lay,
+                       mode, h, g, floor_, gshift, out);
     return hipGetLastError();
 }
 

@@ -26,6 +26,7 @@ LIB_PATH = os.environ.get("GX_LIB", os.path.join(_HERE, "libgx_amd.so"))
 GX_TABLE_PLANES = 1
 GX_TABLE_MATCHES = 2
 GX_ALIGN_MAX_CELL = 4
+GX_STAGED_PLANE_SUMS = 8
 
 # status codes (include/gx.h)
 _CODES = {0: "GX_OK", 1: "GX_EINVAL", 2: "GX_ESEQ", 3: "GX_ERANGE", 4: "GX_ENOMEM", 5: "GX_EHIP",
@@ -68,8 +69,9 @@ STEP_DTYPE = np.dtype([("choice", "u1"), ("pad", "u1", (7,)), ("i", "<u8"), ("j"
 
 # exported symbols (include/gx.h) -- checked by tests/test_abi.py
 EXPORTED = ["gx_last_error", "gx_version", "gx_context_create", "gx_context_destroy", "gx_context_trim",
-            "gx_alignment_table", "gx_table_info", "gx_table_export", "gx_table_export_plane", "gx_retrace",
-            "gx_table_free", "gx_align", "gx_align_batch", "gx_stage_pairs", "gx_run_staged", "gx_run_staged_steps",
+            "gx_alignment_table", "gx_table_info", "gx_table_export", "gx_table_export_plane", "gx_table_export_rows",
+            "gx_table_plane_sums", "gx_retrace", "gx_table_free", "gx_align", "gx_align_batch", "gx_stage_pairs",
+            "gx_run_staged", "gx_run_staged_steps", "gx_staged_plane_sums", "gx_staged_steps",
             "gx_fill_info", "gx_plane_bytes_per_cell", "gx_fasta_load",
             "gx_config_load", "gx_format_alignment", "gx_format_table"]
 
@@ -96,6 +98,10 @@ def lib():
     L.gx_table_info.argtypes = [vp] + [ctypes.POINTER(ctypes.c_uint64)] * 4 + [ctypes.POINTER(ctypes.c_int64)]
     L.gx_table_export.argtypes = [vp, vp, sz]
     L.gx_table_export_plane.argtypes = [vp, ctypes.c_int, vp, sz, ctypes.c_int]
+    L.gx_table_export_rows.argtypes = [vp, ctypes.c_int, sz, sz, vp, sz]
+    L.gx_table_plane_sums.argtypes = [vp, vp]
+    L.gx_staged_plane_sums.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
+    L.gx_staged_steps.argtypes = [vp, sz, vp, sz, ctypes.POINTER(sz)]
     L.gx_retrace.argtypes = [vp, ctypes.c_int, vp, sz, ctypes.POINTER(CResult)]
     L.gx_table_free.argtypes = [vp]
     L.gx_table_free.restype = None
@@ -348,6 +354,20 @@ class AlignmentTable:
         _check(lib().gx_table_export_plane(self.ptr, which, out.ctypes.data, out.size, 0))
         return out
 
+    def rows(self, which: int, row0: int, nrows: int) -> np.ndarray:
+        """int64 rows row0 .. row0+nrows-1 of plane `which`, shape (nrows, m+1)."""
+        m1 = self.shape[1]
+        out = np.zeros((nrows, m1), np.int64)
+        _check(lib().gx_table_export_rows(self.ptr, which, row0, nrows, out.ctypes.data, out.size))
+        return out
+
+    def plane_sums(self) -> List[int]:
+        """Device-side checksums of the I, D, S planes (gx_table_plane_sums):
+        sum over interior cells of value * (1 + i*0x9E3779B1 + j*0x85EBCA77) mod 2^64."""
+        out = np.zeros(3, np.uint64)
+        _check(lib().gx_table_plane_sums(self.ptr, out.ctypes.data))
+        return [int(x) for x in out]
+
     def free(self):
         if self.ptr:
             lib().gx_table_free(self.ptr)
@@ -514,14 +534,32 @@ class StagedPairs:
         _check(lib().gx_stage_pairs(self.ctx.ptr, s1p, n, s2p, m, self.P))
 
     def run(self, scores: Scores, is_local: bool, keep_planes: bool = True, max_cell: bool = False,
-            steps: int = 1):
+            steps: int = 1, plane_sums: bool = False):
         """`steps` back-to-back passes (pipelined one pass deep when > 1) ->
-        (the last pass's results, mean fill ms)."""
+        (the last pass's results, mean fill ms).  plane_sums: also checksum
+        every pass's score planes on the device (self.plane_sums())."""
         res = (CResult * self.P)()
         fms = ctypes.c_double(0)
+        flags = (GX_ALIGN_MAX_CELL if max_cell else 0) | (GX_STAGED_PLANE_SUMS if plane_sums else 0)
         _check(lib().gx_run_staged_steps(self.ctx.ptr, ctypes.byref(scores.c()), int(is_local), int(keep_planes),
-                                         GX_ALIGN_MAX_CELL if max_cell else 0, int(steps), res, ctypes.byref(fms)))
+                                         flags, int(steps), res, ctypes.byref(fms)))
         return list(res), fms.value
+
+    def plane_sums(self) -> np.ndarray:
+        """uint64 [passes, pairs, 3] plane checksums of the last run(plane_sums=True)."""
+        n = ctypes.c_size_t(0)
+        _check(lib().gx_staged_plane_sums(self.ctx.ptr, None, 0, ctypes.byref(n)))
+        out = np.zeros(max(n.value, 1), np.uint64)
+        _check(lib().gx_staged_plane_sums(self.ctx.ptr, out.ctypes.data, out.size, ctypes.byref(n)))
+        return out[: n.value].reshape(-1, self.P, 3)
+
+    def steps(self, pair: int) -> np.ndarray:
+        """The alignment of staged pair `pair` from the last pass of the last run (STEP_DTYPE array)."""
+        n = ctypes.c_size_t(0)
+        _check(lib().gx_staged_steps(self.ctx.ptr, pair, None, 0, ctypes.byref(n)))
+        out = np.zeros(max(n.value, 1), STEP_DTYPE)
+        _check(lib().gx_staged_steps(self.ctx.ptr, pair, out.ctypes.data, out.size, ctypes.byref(n)))
+        return out[: n.value]
 
 
 # ---------------------------------------------------------------------------
@@ -562,6 +600,31 @@ def _pack(seqs: List[bytes]):
     return lens, buf
 
 
+def _broadcast_bytes_list(dist, items, device: str) -> List[bytes]:
+    """Rank 0's list of byte strings on every rank (count + lengths, then the
+    packed bytes: three broadcasts)."""
+    import torch
+    meta = torch.zeros(2, dtype=torch.int64, device=device)
+    if dist.get_rank() == 0:
+        lens, buf = _pack(items)
+        meta[0], meta[1] = len(items), int(lens.sum())
+    dist.broadcast(meta, 0)
+    k, tot = int(meta[0]), int(meta[1])
+    tl = torch.zeros(max(k, 1), dtype=torch.int64, device=device)
+    tb = torch.zeros(max(tot, 1), dtype=torch.uint8, device=device)
+    if dist.get_rank() == 0:
+        if k:
+            tl[:k].copy_(torch.from_numpy(lens))
+        if tot:
+            tb[:tot].copy_(torch.from_numpy(buf.copy()))
+    dist.broadcast(tl, 0)
+    dist.broadcast(tb, 0)
+    lens = tl.cpu().numpy()[:k]
+    raw = tb.cpu().numpy().tobytes()
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    return [raw[int(offs[x]):int(offs[x + 1])] for x in range(k)]
+
+
 def all_vs_all(sequence_container: SequenceContainer, scores: Scores, is_local: bool = False,
                with_self: bool = True, ctx: Optional[Context] = None, dist=None, device: str = "cpu",
                align_fn=None) -> dict:
@@ -581,27 +644,11 @@ def all_vs_all(sequence_container: SequenceContainer, scores: Scores, is_local: 
     seqs = [s.sequence.encode() for s in sequence_container.sequences]
     names = [s.name for s in sequence_container.sequences]
     if dist is not None:
-        import torch
         rank, world = dist.get_rank(), dist.get_world_size()
-        # scatter: broadcast the packed sequences from rank 0
-        meta = torch.zeros(2, dtype=torch.int64, device=device)
-        if rank == 0:
-            lens, buf = _pack(seqs)
-            meta[0], meta[1] = len(seqs), int(lens.sum())
-        dist.broadcast(meta, 0)
-        k, tot = int(meta[0]), int(meta[1])
-        tl = torch.zeros(k, dtype=torch.int64, device=device)
-        tb = torch.zeros(max(tot, 1), dtype=torch.uint8, device=device)
-        if rank == 0:
-            tl.copy_(torch.from_numpy(lens))
-            if tot:
-                tb[:tot].copy_(torch.from_numpy(buf.copy()))
-        dist.broadcast(tl, 0)
-        dist.broadcast(tb, 0)
-        lens = tl.cpu().numpy()
-        raw = tb.cpu().numpy().tobytes()
-        offs = np.concatenate([[0], np.cumsum(lens)])
-        seqs = [raw[int(offs[x]):int(offs[x + 1])] for x in range(k)]
+        # scatter: broadcast rank 0's packed sequences and names (utf-8)
+        seqs = _broadcast_bytes_list(dist, seqs if rank == 0 else None, device)
+        names = [x.decode("utf-8") for x in
+                 _broadcast_bytes_list(dist, [x.encode("utf-8") for x in names] if rank == 0 else None, device)]
     else:
         rank, world = 0, 1
     pairs = all_pairs(len(seqs), with_self)

@@ -98,8 +98,12 @@ int gx_context_trim(gx_context* ctx);
 
 /* ---- alignment_table (algo.rs:151-156) --------------------------------
  * Fills the table of the first two sequences on the GPU.  The table stays in
- * HBM (the reference's (n+1)x(m+1) 48 B cells need 42.9 GB at 30k; planes
- * here take 12 B/cell).  `reverse_sequences` has the semantics of
+ * HBM (the reference's (n+1)x(m+1) 48 B cells need 42.9 GB at 30k).  The
+ * three score planes take 12 B/cell as int32, or 3 B/cell as exact per-cell
+ * byte differences (untracked tables on the anti-diagonal layout whose scores
+ * pass the range proof, gx_plane_bytes_per_cell; untracked global tables also
+ * keep values shifted by (i + j) g on the device).  Every export decodes them
+ * to the reference's int64 values.  `reverse_sequences` has the semantics of
  * is_match(.., true) (sequence.rs:102-115).  On success *table_out owns the
  * table and *matches_at_max holds the second tuple element.  Passing
  * matches_at_max = NULL skips the running-max/LCS tracking (gx_table_info
@@ -126,6 +130,19 @@ int gx_table_export(const gx_table* t, gx_cell* out, size_t out_cells);
 /* Copy one score plane (0 = insert, 1 = delete, 2 = sub) as int64, row-major
  * (i*(m+1)+j) when colmajor = 0, column-major otherwise. */
 int gx_table_export_plane(const gx_table* t, int which, int64_t* out, size_t out_cells, int colmajor);
+
+/* Rows row0 .. row0+rows-1 of one score plane as int64, row-major rows x (m+1)
+ * (a slice of the table: a 30k x 30k plane is 7.2 GB as int64).  Row 0 and
+ * column 0 are the reference's boundary cells (algo.rs:195-220).  No
+ * reference counterpart (the reference materialises the whole Array2). */
+int gx_table_export_rows(const gx_table* t, int which, size_t row0, size_t rows, int64_t* out, size_t out_cells);
+
+/* Checksums of the three score planes, computed on the device from the
+ * stored planes: sums[k] = sum over interior cells (i, j >= 1) of plane k's
+ * value * (1 + i*0x9E3779B1 + j*0x85EBCA77) mod 2^64 (k = 0 insert, 1 delete,
+ * 2 sub; oracle/gx_oracle.c oracle_align_lean folds the same sums).  Requires
+ * GX_TABLE_PLANES.  Verification at sizes where exporting is impractical. */
+int gx_table_plane_sums(const gx_table* t, uint64_t sums[3]);
 
 /* ---- retrace (algo.rs:287-291) -----------------------------------------
  * Walks the table and consumes it (the reference moves the Array2 in); the
@@ -168,6 +185,16 @@ int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_local, int ke
  * device).  out = the last pass's results; *fill_ms_out = mean fill time. */
 int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes, uint32_t flags,
                         int nsteps, gx_result* out, double* fill_ms_out);
+/* flags bit for gx_run_staged(_steps) with keep_planes: after every pass's
+ * fill, the plane checksums of gx_table_plane_sums are computed for every
+ * staged pair (before the planes are reused); gx_staged_plane_sums returns
+ * them as [pass][pair][3] (nsteps * npairs * 3 values).  Verification only. */
+#define GX_STAGED_PLANE_SUMS 8u
+int gx_staged_plane_sums(const gx_context* ctx, uint64_t* out, size_t cap, size_t* n_values);
+/* The alignment (AlignedSequences.alignment) of staged pair `pair` from the
+ * last pass of the last gx_run_staged(_steps) call; *n_steps = its length
+ * (steps may be NULL to query it). */
+int gx_staged_steps(const gx_context* ctx, size_t pair, gx_step* steps, size_t cap, size_t* n_steps);
 /* The last fill launch on ctx: its layout (0: anti-diagonal 128-row strips,
  * 1: column step over 64-row strips), band width (strips per workgroup) and
  * score-plane bytes written per cell (0: none, 12: int32 planes, 3: compact

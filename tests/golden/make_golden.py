@@ -121,13 +121,73 @@ def allvsall_cases(workers: int):
     return names, out
 
 
+def splitmix64_bases(seed: int, length: int) -> bytes:
+    """SURVEY.md 8(d) synthetic DNA (the same generator as bench.py): bytes
+    i.i.d. over ACGT from SplitMix64, base = "ACGT"[x >> 62]."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        k = np.arange(1, length + 1, dtype=np.uint64)
+        z = np.uint64(seed) + k * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return np.frombuffer(b"ACGT", np.uint8)[(z >> np.uint64(62)).astype(np.int64)].tobytes()
+
+
+def synth_pair(k: int, length: int):
+    """Synthetic pair k of length L (bench.py synth_pair: seeds 0x5EED0001/2 + 0x10000 k)."""
+    return (splitmix64_bases(0x5EED0001 + 0x10000 * k, length),
+            splitmix64_bases(0x5EED0002 + 0x10000 * k, length))
+
+
+# Synthetic batches digested by --synthetic: BASELINE configs[1]'s shape (the
+# bench's own 30k pairs, rank 0's 80 at N = 1) and configs[4] (1024 x 1k, and
+# samples of the 4k / 16k / 64k batches).
+SYNTH_SETS = {30000: 80, 1024: 1024, 4096: 64, 16384: 8, 65536: 1}
+
+
+def _synth_job(job):
+    length, k = job
+    a, b = synth_pair(k, length)
+    r = o.align_lean(a, b, CONFIG, is_local=False)
+    assert r.status == 0
+    return length, {"k": k, "n": len(a), "m": len(b), "score": r.score,
+                    "stats": [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps],
+                    "n_steps": int(len(r.choices)), "alignment_sha256": alignment_digest(r.choices, r.steps_i, r.steps_j),
+                    "plane_sums": [str(x) for x in r.extra["plane_sums"]]}
+
+
+def synthetic_cases(workers: int, lengths):
+    from multiprocessing import Pool
+    jobs = [(L, k) for L in lengths for k in range(SYNTH_SETS[L])]
+    jobs.sort(key=lambda x: -x[0])
+    out = {L: [] for L in lengths}
+    with Pool(workers) as pool:
+        for n_done, (L, rec) in enumerate(pool.imap_unordered(_synth_job, jobs, chunksize=1), 1):
+            out[L].append(rec)
+            if L >= 16384 or n_done % 128 == 0:
+                print(f"synthetic L={L} k={rec['k']} done ({n_done}/{len(jobs)})", flush=True)
+    for L in lengths:
+        out[L].sort(key=lambda c: c["k"])
+        with open(os.path.join(HERE, f"synthetic_L{L}.json"), "w") as f:
+            json.dump({"_source": "tests/golden/make_golden.py --synthetic (oracle_align_lean, global, config.toml "
+                                  "scores; pair k = splitmix64 seeds 0x5EED0001/2 + 0x10000 k, bench.py synth_pair)",
+                       "length": L, "scores": list(CONFIG), "cases": out[L]}, f, indent=0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--large", action="store_true")
     ap.add_argument("--allvsall", action="store_true")
+    ap.add_argument("--synthetic", type=str, default=None,
+                    help="comma-separated lengths of SYNTH_SETS to digest, or 'all'")
     ap.add_argument("--workers", type=int, default=7)
     args = ap.parse_args()
     o.build()
+    if args.synthetic:
+        lengths = sorted(SYNTH_SETS) if args.synthetic == "all" else [int(x) for x in args.synthetic.split(",")]
+        synthetic_cases(args.workers, lengths)
+        return
     if args.allvsall:
         names, cases = allvsall_cases(args.workers)
         with open(os.path.join(HERE, "allvsall_digests.json"), "w") as f:

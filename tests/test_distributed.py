@@ -96,7 +96,7 @@ def _avsa_worker(rank, world, port, q):
         return _fake_align(pairs, scores, is_local)
 
     res = gx.all_vs_all(cont, gx.Scores(), dist=dist, device="cpu", align_fn=fn)
-    q.put((rank, res["pairs"], res["records"], res["lengths"], calls))
+    q.put((rank, res["pairs"], res["records"], res["lengths"], calls, res["names"]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -120,9 +120,10 @@ def test_all_vs_all_two_ranks_equals_single_process():
     seqs = [gx.Sequence(f"s{k}", "ACGT"[k % 4] * (50 + 37 * k)) for k in range(7)]
     single = gx.all_vs_all(gx.SequenceContainer(seqs), gx.Scores(), align_fn=_fake_align)
     assert len(single["pairs"]) == 28
-    for rank, pairs, records, lengths, calls in out:
+    for rank, pairs, records, lengths, calls, names in out:
         assert pairs == single["pairs"] and records == single["records"]
         assert lengths == [50 + 37 * k for k in range(7)]
+        assert names == [f"s{k}" for k in range(7)]     # broadcast with the sequences
     # the two shares are disjoint and cover every pair; LPT balances n*m
     shares = gx.lpt_partition([float(a * b) for a, b in
                                ((single["lengths"][i], single["lengths"][j]) for i, j in single["pairs"])], 2)

@@ -1,0 +1,198 @@
+"""GPU parity at the sizes the product runs: the score matrix and the
+alignment of BASELINE configs 2, 3 and 5 and of the bench's own launch,
+against oracle digests (tests/golden/make_golden.py --large / --synthetic).
+
+The score planes of a 30k x 30k table (9e8 cells, 2.7 GB compact or 10.8 GB
+int32 on the device, 21.6 GB as the reference's int64 planes) are compared
+through weighted checksums: for each of the I, D, S planes the sum over the
+interior cells of value * (1 + i*0x9E3779B1 + j*0x85EBCA77) mod 2^64, which
+oracle_align_lean (oracle/gx_oracle.c) folds while it fills.  The device
+computes them from the stored planes with the exports' decode
+(gx_table_plane_sums / GX_STAGED_PLANE_SUMS); test_plane_sums_host_fold pins
+that kernel against a host fold of exported rows.  Alignments are compared
+by the sha256 of the step vector, plus score, statistics and length.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import COMPARISON, CONFIG_SCORES, FASTA, GOLDEN, read_fasta_records
+
+pytestmark = pytest.mark.gpu
+
+W_I, W_J = 0x9E3779B1, 0x85EBCA77
+
+
+def _digest(steps):
+    h = hashlib.sha256()
+    h.update(bytes(steps["choice"].astype(np.uint8)))
+    h.update(steps["i"].astype("<u8").tobytes())
+    h.update(steps["j"].astype("<u8").tobytes())
+    return h.hexdigest()
+
+
+def _synth(L):
+    with open(os.path.join(GOLDEN, f"synthetic_L{L}.json")) as f:
+        return json.load(f)["cases"]
+
+
+def _synth_pair(k, L):
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_golden
+    return make_golden.synth_pair(k, L)
+
+
+def _large_inputs():
+    brca = read_fasta_records(os.path.join(FASTA, "Human-Mouse-BRCA2-cds.fasta"))
+    wuhan = read_fasta_records(os.path.join(COMPARISON, "Covid_Wuhan.fasta"))[0][1]
+    usa = read_fasta_records(os.path.join(COMPARISON, "Covid_USA-CA4.fasta"))[0][1]
+    return {"brca2": (brca[0][1], brca[1][1]), "covid_wuhan_usa": (wuhan, usa)}
+
+
+def _large_cases():
+    with open(os.path.join(GOLDEN, "large_digests.json")) as f:
+        return json.load(f)["cases"]
+
+
+def _check_result(r, steps, c, tag):
+    assert r.score == c["score"], tag
+    assert [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps] == c["stats"], tag
+    assert r.n_steps == c["n_steps"], tag
+    if steps is not None:
+        assert len(steps) == c["n_steps"] and _digest(steps) == c["alignment_sha256"], tag
+
+
+@pytest.mark.parametrize("layout", ["auto", "lay0"])
+@pytest.mark.parametrize("tracked", [True, False], ids=["tracked", "untracked"])
+@pytest.mark.parametrize("case", range(4), ids=[c["name"] for c in _large_cases()])
+def test_large_table_plane_sums(gx, ctx, monkeypatch, case, tracked, layout):
+    """BASELINE configs 2 (Covid 29,903 x 29,882) and 3 (BRCA2 11,382 x
+    10,346), both modes: the whole score matrix (three planes) of
+    alignment_table equals the oracle's, then retrace's alignment.  auto =
+    the single-pair layout (column step, int32 planes); lay0 = the
+    anti-diagonal layout, whose untracked tables keep compact byte planes."""
+    if layout == "lay0":
+        monkeypatch.setenv("GX_LAYOUT", "0")
+    c = _large_cases()[case]
+    a, b = _large_inputs()[c["name"].split("/")[0]]
+    cont = gx.SequenceContainer([gx.Sequence("a", a.decode()), gx.Sequence("b", b.decode())])
+    table, mam = gx.alignment_table(cont, gx.Scores(*c["scores"]), c["is_local"], False, ctx=ctx, max_cell=tracked)
+    info = ctx.fill_info()
+    if layout == "lay0":
+        assert info["layout"] == 0 and info["plane_bytes_per_cell"] == (12 if tracked else 3), info
+    assert table.plane_sums() == [int(x) for x in c["plane_sums"]], (c["name"], info)
+    if tracked:
+        assert mam == c["matches_at_max"] and table.info()["max_cell"] == tuple(c["max_cell"])
+    aln = gx.retrace(cont, table, c["is_local"])
+    assert aln.score == c["score"] and list(aln.start) == c["start"]
+    assert [aln.matches, aln.mismatches, aln.gap_extensions, aln.opening_gaps] == c["stats"]
+    assert len(aln.alignment) == c["n_steps"] and _digest(aln._steps) == c["alignment_sha256"]
+
+
+def _host_fold(table, n, m, chunk=1024):
+    """Weighted plane sums folded on the host from exported int64 rows."""
+    sums = [np.uint64(0)] * 3
+    jw = np.arange(m + 1, dtype=np.uint64) * np.uint64(W_J)
+    for r0 in range(1, n + 1, chunk):
+        rows = min(chunk, n + 1 - r0)
+        iw = np.uint64(1) + np.arange(r0, r0 + rows, dtype=np.uint64)[:, None] * np.uint64(W_I)
+        w = (iw + jw[None, :])[:, 1:]
+        for k in range(3):
+            v = table.rows(k, r0, rows)[:, 1:].view(np.uint64)
+            sums[k] = sums[k] + np.sum(v * w, dtype=np.uint64)
+    return [int(x) for x in sums]
+
+
+@pytest.mark.parametrize("variant", ["local_compact", "global_compact", "global_int32"])
+def test_plane_sums_host_fold(gx, ctx, monkeypatch, variant):
+    """The device checksum kernel against a host fold of the exported rows
+    (gx_table_export_rows, row-chunked), and both against the oracle's
+    plane_sums for BASELINE config 3's pair (1.2e8 cells per plane)."""
+    is_local = variant.startswith("local")
+    if variant.endswith("compact"):
+        monkeypatch.setenv("GX_LAYOUT", "0")
+    c = [x for x in _large_cases() if x["name"] == f"brca2/{'local' if is_local else 'global'}"][0]
+    a, b = _large_inputs()["brca2"]
+    cont = gx.SequenceContainer([gx.Sequence("a", a.decode()), gx.Sequence("b", b.decode())])
+    table, _ = gx.alignment_table(cont, gx.Scores(*c["scores"]), is_local, False, ctx=ctx,
+                                  max_cell=variant.endswith("int32"))
+    assert ctx.fill_info()["plane_bytes_per_cell"] == (12 if variant.endswith("int32") else 3)
+    want = [int(x) for x in c["plane_sums"]]
+    assert table.plane_sums() == want
+    assert _host_fold(table, len(a), len(b)) == want
+    # a row slice also carries the analytic boundary column (algo.rs:195-220)
+    r = table.rows(1, 5, 3)
+    g, h = c["scores"][2], c["scores"][3]
+    assert list(r[:, 0]) == [h + i * g for i in range(5, 8)]
+    table.free()
+
+
+def _staged_check(gx, ctx, pairs, cases, steps=2, **kw):
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, fill_ms = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=steps, plane_sums=True, **kw)
+    assert fill_ms > 0
+    sums = st.plane_sums()
+    assert sums.shape == (steps, len(pairs), 3)
+    for p, c in enumerate(cases):
+        want = [int(x) for x in c["plane_sums"]]
+        for k in range(steps):   # every pass of the pipelined run, not just the last
+            assert [int(x) for x in sums[k, p]] == want, (p, c["k"], "pass", k)
+        _check_result(res[p], st.steps(p), c, (p, c["k"]))
+    return ctx.fill_info()
+
+
+LAUNCHES = {
+    # the bench's headline instantiation: 15-strip bands, compact planes, band-major queue;
+    # a grid of 8 workgroups makes the 64 bands run in 8 rounds with HBM hand-offs between them
+    "w15_grid8": ({"GX_BAND_WAVES": "15", "GX_FILL_GRID": "8"}, (0, 15, 3)),
+    "auto": ({}, None),
+    "int32_planes": ({"GX_PLANES32": "1"}, (0, None, 12)),
+    # every buffer returned to the pool is poisoned: a pass that read the previous pass's data would fail
+    "w15_poison": ({"GX_BAND_WAVES": "15", "GX_FILL_GRID": "16", "GX_POOL_POISON": "1"}, (0, 15, 3)),
+}
+
+
+@pytest.mark.parametrize("launch", sorted(LAUNCHES))
+def test_bench_launch_synthetic_30k(gx, ctx, monkeypatch, launch):
+    """The bench's own staged, untracked, pipelined launch on four of its
+    synthetic 30,000 x 30,000 pairs (pairs 0-3 of bench.py rank 0), three
+    passes: every pass's score matrix, and the last pass's alignments, equal
+    the oracle's."""
+    env, expect = LAUNCHES[launch]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cases = _synth(30000)[:4]
+    pairs = [_synth_pair(c["k"], 30000) for c in cases]
+    info = _staged_check(gx, ctx, pairs, cases, steps=3)
+    if expect:
+        lay, W, pb = expect
+        assert info["layout"] == lay and info["plane_bytes_per_cell"] == pb, info
+        if W:
+            assert info["band_waves"] == W, info
+
+
+@pytest.mark.parametrize("L", [1024, 4096, 16384])
+def test_config5_batches(gx, ctx, L):
+    """BASELINE configs[4]: 1024 x 1k pairs in one batch, and samples of the
+    4k (64 pairs) and 16k (8 pairs) batches, through the staged pipelined
+    path with score planes: every pair's planes and alignment."""
+    cases = _synth(L)
+    pairs = [_synth_pair(c["k"], L) for c in cases]
+    _staged_check(gx, ctx, pairs, cases, steps=2)
+
+
+@pytest.mark.parametrize("layout", ["auto", "lay0"])
+def test_config5_64k_pair(gx, ctx, monkeypatch, layout):
+    """One 65,536 x 65,536 pair of configs[4] (4.3e9 cells): column-step
+    layout with int32 planes (auto) and the anti-diagonal layout with compact
+    planes."""
+    if layout == "lay0":
+        monkeypatch.setenv("GX_LAYOUT", "0")
+    cases = _synth(65536)
+    pairs = [_synth_pair(c["k"], 65536) for c in cases]
+    info = _staged_check(gx, ctx, pairs, cases, steps=1)
+    assert info["plane_bytes_per_cell"] == (3 if layout == "lay0" else 12), info

@@ -9,7 +9,7 @@ TAG=${1:-r01}
 O=gpurun_out/prof_$TAG
 rm -rf "$O" && mkdir -p "$O"
 BENCH_ARGS=${BENCH_ARGS:-}
-timeout -k 10 500 python -m pytest tests -m gpu -x -q > "$O/gpu_tests.log" 2>&1 || { echo TESTS_FAIL; tail -30 "$O/gpu_tests.log"; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$O/gpu_tests.log" 2>&1 || { echo TESTS_FAIL; tail -30 "$O/gpu_tests.log"; exit 1; }
 tail -1 "$O/gpu_tests.log"
 timeout -k 10 600 python bench.py $BENCH_ARGS > "$O/bench.json" 2> "$O/bench.err" || { echo BENCH_FAIL; tail -20 "$O/bench.err"; exit 1; }
 cat "$O/bench.json"
