@@ -216,6 +216,7 @@ struct gx_context {
         DevBuf held[4];                      // traceback buffers the copy stream still reads (until tb_collect)
     } slots[2];
     int last_lay = 0, last_W = 0, last_pbytes = 0;   // the last fill launch (gx_fill_info)
+    int last_chunks = 1;                             // chunks of the last staged / batch call
     // GX_STAGED_PLANE_SUMS: plane checksums of every pass of a staged run
     DevBuf sums_dev;
     unsigned long long* sums_dst = nullptr;          // where the next fill's checksums go (nullptr: off)
@@ -1394,6 +1395,50 @@ extern "C" int gx_align(gx_context* ctx, const uint8_t* s1, size_t n, const uint
 }
 
 // ---------------------------------------------------------------------------
+// chunked batches: a batch whose device footprint exceeds the free HBM runs
+// as contiguous chunks of pairs through the same (reused) device buffers
+
+// Device bytes a fill + traceback of pair (n, m) holds: score planes
+// (plane_bpc per cell), traceback codes (0.25 B/cell), skeleton and hand-off
+// rows, traceback records.
+static double pair_device_bytes(size_t n, size_t m, double plane_bpc) {
+    const double cells = (double)(n + 128) * (double)(m + 64);
+    return cells * (plane_bpc + 0.25) + 64.0 * (double)(m + 64) * (double)(n / 64 + 2) / 8.0 + 65536.0;
+}
+
+// Budget for one chunk: GX_CHUNK_BYTES if set, else the free device memory
+// plus the context's cached buffers, less 4 GiB of headroom.
+static double chunk_budget(gx_context* ctx) {
+    if (const char* e = getenv("GX_CHUNK_BYTES"); e && *e) return atof(e);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 64e9;
+    double cached = 0;
+    for (const DevBuf& b : ctx->free_list) cached += (double)b.cap;
+    return std::max(1e9, (double)fr + cached - 4.0 * (1ull << 30));
+}
+
+// Contiguous [begin, end) ranges of the pairs, each within the budget (a pair
+// larger than the budget runs alone).
+static std::vector<std::pair<size_t, size_t>> plan_chunks(gx_context* ctx, const std::vector<PairHost>& ph,
+                                                          double plane_bpc) {
+    const double budget = chunk_budget(ctx);
+    std::vector<std::pair<size_t, size_t>> out;
+    size_t b = 0;
+    double acc = 0;
+    for (size_t p = 0; p < ph.size(); ++p) {
+        const double x = (ph[p].n && ph[p].m) ? pair_device_bytes(ph[p].n, ph[p].m, plane_bpc) : 0.0;
+        if (p > b && acc + x > budget) {
+            out.emplace_back(b, p);
+            b = p;
+            acc = 0;
+        }
+        acc += x;
+    }
+    out.emplace_back(b, ph.size());
+    return out;
+}
+
+// ---------------------------------------------------------------------------
 // batch of independent pairs (config 4 / 5)
 
 // Labels one batch's walks (host, algo.rs:339-422), pairs on the worker pool:
@@ -1688,14 +1733,22 @@ extern "C" int gx_align_batch(gx_context* ctx, const uint8_t* const* s1, const s
         ph[p] = PairHost{s1[p], s2[p], n[p], m[p]};
         proc[p] = {s1[p], s2[p]};
     }
+    // traceback codes only (no planes); batches beyond the free HBM run in chunks
+    const auto chunks = plan_chunks(ctx, ph, 0.0);
+    ctx->last_chunks = (int)chunks.size();
     std::vector<Walk> walks;
-    rc = batch_core(ctx, ph, proc, hs, sc, is_local, false, (flags & GX_ALIGN_MAX_CELL) != 0, walks, nullptr);
-    if (rc) return rc;
-    for (size_t p = 0; p < npairs; ++p) {
-        out[p] = walks[p].res;
-        if (steps && steps[p]) {
-            rc = copy_steps(walks[p], steps[p], caps ? caps[p] : 0);
-            if (rc) return rc;
+    for (const auto& c : chunks) {
+        std::vector<PairHost> phc(ph.begin() + c.first, ph.begin() + c.second);
+        std::vector<std::pair<const uint8_t*, const uint8_t*>> pc(proc.begin() + c.first, proc.begin() + c.second);
+        rc = batch_core(ctx, phc, pc, hs, sc, is_local, false, (flags & GX_ALIGN_MAX_CELL) != 0, walks, nullptr);
+        if (rc) return rc;
+        for (size_t k = 0; k < phc.size(); ++k) {
+            const size_t p = c.first + k;
+            out[p] = walks[k].res;
+            if (steps && steps[p]) {
+                rc = copy_steps(walks[k], steps[p], caps ? caps[p] : 0);
+                if (rc) return rc;
+            }
         }
     }
     return GX_OK;
@@ -1754,17 +1807,26 @@ extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int
         ph[p] = PairHost{ctx->st_s1[p].data(), ctx->st_s2[p].data(), ctx->st_s1[p].size(), ctx->st_s2[p].size()};
         proc[p] = {ph[p].s1, ph[p].s2};
     }
+    const bool track = (flags & GX_ALIGN_MAX_CELL) != 0;
     std::vector<Walk>& walks = ctx->walk_cache;
-    double fms = 0;
     // GX_STAGED_PLANE_SUMS: every pass's fill is followed by the plane
     // checksum kernel (stream order, before the planes return to the pool)
     const bool want_sums = (flags & GX_STAGED_PLANE_SUMS) && keep_planes;
     const int passes = std::max(nsteps, 1);
-    std::vector<size_t> idx;   // the pairs with an interior, in device-job order (batch_core's rule)
-    for (size_t p = 0; p < P; ++p) if (ph[p].n >= 1 && ph[p].m >= 1) idx.push_back(p);
+    // chunks: each runs its `passes` passes pipelined (pass k's labelling
+    // beside pass k+1's fill); a step is still one pass over every pair
+    const double bpc = keep_planes ? ((!track && !getenv("GX_PLANES32") && d8_planes_ok(sc, is_local)) ? 3.0 : 12.0)
+                                   : 0.0;
+    const auto chunks = plan_chunks(ctx, ph, bpc);
+    // the order in which the fills write their checksum records: chunk, pass, pair with an interior
+    std::vector<std::pair<int, size_t>> sum_order;
+    for (const auto& c : chunks)
+        for (int k = 0; k < passes; ++k)
+            for (size_t p = c.first; p < c.second; ++p)
+                if (ph[p].n >= 1 && ph[p].m >= 1) sum_order.emplace_back(k, p);
     ctx->sums_host.clear();
-    if (want_sums && !idx.empty()) {
-        const size_t bytes = (size_t)passes * idx.size() * 3 * sizeof(unsigned long long);
+    if (want_sums && !sum_order.empty()) {
+        const size_t bytes = sum_order.size() * 3 * sizeof(unsigned long long);
         if (ctx->sums_dev.cap < bytes) {
             if (ctx->sums_dev.p) (void)hipFree(ctx->sums_dev.p);
             ctx->sums_dev = DevBuf{};
@@ -1774,25 +1836,43 @@ extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int
         HIPCHK(hipMemsetAsync(ctx->sums_dev.p, 0, bytes, ctx->stream));
         ctx->sums_dst = (unsigned long long*)ctx->sums_dev.p;
     }
-    rc = batch_core_steps(ctx, ph, proc, hs, sc, is_local, keep_planes != 0, (flags & GX_ALIGN_MAX_CELL) != 0,
-                          passes, walks, &fms, (const uint8_t*)ctx->st_chars.p, &ctx->st_off1,
-                          &ctx->st_off2, &ctx->st_alpha);
+    double fms = 0;
+    if (chunks.size() == 1) {
+        rc = batch_core_steps(ctx, ph, proc, hs, sc, is_local, keep_planes != 0, track, passes, walks, &fms,
+                              (const uint8_t*)ctx->st_chars.p, &ctx->st_off1, &ctx->st_off2, &ctx->st_alpha);
+    } else {
+        walks.resize(P);
+        std::vector<Walk> wc;
+        for (const auto& c : chunks) {
+            const size_t a = c.first, b = c.second;
+            std::vector<PairHost> phc(ph.begin() + a, ph.begin() + b);
+            std::vector<std::pair<const uint8_t*, const uint8_t*>> pc(proc.begin() + a, proc.begin() + b);
+            std::vector<size_t> o1(ctx->st_off1.begin() + a, ctx->st_off1.begin() + b),
+                o2(ctx->st_off2.begin() + a, ctx->st_off2.begin() + b);
+            double f = 0;
+            rc = batch_core_steps(ctx, phc, pc, hs, sc, is_local, keep_planes != 0, track, passes, wc, &f,
+                                  (const uint8_t*)ctx->st_chars.p, &o1, &o2, &ctx->st_alpha);
+            if (rc) break;
+            fms += f;   // a pass over every pair = one pass of each chunk
+            for (size_t k = 0; k < b - a; ++k) std::swap(walks[a + k], wc[k]);
+        }
+    }
+    ctx->last_chunks = (int)chunks.size();
     const size_t filled = ctx->sums_dst ? (size_t)(ctx->sums_dst - (unsigned long long*)ctx->sums_dev.p) : 0;
     ctx->sums_dst = nullptr;
     if (rc) return rc;
     if (want_sums) {
         ctx->sums_host.assign((size_t)passes * P * 3, 0);
-        if (!idx.empty()) {
-            if (filled != (size_t)passes * idx.size() * 3)
-                return fail(GX_EHIP, "plane sums: " + std::to_string(filled / 3) + " pair records for " +
-                                         std::to_string(passes) + " passes of " + std::to_string(idx.size()));
+        if (!sum_order.empty()) {
+            if (filled != sum_order.size() * 3)
+                return fail(GX_EHIP, "plane sums: " + std::to_string(filled / 3) + " pair records, expected " +
+                                         std::to_string(sum_order.size()));
             std::vector<uint64_t> dev(filled);
             HIPCHK(hipStreamSynchronize(ctx->stream));
             HIPCHK(hipMemcpy(dev.data(), ctx->sums_dev.p, filled * sizeof(uint64_t), hipMemcpyDeviceToHost));
-            for (int k = 0; k < passes; ++k)
-                for (size_t q = 0; q < idx.size(); ++q)
-                    for (int c = 0; c < 3; ++c)
-                        ctx->sums_host[((size_t)k * P + idx[q]) * 3 + c] = dev[((size_t)k * idx.size() + q) * 3 + c];
+            for (size_t r = 0; r < sum_order.size(); ++r)
+                for (int c = 0; c < 3; ++c)
+                    ctx->sums_host[((size_t)sum_order[r].first * P + sum_order[r].second) * 3 + c] = dev[r * 3 + c];
         }
     }
     for (size_t p = 0; p < P; ++p) out[p] = walks[p].res;
@@ -1818,6 +1898,8 @@ extern "C" int gx_staged_steps(const gx_context* ctx, size_t pair, gx_step* step
     if (!steps) return GX_OK;
     return copy_steps(w, steps, cap);
 }
+
+extern "C" int gx_batch_chunks(const gx_context* ctx) { return ctx ? ctx->last_chunks : -1; }
 
 extern "C" int gx_fill_info(const gx_context* ctx, int* layout, int* band_waves, int* plane_bytes_per_cell) {
     if (!ctx) return fail(GX_EINVAL, "context is NULL");

@@ -175,7 +175,8 @@ int gx_align_batch(gx_context* ctx, const uint8_t* const* s1, const size_t* n, c
 /* ---- device-resident benchmarking path ---------------------------------
  * Stage one pair per slot in HBM once (gx_stage_pairs), then run the hot
  * path (fill with score planes + traceback) on the staged inputs with no
- * host->device traffic.  Used by bench.py; results and flags as gx_align. */
+ * host->device traffic.  Used by bench.py; results and flags as gx_align.
+ * Batches larger than the free HBM run in chunks (gx_batch_chunks). */
 int gx_stage_pairs(gx_context* ctx, const uint8_t* const* s1, const size_t* n, const uint8_t* const* s2,
                    const size_t* m, size_t npairs);
 int gx_run_staged(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes, uint32_t flags,
@@ -201,6 +202,11 @@ int gx_staged_steps(const gx_context* ctx, size_t pair, gx_step* steps, size_t c
  * planes -- per-cell byte differences, decoded exactly by the exports).  No
  * reference counterpart (measurement only). */
 int gx_fill_info(const gx_context* ctx, int* layout, int* band_waves, int* plane_bytes_per_cell);
+/* Chunks of the last gx_run_staged(_steps) / gx_align_batch call: a batch
+ * whose device footprint (planes, codes, skeleton) exceeds the free HBM runs
+ * as contiguous chunks of pairs through the same device buffers
+ * (GX_CHUNK_BYTES overrides the per-chunk byte budget).  Measurement only. */
+int gx_batch_chunks(const gx_context* ctx);
 /* Score-plane bytes per cell a batch launch (layout 0, no max tracking)
  * writes with these scores: 3 when the compact format's range proof holds
  * (global mode, g, h <= 0, differences within a signed byte), else 12; -1 on

@@ -196,3 +196,35 @@ def test_config5_64k_pair(gx, ctx, monkeypatch, layout):
     pairs = [_synth_pair(c["k"], 65536) for c in cases]
     info = _staged_check(gx, ctx, pairs, cases, steps=1)
     assert info["plane_bytes_per_cell"] == (3 if layout == "lay0" else 12), info
+
+
+@pytest.mark.parametrize("variant", ["compact", "int32"])
+def test_chunked_bench_launch(gx, ctx, monkeypatch, variant):
+    """A staged batch larger than its device budget runs as chunks of pairs
+    through the same buffers (GX_CHUNK_BYTES forces two pairs per chunk):
+    every pass's planes and the last pass's alignments still equal the
+    oracle's."""
+    monkeypatch.setenv("GX_CHUNK_BYTES", "7e9" if variant == "compact" else "25e9")
+    monkeypatch.setenv("GX_LAYOUT", "0")   # two-pair chunks would otherwise take the single-pair layout
+    if variant == "int32":
+        monkeypatch.setenv("GX_PLANES32", "1")
+    cases = _synth(30000)[4:8]
+    pairs = [_synth_pair(c["k"], 30000) for c in cases]
+    info = _staged_check(gx, ctx, pairs, cases, steps=2)
+    assert info["chunks"] == 2, info
+    assert info["plane_bytes_per_cell"] == (3 if variant == "compact" else 12), info
+
+
+def test_config5_1k_chunked(gx, ctx, monkeypatch):
+    """1024 x 1k in uneven chunks (staged path with planes, and the
+    traceback-only gx_align_batch)."""
+    monkeypatch.setenv("GX_CHUNK_BYTES", "1.5e9")
+    cases = _synth(1024)
+    pairs = [_synth_pair(c["k"], 1024) for c in cases]
+    info = _staged_check(gx, ctx, pairs, cases, steps=2)
+    assert info["chunks"] >= 3, info
+    monkeypatch.setenv("GX_CHUNK_BYTES", "0.2e9")
+    out = gx.align_batch(pairs, gx.Scores(*CONFIG_SCORES), False, ctx=ctx, max_cell=False)
+    assert ctx.fill_info()["chunks"] >= 3
+    for (steps, r), c in zip(out, cases):
+        _check_result(r, steps, c, c["k"])

@@ -22,9 +22,13 @@ constexpr int kIters = 256;
 constexpr int kUnroll = 16;
 constexpr int kChains = 8;
 
-enum Op { ADD, MAX, MAX3, DPP, SDWA, CNDMASK, NOPS };
+enum Op { ADD, MAX, MAX3, DPP, SDWA, CNDMASK, SUB, ADDC, BFE, PK_MAX, PK_ADD, PK_SUB, BFI, MOV_DPP, ADD3, MIX_ADD_MAX,
+          CMP, NOPS };
 static const char* kNames[] = {"v_add_u32", "v_max_i32", "v_max3_i32", "v_max_i32_dpp row_shr:1",
-                               "v_sub_u32_sdwa dst_sel:BYTE_1", "v_cndmask_b32"};
+                               "v_sub_u32_sdwa dst_sel:BYTE_1", "v_cndmask_b32", "v_sub_u32", "v_addc_co_u32",
+                               "v_bfe_i32", "v_pk_max_i16", "v_pk_add_u16", "v_pk_sub_i16", "v_bfi_b32",
+                               "v_mov_b32_dpp wave_shr:1", "v_add3_u32", "v_add_u32 + v_max_i32 alternating",
+                               "v_cmp_gt_i32 (SGPR-pair dst)"};
 
 template <int OP>
 __device__ __forceinline__ void step(int& a, int b, int c, unsigned long long msk) {
@@ -37,6 +41,27 @@ __device__ __forceinline__ void step(int& a, int b, int c, unsigned long long ms
         asm volatile("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
                      : "+v"(a) : "v"(b), "v"(c));
     if constexpr (OP == CNDMASK) asm volatile("v_cndmask_b32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "s"(msk));
+    if constexpr (OP == SUB) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (OP == ADDC) {
+        unsigned long long k;
+        asm volatile("v_addc_co_u32 %0, %1, %0, %0, %2" : "+v"(a), "=s"(k) : "s"(msk));
+    }
+    if constexpr (OP == BFE) asm volatile("v_bfe_i32 %0, %1, %0, 8" : "+v"(a) : "v"(b));
+    if constexpr (OP == PK_MAX) asm volatile("v_pk_max_i16 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (OP == PK_ADD) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (OP == PK_SUB) asm volatile("v_pk_sub_i16 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (OP == BFI) asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (OP == MOV_DPP) asm volatile("v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(a) : "v"(b));
+    if constexpr (OP == ADD3) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (OP == CMP) {
+        unsigned long long k;
+        asm volatile("v_cmp_gt_i32 %0, %1, %2" : "=s"(k) : "v"(a), "v"(b));
+        asm volatile("" :: "s"(k));
+    }
+}
+template <>
+__device__ __forceinline__ void step<MIX_ADD_MAX>(int& a, int b, int c, unsigned long long msk) {
+    asm volatile("v_add_u32 %0, %0, %1\n\tv_max_i32 %0, %0, %2" : "+v"(a) : "v"(b), "v"(c));
 }
 
 template <int OP>
@@ -97,7 +122,7 @@ static void run(int cus, int k, bool first) {
     double clk = 0;   // shader clock from the two timers (GHz)
     for (int w = 0; w < waves; ++w) clk += (double)c[w] / ((double)r[w] * 10.0);
     clk /= waves;
-    const double insts = (double)kIters * kUnroll * kChains;
+    const double insts = (double)kIters * kUnroll * kChains * (OP == MIX_ADD_MAX ? 2 : 1);
     // chip-wide: all waves' instructions over the kernel's wall time and every SIMD
     const double chip_cpi = (ms * 1e-3 * clk * 1e9) * (cus * 4) / (insts * waves);
     printf("%s{\"op\": \"%s\", \"waves_per_simd\": %d, \"insts_per_wave\": %.0f, \"median_wave_cycles\": %.0f, "
@@ -132,6 +157,17 @@ int main() {
     sweep<DPP>(cus, first);
     sweep<SDWA>(cus, first);
     sweep<CNDMASK>(cus, first);
+    sweep<SUB>(cus, first);
+    sweep<ADDC>(cus, first);
+    sweep<BFE>(cus, first);
+    sweep<PK_MAX>(cus, first);
+    sweep<PK_ADD>(cus, first);
+    sweep<PK_SUB>(cus, first);
+    sweep<BFI>(cus, first);
+    sweep<MOV_DPP>(cus, first);
+    sweep<ADD3>(cus, first);
+    sweep<MIX_ADD_MAX>(cus, first);
+    sweep<CMP>(cus, first);
     printf("\n]}\n");
     return 0;
 }
