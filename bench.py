@@ -142,20 +142,26 @@ def load_traffic(workload: str):
 
 def load_valu(workload: str):
     """VALU issue profile of this workload's fill (profiles/valu_fill_*.json,
-    made by tools/gpu_valu.sh + tools/valu_summary.py): the compute-side
-    bound once the planes no longer saturate HBM."""
+    made by tools/gpu_valu.sh + tools/valu_summary.py): VALU instructions per
+    cell (SQ_INSTS_VALU), the shader clock under this load and the VALU
+    lane-operation ceiling at the fill's instruction mix, measured by
+    tools/valu_probe.hip -- the bound of the compact-plane fill."""
     d = os.path.join(ROOT, "profiles")
     for name in sorted(os.listdir(d), reverse=True) if os.path.isdir(d) else []:
         if name.startswith("valu_fill") and name.endswith(".json"):
             try:
                 with open(os.path.join(d, name)) as f:
                     v = json.load(f)
+                if "ceiling" not in v:
+                    continue
                 for case in ("planes", "noplanes"):
                     if v.get(case, {}).get("workload") == workload:
                         c = v[case]
                         return {"valu_insts_per_cell": c["valu_insts_per_cell"],
                                 "valu_issue_frac": c["valu_issue_frac"], "clock_ghz": c["clock_ghz"],
-                                "source": name}
+                                "peak_tops": c["valu_lane_ops_peak_tops"],
+                                "cpi_fill_mix": v["ceiling"]["cpi_fill_mix"],
+                                "dual_issued_fraction": c["dual_issued_fraction"], "source": name}
             except Exception:
                 continue
     return None
@@ -266,6 +272,57 @@ def verify_against_golden(staged, scores, is_local, keep_planes, rank: int, P: i
     return len(mine), os.path.relpath(path, ROOT)
 
 
+def simulate_world(args, gx, ctx):
+    """Predicted N-GPU scaling from one GPU: every rank's shard of the
+    workload (LPT share of the 45 all-vs-all pairs, or rank r's synthetic
+    pairs) timed on this GPU in turn, K steps each after one warm-up, plus the
+    whole workload at N = 1.  Since shards share nothing on the data path,
+    the N-GPU step time is the slowest shard's; prints one JSON line.  Not a
+    measurement of N GPUs (no xGMI, no concurrent HBM/power load)."""
+    W = args.simulate_world
+    scores = gx.Scores(*SCORES)
+    strong = args.workload == "allvsall"
+
+    def shard(r, w):
+        if strong:
+            return allvsall_share(gx, r, w)[0]
+        P = args.pairs_per_gpu or 8
+        return rank_pairs(r, P, args.length)
+
+    def timed(pairs):
+        st = gx.StagedPairs(pairs, ctx=ctx)
+        keep = args.planes if strong else not args.no_planes
+        st.run(scores, False, keep)
+        t0 = time.perf_counter()
+        st.run(scores, False, keep, steps=args.steps)
+        return (time.perf_counter() - t0) / args.steps * 1e3
+
+    per = []
+    for r in range(W):
+        pr = shard(r, W)
+        per.append({"rank": r, "pairs": len(pr), "cells": sum(len(a) * len(b) for a, b in pr),
+                    "ms_per_step": round(timed(pr), 3)})
+        log(f"simulated rank {r}/{W}: {per[-1]}")
+    full = shard(0, 1)
+    t1 = timed(full)
+    cells1 = sum(len(a) * len(b) for a, b in full)
+    tmax = max(p["ms_per_step"] for p in per)
+    cells_w = sum(p["cells"] for p in per)
+    eff = t1 / (W * tmax) if strong else per[0]["ms_per_step"] / tmax
+    print(json.dumps({
+        "metric": "GCUPS (DP cell updates/s) at 30k×30k NW, 1/2/4/8 MI355X; % HBM roofline",
+        "simulated_world": W, "scaling": "strong" if strong else "weak",
+        "workload": "all-vs-all of the 10 comparison_data genomes (45 pairs i<j), LPT shares" if strong else
+                    f"synthetic {args.length}x{args.length} pairs, {per[0]['pairs']} per rank",
+        "per_rank": per, "n1": {"pairs": len(full), "ms_per_step": round(t1, 3),
+                                "gcups": round(cells1 / t1 / 1e6, 3)},
+        "predicted": {"ms_per_step": tmax, "gcups": round(cells_w / tmax / 1e6, 3),
+                      "efficiency": round(eff, 4),
+                      "basis": "each rank's shard timed alone on one MI355X; N-GPU step = slowest shard "
+                               "(no data-path collective)"},
+        "steps": args.steps}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -286,8 +343,13 @@ def main():
                          "Covid_Wuhan x Covid_USA-CA4 global; brca2: config 3, the Human x Mouse BRCA2 cds pair "
                          "local (one copy per rank)")
     ap.add_argument("--planes", action="store_true", help="allvsall: also write the score planes")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="1 GPU only: time every rank's shard of an N-GPU run in turn and print the predicted "
+                         "N-GPU step time and scaling efficiency (not the headline line)")
     ap.add_argument("--single-pair-steps", type=int, default=5,
                     help="also time BASELINE config 2's shape alone (one pair, latency), 1 GPU only; 0 = skip")
+    ap.add_argument("--int32-steps", type=int, default=2,
+                    help="also time the batch with int32 score planes (12 B/cell, HBM roofline), 1 GPU only; 0 = skip")
     ap.add_argument("--no-plane-steps", type=int, default=2,
                     help="also time the batch without plane stores (compute ceiling), 1 GPU only; 0 = skip")
     args = ap.parse_args()
@@ -304,7 +366,11 @@ def main():
         dist = tdist
 
     import gxamd as gx
-    ctx = gx.Context(local_rank)
+    ctx = gx.Context(gx.device_for_rank(local_rank))
+    if args.simulate_world > 1 and world == 1:
+        simulate_world(args, gx, ctx)
+        ctx.close()
+        return
     P, L = args.pairs_per_gpu, args.length
     scores = gx.Scores(*SCORES)
     if P is None:
@@ -377,6 +443,31 @@ def main():
     fill_bytes = bytes_per_cell * cells_rank
     achieved = fill_bytes / (avg_fill_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(workload)
+    valu = load_valu(workload)
+    hbm = {"bound": "hbm", "achieved": round(achieved, 1) if keep_planes else None,
+           "peak": PEAK_HBM_GBS, "unit": "GB/s",
+           "frac": round(achieved / PEAK_HBM_GBS, 4) if keep_planes else None,
+           "frac_of_measured_copy_ceiling": round(achieved / MEASURED_HBM_GBS, 4) if keep_planes else None,
+           "traffic": traffic, "traffic_source": traffic_src,
+           "kernel": "gx::fill_kernel", "fill_ms_avg": round(avg_fill_ms, 3),
+           "algorithmic_bytes_per_cell": bytes_per_cell,
+           "algorithmic_bytes_per_launch": fill_bytes}
+    if valu is not None and keep_planes and bytes_per_cell == 3:
+        # compact planes: the fill is bound by VALU issue, not HBM -- lane-ops
+        # per launch (VALU/cell x cells, SQ_INSTS_VALU profile) over the live
+        # fill time, against the probe-measured ceiling at the fill's mix
+        ach = valu["valu_insts_per_cell"] * cells_rank / (avg_fill_ms * 1e-3) / 1e12
+        roofline = {"bound": "valu", "achieved": round(ach, 3), "peak": valu["peak_tops"], "unit": "TOP/s",
+                    "frac": round(ach / valu["peak_tops"], 4), "traffic": traffic, "traffic_source": traffic_src,
+                    "kernel": "gx::fill_kernel", "fill_ms_avg": round(avg_fill_ms, 3),
+                    "algorithmic_ops_per_cell": valu["valu_insts_per_cell"],
+                    "algorithmic_ops_per_launch": round(valu["valu_insts_per_cell"] * cells_rank),
+                    "ops": "int32 VALU lane-operations (wave64 VALU instructions x 64)",
+                    "peak_basis": f"1024 SIMDs x 64 lanes x {valu['clock_ghz']} GHz / {valu['cpi_fill_mix']} cycles "
+                                  f"per wave64 VALU instruction at the fill's mix (tools/valu_probe.hip)",
+                    "source": valu["source"], "hbm": hbm}
+    else:
+        roofline = hbm
 
     out = {
         "metric": "GCUPS (DP cell updates/s) at 30k×30k NW, 1/2/4/8 MI355X; % HBM roofline",
@@ -393,16 +484,9 @@ def main():
         "data": "synthetic" if args.workload == "synthetic" else "reference FASTA data (tests/golden)",
         "config": {"workload": workload, "pairs_per_gpu": P, "seq_len": L if args.workload == "synthetic" else None,
                    "cells_per_step": total_cells, "parallelism": f"pairs sharded over {world} GPU(s)"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if keep_planes else None,
-                     "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": round(achieved / PEAK_HBM_GBS, 4) if keep_planes else None,
-                     "frac_of_measured_copy_ceiling": round(achieved / MEASURED_HBM_GBS, 4) if keep_planes else None,
-                     "traffic": traffic, "traffic_source": traffic_src,
-                     "kernel": "gx::fill_kernel", "fill_ms_avg": round(avg_fill_ms, 3),
-                     "algorithmic_bytes_per_cell": bytes_per_cell,
-                     "algorithmic_bytes_per_launch": fill_bytes},
+        "roofline": roofline,
         "fill_launch": finfo,
-        "valu": load_valu(workload),
+        "valu": valu,
         "fill_gcups_per_gpu": round(cells_rank / (avg_fill_ms * 1e-3) / 1e9, 3),
         "traceback_us_pair0": int(np.mean(tb_us)),
     }
@@ -417,6 +501,27 @@ def main():
                          "fields": "score, statistics, alignment sha256" + (", I/D/S plane checksums" if keep_planes
                                                                             else ""),
                          "source": src, "pass": "one extra untimed pass of the same staged launch"}
+    if world == 1 and keep_planes and bytes_per_cell == 3 and args.int32_steps > 0:
+        # the same batch with int32 score planes (12 B/cell, the HBM-bound
+        # format of SURVEY 8(d)); batches beyond the free HBM run in chunks
+        os.environ["GX_PLANES32"] = "1"
+        try:
+            staged.run(scores, args.local, True)
+            t2 = time.perf_counter()
+            _, fms2 = staged.run(scores, args.local, True, steps=args.int32_steps)
+            e2 = time.perf_counter() - t2
+            fi2 = ctx.fill_info()
+        finally:
+            del os.environ["GX_PLANES32"]
+        a2 = 12 * cells_rank / (fms2 * 1e-3) / 1e9
+        out["int32_planes"] = {"gcups": round(cells_rank * args.int32_steps / e2 / 1e9, 3),
+                               "ms_per_step": round(e2 / args.int32_steps * 1e3, 3),
+                               "fill_ms_avg": round(fms2, 3), "steps": args.int32_steps,
+                               "chunks": fi2["chunks"], "fill_launch": fi2,
+                               "roofline": {"bound": "hbm", "achieved": round(a2, 1), "peak": PEAK_HBM_GBS,
+                                            "unit": "GB/s", "frac": round(a2 / PEAK_HBM_GBS, 4),
+                                            "frac_of_measured_copy_ceiling": round(a2 / MEASURED_HBM_GBS, 4),
+                                            "algorithmic_bytes_per_cell": 12}}
     if world == 1 and keep_planes and args.no_plane_steps > 0:
         # the same batch without plane stores: the fill's compute ceiling
         staged.run(scores, args.local, False)
@@ -438,7 +543,13 @@ def main():
                               "fill_ms_avg": round(float(np.mean(f1)), 3), "steps": args.single_pair_steps}
         del one
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(pairs[0][0], pairs[0][1], args.cpu_seconds, args.local)
+        if len(pairs[0][1]) > 30000:
+            # the reference layout needs (n+1)(m+1) x 48 B (197 GB at 64k)
+            out["cpu_baseline"] = {"value": None, "unit": "GCUPS", "cores": 1, "kind": "port",
+                                   "sample": "N/A: the reference-layout table of one pair exceeds host memory "
+                                             "(SURVEY.md 8(d))"}
+        else:
+            out["cpu_baseline"] = cpu_baseline(pairs[0][0], pairs[0][1], args.cpu_seconds, args.local)
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

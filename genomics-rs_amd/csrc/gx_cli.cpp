@@ -189,7 +189,27 @@ int run_all_vs_all(const gx_scores& sc, const std::string& type, const std::stri
         fprintf(stderr, "[ERROR] no HIP device\n");
         return 1;
     }
-    if (ngpu <= 0 || ngpu > ndev) ngpu = ndev;
+    // GX_DEVICE_MAP=d0,d1,...: logical shard g runs on device map[g % len]
+    // (e.g. "0,0,0,0" runs a 4-shard plan on one GPU: the multi-GPU code path
+    // with several contexts on one device); without it shards clamp to the
+    // visible devices
+    std::vector<int> devmap;
+    if (const char* dm = getenv("GX_DEVICE_MAP"); dm && *dm) {
+        for (const char* q = dm; *q;) {
+            char* end = nullptr;
+            const long d = strtol(q, &end, 10);
+            if (end == q) break;
+            if (d < 0 || d >= ndev) { fprintf(stderr, "[ERROR] GX_DEVICE_MAP: no HIP device %ld\n", d); return 1; }
+            devmap.push_back((int)d);
+            q = *end == ',' ? end + 1 : end;
+        }
+    }
+    if (devmap.empty()) {
+        if (ngpu <= 0 || ngpu > ndev) ngpu = ndev;
+        for (int g = 0; g < ngpu; ++g) devmap.push_back(g);
+    } else if (ngpu <= 0) {
+        ngpu = (int)devmap.size();
+    }
     auto bins = lpt(w, ngpu);
     std::vector<gx_result> res(pairs.size());
     std::vector<int> rcs(ngpu, GX_OK);
@@ -201,7 +221,7 @@ int run_all_vs_all(const gx_scores& sc, const std::string& type, const std::stri
             const auto& b = bins[g];
             if (b.empty()) return;
             gx_context* ctx = nullptr;
-            int rc = gx_context_create(g, &ctx);
+            int rc = gx_context_create(devmap[g % devmap.size()], &ctx);
             if (rc == GX_OK) {
                 std::vector<const uint8_t*> a1, a2;
                 std::vector<size_t> n1, n2;
@@ -227,8 +247,14 @@ int run_all_vs_all(const gx_scores& sc, const std::string& type, const std::stri
             return rcs[g] == GX_EPANIC ? 101 : 1;
         }
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-    fprintf(stderr, "[INFO] Time taken to compare: %.0f us (%.0f ms), %zu pairs on %d GPU(s), %.1f GCUPS\n", us,
+    fprintf(stderr, "[INFO] Time taken to compare: %.0f us (%.0f ms), %zu pairs on %d shard(s), %.1f GCUPS\n", us,
             us / 1e3, pairs.size(), ngpu, cells / us / 1e3);
+    for (int g = 0; g < ngpu; ++g) {
+        double cg = 0;
+        for (size_t p : bins[g]) cg += w[p];
+        fprintf(stderr, "[INFO] shard %d: device %d, %zu pairs, %.3g cells\n", g, devmap[g % devmap.size()],
+                bins[g].size(), cg);
+    }
     // matrix in the reference's layout: row j, column i filled for i <= j (main.rs:253-264)
     std::vector<const gx_result*> cellp(K * K, nullptr);
     for (size_t p = 0; p < pairs.size(); ++p) cellp[pairs[p].second * K + pairs[p].first] = &res[p];

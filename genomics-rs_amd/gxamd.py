@@ -315,9 +315,19 @@ class Context:
 _default_ctx: dict = {}
 
 
+def device_for_rank(local_rank: int) -> int:
+    """HIP device of a local rank: GX_DEVICE_MAP="d0,d1,..." maps rank r to
+    map[r % len] (several ranks may share one GPU, e.g. "0,0" to run the
+    two-rank path on a one-GPU box); otherwise the rank itself."""
+    dm = os.environ.get("GX_DEVICE_MAP", "")
+    devs = [int(x) for x in dm.split(",") if x.strip()]
+    return devs[local_rank % len(devs)] if devs else local_rank
+
+
 def default_context(device: Optional[int] = None) -> Context:
     if device is None:
-        device = int(os.environ.get("LOCAL_RANK", "0")) if "GX_DEVICE" not in os.environ else int(os.environ["GX_DEVICE"])
+        device = device_for_rank(int(os.environ.get("LOCAL_RANK", "0"))) if "GX_DEVICE" not in os.environ \
+            else int(os.environ["GX_DEVICE"])
     if device not in _default_ctx:
         _default_ctx[device] = Context(device)
     return _default_ctx[device]

@@ -104,3 +104,66 @@ def test_cli_align_small_prints_table_and_display(gx, oracle, tmp_path, mode):
                        timeout=120, env=dict(os.environ, NO_COLOR="1"))
     assert p.returncode == 0, p.stderr
     assert p.stdout == want
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_cli_all_vs_all_sharded_on_one_gpu(gx, tmp_path, shards):
+    """The CLI's multi-GPU path (one context and thread per shard, LPT split,
+    results merged into one matrix) with `shards` logical shards mapped onto
+    device 0 (GX_DEVICE_MAP): the TSV equals the oracle digests'."""
+    g = _golden()
+    cfg = tmp_path / "config.toml"
+    cfg.write_text("[scores]\ns_match = %d\ns_mismatch = %d\ng = %d\nh = %d\n" % tuple(g["scores"]))
+    tsv = tmp_path / "similarity_matrix.tsv"
+    p = subprocess.run([CLI, "-c", str(cfg), "all-vs-all", "-d", COMPARISON, "-o", str(tsv), "-g", str(shards)],
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, GX_DEVICE_MAP=",".join(["0"] * shards)))
+    assert p.returncode == 0, p.stderr
+    assert f"on {shards} shard(s)" in p.stderr
+    assert sum(f"[INFO] shard {k}: device 0" in p.stderr for k in range(shards)) == shards
+    pairs, recs = _golden_result(g)
+    want = {"names": g["names"], "lengths": [0] * len(g["names"]), "pairs": pairs, "records": recs}
+    assert tsv.read_text() == gx.similarity_tsv(want)
+
+
+def _avsa_rank(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "genomics-rs_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), GX_DEVICE_MAP="0")
+    import torch.distributed as dist
+    import gxamd as gx
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cont = _container(gx) if rank == 0 else gx.SequenceContainer()
+    g = _golden()
+    res = gx.all_vs_all(cont, gx.Scores(*g["scores"]), is_local=False, with_self=True, dist=dist, device="cpu")
+    q.put((rank, res["pairs"], res["records"], res["names"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_all_vs_all_two_ranks_on_one_gpu():
+    """gxamd.all_vs_all's distributed path with the real GPU aligner: two
+    ranks (gloo for the broadcast / all-gather, both on device 0 through
+    GX_DEVICE_MAP) each align their LPT share; every rank ends with the
+    oracle's records for all 55 pairs."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_avsa_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        out = sorted(q.get(timeout=240) for _ in range(2))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    g = _golden()
+    pairs, recs = _golden_result(g)
+    for rank, prs, records, names in out:
+        assert prs == pairs and records == recs and names == g["names"], rank

@@ -46,3 +46,11 @@ if steady:
     c = collections.Counter(steady[-1][1])
     for op, n in c.most_common(30):
         print(f"   {op:26s}{n}")
+    if os.environ.get("GX_ISA_JSON"):
+        import json
+        valu = {op: n for op, n in c.items() if op.startswith("v_")}
+        with open(os.environ["GX_ISA_JSON"], "w") as f:
+            json.dump({"kernel": m.group(1), "block": steady[-1][0], "cells_per_lane": 8, "valu": valu,
+                       "valu_total": sum(valu.values()),
+                       "dual_rate": sum(n for op, n in valu.items() if op in ("v_add_u32_e32", "v_sub_u32_e32")),
+                       "source": "tools/isa_mix.py (steady-state 4-step group: 4 steps x 2 rows per lane)"}, f, indent=1)

@@ -23,12 +23,12 @@ constexpr int kUnroll = 16;
 constexpr int kChains = 8;
 
 enum Op { ADD, MAX, MAX3, DPP, SDWA, CNDMASK, SUB, ADDC, BFE, PK_MAX, PK_ADD, PK_SUB, BFI, MOV_DPP, ADD3, MIX_ADD_MAX,
-          CMP, NOPS };
+          CMP, MOV, NOPS };
 static const char* kNames[] = {"v_add_u32", "v_max_i32", "v_max3_i32", "v_max_i32_dpp row_shr:1",
                                "v_sub_u32_sdwa dst_sel:BYTE_1", "v_cndmask_b32", "v_sub_u32", "v_addc_co_u32",
                                "v_bfe_i32", "v_pk_max_i16", "v_pk_add_u16", "v_pk_sub_i16", "v_bfi_b32",
                                "v_mov_b32_dpp wave_shr:1", "v_add3_u32", "v_add_u32 + v_max_i32 alternating",
-                               "v_cmp_gt_i32 (SGPR-pair dst)"};
+                               "v_cmp_gt_i32 (SGPR-pair dst)", "v_mov_b32"};
 
 template <int OP>
 __device__ __forceinline__ void step(int& a, int b, int c, unsigned long long msk) {
@@ -53,6 +53,7 @@ __device__ __forceinline__ void step(int& a, int b, int c, unsigned long long ms
     if constexpr (OP == BFI) asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(a) : "v"(b), "v"(c));
     if constexpr (OP == MOV_DPP) asm volatile("v_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(a) : "v"(b));
     if constexpr (OP == ADD3) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (OP == MOV) asm volatile("v_mov_b32 %0, %1" : "=v"(a) : "v"(b));
     if constexpr (OP == CMP) {
         unsigned long long k;
         asm volatile("v_cmp_gt_i32 %0, %1, %2" : "=s"(k) : "v"(a), "v"(b));
@@ -168,6 +169,7 @@ int main() {
     sweep<ADD3>(cus, first);
     sweep<MIX_ADD_MAX>(cus, first);
     sweep<CMP>(cus, first);
+    sweep<MOV>(cus, first);
     printf("\n]}\n");
     return 0;
 }

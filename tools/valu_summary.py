@@ -1,15 +1,23 @@
 #!/usr/bin/env python3
-"""Summarise tools/gpu_valu.sh (rocprofv3 --pmc SQ_INSTS_VALU ... GRBM_GUI_ACTIVE)
-into profiles/valu_fill_<tag>.json: VALU instructions per cell and the VALU
-issue fraction of the batch fill, with and without score planes.
+"""Summarise tools/gpu_valu.sh into profiles/valu_fill_<tag>.json: the batch
+fill's VALU instructions per cell, and how close it runs to the VALU issue
+ceiling MEASURED on this chip (tools/valu_probe.hip), with and without score
+planes.
 
-    python tools/valu_summary.py gpurun_out/valu_<tag> <tag>
+    python tools/valu_summary.py gpurun_out/valu_<tag> <tag> [profiles/isa_mix_fill_*.json]
 
-issue_frac = SQ_INSTS_VALU x 4 cycles (a wave64 VALU op occupies a 16-lane
-SIMD for 4 cycles) / (kernel cycles x 1024 SIMDs), kernel cycles =
-GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs; MI355X_MICROARCH.md "DVFS").
-SQ_WAVE_CYCLES counts quad-cycles (its ratio to the kernel cycles is the
-resident waves / 4)."""
+Ceiling.  valu_probe times independent streams of one instruction form at 1,
+2, 4 and 8 waves per SIMD over the whole chip (kernel wall time x clock x
+SIMDs / instructions).  At the fill's occupancy (a 15 + 1-wave workgroup per
+CU = 4 waves per SIMD) a SIMD retires one wave64 v_max_i32 / v_cndmask_b32 /
+v_cmp / DPP / SDWA / v_bfe / v_pk_* per ~4.3 cycles, and one VOP2 v_add_u32 /
+v_sub_u32 per ~2.4 (the dual-issue rate, SQ_ACTIVE_INST_VALU2).  The fill's
+steady-state mix (tools/isa_mix.py) weights the two:
+    cpi = f_dual x cpi(v_add_u32) + (1 - f_dual) x cpi(rest)
+    issue_frac = SQ_INSTS_VALU x cpi / (kernel cycles x 1024 SIMDs)
+kernel cycles = GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the 8 XCDs).  The VALU
+roofline in lane-operations: peak = 1024 SIMDs x 64 lanes x clock / cpi,
+achieved = SQ_INSTS_VALU x 64 / kernel time."""
 import glob
 import json
 import os
@@ -18,6 +26,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SIMDS = 256 * 4
+FILL_WAVES_PER_SIMD = 4
+DUAL = ("v_add_u32", "v_sub_u32", "v_mov_b32")
 
 
 def counters(d):
@@ -29,39 +39,70 @@ def counters(d):
             "group by kernel_name, counter_name"):
         if "fill_kernel" in kname:
             out.setdefault(kname, {"duration_ns": dur})[ctr] = avg
-    # the batch fill: the longest fill launch
-    k = max(out, key=lambda n: out[n]["duration_ns"])
+    k = max(out, key=lambda n: out[n]["duration_ns"])   # the batch fill: the longest fill launch
     return k, out[k]
+
+
+def probe_cpi(probe, waves=FILL_WAVES_PER_SIMD):
+    dual, rest = [], []
+    for r in probe["results"]:
+        if r["waves_per_simd"] != waves or "alternating" in r["op"]:
+            continue
+        (dual if r["op"] in DUAL else rest).append(r["chip_cycles_per_inst_per_simd"])
+    return sum(dual) / len(dual), sum(rest) / len(rest)
 
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
-    res = {"source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS "
-                     "GRBM_GUI_ACTIVE, bench.py --steps 2 --warmup 1 (tools/gpu_valu.sh)"}
+    mix_path = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "profiles", "isa_mix_fill_r02.json")
+    with open(os.path.join(src, "valu_probe.json")) as f:
+        probe = json.load(f)
+    with open(mix_path) as f:
+        mix = json.load(f)
+    cpi_dual, cpi_rest = probe_cpi(probe)
+    f_dual = mix["dual_rate"] / mix["valu_total"]
+    cpi = f_dual * cpi_dual + (1 - f_dual) * cpi_rest
+    res = {"source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CU_CYCLES SQ_CYCLES SQ_WAVE_CYCLES "
+                     "SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE, bench.py --steps 2 "
+                     "--warmup 1 (tools/gpu_valu.sh); ceiling from tools/valu_probe.hip",
+           "ceiling": {"waves_per_simd": FILL_WAVES_PER_SIMD, "cpi_dual_rate_ops": round(cpi_dual, 3),
+                       "cpi_other_ops": round(cpi_rest, 3), "dual_rate_fraction_of_fill_valu": round(f_dual, 4),
+                       "cpi_fill_mix": round(cpi, 3), "isa_mix": os.path.relpath(mix_path, ROOT),
+                       "probe": "valu_probe (chip wall time x clock x SIMDs / instructions)"}}
     for case in ("planes", "noplanes"):
         k, v = counters(os.path.join(src, case))
         with open(os.path.join(src, f"{case}.json")) as f:
             bench = json.loads(f.read().strip().splitlines()[-1])
         cells = bench["config"]["cells_per_step"] // bench["n_gpus"]
         cyc = v["GRBM_GUI_ACTIVE"] / 8
+        dur = v["duration_ns"] * 1e-9
+        clk = cyc / dur
+        insts = v["SQ_INSTS_VALU"]
         res[case] = {
             "workload": bench["config"]["workload"], "kernel": k,
-            "duration_ms": round(v["duration_ns"] / 1e6, 3),
-            "clock_ghz": round(cyc / v["duration_ns"], 3),
-            "valu_insts_per_cell": round(v["SQ_INSTS_VALU"] * 64 / cells, 2),
+            "duration_ms": round(dur * 1e3, 3),
+            "clock_ghz": round(clk / 1e9, 3),
+            "valu_insts_per_cell": round(insts * 64 / cells, 2),
             "salu_insts_per_cell": round(v["SQ_INSTS_SALU"] * 64 / cells, 2),
-            "lds_insts_per_cell": round(v["SQ_INSTS_LDS"] * 64 / cells, 2),
-            "valu_issue_frac": round(v["SQ_INSTS_VALU"] * 4 / (cyc * SIMDS), 4),
+            "valu_issue_frac": round(insts * cpi / (cyc * SIMDS), 4),
+            "valu_issue_frac_at_4_cycles": round(insts * 4 / (cyc * SIMDS), 4),
+            "dual_issued_fraction": round(v["SQ_ACTIVE_INST_VALU2"] / insts, 4),
+            "valu_lane_ops_achieved_tops": round(insts * 64 / dur / 1e12, 3),
+            "valu_lane_ops_peak_tops": round(SIMDS * 64 * clk / cpi / 1e12, 3),
+            "fill_gcups": round(cells / dur / 1e9, 1),
+            "fill_gcups_ceiling_at_this_mix": round(SIMDS * 64 * clk / cpi / (insts * 64 / cells) / 1e9, 1),
             "resident_waves": round(v["SQ_WAVE_CYCLES"] * 4 / cyc, 1),
             "raw": v,
         }
     p = os.path.join(ROOT, "profiles", f"valu_fill_{tag}.json")
     with open(p, "w") as f:
         json.dump(res, f, indent=1)
+    print("cpi", res["ceiling"])
     for case in ("planes", "noplanes"):
         r = res[case]
         print(case, r["duration_ms"], "ms", r["clock_ghz"], "GHz VALU/cell", r["valu_insts_per_cell"],
-              "issue", r["valu_issue_frac"], "waves", r["resident_waves"])
+              "issue", r["valu_issue_frac"], "dual", r["dual_issued_fraction"], "ceiling GCUPS",
+              r["fill_gcups_ceiling_at_this_mix"], "fill", r["fill_gcups"])
 
 
 if __name__ == "__main__":
