@@ -15,9 +15,9 @@ timeout -k 10 600 python bench.py $BENCH_ARGS > "$O/bench.json" 2> "$O/bench.err
 cat "$O/bench.json"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt -- python3 bench.py $BENCH_ARGS --no-cpu-baseline \
     > "$O/kt_bench.json" 2> "$O/kt.err" || { echo KT_FAIL; tail -20 "$O/kt.err"; exit 1; }
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$O/pw" -o pw -- python3 bench.py $BENCH_ARGS --no-cpu-baseline --steps 2 --warmup 1 \
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d "$O/pw" -o pw -- python3 bench.py $BENCH_ARGS --no-cpu-baseline --steps 2 --warmup 1 --int32-steps 0 --no-plane-steps 0 --single-pair-steps 0 --no-verify \
     > "$O/pw_bench.json" 2> "$O/pw.err" || { echo PMCW_FAIL; tail -20 "$O/pw.err"; exit 1; }
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$O/pf" -o pf -- python3 bench.py $BENCH_ARGS --no-cpu-baseline --steps 2 --warmup 1 \
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d "$O/pf" -o pf -- python3 bench.py $BENCH_ARGS --no-cpu-baseline --steps 2 --warmup 1 --int32-steps 0 --no-plane-steps 0 --single-pair-steps 0 --no-verify \
     > "$O/pf_bench.json" 2> "$O/pf.err" || { echo PMCF_FAIL; tail -20 "$O/pf.err"; exit 1; }
 find "$O" -name "*.csv" | head -20
 echo PROFILE_DONE

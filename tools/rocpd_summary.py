@@ -73,7 +73,7 @@ def main():
         "write_bytes_per_launch": int(wr),
         "fetch_bytes_per_launch_corrected": int(rd),
         "hbm_bytes_per_launch": int(wr + rd),
-        "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"],
+        "algorithmic_bytes_per_launch": bench["roofline"].get("hbm", bench["roofline"])["algorithmic_bytes_per_launch"],
         "correction": "WRITE_SIZE KiB x1024 (exact for 16-B/lane stores); FETCH_SIZE KiB x1024 x2 (gfx950 "
                       "reports half of wide coalesced reads; MI355X_MICROARCH.md 'HBM')",
         "raw": pmc,

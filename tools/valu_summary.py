@@ -27,7 +27,6 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SIMDS = 256 * 4
 FILL_WAVES_PER_SIMD = 4
-DUAL = ("v_add_u32", "v_sub_u32", "v_mov_b32")
 
 
 def counters(d):
@@ -44,12 +43,19 @@ def counters(d):
 
 
 def probe_cpi(probe, waves=FILL_WAVES_PER_SIMD):
-    dual, rest = [], []
+    """(cpi of the dual-rate forms, cpi of the rest, names of the dual-rate
+    forms): a form is dual-rate when the probe retires it in < 3 cycles."""
+    dual, rest, names = [], [], set()
     for r in probe["results"]:
         if r["waves_per_simd"] != waves or "alternating" in r["op"]:
             continue
-        (dual if r["op"] in DUAL else rest).append(r["chip_cycles_per_inst_per_simd"])
-    return sum(dual) / len(dual), sum(rest) / len(rest)
+        x = r["chip_cycles_per_inst_per_simd"]
+        if x < 3.0:
+            dual.append(x)
+            names.add(r["op"])
+        else:
+            rest.append(x)
+    return sum(dual) / len(dual), sum(rest) / len(rest), names
 
 
 def main():
@@ -59,14 +65,16 @@ def main():
         probe = json.load(f)
     with open(mix_path) as f:
         mix = json.load(f)
-    cpi_dual, cpi_rest = probe_cpi(probe)
-    f_dual = mix["dual_rate"] / mix["valu_total"]
+    cpi_dual, cpi_rest, dual_names = probe_cpi(probe)
+    n_dual = sum(n for op, n in mix["valu"].items() if op.replace("_e32", "").replace("_e64", "") in dual_names)
+    f_dual = n_dual / mix["valu_total"]
     cpi = f_dual * cpi_dual + (1 - f_dual) * cpi_rest
     res = {"source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CU_CYCLES SQ_CYCLES SQ_WAVE_CYCLES "
                      "SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE, bench.py --steps 2 "
                      "--warmup 1 (tools/gpu_valu.sh); ceiling from tools/valu_probe.hip",
            "ceiling": {"waves_per_simd": FILL_WAVES_PER_SIMD, "cpi_dual_rate_ops": round(cpi_dual, 3),
-                       "cpi_other_ops": round(cpi_rest, 3), "dual_rate_fraction_of_fill_valu": round(f_dual, 4),
+                       "cpi_other_ops": round(cpi_rest, 3), "dual_rate_forms": sorted(dual_names),
+                       "dual_rate_fraction_of_fill_valu": round(f_dual, 4),
                        "cpi_fill_mix": round(cpi, 3), "isa_mix": os.path.relpath(mix_path, ROOT),
                        "probe": "valu_probe (chip wall time x clock x SIMDs / instructions)"}}
     for case in ("planes", "noplanes"):
