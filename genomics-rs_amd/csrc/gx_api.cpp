@@ -39,6 +39,10 @@ hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, 
                             int floor_, int gshift, int row0, int rows, hipStream_t st);
 hipError_t launch_plane_sums(const PairDev* d_pairs, int npairs, int max_strips, int lay, int mode, int h, int g,
                              int floor_, int gshift, unsigned long long* out, hipStream_t st);
+hipError_t launch_fill_wide(const WideDev* d_pairs, int npairs, WideScores sc, WideRes* d_res, int local, int track,
+                            hipStream_t st);
+hipError_t launch_wide_plane_sums(const int64_t* pI, const int64_t* pD, const int64_t* pS, int n, int m,
+                                  unsigned long long* out, hipStream_t st);
 }  // namespace gx
 
 using namespace gx;
@@ -383,25 +387,40 @@ struct HostScores {
 static int64_t wadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
 static int64_t wmul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
 
-static int check_scores(const gx_scores* s, size_t n, size_t m, HostScores* hs, Scores32* sc, int is_local) {
+// `wide` (may be NULL): set when the job is outside the exact-int32 range of
+// the main fill and must take the int64 fill (gx_wide.hip) instead; with
+// wide == NULL such a job is refused with GX_ERANGE.
+static int check_scores(const gx_scores* s, size_t n, size_t m, HostScores* hs, Scores32* sc, int is_local,
+                        bool* wide = nullptr) {
     if (!s) return fail(GX_EINVAL, "scores is NULL");
     hs->sm = s->s_match; hs->smm = s->s_mismatch; hs->g = s->g; hs->h = s->h;
-    const int64_t lim = (int64_t)1 << 24;
-    if (llabs(s->s_match) > lim || llabs(s->s_mismatch) > lim || llabs(s->g) > lim || llabs(s->h) > lim)
-        return fail(GX_ERANGE, "score magnitudes above 2^24 are outside the exact int32 device range");
-    const int64_t gh = s->g + s->h;
-    hs->neg_inf = wadd(INT64_MIN, gh < 0 ? -gh : gh);
+    const uint64_t ugh = (uint64_t)s->g + (uint64_t)s->h;   // g + h as the reference's release build adds it
+    const int64_t gh = (int64_t)ugh;
+    hs->neg_inf = wadd(INT64_MIN, gh < 0 ? (int64_t)(0 - ugh) : gh);
+    if (wide) *wide = false;
+    if (n >= (size_t)1 << 30 || m >= (size_t)1 << 30) return fail(GX_ERANGE, "sequence longer than 2^30");
+    const char* why = nullptr;
+    const uint64_t lim = (uint64_t)1 << 24;
+    auto mag = [](int64_t v) { return v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v; };
+    if (mag(s->s_match) > lim || mag(s->s_mismatch) > lim || mag(s->g) > lim || mag(s->h) > lim)
+        why = "score magnitudes above 2^24 are outside the exact int32 device range";
     // The reference adds g and h+g to neg_inf at the boundary; when that
     // wraps (possible only for g < 0 < h with |g+h| < |g|) its release build
     // produces wrapped giants that the int32 path cannot reproduce.
-    if (s->g < 0 && llabs(gh) < llabs(s->g))
-        return fail(GX_ERANGE, "g < 0 < h with |g+h| < |g|: the reference's boundary arithmetic wraps");
-    // every interior magnitude <= (n + m + 2) * (|sm| + |smm| + |g| + |h|) + |h|
-    const double bound = (double)(n + m + 2) * (double)(llabs(s->s_match) + llabs(s->s_mismatch) + llabs(s->g) +
-                                                        llabs(s->h)) + (double)llabs(s->h);
-    if (bound >= (double)(1 << 28))
-        return fail(GX_ERANGE, "|score| bound exceeds 2^28: outside the exact int32 device range");
-    if (n > (size_t)1 << 26 || m > (size_t)1 << 26) return fail(GX_ERANGE, "sequence longer than 2^26");
+    else if (s->g < 0 && mag(gh) < mag(s->g))
+        why = "g < 0 < h with |g+h| < |g|: the reference's boundary arithmetic wraps";
+    else {
+        // every interior magnitude <= (n + m + 2) * (|sm| + |smm| + |g| + |h|) + |h|
+        const double bound = (double)(n + m + 2) * (double)(mag(s->s_match) + mag(s->s_mismatch) + mag(s->g) +
+                                                            mag(s->h)) + (double)mag(s->h);
+        if (bound >= (double)(1 << 28)) why = "|score| bound exceeds 2^28: outside the exact int32 device range";
+        else if (n > (size_t)1 << 26 || m > (size_t)1 << 26) why = "sequence longer than 2^26";
+    }
+    if (why) {
+        if (!wide) return fail(GX_ERANGE, why);
+        *wide = true;   // the int64 fill computes it
+        return GX_OK;
+    }
     sc->sm = (int)s->s_match; sc->smm = (int)s->s_mismatch; sc->g = (int)s->g; sc->h = (int)s->h;
     sc->hg = (int)(s->h + s->g);
     sc->floor_ = is_local ? 0 : kNeg;
@@ -574,6 +593,11 @@ struct FillJob {
     bool shift = false;                 // values kept as V - (i + j) g (Scores32.shift)
     int g = 0;
     double fill_ms = 0.0;
+    // the int64 fill (gx_wide.hip): its own buffers and results
+    bool wide = false;
+    DevBuf wrows, wdesc, wres_d;
+    std::vector<WideDev> wd;
+    std::vector<WideRes> wres;
 };
 
 // Shifted fills (Scores32.shift) report score_max(n, m) as H - (n + m) g.
@@ -587,6 +611,7 @@ static void job_release(gx_context* ctx, FillJob& j) {
     pool_put(ctx, j.chars); pool_put(ctx, j.planes); pool_put(ctx, j.codes); pool_put(ctx, j.feed);
     pool_put(ctx, j.progress); pool_put(ctx, j.sres); pool_put(ctx, j.pres); pool_put(ctx, j.pairs);
     pool_put(ctx, j.counter); pool_put(ctx, j.skel);
+    pool_put(ctx, j.wrows); pool_put(ctx, j.wdesc); pool_put(ctx, j.wres_d);
 }
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -822,6 +847,104 @@ static int fill_collect(gx_context* ctx, FillJob& job) {
     return GX_OK;
 }
 
+// The int64 fill (gx_wide.hip) of jobs outside the exact-int32 range: one
+// wave per pair, outputs in the column-step layout's code / skeleton formats
+// (job.lay = 1), int64 planes row-major.  Synchronous.
+static int run_fill_wide(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc,
+                         const std::vector<PairHost>& ph, const HostScores& hs, int is_local, bool planes, bool track,
+                         bool lcs, FillJob& job) {
+    const size_t P = ph.size();
+    job.wide = true;
+    job.lay = 1;
+    job.W = 1;
+    lcs = lcs && planes;
+    track = track || lcs;
+    job.planes_on = planes; job.lcs_on = lcs; job.track_on = track;
+    ctx->last_lay = 1; ctx->last_W = 1; ctx->last_pbytes = planes ? 24 : 0;
+    job.pd.assign(P, PairDev{});
+    job.wd.assign(P, WideDev{});
+    size_t chars = 0, codes = 0, skel = 0, rows = 0, cells = 0;
+    std::vector<size_t> c1o(P), c2o(P), co(P), so(P), ro(P), po(P);
+    for (size_t p = 0; p < P; ++p) {
+        const int n = (int)ph[p].n, m = (int)ph[p].m;
+        PairDev& d = job.pd[p];
+        d.n = n; d.m = m;
+        d.strips = ceil_div(n, kStripRows1);
+        d.t16 = ceil_div(m + 1, 16);
+        d.t4 = d.t16 * 4;
+        d.skel_stride = (int)align_up((size_t)m + 1, 64);
+        c1o[p] = chars; chars += align_up(n, 64);
+        c2o[p] = chars; chars += align_up(m, 64);
+        co[p] = codes; codes += (size_t)d.strips * d.t16 * kWave;
+        so[p] = skel; skel += (size_t)d.strips * d.skel_stride;
+        ro[p] = rows; rows += (size_t)d.strips * (m + 1);
+        po[p] = cells; cells += (size_t)n * m;
+    }
+    int rc;
+    if ((rc = pool_get(ctx, std::max<size_t>(chars, 1), &job.chars)) ||
+        (rc = pool_get(ctx, std::max<size_t>(codes, 1) * sizeof(uint32_t), &job.codes)) ||
+        (rc = pool_get(ctx, std::max<size_t>(skel, 1) * sizeof(int), &job.skel)) ||
+        (rc = pool_get(ctx, std::max<size_t>(rows, 1) * sizeof(WideRow), &job.wrows)) ||
+        (rc = pool_get(ctx, P * sizeof(WideDev), &job.wdesc)) || (rc = pool_get(ctx, P * sizeof(WideRes), &job.wres_d)))
+        return rc;
+    const size_t nplane = lcs ? 3 * sizeof(int64_t) + sizeof(unsigned) : 3 * sizeof(int64_t);
+    if (planes && (rc = pool_get(ctx, std::max<size_t>(cells, 1) * nplane, &job.planes))) return rc;
+    std::vector<uint8_t> hc(std::max<size_t>(chars, 1), 0);
+    for (size_t p = 0; p < P; ++p) {
+        if (ph[p].n) memcpy(&hc[c1o[p]], proc[p].first, ph[p].n);
+        if (ph[p].m) memcpy(&hc[c2o[p]], proc[p].second, ph[p].m);
+    }
+    for (size_t p = 0; p < P; ++p) {
+        PairDev& d = job.pd[p];
+        WideDev& w = job.wd[p];
+        d.codes = (uint32_t*)job.codes.p + co[p];
+        d.skel = (int*)job.skel.p + so[p];
+        w.c1 = (const uint8_t*)job.chars.p + c1o[p];
+        w.c2 = (const uint8_t*)job.chars.p + c2o[p];
+        w.n = d.n; w.m = d.m; w.strips = d.strips; w.t16 = d.t16;
+        w.codes = d.codes; w.skel = d.skel; w.skel_stride = d.skel_stride;
+        w.rows = (WideRow*)job.wrows.p + ro[p];
+        if (planes) {
+            int64_t* base = (int64_t*)job.planes.p;
+            w.pI = (long long*)(base + po[p]);
+            w.pD = (long long*)(base + cells + po[p]);
+            w.pS = (long long*)(base + 2 * cells + po[p]);
+            w.pL = lcs ? (unsigned*)(base + 3 * cells) + po[p] : nullptr;
+        }
+    }
+    HIPCHK(hipMemcpyAsync(job.chars.p, hc.data(), hc.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(job.wdesc.p, job.wd.data(), P * sizeof(WideDev), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemsetAsync(job.wres_d.p, 0, P * sizeof(WideRes), ctx->stream));
+    const WideScores ws{hs.sm, hs.smm, hs.g, hs.h, hs.neg_inf};
+    HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+    HIPCHK(launch_fill_wide((const WideDev*)job.wdesc.p, (int)P, ws, (WideRes*)job.wres_d.p, is_local ? 1 : 0,
+                            track ? 1 : 0, ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+    if (ctx->sums_dst && planes) {   // staged checksum run
+        for (size_t p = 0; p < P; ++p) {
+            HIPCHK(launch_wide_plane_sums((const int64_t*)job.wd[p].pI, (const int64_t*)job.wd[p].pD,
+                                          (const int64_t*)job.wd[p].pS, job.wd[p].n, job.wd[p].m, ctx->sums_dst,
+                                          ctx->stream));
+            ctx->sums_dst += 3;
+        }
+    }
+    job.wres.assign(P, WideRes{});
+    HIPCHK(hipMemcpyAsync(job.wres.data(), job.wres_d.p, P * sizeof(WideRes), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    job.fill_ms = ms;
+    // the traceback's start columns and the tables' max cell in the PairRes view
+    job.res.assign(P, PairRes{});
+    for (size_t p = 0; p < P; ++p) {
+        job.res[p].max_i = job.wres[p].max_i; job.res[p].max_j = job.wres[p].max_j;
+        job.res[p].mam = (int)job.wres[p].mam;
+        job.res[p].lmax_i = job.wres[p].lmax_i; job.res[p].lmax_j = job.wres[p].lmax_j;
+        job.res[p].end_E = job.wres[p].end_E; job.res[p].lmax_E = job.wres[p].lmax_E;
+    }
+    return GX_OK;
+}
+
 // ---------------------------------------------------------------------------
 // tables
 
@@ -836,7 +959,19 @@ struct gx_table {
     uint32_t flags = 0;
 };
 
-static int start_cell(const gx_table* t, const PairRes& r, uint64_t* si, uint64_t* sj, int64_t* score);
+// What the start cell search needs from a fill's results (int32 or int64 fill).
+struct StartIn {
+    int64_t end_SM, lmax_val;
+    uint64_t lmax_i, lmax_j;
+};
+static StartIn start_in(const FillJob& job, size_t p) {
+    if (job.wide) return StartIn{job.wres[p].end_SM, job.wres[p].lmax_val, (uint64_t)job.wres[p].lmax_i,
+                                 (uint64_t)job.wres[p].lmax_j};
+    const PairRes& r = job.res[p];
+    return StartIn{r.end_SM, r.lmax_val, (uint64_t)r.lmax_i, (uint64_t)r.lmax_j};
+}
+static StartIn start_in(const PairRes& r) { return StartIn{r.end_SM, r.lmax_val, (uint64_t)r.lmax_i, (uint64_t)r.lmax_j}; }
+static int start_cell(const gx_table* t, const StartIn& r, uint64_t* si, uint64_t* sj, int64_t* score);
 
 
 static bool tb_match(const uint8_t* s1, size_t n, const uint8_t* s2, size_t m, uint64_t i, uint64_t j) {
@@ -1085,7 +1220,7 @@ struct RecordsSrc {
 
 
 // Start cell + score (algo.rs:306-331).
-static int start_cell_common(const HostScores& hs, int is_local, size_t n, size_t m, const PairRes& r,
+static int start_cell_common(const HostScores& hs, int is_local, size_t n, size_t m, const StartIn& r,
                              uint64_t* si, uint64_t* sj, int64_t* score) {
     if (!is_local) {
         *si = n; *sj = m;
@@ -1113,12 +1248,12 @@ static int start_cell_common(const HostScores& hs, int is_local, size_t n, size_
         boundary_cell(hs, i, 0, &I, &D, &S);
         consider(smax(I, S, D, 1), i, 0);
     }
-    if (n >= 1 && m >= 1) consider(r.lmax_val, (uint64_t)r.lmax_i, (uint64_t)r.lmax_j);
+    if (n >= 1 && m >= 1) consider(r.lmax_val, r.lmax_i, r.lmax_j);
     *si = bi; *sj = bj; *score = best;
     return GX_OK;
 }
 
-static int start_cell(const gx_table* t, const PairRes& r, uint64_t* si, uint64_t* sj, int64_t* score) {
+static int start_cell(const gx_table* t, const StartIn& r, uint64_t* si, uint64_t* sj, int64_t* score) {
     return start_cell_common(t->hs, t->is_local, t->s1.size(), t->s2.size(), r, si, sj, score);
 }
 
@@ -1133,7 +1268,8 @@ extern "C" int gx_alignment_table(gx_context* ctx, const uint8_t* s1, size_t n, 
     t->ctx = ctx;
     t->is_local = is_local;
     t->flags = flags;
-    int rc = check_scores(scores, n, m, &t->hs, &t->sc, is_local);
+    bool wide = false;
+    int rc = check_scores(scores, n, m, &t->hs, &t->sc, is_local, &wide);
     if (!rc) rc = processed_chars(s1, n, s2, m, reverse_sequences, t->c1, t->c2);
     if (rc) { delete t; return rc; }
     t->s1.assign(s1, s1 + n);
@@ -1146,7 +1282,8 @@ extern "C" int gx_alignment_table(gx_context* ctx, const uint8_t* s1, size_t n, 
     const bool planes = (flags & (GX_TABLE_PLANES | GX_TABLE_MATCHES)) != 0;
     const bool lcs = (flags & GX_TABLE_MATCHES) != 0;
     if (n >= 1 && m >= 1) {
-        rc = run_fill(ctx, proc, ph, t->sc, is_local, planes, matches_at_max != nullptr, lcs, t->job);
+        rc = wide ? run_fill_wide(ctx, proc, ph, t->hs, is_local, planes, matches_at_max != nullptr, lcs, t->job)
+                  : run_fill(ctx, proc, ph, t->sc, is_local, planes, matches_at_max != nullptr, lcs, t->job);
         if (rc) { job_release(ctx, t->job); delete t; return rc; }
     } else {
         t->job.res.assign(1, PairRes{});
@@ -1156,7 +1293,8 @@ extern "C" int gx_alignment_table(gx_context* ctx, const uint8_t* s1, size_t n, 
     if (log_info())
         fprintf(stderr, "[gx INFO] Table initialization complete, time taken: %lldus\n",
                 (long long)(t->job.fill_ms * 1000.0));
-    if (matches_at_max) *matches_at_max = (n >= 1 && m >= 1) ? (uint64_t)t->job.res[0].mam : 0;
+    if (matches_at_max)
+        *matches_at_max = (n >= 1 && m >= 1) ? (t->job.wide ? t->job.wres[0].mam : (uint64_t)t->job.res[0].mam) : 0;
     *table_out = t;
     return GX_OK;
 }
@@ -1207,13 +1345,42 @@ static int fetch_plane32(const gx_table* t, int which, std::vector<int32_t>& out
     return fetch_rows32(t, which, 0, t->s1.size() + 1, out);
 }
 
+// The int64 fill's planes: rows row0 .. row0 + rows - 1 of plane `which`
+// (0-2; 3 = the LCS plane) as int64, rows x (m+1) (column 0 and row 0 undefined).
+static int fetch_rows_wide(const gx_table* t, int which, size_t row0, size_t rows, std::vector<int64_t>& out) {
+    const size_t n = t->s1.size(), m = t->s2.size();
+    out.assign(rows * (m + 1), 0);
+    if (n == 0 || m == 0 || rows == 0) return GX_OK;
+    const WideDev& w = t->job.wd[0];
+    if (!w.pI || (which == 3 && !w.pL))
+        return fail(GX_EINVAL, "plane not kept: build the table with GX_TABLE_PLANES / GX_TABLE_MATCHES");
+    const size_t i0 = std::max<size_t>(row0, 1), i1 = std::min(row0 + rows, n + 1);
+    if (i1 <= i0) return GX_OK;
+    std::vector<int64_t> tmp((i1 - i0) * m);
+    std::vector<unsigned> tl;
+    hipError_t e;
+    if (which == 3) {
+        tl.resize((i1 - i0) * m);
+        e = hipMemcpy(tl.data(), w.pL + (i0 - 1) * m, tl.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
+        for (size_t k = 0; k < tl.size(); ++k) tmp[k] = tl[k];
+    } else {
+        const long long* src = which == 0 ? w.pI : which == 1 ? w.pD : w.pS;
+        e = hipMemcpy(tmp.data(), src + (i0 - 1) * m, tmp.size() * sizeof(int64_t), hipMemcpyDeviceToHost);
+    }
+    if (e != hipSuccess) return fail(GX_EHIP, std::string("export: ") + hipGetErrorString(e));
+    for (size_t i = i0; i < i1; ++i)
+        memcpy(&out[(i - row0) * (m + 1) + 1], &tmp[(i - i0) * m], m * sizeof(int64_t));
+    return GX_OK;
+}
+
 // Rows row0 .. row0 + rows - 1 of plane `which` as int64 into out (row-major
 // rows x (m+1), or column-major with leading dimension ld_rows when colmajor).
 static int export_rows(const gx_table* t, int which, size_t row0, size_t rows, int64_t* out, int colmajor,
                        size_t ld_rows) {
     const size_t m = t->s2.size();
     std::vector<int32_t> p32;
-    int rc = fetch_rows32(t, which, row0, rows, p32);
+    std::vector<int64_t> p64;
+    int rc = t->job.wide ? fetch_rows_wide(t, which, row0, rows, p64) : fetch_rows32(t, which, row0, rows, p32);
     if (rc) return rc;
     for (size_t r = 0; r < rows; ++r) {
         const size_t i = row0 + r;
@@ -1224,7 +1391,7 @@ static int export_rows(const gx_table* t, int which, size_t row0, size_t rows, i
                 boundary_cell(t->hs, i, j, &I, &D, &S);
                 v = which == 0 ? I : which == 1 ? D : S;
             } else {
-                v = p32[r * (m + 1) + j];
+                v = t->job.wide ? p64[r * (m + 1) + j] : p32[r * (m + 1) + j];
             }
             out[colmajor ? r + j * ld_rows : r * (m + 1) + j] = v;
         }
@@ -1269,7 +1436,7 @@ extern "C" int gx_table_plane_sums(const gx_table* t, uint64_t* sums) {
     const size_t n = t->s1.size(), m = t->s2.size();
     sums[0] = sums[1] = sums[2] = 0;
     if (n == 0 || m == 0) return GX_OK;
-    if (!t->job.pd[0].pI)
+    if (t->job.wide ? !t->job.wd[0].pI : !t->job.pd[0].pI)
         return fail(GX_EINVAL, "planes not kept: build the table with GX_TABLE_PLANES / GX_TABLE_MATCHES");
     gx_context* ctx = t->ctx;
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1277,7 +1444,10 @@ extern "C" int gx_table_plane_sums(const gx_table* t, uint64_t* sums) {
     DevBuf buf;
     int rc = pool_get(ctx, 3 * sizeof(unsigned long long), &buf);
     if (rc) return rc;
-    hipError_t e = enqueue_plane_sums(ctx, t->job, t->sc, (unsigned long long*)buf.p);
+    const WideDev* w = t->job.wide ? &t->job.wd[0] : nullptr;
+    hipError_t e = w ? launch_wide_plane_sums((const int64_t*)w->pI, (const int64_t*)w->pD, (const int64_t*)w->pS,
+                                              w->n, w->m, (unsigned long long*)buf.p, ctx->stream)
+                     : enqueue_plane_sums(ctx, t->job, t->sc, (unsigned long long*)buf.p);
     if (e == hipSuccess) e = hipMemcpyAsync(sums, buf.p, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     pool_put(ctx, buf);
@@ -1291,10 +1461,37 @@ extern "C" int gx_table_export(const gx_table* t, gx_cell* out, size_t out_cells
     if (out_cells < (n + 1) * (m + 1)) return fail(GX_ECAP, "out too small");
     std::lock_guard<std::mutex> lk(t->ctx->mu);
     HIPCHK(hipSetDevice(t->ctx->device));
-    std::vector<int32_t> pI, pD, pS, pL;
-    int rc;
-    if ((rc = fetch_plane32(t, 0, pI)) || (rc = fetch_plane32(t, 1, pD)) || (rc = fetch_plane32(t, 2, pS))) return rc;
     const bool have_l = t->job.lcs_on;
+    int rc;
+    if (t->job.wide) {   // int64 planes (gx_wide.hip)
+        std::vector<int64_t> wI, wD, wS, wL;
+        if ((rc = fetch_rows_wide(t, 0, 0, n + 1, wI)) || (rc = fetch_rows_wide(t, 1, 0, n + 1, wD)) ||
+            (rc = fetch_rows_wide(t, 2, 0, n + 1, wS)))
+            return rc;
+        if (have_l && (rc = fetch_rows_wide(t, 3, 0, n + 1, wL))) return rc;
+        auto Lw = [&](size_t i, size_t j) -> uint64_t {
+            return (i == 0 || j == 0 || !have_l) ? 0 : (uint64_t)wL[i * (m + 1) + j];
+        };
+        for (size_t i = 0; i <= n; ++i)
+            for (size_t j = 0; j <= m; ++j) {
+                gx_cell c{};
+                if (i == 0 || j == 0) {
+                    boundary_cell(t->hs, i, j, &c.insert_score, &c.delete_score, &c.sub_score);
+                } else {
+                    const size_t o = i * (m + 1) + j;
+                    c.insert_score = wI[o]; c.delete_score = wD[o]; c.sub_score = wS[o];
+                    if (have_l) {
+                        c.insert_matches = Lw(i, j - 1);
+                        c.delete_matches = Lw(i - 1, j);
+                        c.sub_matches = Lw(i - 1, j - 1) + (t->c1[i - 1] == t->c2[j - 1] ? 1 : 0);
+                    }
+                }
+                out[i + j * (n + 1)] = c;
+            }
+        return GX_OK;
+    }
+    std::vector<int32_t> pI, pD, pS, pL;
+    if ((rc = fetch_plane32(t, 0, pI)) || (rc = fetch_plane32(t, 1, pD)) || (rc = fetch_plane32(t, 2, pS))) return rc;
     if (have_l && (rc = fetch_plane32(t, 3, pL))) return rc;
     auto L = [&](size_t i, size_t j) -> uint64_t {
         if (i == 0 || j == 0 || !have_l) return 0;
@@ -1351,7 +1548,7 @@ extern "C" int gx_retrace(gx_table* t, int is_local, gx_step* steps, size_t cap,
         uint64_t si, sj;
         int64_t score;
         const PairRes r = t->job.res[0];
-        start_cell(t, r, &si, &sj, &score);
+        start_cell(t, start_in(t->job, 0), &si, &sj, &score);
         if (log_info()) fprintf(stderr, "[gx INFO] Starting at (%llu, %llu)\n", (unsigned long long)si,
                                 (unsigned long long)sj);
         TbOut tb;
@@ -1484,6 +1681,50 @@ static int label_batch(gx_context* ctx, const std::vector<PairHost>& ph, const H
     return GX_OK;
 }
 
+// A batch through the int64 fill (jobs outside the exact-int32 range): fill,
+// host start cells, device traceback, host labelling.  Synchronous, one pass.
+static int batch_core_wide(gx_context* ctx, const std::vector<PairHost>& ph,
+                           const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc, const HostScores& hs,
+                           int is_local, bool planes, bool track, std::vector<Walk>& walks, double* fill_ms) {
+    const size_t P = ph.size();
+    std::vector<size_t> idx;
+    for (size_t p = 0; p < P; ++p) if (ph[p].n >= 1 && ph[p].m >= 1) idx.push_back(p);
+    std::vector<PairHost> dph;
+    std::vector<std::pair<const uint8_t*, const uint8_t*>> dproc;
+    for (size_t p : idx) { dph.push_back(ph[p]); dproc.push_back(proc[p]); }
+    FillJob job;
+    std::vector<PairRes> res(P, PairRes{});
+    std::vector<StartIn> sin(P, StartIn{0, 0, 0, 0});
+    std::vector<uint64_t> si(P), sj(P);
+    std::vector<int64_t> score(P);
+    TbOut& tb = ctx->tb_cache;
+    tb.ms = 0;
+    int rc = GX_OK;
+    if (!idx.empty()) {
+        rc = run_fill_wide(ctx, dproc, dph, hs, is_local, planes, track, false, job);
+        if (rc) { job_release(ctx, job); return rc; }
+        for (size_t k = 0; k < idx.size(); ++k) { res[idx[k]] = job.res[k]; sin[idx[k]] = start_in(job, k); }
+    }
+    for (size_t p = 0; p < P; ++p) start_cell_common(hs, is_local, ph[p].n, ph[p].m, sin[p], &si[p], &sj[p], &score[p]);
+    if (!idx.empty()) {
+        std::vector<TbStart> starts(idx.size());
+        for (size_t k = 0; k < idx.size(); ++k) {
+            const size_t p = idx[k];
+            starts[k] = (si[p] >= 1 && sj[p] >= 1)
+                            ? TbStart{(int)si[p], (int)sj[p], is_local ? res[p].lmax_E : res[p].end_E}
+                            : TbStart{0, 0, 0};
+        }
+        rc = run_traceback(ctx, job, starts, tb);
+    }
+    if (fill_ms) *fill_ms = job.fill_ms;
+    const double fms = job.fill_ms;
+    job_release(ctx, job);
+    if (rc) return rc;
+    std::vector<int> dev_of(P, -1);
+    for (size_t k = 0; k < idx.size(); ++k) dev_of[idx[k]] = (int)k;
+    return label_batch(ctx, ph, hs, is_local, track, dev_of, si, sj, score, res, tb, fms, walks);
+}
+
 static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
                       const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc, const HostScores& hs,
                       const Scores32& sc, int is_local, bool planes, bool track, std::vector<Walk>& walks,
@@ -1524,7 +1765,7 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
         for (size_t k = 0; k < idx.size(); ++k) res[idx[k]] = job.res[k];
     }
     const auto c1 = clk::now();
-    for (size_t p = 0; p < P; ++p) start_cell_common(hs, is_local, ph[p].n, ph[p].m, res[p], &si[p], &sj[p], &score[p]);
+    for (size_t p = 0; p < P; ++p) start_cell_common(hs, is_local, ph[p].n, ph[p].m, start_in(res[p]), &si[p], &sj[p], &score[p]);
     if (!idx.empty()) {
         for (size_t k = 0; k < idx.size(); ++k) {
             const size_t p = idx[k];
@@ -1621,7 +1862,7 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
         fsum += jobs[s].fill_ms;
         for (size_t q = 0; q < idx.size(); ++q) res[idx[q]] = jobs[s].res[q];
         for (size_t p = 0; p < P; ++p)
-            start_cell_common(hs, is_local, ph[p].n, ph[p].m, res[p], &si[p], &sj[p], &score[p]);
+            start_cell_common(hs, is_local, ph[p].n, ph[p].m, start_in(res[p]), &si[p], &sj[p], &score[p]);
         for (size_t q = 0; q < idx.size(); ++q) {
             const size_t p = idx[q];
             starts[q] = (si[p] >= 1 && sj[p] >= 1)
@@ -1654,7 +1895,7 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
             fsum += jobs[s].fill_ms;
             for (size_t q = 0; q < idx.size(); ++q) res[idx[q]] = jobs[s].res[q];
             for (size_t p = 0; p < P; ++p)
-                start_cell_common(hs, is_local, ph[p].n, ph[p].m, res[p], &si[p], &sj[p], &score[p]);
+                start_cell_common(hs, is_local, ph[p].n, ph[p].m, start_in(res[p]), &si[p], &sj[p], &score[p]);
             return GX_OK;
         };
         using clk = std::chrono::steady_clock;
@@ -1725,7 +1966,8 @@ extern "C" int gx_align_batch(gx_context* ctx, const uint8_t* const* s1, const s
     for (size_t p = 0; p < npairs; ++p) { nmax = std::max(nmax, n[p]); mmax = std::max(mmax, m[p]); }
     HostScores hs;
     Scores32 sc;
-    int rc = check_scores(scores, nmax, mmax, &hs, &sc, is_local);
+    bool wide = false;
+    int rc = check_scores(scores, nmax, mmax, &hs, &sc, is_local, &wide);
     if (rc) return rc;
     std::vector<PairHost> ph(npairs);
     std::vector<std::pair<const uint8_t*, const uint8_t*>> proc(npairs);
@@ -1740,7 +1982,8 @@ extern "C" int gx_align_batch(gx_context* ctx, const uint8_t* const* s1, const s
     for (const auto& c : chunks) {
         std::vector<PairHost> phc(ph.begin() + c.first, ph.begin() + c.second);
         std::vector<std::pair<const uint8_t*, const uint8_t*>> pc(proc.begin() + c.first, proc.begin() + c.second);
-        rc = batch_core(ctx, phc, pc, hs, sc, is_local, false, (flags & GX_ALIGN_MAX_CELL) != 0, walks, nullptr);
+        rc = wide ? batch_core_wide(ctx, phc, pc, hs, is_local, false, (flags & GX_ALIGN_MAX_CELL) != 0, walks, nullptr)
+                  : batch_core(ctx, phc, pc, hs, sc, is_local, false, (flags & GX_ALIGN_MAX_CELL) != 0, walks, nullptr);
         if (rc) return rc;
         for (size_t k = 0; k < phc.size(); ++k) {
             const size_t p = c.first + k;
@@ -1799,7 +2042,8 @@ extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int
     for (size_t p = 0; p < P; ++p) { nmax = std::max(nmax, ctx->st_s1[p].size()); mmax = std::max(mmax, ctx->st_s2[p].size()); }
     HostScores hs;
     Scores32 sc;
-    int rc = check_scores(scores, nmax, mmax, &hs, &sc, is_local);
+    bool wide = false;
+    int rc = check_scores(scores, nmax, mmax, &hs, &sc, is_local, &wide);
     if (rc) return rc;
     std::vector<PairHost> ph(P);
     std::vector<std::pair<const uint8_t*, const uint8_t*>> proc(P);
@@ -1808,6 +2052,50 @@ extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int
         proc[p] = {ph[p].s1, ph[p].s2};
     }
     const bool track = (flags & GX_ALIGN_MAX_CELL) != 0;
+    if (wide) {   // int64 fill: one synchronous pass at a time (a rare path, no pipelining or chunking)
+        std::vector<Walk>& walks = ctx->walk_cache;
+        const int passes = std::max(nsteps, 1);
+        const bool want_sums = (flags & GX_STAGED_PLANE_SUMS) && keep_planes;
+        size_t nint = 0;
+        for (size_t p = 0; p < P; ++p) nint += (ph[p].n >= 1 && ph[p].m >= 1);
+        ctx->sums_host.clear();
+        if (want_sums && nint) {
+            const size_t bytes = (size_t)passes * nint * 3 * sizeof(unsigned long long);
+            if (ctx->sums_dev.cap < bytes) {
+                if (ctx->sums_dev.p) (void)hipFree(ctx->sums_dev.p);
+                ctx->sums_dev = DevBuf{};
+                HIPCHK(hipMalloc(&ctx->sums_dev.p, bytes));
+                ctx->sums_dev.cap = bytes;
+            }
+            ctx->sums_dst = (unsigned long long*)ctx->sums_dev.p;
+        }
+        double fsum = 0;
+        for (int k = 0; k < passes && !rc; ++k) {
+            double f = 0;
+            rc = batch_core_wide(ctx, ph, proc, hs, is_local, keep_planes != 0, track, walks, &f);
+            fsum += f;
+        }
+        ctx->sums_dst = nullptr;
+        ctx->last_chunks = 1;
+        if (rc) return rc;
+        if (want_sums) {
+            ctx->sums_host.assign((size_t)passes * P * 3, 0);
+            if (nint) {
+                std::vector<uint64_t> dev((size_t)passes * nint * 3);
+                HIPCHK(hipMemcpy(dev.data(), ctx->sums_dev.p, dev.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+                size_t r = 0;
+                for (int k = 0; k < passes; ++k)
+                    for (size_t p = 0; p < P; ++p)
+                        if (ph[p].n >= 1 && ph[p].m >= 1) {
+                            for (int c = 0; c < 3; ++c) ctx->sums_host[((size_t)k * P + p) * 3 + c] = dev[r * 3 + c];
+                            ++r;
+                        }
+            }
+        }
+        for (size_t p = 0; p < P; ++p) out[p] = walks[p].res;
+        if (fill_ms_out) *fill_ms_out = fsum / passes;
+        return GX_OK;
+    }
     std::vector<Walk>& walks = ctx->walk_cache;
     // GX_STAGED_PLANE_SUMS: every pass's fill is followed by the plane
     // checksum kernel (stream order, before the planes return to the pool)

@@ -140,6 +140,34 @@ struct TbDev {           // per-pair traceback job
     int* end_ij;           // out: [4] {i, j} where the walk leaves the interior, first strip, rounds
 };
 
+// ---- wide (int64) fill (gx_wide.hip): jobs outside the exact-int32 range --
+struct WideScores {
+    long long sm, smm, g, h;
+    long long neg_inf;   // i64::MIN + |g + h| (algo.rs:166)
+};
+struct __attribute__((aligned(8))) WideRow {   // one cell of a strip's bottom row, for the strip below
+    long long dd, sm;    // delete successor score_max(hg, hg, g), score_max(0, 0, 0)
+    unsigned lm, pad;    // max_matches
+};
+struct WideRes {
+    long long max_val, lmax_val, end_SM;
+    unsigned long long mam;
+    int max_i, max_j, lmax_i, lmax_j, lmax_E, end_E, pad0, pad1;
+};
+struct WideDev {
+    const uint8_t* c1;
+    const uint8_t* c2;
+    int n, m, strips, t16;
+    long long* pI;       // int64 planes, row-major n x m interior (nullptr: not kept)
+    long long* pD;
+    long long* pS;
+    unsigned* pL;        // LCS plane (max_matches), or nullptr
+    uint32_t* codes;     // codes[strip][t16][64] (layout-1 format)
+    int* skel;           // [strips][skel_stride]: landing column + 64 of the strip's bottom row
+    WideRow* rows;       // [strips][m + 1] bottom rows
+    int skel_stride, pad;
+};
+
 // Band-boundary progress counters sit 256 B apart: every I/O wave polls its
 // own, and neighbouring counters in one cache line would put all of a
 // batch's polls on one L2 channel.
