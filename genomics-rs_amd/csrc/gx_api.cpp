@@ -1047,7 +1047,12 @@ static int label_walk(const HostScores& hs, int is_local, const uint8_t* s1, siz
             last = GX_DELETE;
             di = true; dj = false;
         } else {
-            if (is_local && mx == 0) break;
+            if (is_local && mx == 0) {
+                if (log_info())   // algo.rs:403
+                    fprintf(stderr, "[gx INFO] Ending local alignment at (%llu, %llu)\n", (unsigned long long)i,
+                            (unsigned long long)j);
+                break;
+            }
             return fail(GX_EPANIC, "Unexpected score during retrace: " + std::to_string(mx) + " at (" +
                                        std::to_string(i) + ", " + std::to_string(j) + ")");
         }

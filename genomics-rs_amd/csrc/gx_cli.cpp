@@ -130,9 +130,8 @@ int run_align(const gx_scores& sc, const std::string& type, const std::string& f
         if (rc != GX_OK) { gx_context_destroy(ctx); return fail_msg("align", rc); }
         fprintf(stderr, "[WARN] Sequence table too large to visualize\n");
     }
-    fprintf(stderr, "[INFO] Table initialization complete, time taken: %lldus\n", (long long)res.fill_us);
-    fprintf(stderr, "[INFO] Retrace complete, time taken: %lldus\n", (long long)res.retrace_us);
-    fprintf(stderr, "[INFO] Retrace alignment size: %llu\n", (unsigned long long)res.n_steps);
+    // (the library logs the table shape, its fill time, the start cell and the
+    // retrace lines of algo.rs:175-179, 274-277, 325, 428-436 under GX_LOG=info)
     fputs(table_txt.c_str(), stdout);
     size_t need_txt = 0;
     gx_format_alignment(s1, n, s2, m, steps.data(), res.n_steps, &res, nullptr, 0, &need_txt);
@@ -287,6 +286,8 @@ int run_all_vs_all(const gx_scores& sc, const std::string& type, const std::stri
 }  // namespace
 
 int main(int argc, char** argv) {
+    // main.rs:91-96: the CLI logs at info unless told otherwise
+    setenv("GX_LOG", getenv("GX_LOG") ? getenv("GX_LOG") : "info", 1);
     std::string config = "config.toml", type, fasta, dir, tsv = "similarity_matrix.tsv", mode;
     int ngpu = 0;
     bool with_self = true;

@@ -16,6 +16,19 @@ int gx_internal_fail(int code, const std::string& msg);  // gx_api.cpp (shared g
 
 namespace {
 int hfail(int code, const std::string& m) { return gx_internal_fail(code, m); }
+// The reference's log::info! / warn! lines on the Display path, on stderr
+// when GX_LOG asks for them (info / debug: both; warn: warnings only) -- the
+// reference's CLI logs at info unless RUST_LOG says otherwise (main.rs:91-96).
+int log_level() {
+    const char* e = getenv("GX_LOG");
+    if (!e) return 0;
+    if (!strcmp(e, "debug")) return 3;
+    if (!strcmp(e, "info")) return 2;
+    if (!strcmp(e, "warn")) return 1;
+    return 0;
+}
+void log_info_line(const std::string& m) { if (log_level() >= 2) fprintf(stderr, "[gx INFO] %s\n", m.c_str()); }
+void log_warn_line(const std::string& m) { if (log_level() >= 1) fprintf(stderr, "[gx WARN] %s\n", m.c_str()); }
 
 // ---- UTF-8 / whitespace helpers (BufRead::lines, str::trim) --------------
 bool utf8_valid(const unsigned char* s, size_t len) {
@@ -330,6 +343,17 @@ extern "C" int gx_format_alignment(const uint8_t* s1, size_t n, const uint8_t* s
                                    size_t n_steps, const gx_result* res, char* out, size_t cap, size_t* needed) {
     if ((!s1 && n) || (!s2 && m) || (!steps && n_steps) || !res) return hfail(GX_EINVAL, "NULL argument");
     const size_t W = 200;  // DISP_MAX_WIDTH (display.rs:7)
+    // display.rs:12-18 (logged once per rendering: the size query of a
+    // two-call use -- out == NULL -- stays silent)
+    if (out) {
+        if (n <= W && m <= W) {
+            log_info_line("Original Sequences:");
+            log_info_line(std::string((const char*)s1, n));
+            log_info_line(std::string((const char*)s2, m));
+        } else {
+            log_warn_line("Sequences are too long to display.");
+        }
+    }
     std::string f, s1o, alo, s2o;
     size_t s1i = 0, s2i = 0, hl = 0, ai = 0;
     while (ai < n_steps) {
@@ -411,6 +435,10 @@ extern "C" int gx_format_table(const uint8_t* s1, size_t n, const uint8_t* s2, s
     if ((!s1 && n) || (!s2 && m) || (!steps && n_steps)) return hfail(GX_EINVAL, "NULL argument");
     const size_t W = 200;  // DISP_MAX_WIDTH (display.rs:7)
     std::string f;
+    if (out) {   // display.rs:139-144
+        if (n < W && m < W * 10) log_info_line("Computing sequence table visualization...");
+        else log_warn_line("Sequence table too large to visualize");
+    }
     if (n < W && m < W * 10) {
         if (!insert_plane || !delete_plane || !sub_plane) return hfail(GX_EINVAL, "NULL score plane");
         // chars().nth(k).unwrap() for k < byte length panics on multi-byte text

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes
 import enum
+import logging
 import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence as Seq, Tuple
@@ -21,6 +22,7 @@ from typing import List, Optional, Sequence as Seq, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+_log = logging.getLogger("gxamd")
 LIB_PATH = os.environ.get("GX_LIB", os.path.join(_HERE, "libgx_amd.so"))
 
 GX_TABLE_PLANES = 1
@@ -408,6 +410,8 @@ def alignment_table(sequence_container: SequenceContainer, scores: Scores, is_lo
     0): the untracked fill, whose score planes are kept in the compact
     byte format (gx_api.cpp d8_planes_ok) when the table is built on layout 0."""
     a, b = _first_two(sequence_container)
+    if len(sequence_container.sequences) > 2:   # algo.rs:161-163
+        _log.warning("More than two sequences found. Only the first two will be used.")
     s1, s2 = a.sequence.encode(), b.sequence.encode()
     ctx = ctx or default_context()
     x, px = _buf(s1)

@@ -218,3 +218,44 @@ def test_plane_bytes_per_cell(gx, scores, local, monkeypatch):
     assert gx.plane_bytes_per_cell(gx.Scores(*scores), local) == _d8_rule(*scores, local)
     monkeypatch.setenv("GX_PLANES32", "1")
     assert gx.plane_bytes_per_cell(gx.Scores(*scores), local) == 12
+
+
+def test_display_log_lines():
+    """display.rs:12-18 and 139-144: the Display and table renderings log the
+    reference's info / warn lines on stderr under GX_LOG (CPU only: the
+    formatting is host code)."""
+    import subprocess
+    import sys
+    code = r'''
+import ctypes, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+import gxamd as gx
+L = gx.lib()
+for n in (5, 300):
+    a = b"A" * n
+    steps = np.zeros(n, gx.STEP_DTYPE)
+    for k in range(n):
+        steps[k]["choice"] = 0; steps[k]["i"] = n - k; steps[k]["j"] = n - k
+    res = gx.CResult(n, n, 0, 0, 0, n, 0, 0, 0, 0, 0, 0, 0)
+    buf = ctypes.create_string_buffer(1 << 16)
+    need = ctypes.c_size_t(0)
+    assert L.gx_format_alignment(a, n, a, n, steps.ctypes.data, n, ctypes.byref(res), buf, len(buf), ctypes.byref(need)) == 0
+    pl = np.zeros((n + 1) * (n + 1), np.int64)
+    L.gx_format_table(a, n, a, n, steps.ctypes.data, n, pl.ctypes.data, pl.ctypes.data, pl.ctypes.data, 0, buf, len(buf), None)
+'''
+    import os
+    from conftest import ROOT
+    env = dict(os.environ, GX_LOG="info")
+    p = subprocess.run([sys.executable, "-c", code, os.path.join(ROOT, "genomics-rs_amd")], capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert p.returncode == 0, p.stderr
+    err = p.stderr
+    assert "[gx INFO] Original Sequences:\n[gx INFO] AAAAA\n[gx INFO] AAAAA\n" in err
+    assert "[gx WARN] Sequences are too long to display." in err
+    assert "[gx INFO] Computing sequence table visualization..." in err
+    assert "[gx WARN] Sequence table too large to visualize" in err
+    env["GX_LOG"] = "off"
+    p = subprocess.run([sys.executable, "-c", code, os.path.join(ROOT, "genomics-rs_amd")], capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert p.returncode == 0 and "[gx " not in p.stderr
