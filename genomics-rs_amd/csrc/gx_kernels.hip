@@ -25,147 +25,10 @@
 #include <limits.h>
 #include "gx_internal.h"
 
+#include "gx_device.h"
+
 namespace gx {
 
-// Explicit address spaces.  Generic (flat) accesses count on both vmcnt and
-// lgkmcnt, so a flat LDS poll would also wait for every outstanding HBM
-// store; LDS counters are therefore AS3 and global words AS1.
-typedef __attribute__((address_space(1))) int gint;
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(3))) volatile int lds_int;
-
-#define DPP_WAVE_SHR1 0x138
-
-__device__ __forceinline__ int shr1(int old, int src) {
-    // lane l <- src[l-1]; lane 0 keeps `old` (bound_ctrl off)
-    return __builtin_amdgcn_update_dpp(old, src, DPP_WAVE_SHR1, 0xF, 0xF, false);
-}
-__device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
-
-__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// Every spin is bounded (~2^25 sleeps, seconds): on expiry the wave records a
-// timeout in *status and carries on, so the grid always drains; the host
-// turns a non-zero status into GX_EHIP.
-constexpr unsigned kSpinLimit = 1u << 25;
-
-__device__ __forceinline__ unsigned wait_ge(lds_int* p, int v, int* status) {
-    unsigned it = 0;
-    for (; *p < v; ++it) {
-        if (it > kSpinLimit) { __hip_atomic_store((gint*)status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    asm volatile("" ::: "memory");
-    return it;
-}
-
-__device__ __forceinline__ int ld_agent(const int* p) {
-    return __hip_atomic_load((gint*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(int* p, int v) {
-    __hip_atomic_store((gint*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ Rec ld_rec_agent(const Rec* p) {
-    const gu64* q = (const gu64*)p;
-    unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    Rec r;
-    r.dd = (int)(a & 0xffffffffu); r.sm = (int)(a >> 32);
-    r.l = (int)(b & 0xffffffffu);  r.c2 = (int)(b >> 32);
-    return r;
-}
-__device__ __forceinline__ void st_rec_agent(Rec* p, Rec r) {
-    gu64* q = (gu64*)p;
-    __hip_atomic_store(q, (unsigned long long)(unsigned)r.dd | ((unsigned long long)(unsigned)r.sm << 32),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 1, (unsigned long long)(unsigned)r.l | ((unsigned long long)(unsigned)r.c2 << 32),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Ring slot of column c.  The producer pushes column c at step c + 63 and the
-// consumer reads it at step c - 1, so with 16-step sub-blocks both touch 16
-// consecutive, 16-aligned slots per sub-block (constant LDS offsets).
-__device__ __forceinline__ int ring_slot(int c) { return (c + 15) & (kRing - 1); }
-
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-    return (uint32_t)(uintptr_t)p;   // low 32 bits of a generic LDS address = LDS offset
-}
-
-// Global-address-space views: stores through them compile to global_store
-// (counted on vmcnt only).  Through a generic pointer they become flat_store,
-// which also counts on lgkmcnt and makes every LDS wait wait for HBM stores.
-typedef int v4i __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) v4i gv4i;
-typedef __attribute__((address_space(1))) uint32_t guint;
-__device__ __forceinline__ void gstore4(int32_t* p, int4 v) {
-    v4i x = {v.x, v.y, v.z, v.w};
-    *(gv4i*)p = x;
-}
-__device__ __forceinline__ void gstore1(uint32_t* p, uint32_t v) { *(guint*)p = v; }
-#ifndef GX_PLANE_AUX
-#define GX_PLANE_AUX 2   // nt: the planes are written once and never read back here
-#endif
-// Plane stores: one 16-B store per lane through a buffer descriptor of the
-// sub-block (uniform base, per-lane offset + immediate; the compiler places
-// the wait states for the SGPR operands).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p, int bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
-}
-__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t voff, int4 v) {
-#ifndef GX_DIAG_NO_PLANES
-    v4i x = {v.x, v.y, v.z, v.w};
-    __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)voff, 0, GX_PLANE_AUX);
-#endif
-}
-
-// Compact planes (plane mode 3, layout 0, global untracked launches whose
-// scores pass the host's range proof, gx_api.cpp d8_planes_ok): per cell one
-// signed byte each of
-//     x_I = I(i,j) - I(i,j-1),  x_S = S(i,j) - I(i,j),  x_D = D(i,j) - I(i,j)
-// in the int32 plane layout with bytes for ints (4 steps of a row = one dword
-// per lane).  The decoder (export_d8_kernel) rebuilds a row with one running
-// sum.  put_byte<K> writes (a - b) into byte K of acc in one VALU op (SDWA,
-// other bytes preserved; byte 0 clears the rest).
-template <int K>
-__device__ __forceinline__ void put_byte(uint32_t& acc, int a, int b) {
-    if constexpr (K == 0)
-        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:DWORD"
-            : "=v"(acc) : "v"(a), "v"(b));
-    else if constexpr (K == 1)
-        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-            : "+v"(acc) : "v"(a), "v"(b));
-    else if constexpr (K == 2)
-        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-            : "+v"(acc) : "v"(a), "v"(b));
-    else
-        asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
-            : "+v"(acc) : "v"(a), "v"(b));
-}
-__device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t v) {
-#ifndef GX_DIAG_NO_PLANES
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, 0, GX_PLANE_AUX);
-#endif
-}
-
-// Per-strip descriptor store: VGPR offset + SGPR soffset + immediate (a
-// group's offset inside the strip's plane), no descriptor SALU per group.
-__device__ __forceinline__ void bstore1_so(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff, uint32_t imm,
-                                           uint32_t v) {
-#ifndef GX_DIAG_NO_PLANES
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)(voff + imm), soff, GX_PLANE_AUX);
-#endif
-}
-#ifndef GX_D8_STRIPDESC
-#define GX_D8_STRIPDESC 0   // 1: compact planes through one descriptor per strip plane (measured
-                            // 0.8 % slower than one per sub-block, profiles/r01n_d8_desc_ab.txt)
-#endif
-
-// Occupancy floor (waves per SIMD), which sets the fill kernel's VGPR cap
-// (512 / floor, at most 256): one workgroup per CU, so the floor is the
-// workgroup's waves per SIMD.  The variants that also track the maxima
-// (first max + LCS, local mode) carry more state per row and get 256 VGPRs
-// (8-wave workgroups at most).
 #ifndef GX_D8_PIPE
 #define GX_D8_PIPE 0   // 1: compact plane stores issued during the next group (9..12-wave
                        // workgroups); measured 2 % slower than storing at the group end
@@ -252,24 +115,6 @@ __device__ __forceinline__ void push63_pub(uint32_t base, const LaneState& st, u
             : "memory");
 }
 
-// Skeleton stores of lane 63's landing columns through a buffer descriptor:
-// every lane issues them, the other lanes' offsets lie past the descriptor's
-// range (kSkelOff) and are dropped by the range check -- no exec switch.
-// Full groups store their four columns at once; ramp groups one per step.
-constexpr uint32_t kSkelOff = 0x40000000u;
-// (GX_DIAG_* builds drop a kind of store, for timing only: tools/strip_pace.py)
-__device__ __forceinline__ void skel_store(__amdgpu_buffer_rsrc_t r, uint32_t voff, int E) {
-#ifndef GX_DIAG_NO_SKEL
-    __builtin_amdgcn_raw_buffer_store_b32(E, r, (int)voff, 0, 0);
-#endif
-}
-__device__ __forceinline__ void skel_store4(__amdgpu_buffer_rsrc_t r, uint32_t voff, int e0, int e1, int e2, int e3) {
-#ifndef GX_DIAG_NO_SKEL
-    v4i x = {e0, e1, e2, e3};
-    __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)voff, 0, 0);
-#endif
-}
-
 constexpr int kPushScratch = 128;   // uint32 per wave: 64 lanes x 4 B + a sub-block's record offsets (252 B)
 // Full-group pushes without an exec switch: every lane writes, lane 63 to
 // the ring slot and the other lanes to their own scratch slots in LDS
@@ -293,48 +138,6 @@ __device__ __forceinline__ void push_all(uint32_t vaddr, const LaneState& st) {
             : "v"(vaddr), "v"(st.b.Dd), "v"(st.b.SM), "v"(st.c2c), "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8)
             : "memory");
 }
-// ... and the ring's write counter (lane 63: the counter; others: scratch)
-__device__ __forceinline__ void publish_all(uint32_t caddr, int cnt) {
-    asm volatile("ds_write_b32 %0, %1" : : "v"(caddr), "v"(cnt) : "memory");
-}
-
-// A wave-uniform pointer forced into an SGPR pair (for "s" asm operands).
-__device__ __forceinline__ const int* uniform_ptr(const int* p) {
-    const uint64_t v = (uint64_t)(uintptr_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return (const int*)(uintptr_t)(((uint64_t)hi << 32) | lo);
-}
-
-// exec mask selecting lane 63 (or no lane), forced into an SGPR pair: the
-// "s" asm operand of the pushes must not be given a VGPR.
-__device__ __forceinline__ unsigned long long lane63_mask(bool on) {
-    return (unsigned long long)__builtin_amdgcn_readfirstlane(on ? 0x80000000u : 0u) << 32;
-}
-
-// One lane stores an LDS counter (exec = lane 0 only, no branch).
-__device__ __forceinline__ void lds_store_lane0(lds_int* p, int v) {
-    asm volatile(
-        "s_mov_b64 exec, 1\n\t"
-        "ds_write_b32 %0, %1\n\t"
-        "s_mov_b64 exec, -1"
-        :
-        : "v"((uint32_t)(uintptr_t)p), "v"(v)
-        : "memory");
-}
-
-// Small-alphabet scoring (TBL): the host maps the job's <= 4 distinct
-// processed bytes to codes 0..3 (Scores32.sym); a row's table holds
-// score(c1, sym[k]) as signed byte k.
-__device__ __forceinline__ int sym_code(int c, const Scores32& sc) {
-    return c == sc.sym[1] ? 1 : c == sc.sym[2] ? 2 : c == sc.sym[3] ? 3 : 0;
-}
-__device__ __forceinline__ int score_table(int c1, const Scores32& sc) {
-    int t = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) t |= ((c1 == sc.sym[k] ? sc.sm : sc.smm) & 0xFF) << (8 * k);
-    return t;
-}
-
 // One cell of the Gotoh recurrence (algo.rs:222-268) for the row in `st`,
 // given the cell above (dd_in = its delete-successor = D(i, j), sm_in =
 // score_max(i-1, j), l_in = max_matches(i-1, j), e_up = its landing column)
