@@ -39,6 +39,8 @@ hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, 
                             int floor_, int gshift, int row0, int rows, hipStream_t st);
 hipError_t launch_plane_sums(const PairDev* d_pairs, int npairs, int max_strips, int lay, int mode, int h, int g,
                              int floor_, int gshift, unsigned long long* out, hipStream_t st);
+hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int ntwins, int total_bands, int* d_counter,
+                          PairRes* d_pres, Scores32 sc, int grid, hipStream_t st);
 hipError_t launch_fill_wide(const WideDev* d_pairs, int npairs, WideScores sc, WideRes* d_res, int local, int track,
                             hipStream_t st);
 hipError_t launch_wide_plane_sums(const int64_t* pI, const int64_t* pD, const int64_t* pS, int n, int m,
@@ -221,6 +223,7 @@ struct gx_context {
     } slots[2];
     int last_lay = 0, last_W = 0, last_pbytes = 0;   // the last fill launch (gx_fill_info)
     int last_chunks = 1;                             // chunks of the last staged / batch call
+    int last_twin = 0;                               // the last fill was the twin (packed 16-bit) fill
     // GX_STAGED_PLANE_SUMS: plane checksums of every pass of a staged run
     DevBuf sums_dev;
     unsigned long long* sums_dst = nullptr;          // where the next fill's checksums go (nullptr: off)
@@ -591,6 +594,7 @@ struct FillJob {
     bool planes_on = false, lcs_on = false, track_on = false;
     bool d8 = false;                    // compact byte planes (d8_planes_ok)
     bool shift = false;                 // values kept as V - (i + j) g (Scores32.shift)
+    bool twin = false;                  // the twin fill (gx_fill_pk.hip): pairs 2q, 2q+1 share every band
     int g = 0;
     double fill_ms = 0.0;
     // the int64 fill (gx_wide.hip): its own buffers and results
@@ -622,6 +626,33 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // matches_at_max, algo.rs:258-262, 279); lcs: also keep the LCS plane.
 static hipError_t enqueue_plane_sums(gx_context* ctx, const FillJob& job, const Scores32& sc, unsigned long long* out);
 
+// The twin fill (gx_fill_pk.hip): two pairs of equal shape per band, one in
+// each 16-bit half.  Its values are kept relative to bases that a band's
+// strips inherit from its top row (see the file header); a value of strip k
+// of a W-strip band lies within D (192 (k + 1) + 16) + 2 (|a| + |smax| + |smin|)
+// of its base, D = max |V''(i,j) - V''(i',j')| over neighbours = max(|a - g|,
+// |U - g|) (the range proof of d8_planes_ok).  Returns the widest admissible
+// band width <= W_want from {4, 8, 15}, or 0 when the twin fill does not apply
+// (shape, mode, scores, GX_TWIN=0).
+static int twin_width(const std::vector<PairHost>& ph, const Scores32& sc, int is_local, bool track, bool lcs, int lay,
+                      bool planes, bool d8, int W_want) {
+    if (const char* e = getenv("GX_TWIN"); e && !strcmp(e, "0")) return 0;
+    if (lay != 0 || is_local || track || lcs || (planes && !d8) || sc.g > 0 || sc.h > 0) return 0;
+    if (ph.empty() || ph.size() % 2) return 0;
+    for (size_t q = 0; q + 1 < ph.size(); q += 2)
+        if (ph[q].n != ph[q + 1].n || ph[q].m != ph[q + 1].m || ph[q].m + 80 > 32000) return 0;
+    const long long g = sc.g, a = (long long)sc.h + sc.g;
+    const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
+    const long long U = std::max(0LL, smax - a);
+    const long long D = std::max(std::llabs(a - g), std::llabs(U - g));
+    for (int W : {15, 8, 4}) {
+        if (W > W_want && W != 4) continue;
+        const long long bound = D * (192LL * W + 16) + 2 * (std::llabs(a) + std::llabs(smax) + std::llabs(smin)) + 64;
+        if (bound < 30000) return W;
+    }
+    return 0;
+}
+
 static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc,
                     const std::vector<PairHost>& ph, const Scores32& sc, int is_local, bool planes, bool track,
                     bool lcs, FillJob& job, const uint8_t* chars_dev = nullptr,
@@ -650,12 +681,25 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                      scl.smm >= -128 && scl.smm <= 127 && !getenv("GX_NO_SCORE_TABLE");
     if (tbl)
         for (int k = 0; k < 4; ++k) scl.sym[k] = alpha->sym[k];
-    job.W = W;
     job.planes_on = planes; job.lcs_on = lcs; job.track_on = track;
     const bool d8 = planes && lay == 0 && !track && d8_planes_ok(sc, is_local);
     job.d8 = d8;
+    // twin fill: half as many band jobs (each carries two pairs); the band
+    // width follows the usual rule on the twins' strips (GX_BAND_WAVES forces it)
+    int Wt = 0;
+    {
+        int wt_want = 15;
+        if (const char* e = getenv("GX_BAND_WAVES")) wt_want = atoi(e);
+        else wt_want = fill_band_waves(false, total_strips / 2, fill_grid_cap(ctx->device), lay, min_strips);
+        Wt = twin_width(ph, sc, is_local, track, lcs, lay, planes, d8, wt_want);
+    }
+    const bool twin = Wt > 0;
+    job.twin = twin;
+    ctx->last_twin = twin ? 1 : 0;
+    const int Wf = twin ? Wt : W;   // band width of the launch
     const size_t plane_esz = d8 ? 1 : sizeof(int32_t);
-    ctx->last_lay = lay; ctx->last_W = W;
+    job.W = Wf;
+    ctx->last_lay = lay; ctx->last_W = Wf;
     ctx->last_pbytes = planes ? (int)(plane_esz * 3) : 0;
     const size_t P = ph.size();
     job.pd.assign(P, PairDev{});
@@ -668,7 +712,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         PairDev& d = job.pd[p];
         d.n = n; d.m = m;
         d.strips = ceil_div(n, SR);
-        d.bands = ceil_div(d.strips, W);
+        d.bands = ceil_div(d.strips, Wf);
         // steps per strip: layout 0, lane 63 pushes column m at step m + 63; layout 1, column m at step m - 1
         const int T = lay ? m + 1 : m + kWave;
         d.t16 = ceil_div(T, 16);
@@ -677,15 +721,20 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         d.strip_base = strips;
         d.feed_stride = (int)align_up((size_t)m + 1 + 64, 16);
         d.skel_stride = (int)align_up((size_t)m + 1, 64);
-        bands += d.bands;
+        const bool second = twin && (p & 1);   // the twin's second pair: its bands, feed and skeleton are the first's
+        if (!second) bands += d.bands;
         strips += d.strips;
         c1o[p] = chars_bytes; chars_bytes += align_up(n, 64);
         c2o[p] = chars_bytes; chars_bytes += align_up(m, 64);
         po[p] = plane_elems; plane_elems += (size_t)d.strips * d.t4 * (lay ? kGroupInts1 : kGroupInts);
         co[p] = code_elems; code_elems += (size_t)d.strips * d.t16 * SR;
-        so[p] = skel_elems; skel_elems += (size_t)d.strips * d.skel_stride;
-        fo[p] = feed_recs; feed_recs += (size_t)std::max(d.bands - 1, 0) * d.feed_stride;
-        gofs[p] = prog_elems; prog_elems += (size_t)std::max(d.bands - 1, 0) * kProgStride;
+        so[p] = second ? so[p - 1] : skel_elems;
+        if (!second) skel_elems += (size_t)d.strips * d.skel_stride;
+        // twin feed records are 32 B (gx_fill_pk.hip RecW): two Rec slots per column
+        fo[p] = second ? fo[p - 1] : feed_recs;
+        if (!second) feed_recs += (size_t)std::max(d.bands - 1, 0) * d.feed_stride * (twin ? 2 : 1);
+        gofs[p] = second ? gofs[p - 1] : prog_elems;
+        if (!second) prog_elems += (size_t)std::max(d.bands - 1, 0) * kProgStride;
     }
     job.total_bands = bands;
     job.total_strips = strips;
@@ -709,7 +758,13 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     order.reserve(2 * (size_t)bands);
     {
         const char* bo = getenv("GX_BAND_ORDER");
-        if (bo && !strcmp(bo, "pair")) {
+        if (twin) {   // band-major over the twins: entries (twin q, band)
+            int maxb = 0;
+            for (size_t p = 0; p < P; p += 2) maxb = std::max(maxb, job.pd[p].bands);
+            for (int lb = 0; lb < maxb; ++lb)
+                for (size_t p = 0; p < P; p += 2)
+                    if (lb < job.pd[p].bands) { order.push_back((int)(p / 2)); order.push_back(lb); }
+        } else if (bo && !strcmp(bo, "pair")) {
             for (size_t p = 0; p < P; ++p)
                 for (int lb = 0; lb < job.pd[p].bands; ++lb) { order.push_back((int)p); order.push_back(lb); }
         } else {
@@ -771,7 +826,10 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     const auto h_launch = std::chrono::steady_clock::now();
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].fb : ctx->ev0, eve = slot >= 0 ? ctx->slots[slot].fe : ctx->ev1;
     HIPCHK(hipEventRecord(evb, ctx->stream));
-    if (bands > 0)
+    if (bands > 0 && twin)
+        HIPCHK(launch_fill_pk(Wf, planes ? 1 : 0, (const PairDev*)job.pairs.p, (int)(P / 2), bands, (int*)job.counter.p,
+                              (PairRes*)job.pres.p, scl, grid, ctx->stream));
+    else if (bands > 0)
         HIPCHK(launch_fill(W, lay, is_local != 0, planes ? (d8 ? 2 : 1) : 0, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
                            (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, ctx->stream));
     HIPCHK(hipEventRecord(eve, ctx->stream));   // evb..eve brackets the fill kernel alone
@@ -1110,6 +1168,7 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
         t.seg = (int*)seg.p + 4 * so[p];
         t.recs = (uint32_t*)recs.p + so[p] * SR;
         t.srows = SR;
+        t.skel_half = job.twin ? (int)(p & 1) : -1;
         t.end_ij = (int*)cnt.p + 4 * p;
     }
     TbDev* pin_jobs = (TbDev*)(slot >= 0 ? pinned_grow(ctx->slots[slot].tjpin, P * sizeof(TbDev))
@@ -1284,6 +1343,12 @@ extern "C" int gx_alignment_table(gx_context* ctx, const uint8_t* s1, size_t n, 
     }
     std::vector<PairHost> ph{PairHost{t->s1.data(), t->s2.data(), n, m}};
     std::vector<std::pair<const uint8_t*, const uint8_t*>> proc{{t->c1.data(), t->c2.data()}};
+    // GX_TABLE_TWIN=1 (verification): fill the table with the twin fill, the
+    // pair beside a copy of itself, so that its planes can be exported
+    if (const char* e = getenv("GX_TABLE_TWIN"); e && !strcmp(e, "1") && !wide) {
+        ph.push_back(ph[0]);
+        proc.push_back(proc[0]);
+    }
     const bool planes = (flags & (GX_TABLE_PLANES | GX_TABLE_MATCHES)) != 0;
     const bool lcs = (flags & GX_TABLE_MATCHES) != 0;
     if (n >= 1 && m >= 1) {
@@ -2193,6 +2258,7 @@ extern "C" int gx_staged_steps(const gx_context* ctx, size_t pair, gx_step* step
 }
 
 extern "C" int gx_batch_chunks(const gx_context* ctx) { return ctx ? ctx->last_chunks : -1; }
+extern "C" int gx_fill_twin(const gx_context* ctx) { return ctx ? ctx->last_twin : -1; }
 
 extern "C" int gx_fill_info(const gx_context* ctx, int* layout, int* band_waves, int* plane_bytes_per_cell) {
     if (!ctx) return fail(GX_EINVAL, "context is NULL");

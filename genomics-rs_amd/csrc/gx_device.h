@@ -168,6 +168,8 @@ __device__ __forceinline__ void skel_store4(__amdgpu_buffer_rsrc_t r, uint32_t v
 #endif
 }
 
+constexpr int kPushScratch = 128;   // uint32 per wave: 64 lanes x 4 B + a sub-block's record offsets (252 B)
+
 // ... and the ring's write counter (lane 63: the counter; others: scratch)
 __device__ __forceinline__ void publish_all(uint32_t caddr, int cnt) {
     asm volatile("ds_write_b32 %0, %1" : : "v"(caddr), "v"(cnt) : "memory");

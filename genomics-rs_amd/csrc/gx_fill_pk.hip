@@ -1,0 +1,638 @@
+// gx_fill_pk.hip -- the twin fill: two independent pairs of the same shape
+// (n, m) swept by one band of waves, one pair in each 16-bit half of every
+// register (VOP3P packed arithmetic: one v_pk_max_i16 / v_pk_add_u16 /
+// v_pk_mad_u16 computes the same cell of both pairs).  Specialised to the
+// batch path's untracked global fill on the anti-diagonal layout (layout 0,
+// gx_internal.h) with compact score planes (or none): the same strips, bands,
+// rings, band hand-offs, codes and compact planes as gx_kernels.hip's
+// fill_kernel, the same recurrence on the shifted values V - (i + j) g
+// (DESIGN.md 4.3), so the traceback and the exports are unchanged.
+//
+// 16-bit values.  A strip's values span a few thousand around a moving
+// reference, far less than 2^15, but not their absolute magnitude (V'' reaches
+// ~4e4 at the end of a 30k pair).  Every value is therefore kept relative to a
+// per-pair base B (int32, a wave-uniform SGPR pair), exact modulo 2^16:
+//   * the I/O wave of a band picks the base of each 16-column block of the
+//     band's top row (the first column's score_max) and of column 0;
+//   * a strip adopts, at each 16-step sub-block, the base of the block it
+//     consumes (its producer wrote it beside the records), shifting its state
+//     by the difference (ten v_pk_sub per sub-block), so ring records never
+//     need converting; the blocks it pushes carry that same base;
+//   * the I/O wave converts the band's bottom row back to int32 for HBM.
+// The host admits a launch only when the worst-case spread of a band's values
+// around the inherited bases stays below 2^15 (gx_api.cpp twin_ok).
+// Comparisons and max are exact on values within 2^15 of each other, so the
+// codes, landing columns, planes and results equal the int32 fill's.
+#include "gx_device.h"
+
+namespace gx {
+
+typedef short s2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s2 as_s2(uint32_t x) { return __builtin_bit_cast(s2, x); }
+__device__ __forceinline__ uint32_t as_u(s2 x) { return __builtin_bit_cast(uint32_t, x); }
+// VOP3P arithmetic on the two halves.  The sign masks pass through an empty
+// asm so that the compiler keeps them as bit masks (v_bfi_b32, v_and_or_b32):
+// seen as sign splats, the bit-selects are lowered to per-half compares and
+// selects.  (Non-empty inline asm here costs an s_nop after each statement.)
+__device__ __forceinline__ uint32_t pmax(uint32_t a, uint32_t b) {
+    return as_u(__builtin_elementwise_max(as_s2(a), as_s2(b)));
+}
+__device__ __forceinline__ uint32_t padd(uint32_t a, uint32_t b) { return as_u(as_s2(a) + as_s2(b)); }
+__device__ __forceinline__ uint32_t padds(uint32_t a, uint32_t b) { return padd(a, b); }
+__device__ __forceinline__ uint32_t psub(uint32_t a, uint32_t b) { return as_u(as_s2(a) - as_s2(b)); }
+__device__ __forceinline__ uint32_t psubs(uint32_t a, uint32_t b) { return psub(a, b); }
+// 0xFFFF in each half whose value is negative, else 0
+__device__ __forceinline__ uint32_t psign(uint32_t a) {
+    uint32_t m = as_u(as_s2(a) >> (s2){15, 15});
+    asm("" : "+v"(m));
+    return m;
+}
+// (m & a) | (~m & b)
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t d;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(d) : "v"(m), "v"(a), "v"(b));
+    return d;
+}
+// code bit-planes: each half shifted left by one, the sign mask's low bit shifted in
+__device__ __forceinline__ uint32_t pcode(uint32_t c, uint32_t m) {
+    const uint32_t t = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u2, c) << (u2){1, 1});
+    uint32_t d;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(d) : "v"(m), "s"(0x00010001u), "v"(t));
+    return d;
+}
+// 0 where the two bytes match, 1 elsewhere (per half)
+__device__ __forceinline__ uint32_t pmis(uint32_t c1, uint32_t c2) {
+    uint32_t d;
+    asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(d) : "v"(c1 ^ c2));
+    return d;
+}
+// a * b + c per half (mod 2^16)
+__device__ __forceinline__ uint32_t pmad(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ uint32_t pk2(int lo, int hi) { return ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16); }
+__device__ __forceinline__ int lo16(uint32_t x) { return (int)(short)(x & 0xFFFFu); }
+__device__ __forceinline__ int hi16(uint32_t x) { return (int)(short)(x >> 16); }
+
+// (a - b) of half H into byte K of acc (SDWA; byte 0 clears the rest)
+template <int K, int H>
+__device__ __forceinline__ void put_byte_h(uint32_t& acc, uint32_t a, uint32_t b) {
+#define GX_PBH(DST, UNUSED, SEL)                                                                         \
+    asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:" DST " dst_unused:" UNUSED " src0_sel:" SEL " src1_sel:" SEL \
+        : "+v"(acc) : "v"(a), "v"(b))
+#define GX_PBH0(SEL)                                                                                          \
+    asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:" SEL " src1_sel:" SEL        \
+        : "=v"(acc) : "v"(a), "v"(b))
+    if constexpr (K == 0 && H == 0) GX_PBH0("WORD_0");
+    if constexpr (K == 1 && H == 0) GX_PBH("BYTE_1", "UNUSED_PRESERVE", "WORD_0");
+    if constexpr (K == 2 && H == 0) GX_PBH("BYTE_2", "UNUSED_PRESERVE", "WORD_0");
+    if constexpr (K == 3 && H == 0) GX_PBH("BYTE_3", "UNUSED_PRESERVE", "WORD_0");
+    if constexpr (K == 0 && H == 1) GX_PBH0("WORD_1");
+    if constexpr (K == 1 && H == 1) GX_PBH("BYTE_1", "UNUSED_PRESERVE", "WORD_1");
+    if constexpr (K == 2 && H == 1) GX_PBH("BYTE_2", "UNUSED_PRESERVE", "WORD_1");
+    if constexpr (K == 3 && H == 1) GX_PBH("BYTE_3", "UNUSED_PRESERVE", "WORD_1");
+#undef GX_PBH
+#undef GX_PBH0
+}
+
+// The compact plane bytes of step U (both pairs, both rows), as soon as the
+// step's cells exist (keeping a group's cells for the end costs 32 VGPRs).
+template <int U>
+__device__ __forceinline__ void bytes_step(uint32_t (&xI)[2][2], uint32_t (&xS)[2][2], uint32_t (&xD)[2][2],
+                                           const uint32_t (&oI)[2], const uint32_t (&oD)[2], const uint32_t (&oS)[2],
+                                           const uint32_t (&oL)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        put_byte_h<U, 0>(xI[0][h], oI[h], oL[h]); put_byte_h<U, 0>(xS[0][h], oS[h], oI[h]);
+        put_byte_h<U, 0>(xD[0][h], oD[h], oI[h]);
+        put_byte_h<U, 1>(xI[1][h], oI[h], oL[h]); put_byte_h<U, 1>(xS[1][h], oS[h], oI[h]);
+        put_byte_h<U, 1>(xD[1][h], oD[h], oI[h]);
+    }
+}
+
+// Packed scores (both halves equal): h, sm'' = s_match - 2g, dsm = (s_mismatch - 2g) - sm''
+struct PkScores {
+    uint32_t h, smp, dsm;
+};
+
+// One row of a lane, both pairs: the cell left of the one being computed.
+struct RowPk {
+    uint32_t I, SD, Dd, SMp, SMtl;   // insert, max(sub, delete), delete successor, score_max + sm'', SMp(i-1, j-1)
+    uint32_t cI, cD;                 // code bit-planes (16 steps, one per half)
+    uint32_t E, Etl;                 // landing columns (int16 per half)
+};
+struct LanePk {
+    RowPk a, b;
+    uint32_t c2c;                    // s2[j-1] of both pairs (bytes in the halves)
+};
+
+// algo.rs:222-268 on the shifted values, both pairs at once; MASKED keeps
+// the lanes outside columns 1..m unchanged.
+template <bool MASKED>
+__device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const uint32_t sm_in, const uint32_t e_up,
+                                        const uint32_t c2, const uint32_t c1, const bool act, const PkScores& k,
+                                        uint32_t& oI, uint32_t& oD, uint32_t& oS, uint32_t& oIold) {
+    const uint32_t In = pmax(st.I, padds(st.SD, k.h));            // max(I, max(S,D) + h)   (algo.rs:231-236)
+    const uint32_t Sn = pmad(pmis(c1, c2), k.dsm, st.SMtl);        // SM(i-1,j-1) + s''       (algo.rs:245-248)
+    const uint32_t Dn = dd_in;                                     // (algo.rs:238-243, from the row above)
+    const uint32_t IS = pmax(In, Sn);
+    const uint32_t SMn = pmax(IS, Dn);
+    const uint32_t SDn = pmax(Sn, Dn);
+    const uint32_t Ddn = pmax(padds(IS, k.h), Dn);                 // D(i+1, j)
+    // retrace priority S > I > D (algo.rs:351-400): m1 = I beats S, m2 = D beats both
+    const uint32_t m1 = psign(psub(Sn, In)), m2 = psign(psub(IS, Dn));
+    const uint32_t E1 = bfi(m1, st.E, st.Etl);
+    const uint32_t En = bfi(m2, e_up, E1);
+    const uint32_t cIn = pcode(st.cI, m1);
+    const uint32_t cDn = pcode(st.cD, m2);
+    const uint32_t SMpn = padds(SMn, k.smp);
+    oI = In; oD = Dn; oS = Sn; oIold = st.I;
+    if (MASKED) {
+        st.I = act ? In : st.I; st.SD = act ? SDn : st.SD; st.Dd = act ? Ddn : st.Dd; st.SMp = act ? SMpn : st.SMp;
+        st.E = act ? En : st.E;
+    } else {
+        st.I = In; st.SD = SDn; st.Dd = Ddn; st.SMp = SMpn; st.E = En;
+    }
+    st.cI = cIn; st.cD = cDn;
+    st.SMtl = sm_in;
+    st.Etl = e_up;
+}
+
+template <bool MASKED>
+__device__ __forceinline__ void dp_step_pk(LanePk& st, const Rec& r, const int t, const int lane, const int m,
+                                           const uint32_t c1a, const uint32_t c1b, const PkScores& k,
+                                           uint32_t (&oI)[2], uint32_t (&oD)[2], uint32_t (&oS)[2],
+                                           uint32_t (&oL)[2]) {
+    const uint32_t dd_in = (uint32_t)shr1(r.dd, (int)st.b.Dd);
+    const uint32_t sm_in = (uint32_t)shr1(r.sm, (int)st.b.SMp);
+    const uint32_t c2 = (uint32_t)shr1(r.c2, (int)st.c2c);
+    const uint32_t e_in = (uint32_t)shr1((int)pk2(t + 1, t + 1), (int)st.b.E);   // lane 0: its own column
+    const bool act = MASKED ? (unsigned)(t - lane) < (unsigned)m : true;
+    cell_pk<MASKED>(st.a, dd_in, sm_in, e_in, c2, c1a, act, k, oI[0], oD[0], oS[0], oL[0]);
+    cell_pk<MASKED>(st.b, st.a.Dd, st.a.SMp, st.a.E, c2, c1b, act, k, oI[1], oD[1], oS[1], oL[1]);
+    st.c2c = c2;
+}
+
+template <int U>
+__device__ __forceinline__ void push63_pk(uint32_t base, const LanePk& st, unsigned long long m63) {
+    asm volatile(
+        "s_mov_b64 exec, %0\n\t"
+        "ds_write2_b32 %1, %2, %3 offset0:%5 offset1:%6\n\t"
+        "ds_write_b32 %1, %4 offset:%7\n\t"
+        "s_mov_b64 exec, -1"
+        :
+        : "s"(m63), "v"(base), "v"(st.b.Dd), "v"(st.b.SMp), "v"(st.c2c), "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8)
+        : "memory");
+}
+template <int U>
+__device__ __forceinline__ void push_all_pk(uint32_t vaddr, const LanePk& st) {
+    asm volatile(
+        "ds_write2_b32 %0, %1, %2 offset0:%4 offset1:%5\n\t"
+        "ds_write_b32 %0, %3 offset:%6"
+        :
+        : "v"(vaddr), "v"(st.b.Dd), "v"(st.b.SMp), "v"(st.c2c), "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8)
+        : "memory");
+}
+
+__device__ __forceinline__ void read4_pk(Rec (&r)[4], const Rec* rin) {
+    r[0] = rin[0]; r[1] = rin[1]; r[2] = rin[2]; r[3] = rin[3];
+}
+
+// Bases of a ring: slot 0 = column 0; slot 1 + (b mod kBaseSlots) = block b
+// (columns 16b+1 .. 16b+16); two ints (the two pairs) each.
+constexpr int kBaseSlots = 32;
+// (as lds_int pairs: slot k = ints 2k, 2k + 1)
+
+struct WavePk {
+    uint8_t* pI[2]; uint8_t* pD[2]; uint8_t* pS[2];   // this strip's compact planes, per pair
+    uint32_t* codes[2];
+    const Rec* ring_in;
+    lds_int* wcnt_in;
+    lds_int* wcnt_out;
+    lds_int* base_in;
+    lds_int* base_out;
+    int* status;
+    __amdgpu_buffer_rsrc_t skel_rsrc;
+    uint32_t skel_voff;
+    uint32_t scratch;
+    uint32_t cnt_addr;
+    int m, lane;
+    uint32_t c1a, c1b;
+    int B0, B1;                                       // current bases (wave-uniform)
+};
+
+template <int PLANES, bool MASKED, int G4>
+__device__ __forceinline__ void group4_pk(LanePk& st, Rec (&nxt)[4], WavePk& w, const PkScores& k, const int t0,
+                                          const uint32_t out_base, const bool push_on, const size_t sb_off) {
+    const int t = t0 + 4 * G4;
+    Rec cur[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
+    const int need = min(t + 8, w.m) + 1;
+    const int seen_v = *w.wcnt_in;
+    asm volatile("" ::: "memory");
+    read4_pk(nxt, w.ring_in + ring_slot(t + 5));
+    uint32_t bI[4][2], bD[4][2], bS[4][2], bL[4][2];
+    uint32_t xI[2][2], xS[2][2], xD[2][2];   // compact plane dwords [pair][row], filled step by step
+    const int col0 = t - (kWave - 1);
+    if (MASKED) {
+        auto sko = [&](int c) { return (c >= 0 && c <= w.m) ? w.skel_voff + 4u * (uint32_t)c : kSkelOff; };
+        push63_pk<4 * G4 + 0>(out_base, st, lane63_mask(push_on && col0 >= 0 && col0 <= w.m));
+        dp_step_pk<true>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, k, bI[0], bD[0], bS[0], bL[0]);
+        if (PLANES) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
+        skel_store(w.skel_rsrc, sko(col0 + 1), (int)st.b.E);
+        push63_pk<4 * G4 + 1>(out_base, st, lane63_mask(push_on && col0 + 1 >= 0 && col0 + 1 <= w.m));
+        dp_step_pk<true>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, k, bI[1], bD[1], bS[1], bL[1]);
+        if (PLANES) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
+        skel_store(w.skel_rsrc, sko(col0 + 2), (int)st.b.E);
+        push63_pk<4 * G4 + 2>(out_base, st, lane63_mask(push_on && col0 + 2 >= 0 && col0 + 2 <= w.m));
+        dp_step_pk<true>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, k, bI[2], bD[2], bS[2], bL[2]);
+        if (PLANES) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
+        skel_store(w.skel_rsrc, sko(col0 + 3), (int)st.b.E);
+        push63_pk<4 * G4 + 3>(out_base, st, lane63_mask(push_on && col0 + 3 >= 0 && col0 + 3 <= w.m));
+        if (push_on && col0 + 3 >= 0 && col0 <= w.m) lds_store_lane0(w.wcnt_out, min(col0 + 3, w.m) + 1);
+        dp_step_pk<true>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, k, bI[3], bD[3], bS[3], bL[3]);
+        if (PLANES) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
+        skel_store(w.skel_rsrc, sko(col0 + 4), (int)st.b.E);
+    } else {
+        const uint32_t pa = push_on && w.lane == kWave - 1 ? out_base : w.scratch;
+        push_all_pk<4 * G4 + 0>(pa, st);
+        dp_step_pk<false>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, k, bI[0], bD[0], bS[0], bL[0]);
+        if (PLANES) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
+        const uint32_t e0 = st.b.E;
+        push_all_pk<4 * G4 + 1>(pa, st);
+        dp_step_pk<false>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, k, bI[1], bD[1], bS[1], bL[1]);
+        if (PLANES) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
+        const uint32_t e1 = st.b.E;
+        push_all_pk<4 * G4 + 2>(pa, st);
+        dp_step_pk<false>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, k, bI[2], bD[2], bS[2], bL[2]);
+        if (PLANES) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
+        const uint32_t e2 = st.b.E;
+        push_all_pk<4 * G4 + 3>(pa, st);
+        publish_all(w.cnt_addr, col0 + 3 + 1);
+        dp_step_pk<false>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, k, bI[3], bD[3], bS[3], bL[3]);
+        if (PLANES) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
+        skel_store4(w.skel_rsrc, w.skel_voff + 4u * (uint32_t)(col0 + 1), (int)e0, (int)e1, (int)e2, (int)st.b.E);
+    }
+    if (PLANES) {
+        // compact planes of both pairs (bytes_step): x_I = I - I(j-1) (shifted:
+        // x_I - g), x_S = S - I, x_D = D - I, one byte per cell
+        constexpr int kSubBytes = kSub / 4 * kGroupInts;
+        constexpr uint32_t kG = G4 * kGroupInts;
+        const uint32_t v0 = (uint32_t)w.lane * 4u + kG, v1 = v0 + kWave * 4;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const auto rI = rsrc_of(w.pI[p] + sb_off, kSubBytes), rD = rsrc_of(w.pD[p] + sb_off, kSubBytes),
+                       rS = rsrc_of(w.pS[p] + sb_off, kSubBytes);
+            bstore1(rI, v0, xI[p][0]); bstore1(rS, v0, xS[p][0]); bstore1(rD, v0, xD[p][0]);
+            bstore1(rI, v1, xI[p][1]); bstore1(rS, v1, xS[p][1]); bstore1(rD, v1, xD[p][1]);
+        }
+    }
+    if (__builtin_amdgcn_readfirstlane(seen_v) < need) {
+        wait_ge(w.wcnt_in, need, w.status);
+        read4_pk(nxt, w.ring_in + ring_slot(t + 5));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// The bases of block `blk` of ring `in` (slot 1 + blk mod kBaseSlots).
+__device__ __forceinline__ int2 base_of(lds_int* b, int blk) {
+    const int k = 1 + (blk & (kBaseSlots - 1));
+    return make_int2(__builtin_amdgcn_readfirstlane(b[2 * k]), __builtin_amdgcn_readfirstlane(b[2 * k + 1]));
+}
+
+// Shift every value of the lane state to new bases (delta = new - old).
+__device__ __forceinline__ void rebase_row(RowPk& r, uint32_t dpk) {
+    r.I = psubs(r.I, dpk); r.SD = psubs(r.SD, dpk); r.Dd = psubs(r.Dd, dpk);
+    r.SMp = psubs(r.SMp, dpk); r.SMtl = psubs(r.SMtl, dpk);
+}
+__device__ __forceinline__ void rebase(LanePk& st, uint32_t dpk) {
+    rebase_row(st.a, dpk);
+    rebase_row(st.b, dpk);
+}
+
+template <int PLANES, bool MASKED>
+__device__ __forceinline__ void sub_block_pk(LanePk& st, Rec (&nxt)[4], WavePk& w, const PkScores& k, const int t0,
+                                             const uint32_t out_base, const bool push_on, const size_t sb_off) {
+    group4_pk<PLANES, MASKED, 0>(st, nxt, w, k, t0, out_base, push_on, sb_off);
+    group4_pk<PLANES, MASKED, 1>(st, nxt, w, k, t0, out_base, push_on, sb_off);
+    group4_pk<PLANES, MASKED, 2>(st, nxt, w, k, t0, out_base, push_on, sb_off);
+    group4_pk<PLANES, MASKED, 3>(st, nxt, w, k, t0, out_base, push_on, sb_off);
+}
+
+// Initial state of row i (column 0, algo.rs:204-211) in shifted values:
+// H(i, 0) = h + i g -> h; I = H + h (compact planes' seed) -> 2h;
+// delete successor (row i+1) -> h; relative to the bases (B0, B1).
+__device__ __forceinline__ void init_row_pk(RowPk& rs, const Scores32& sc, int B0, int B1, const PkScores& k) {
+    rs.I = pk2(2 * sc.h - B0, 2 * sc.h - B1);
+    rs.SD = pk2(sc.h - B0, sc.h - B1);
+    rs.Dd = pk2(sc.h - B0, sc.h - B1);
+    rs.SMp = padds(pk2(sc.h - B0, sc.h - B1), k.smp);
+    rs.SMtl = 0;
+    rs.cI = 0; rs.cD = 0;
+}
+
+template <int PLANES>
+__device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int s, const int lane, const Scores32& sc,
+                                const PkScores& k, const Rec* ring_in, Rec* ring_out, lds_int* wcnt_in,
+                                lds_int* rcnt_in, lds_int* wcnt_out, lds_int* rcnt_out, lds_int* base_in,
+                                lds_int* base_out, const bool has_consumer, PairRes* pres0, PairRes* pres1,
+                                int* status, const uint32_t scratch_base) {
+    const int n = P0.n, m = P0.m;
+    const int ia = s * kStripRows + kRowsPerLane * lane + 1;
+    const bool ok_a = ia <= n, ok_b = ia + 1 <= n;
+    WavePk w;
+    {
+        const size_t strip_planes = (size_t)s * P0.t4 * kGroupInts;   // bytes per compact plane per strip
+        w.pI[0] = PLANES ? (uint8_t*)P0.pI + strip_planes : nullptr;
+        w.pD[0] = PLANES ? (uint8_t*)P0.pD + strip_planes : nullptr;
+        w.pS[0] = PLANES ? (uint8_t*)P0.pS + strip_planes : nullptr;
+        w.pI[1] = PLANES ? (uint8_t*)P1.pI + strip_planes : nullptr;
+        w.pD[1] = PLANES ? (uint8_t*)P1.pD + strip_planes : nullptr;
+        w.pS[1] = PLANES ? (uint8_t*)P1.pS + strip_planes : nullptr;
+        w.codes[0] = P0.codes + (size_t)s * P0.t16 * kWave * kRowsPerLane;
+        w.codes[1] = P1.codes + (size_t)s * P0.t16 * kWave * kRowsPerLane;
+    }
+    w.ring_in = ring_in; w.wcnt_in = wcnt_in; w.wcnt_out = wcnt_out; w.status = status;
+    w.base_in = base_in; w.base_out = base_out;
+    // the twin's packed skeleton (P0.skel): int16 landing columns of both pairs per column
+    w.skel_rsrc = rsrc_of(uniform_ptr(P0.skel + (size_t)s * P0.skel_stride), has_consumer ? 4 * (m + 1) : 0);
+    w.skel_voff = lane == kWave - 1 ? 0u : kSkelOff;
+    w.scratch = scratch_base + 4u * (uint32_t)lane;
+    w.cnt_addr = (has_consumer && lane == kWave - 1) ? lds_addr((const void*)wcnt_out) : w.scratch;
+    w.m = m; w.lane = lane;
+    w.c1a = pk2(ok_a ? (int)P0.c1[ia - 1] : 0x100, ok_a ? (int)P1.c1[ia - 1] : 0x100);
+    w.c1b = pk2(ok_b ? (int)P0.c1[ia] : 0x100, ok_b ? (int)P1.c1[ia] : 0x100);
+
+    // column 0 of the row above: its bases and record (published with the ring's first counter)
+    wait_ge(wcnt_in, min(4, m) + 1, status);
+    w.B0 = __builtin_amdgcn_readfirstlane(base_in[0]);   // slot 0: column 0
+    w.B1 = __builtin_amdgcn_readfirstlane(base_in[1]);
+    LanePk st;
+    init_row_pk(st.a, sc, w.B0, w.B1, k);
+    init_row_pk(st.b, sc, w.B0, w.B1, k);
+    st.c2c = 0;
+    st.b.SMtl = st.a.SMp;                                   // (A, 0) is row B's top-left for column 1
+    st.a.E = pk2(-(kRowsPerLane * lane + 1), -(kRowsPerLane * lane + 1));
+    st.b.E = pk2(-(kRowsPerLane * lane + 2), -(kRowsPerLane * lane + 2));
+    st.b.Etl = st.a.E;
+    if (has_consumer) {
+        if (lane == kWave - 1) ring_out[ring_slot(0)] = Rec{(int)st.b.Dd, (int)st.b.SMp, 0, 0};
+        if (lane == 0) { base_out[0] = w.B0; base_out[1] = w.B1; }
+        lds_wait();
+        if (lane == 0) *wcnt_out = 1;
+    }
+    Rec nxt[4];
+    {
+        const Rec r0 = ring_in[ring_slot(0)];
+        st.a.SMtl = (uint32_t)shr1(r0.sm, (int)st.b.SMp);
+        st.a.Etl = (uint32_t)shr1(0, (int)st.b.E);
+        read4_pk(nxt, ring_in + ring_slot(1));
+    }
+    const int T = m + kWave;
+    for (int t0 = 0; t0 < T; t0 += kSub) {
+        const int last_col = min(t0 + kSub - 1 - (kWave - 1), m);
+        if (has_consumer && last_col >= kRing) wait_ge(rcnt_out, last_col - kRing + 1, status);
+        // adopt the bases of the block consumed now (columns t0+1 .. t0+16); the
+        // block pushed now (columns t0-62 .. t0-47, block t0/16 - 4) carries them
+        const int blk = t0 >> 4;
+        if (t0 < m) {
+            const int2 nb = base_of(base_in, blk);
+            if (nb.x != w.B0 || nb.y != w.B1) {
+                rebase(st, pk2(nb.x - w.B0, nb.y - w.B1));
+                w.B0 = nb.x; w.B1 = nb.y;
+            }
+        }
+        // (sub-block 3 pushes column 0 again, now in the current bases: slot 0
+        // follows it; the consumer reads both only once the counter passes 4)
+        if (has_consumer && blk >= 3 && lane == 0) {
+            const int kk = blk == 3 ? 0 : 1 + ((blk - 4) & (kBaseSlots - 1));
+            base_out[2 * kk] = w.B0;
+            base_out[2 * kk + 1] = w.B1;
+        }
+        const size_t sb_off = (size_t)(t0 >> 2) * kGroupInts;
+        const bool full = (t0 >= kWave) && (t0 + kSub - 1 <= m - 1);
+        const uint32_t out_base = lds_addr(ring_out + ring_slot(t0 - (kWave - 1)));
+        if (full) sub_block_pk<PLANES, false>(st, nxt, w, k, t0, out_base, has_consumer, sb_off);
+        else sub_block_pk<PLANES, true>(st, nxt, w, k, t0, out_base, has_consumer, sb_off);
+        {   // code words of both pairs: codes[strip][t/16][lane][row-in-lane]
+            typedef unsigned v2u __attribute__((ext_vector_type(2)));
+            typedef __attribute__((address_space(1))) v2u gv2u;
+            const v2u c0 = {(st.a.cD << 16) | (st.a.cI & 0xFFFFu), (st.b.cD << 16) | (st.b.cI & 0xFFFFu)};
+            const v2u c1 = {(st.a.cD & 0xFFFF0000u) | (st.a.cI >> 16), (st.b.cD & 0xFFFF0000u) | (st.b.cI >> 16)};
+            const size_t wo = ((size_t)(t0 >> 4) * kWave + lane) * kRowsPerLane;
+            *(gv2u*)(w.codes[0] + wo) = c0;
+            *(gv2u*)(w.codes[1] + wo) = c1;
+        }
+        lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
+    }
+    // cell (n, m) of both pairs: score_max (shifted, absolute) and landing column
+    const bool fa = ok_a && ia == n, fb = ok_b && ia + 1 == n;
+    if (fa || fb) {
+        const uint32_t sm = psubs(fa ? st.a.SMp : st.b.SMp, k.smp), e = fa ? st.a.E : st.b.E;
+        pres0->end_SM = lo16(sm) + w.B0; pres0->end_E = lo16(e);
+        pres1->end_SM = hi16(sm) + w.B1; pres1->end_E = hi16(e);
+    }
+}
+
+// Record of the band hand-off rows (HBM): both pairs, absolute (int32).
+struct __attribute__((aligned(16))) RecW {
+    int dd0, dd1, sm0, sm1;   // delete successor, score_max + sm'' (shifted values)
+    int c2, pad0, pad1, pad2; // s2[j-1] of both pairs (packed bytes)
+};
+
+// I/O wave of a twin band: ring 0 from row 0 (analytic) or the previous
+// band's bottom row (absolute -> relative to the bases it picks per block);
+// ring W to HBM (relative -> absolute with the last strip's bases).
+__device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, const int lane, const Scores32& sc,
+                           const PkScores& k, Rec* ring0, const Rec* ringW, lds_int* wcnt0, lds_int* rcnt0,
+                           lds_int* wcntW, lds_int* rcntW, lds_int* base0, lds_int* baseW, const bool do_out,
+                           int* status) {
+    const int m = P0.m;
+    constexpr int CH = 16;
+    int in_next = 0, out_next = 0;
+    RecW* feed = reinterpret_cast<RecW*>(P0.feed);
+    const RecW* feed_in = lb > 0 ? feed + (size_t)(lb - 1) * P0.feed_stride : nullptr;
+    RecW* feed_out = do_out ? feed + (size_t)lb * P0.feed_stride : nullptr;
+    const int* prog_in = lb > 0 ? P0.progress + (size_t)(lb - 1) * kProgStride : nullptr;
+    int* prog_out = do_out ? P0.progress + (size_t)lb * kProgStride : nullptr;
+    const int smp = sc.sm;              // sm'' (the launch's scores carry the shift's -2g, Scores32.shift)
+    unsigned idle = 0;
+    int bprev0 = 0, bprev1 = 0;         // bases of the block before the current chunk's first column
+    while (in_next <= m || (do_out && out_next <= m)) {
+        bool moved = false;
+        if (in_next <= m) {
+            const int chunk = min(CH, m + 1 - in_next);
+            bool ok = in_next + chunk - 1 < *rcnt0 + kRing;
+            if (ok && lb > 0) ok = ld_agent(prog_in) > in_next + chunk - 1;
+            if (ok) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const int j = in_next + lane;
+                int dd0 = 0, dd1 = 0, sm0 = 0, sm1 = 0, c2 = 0;
+                if (lane < chunk) {
+                    if (lb == 0) {   // row 0 (algo.rs:195-202, 213-220), shifted: D' = 2h, SM = h
+                        if (j == 0) { dd0 = dd1 = 0; sm0 = sm1 = smp; c2 = 0; }
+                        else {
+                            dd0 = dd1 = 2 * sc.h;
+                            sm0 = sm1 = sc.h + smp;
+                            c2 = (int)pk2(P0.c2[j - 1], P1.c2[j - 1]);
+                        }
+                    } else {
+                        const gu64* q = (const gu64*)(feed_in + j);
+                        const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const unsigned long long c = __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        dd0 = (int)(a & 0xffffffffu); dd1 = (int)(a >> 32);
+                        sm0 = (int)(b & 0xffffffffu); sm1 = (int)(b >> 32);
+                        c2 = (int)(c & 0xffffffffu);
+                    }
+                }
+                // bases: column 0 -> slot 0; block c (columns 16c+1 ..) from its first column
+                const int c0 = in_next >> 4;                     // chunk = columns 16c0 .. 16c0+15
+                if (in_next == 0) {
+                    bprev0 = __builtin_amdgcn_readlane(sm0, 0);
+                    bprev1 = __builtin_amdgcn_readlane(sm1, 0);
+                    if (lane == 0) { base0[0] = bprev0; base0[1] = bprev1; }
+                }
+                int nb0 = bprev0, nb1 = bprev1;
+                if (chunk > 1) {
+                    nb0 = __builtin_amdgcn_readlane(sm0, 1);
+                    nb1 = __builtin_amdgcn_readlane(sm1, 1);
+                    if (lane == 0) {
+                        const int kk = 1 + (c0 & (kBaseSlots - 1));
+                        base0[2 * kk] = nb0;
+                        base0[2 * kk + 1] = nb1;
+                    }
+                }
+                if (lane < chunk) {
+                    // lane 0 (column 16 c0) belongs to the previous block (or column 0)
+                    const int u0 = lane == 0 ? bprev0 : nb0, u1 = lane == 0 ? bprev1 : nb1;
+                    Rec r;
+                    r.dd = (int)pk2(dd0 - u0, dd1 - u1);
+                    r.sm = (int)pk2(sm0 - u0, sm1 - u1);
+                    r.c2 = c2;
+                    r.l = 0;
+                    ring0[ring_slot(j)] = r;
+                }
+                bprev0 = nb0; bprev1 = nb1;
+                lds_wait();
+                if (lane == 0) *wcnt0 = in_next + chunk;
+                in_next += chunk;
+                moved = true;
+            }
+        }
+        if (do_out && out_next <= m) {
+            const int avail = *wcntW;
+            const int chunk = min(CH, avail - out_next);
+            if (chunk == CH || (avail == m + 1 && chunk > 0)) {
+                const int j = out_next + lane;
+                if (lane < chunk) {
+                    const Rec r = ringW[ring_slot(j)];
+                    const int kk = j == 0 ? 0 : 1 + (((j - 1) >> 4) & (kBaseSlots - 1));
+                    const int2 b = make_int2(baseW[2 * kk], baseW[2 * kk + 1]);
+                    const unsigned long long a =
+                        (unsigned long long)(unsigned)(lo16((uint32_t)r.dd) + b.x) |
+                        ((unsigned long long)(unsigned)(hi16((uint32_t)r.dd) + b.y) << 32);
+                    const unsigned long long bb =
+                        (unsigned long long)(unsigned)(lo16((uint32_t)r.sm) + b.x) |
+                        ((unsigned long long)(unsigned)(hi16((uint32_t)r.sm) + b.y) << 32);
+                    gu64* q = (gu64*)(feed_out + j);
+                    __hip_atomic_store(q, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(q + 1, bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(q + 2, (unsigned long long)(unsigned)r.c2, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+                vm_wait();
+                lds_wait();
+                if (lane == 0) {
+                    *rcntW = out_next + chunk;
+                    st_agent(prog_out, out_next + chunk);
+                }
+                out_next += chunk;
+                moved = true;
+            }
+        }
+        if (moved) idle = 0;
+        else if (++idle > kSpinLimit) {
+            __hip_atomic_store((gint*)status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        } else {
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
+// Twin fill: pairs 2q and 2q+1 of the launch share every band; queue entry b
+// of the order table = (twin q, band lb).
+template <int W, int PLANES>
+__global__ __launch_bounds__((W + 1) * kWave, (W + 1 + 3) / 4) void fill_pk_kernel(
+    const PairDev* __restrict__ pairs, const int ntwins, const int total_bands, int* band_counter, PairRes* pres,
+    const Scores32 sc) {
+    __shared__ Rec rings[W + 1][kRing];
+    __shared__ uint32_t push_scratch[W][kPushScratch];
+    __shared__ int bases[W + 1][2 * (1 + kBaseSlots)];
+    __shared__ int wcnt[W + 1];
+    __shared__ int rcnt[W + 1];
+    __shared__ int band_sh;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int smp = sc.sm, smmp = sc.smm;   // s - 2g: the launch's scores carry the shift (Scores32.shift)
+    const PkScores k{pk2(sc.h, sc.h), pk2(smp, smp), pk2(smmp - smp, smmp - smp)};
+    for (;;) {
+        if (threadIdx.x == 0) band_sh = atomicAdd(band_counter, 1);
+        if (threadIdx.x < W + 1) { wcnt[threadIdx.x] = 0; rcnt[threadIdx.x] = 0; }
+        __syncthreads();
+        const int b = __builtin_amdgcn_readfirstlane(band_sh);
+        if (b >= total_bands) return;
+        const int2 ob = reinterpret_cast<const int2*>(pairs + 2 * ntwins)[b];
+        const int q = __builtin_amdgcn_readfirstlane(ob.x);
+        const PairDev& P0 = pairs[2 * q];
+        const PairDev& P1 = pairs[2 * q + 1];
+        const int lb = __builtin_amdgcn_readfirstlane(ob.y);
+        const int s0 = lb * W;
+        if (wave < W) {
+            const int s = s0 + wave;
+            if (s < P0.strips) {
+                const bool last_in_band = wave == W - 1;
+                const bool has_consumer = last_in_band ? (lb + 1 < P0.bands) : (s + 1 < P0.strips);
+                compute_wave_pk<PLANES>(P0, P1, s, lane, sc, k, rings[wave], rings[wave + 1], (lds_int*)&wcnt[wave],
+                                        (lds_int*)&rcnt[wave], (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1],
+                                        (lds_int*)bases[wave], (lds_int*)bases[wave + 1], has_consumer,
+                                        pres + 2 * q, pres + 2 * q + 1, band_counter + 1,
+                                        lds_addr(push_scratch[wave]));
+            }
+        } else {
+            io_wave_pk(P0, P1, lb, lane, sc, k, rings[0], rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0],
+                       (lds_int*)&wcnt[W], (lds_int*)&rcnt[W], (lds_int*)bases[0], (lds_int*)bases[W],
+                       lb + 1 < P0.bands, band_counter + 1);
+        }
+        __syncthreads();
+    }
+}
+
+template <int W0, int... Ws>
+static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int ntwins, int total_bands, int* d_counter,
+                              PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
+    if (W == W0) {
+        if (planes)
+            hipLaunchKernelGGL((fill_pk_kernel<W0, 1>), dim3(grid), dim3((W0 + 1) * kWave), 0, st, d_pairs, ntwins,
+                               total_bands, d_counter, d_pres, sc);
+        else
+            hipLaunchKernelGGL((fill_pk_kernel<W0, 0>), dim3(grid), dim3((W0 + 1) * kWave), 0, st, d_pairs, ntwins,
+                               total_bands, d_counter, d_pres, sc);
+        return hipGetLastError();
+    }
+    if constexpr (sizeof...(Ws) > 0) return launch_pk_w<Ws...>(W, planes, d_pairs, ntwins, total_bands, d_counter,
+                                                               d_pres, sc, grid, st);
+    return hipErrorInvalidValue;
+}
+
+// Twin launch: W from {4, 8, 15}; planes: 0 none, 1 compact.
+hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int ntwins, int total_bands, int* d_counter,
+                          PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
+    return launch_pk_w<4, 8, 15>(W, planes, d_pairs, ntwins, total_bands, d_counter, d_pres, sc, grid, st);
+}
+
+}  // namespace gx

@@ -135,6 +135,7 @@ struct TbDev {           // per-pair traceback job
     int start_E;           // landing column of the start cell (PairRes.end_E / lmax_E)
     const int* start_E_dev;// or, when non-null, read on the device (the fill's PairRes.end_E: no host round trip)
     int srows;             // rows per strip: 128 (layout 0, anti-diagonal) or 64 (layout 1, column-step)
+    int skel_half;         // -1: int32 skeleton; 0 / 1: the low / high int16 of a twin fill's packed skeleton
     int* seg;              // out: [strips][4] {entry_i, entry_j, records, active} per strip on the path
     uint32_t* recs;        // out: [strips][kStripRows] one record per row, (insert run << 2) | kind
     int* end_ij;           // out: [4] {i, j} where the walk leaves the interior, first strip, rounds

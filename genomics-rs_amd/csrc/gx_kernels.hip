@@ -115,7 +115,6 @@ __device__ __forceinline__ void push63_pub(uint32_t base, const LaneState& st, u
             : "memory");
 }
 
-constexpr int kPushScratch = 128;   // uint32 per wave: 64 lanes x 4 B + a sub-block's record offsets (252 B)
 // Full-group pushes without an exec switch: every lane writes, lane 63 to
 // the ring slot and the other lanes to their own scratch slots in LDS
 // (per-lane address vaddr, chosen once per sub-block), so the wave never
@@ -1375,6 +1374,7 @@ __global__ void tb_chase_kernel(const TbDev* __restrict__ jobs) {
             s -= 1;                                               // enters strip s at its bottom row
             J.seg[4 * s + 0] = (s + 1) * SR; J.seg[4 * s + 1] = E; J.seg[4 * s + 3] = 1;
             E = ((gcint*)J.skel)[(size_t)s * J.skel_stride + E];
+            if (J.skel_half >= 0) E = (int)(short)((unsigned)E >> (16 * J.skel_half));   // twin fill (gx_fill_pk.hip)
             if (SR == kStripRows1) E -= 64;                        // layout 1 stores E + 64
         }
     }

@@ -74,7 +74,7 @@ EXPORTED = ["gx_last_error", "gx_version", "gx_context_create", "gx_context_dest
             "gx_alignment_table", "gx_table_info", "gx_table_export", "gx_table_export_plane", "gx_table_export_rows",
             "gx_table_plane_sums", "gx_retrace", "gx_table_free", "gx_align", "gx_align_batch", "gx_stage_pairs",
             "gx_run_staged", "gx_run_staged_steps", "gx_staged_plane_sums", "gx_staged_steps",
-            "gx_fill_info", "gx_batch_chunks", "gx_plane_bytes_per_cell", "gx_fasta_load",
+            "gx_fill_info", "gx_batch_chunks", "gx_fill_twin", "gx_plane_bytes_per_cell", "gx_fasta_load",
             "gx_config_load", "gx_format_alignment", "gx_format_table"]
 
 _lib = None
@@ -118,6 +118,7 @@ def lib():
                                       ctypes.c_int, vp, ctypes.POINTER(ctypes.c_double)]
     L.gx_fill_info.argtypes = [vp] + [ctypes.POINTER(ctypes.c_int)] * 3
     L.gx_batch_chunks.argtypes = [vp]
+    L.gx_fill_twin.argtypes = [vp]
     L.gx_plane_bytes_per_cell.argtypes = [ctypes.POINTER(CScores), ctypes.c_int]
     L.gx_fasta_load.argtypes = [ctypes.c_char_p, vp, sz, vp, vp, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.gx_config_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(CScores)]
@@ -305,7 +306,7 @@ class Context:
         v = [ctypes.c_int() for _ in range(3)]
         _check(lib().gx_fill_info(self.ptr, *[ctypes.byref(x) for x in v]))
         return {"layout": v[0].value, "band_waves": v[1].value, "plane_bytes_per_cell": v[2].value,
-                "chunks": lib().gx_batch_chunks(self.ptr)}
+                "chunks": lib().gx_batch_chunks(self.ptr), "twin": lib().gx_fill_twin(self.ptr)}
 
     def __del__(self):
         try:

@@ -1,0 +1,129 @@
+"""GPU parity of the twin fill (genomics-rs_amd/csrc/gx_fill_pk.hip): batches
+whose pairs come in equal shapes run two pairs per band, one in each 16-bit
+half of every register, with values kept relative to per-block bases.  Every
+result -- alignment, statistics, the compact score planes -- must equal the
+oracle's, on shapes around the strip and band edges, with bands queued for
+workgroups (small grids) and at every band width, and under scores near the
+twin fill's admission bound."""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import CONFIG_SCORES
+
+pytestmark = pytest.mark.gpu
+
+NAMES = ["Match", "Mismatch", "Insert", "Delete", "OpenInsert", "OpenDelete"]
+SHAPES = [(1, 1), (5, 9), (63, 64), (64, 63), (128, 129), (129, 300), (257, 256), (700, 257), (300, 1000),
+          (1000, 77)]
+# the twin fill is a variant of the anti-diagonal layout, which small batches
+# would not get by default (they take the column-step layout)
+LAUNCH = {"auto": {"GX_LAYOUT": "0"}, "w4_grid2": {"GX_LAYOUT": "0", "GX_BAND_WAVES": "4", "GX_FILL_GRID": "2"},
+          "w8_grid3": {"GX_LAYOUT": "0", "GX_BAND_WAVES": "8", "GX_FILL_GRID": "3"},
+          "w15_grid2": {"GX_LAYOUT": "0", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "2"}}
+
+
+def _steps_list(steps):
+    return [(NAMES[int(c)], int(i), int(j)) for c, i, j in zip(steps["choice"], steps["i"], steps["j"])]
+
+
+def _twin_pairs(seed, shapes, per_shape=2, alphas=(b"ACGT", b"AC", b"ACGTN", b"A")):
+    rng = random.Random(seed)
+    pairs = []
+    for n, m in shapes:
+        for _ in range(per_shape):
+            al = rng.choice(alphas)
+            pairs.append((bytes(rng.choice(al) for _ in range(n)), bytes(rng.choice(al) for _ in range(m))))
+    return pairs
+
+
+@pytest.fixture(params=sorted(LAUNCH))
+def launch(request, monkeypatch):
+    for k, v in LAUNCH[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+def test_twin_batch_alignments(gx, ctx, oracle, launch):
+    """gx_align_batch (traceback-only twin fill): every alignment."""
+    pairs = _twin_pairs(7, SHAPES)
+    out = gx.align_batch(pairs, gx.Scores(*CONFIG_SCORES), False, ctx=ctx, max_cell=False)
+    assert ctx.fill_info()["twin"] == 1
+    for (a, b), (steps, r) in zip(pairs, out):
+        o = oracle.align(a, b, CONFIG_SCORES)
+        assert _steps_list(steps) == o.alignment(), (len(a), len(b))
+        assert (r.score, r.matches, r.mismatches, r.gap_extensions, r.opening_gaps) == \
+               (o.score, o.matches, o.mismatches, o.gap_extensions, o.opening_gaps)
+
+
+def test_twin_staged_planes(gx, ctx, oracle, launch):
+    """The staged, pipelined path with compact planes through the twin fill:
+    every pass's plane checksums and the last pass's alignments."""
+    pairs = _twin_pairs(11, SHAPES, per_shape=4)
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=3, plane_sums=True)
+    info = ctx.fill_info()
+    assert info["twin"] == 1 and info["plane_bytes_per_cell"] == 3, info
+    sums = st.plane_sums()
+    for p, (a, b) in enumerate(pairs):
+        o = oracle.align_lean(a, b, CONFIG_SCORES)
+        for k in range(3):
+            assert [int(x) for x in sums[k, p]] == o.extra["plane_sums"], (p, len(a), len(b), k)
+        assert res[p].score == o.score and res[p].n_steps == len(o.choices)
+        assert _steps_list(st.steps(p)) == o.alignment(), (p, len(a), len(b))
+
+
+@pytest.mark.parametrize("scores", [(1, -2, -2, -5), (2, -3, -2, -4), (5, -4, 0, -10), (1, -1, 0, 0), (3, -3, -1, -1),
+                                    (4, -4, -2, -2)])
+def test_twin_scoring_variants(gx, ctx, oracle, monkeypatch, scores):
+    """Other scores: the twin fill where the admission bound holds (else the
+    scalar fill), bit-exact either way; with and without planes."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    pairs = _twin_pairs(hash(scores) & 0xffff, [(200, 300), (129, 130), (700, 40)], per_shape=2)
+    out = gx.align_batch(pairs, gx.Scores(*scores), False, ctx=ctx, max_cell=False)
+    for (a, b), (steps, r) in zip(pairs, out):
+        o = oracle.align(a, b, scores)
+        assert _steps_list(steps) == o.alignment() and r.score == o.score, (scores, len(a), len(b))
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, _ = st.run(gx.Scores(*scores), False, keep_planes=True, steps=1, plane_sums=True)
+    sums = st.plane_sums()
+    for p, (a, b) in enumerate(pairs):
+        o = oracle.align_lean(a, b, scores)
+        assert [int(x) for x in sums[0, p]] == o.extra["plane_sums"] and res[p].score == o.score, (scores, p)
+
+
+def test_twin_matches_scalar_fill(gx, ctx, monkeypatch):
+    """The twin and the scalar fill give identical results and planes on the same batch."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    pairs = _twin_pairs(5, [(600, 700), (333, 333)], per_shape=4, alphas=(b"ACGT",))
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    r1, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, plane_sums=True)
+    s1 = st.plane_sums().copy()
+    assert ctx.fill_info()["twin"] == 1
+    monkeypatch.setenv("GX_TWIN", "0")
+    r0, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, plane_sums=True)
+    assert ctx.fill_info()["twin"] == 0
+    assert np.array_equal(s1, st.plane_sums())
+    assert [(r.score, r.n_steps, r.matches) for r in r1] == [(r.score, r.n_steps, r.matches) for r in r0]
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (64, 16), (129, 16), (200, 40), (300, 20), (257, 300), (640, 129)])
+def test_twin_table_planes(gx, ctx, oracle, monkeypatch, shape):
+    """GX_TABLE_TWIN=1 fills an alignment table with the twin fill (the pair
+    beside a copy of itself): every exported plane cell and the alignment."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    monkeypatch.setenv("GX_TABLE_TWIN", "1")
+    monkeypatch.setenv("GX_NO_TABLE_PRINT", "1")
+    n, m = shape
+    rng = random.Random(n * 7919 + m)
+    a = bytes(rng.choice(b"ACGT") for _ in range(n))
+    b = bytes(rng.choice(b"ACGT") for _ in range(m))
+    cont = gx.SequenceContainer([gx.Sequence("a", a.decode()), gx.Sequence("b", b.decode())])
+    t, _ = gx.alignment_table(cont, gx.Scores(*CONFIG_SCORES), False, False, ctx=ctx, max_cell=False)
+    assert ctx.fill_info()["twin"] == 1
+    o = oracle.align(a, b, CONFIG_SCORES, want_planes=True)
+    for k in range(3):
+        assert np.array_equal(t.plane(k), o.planes[k]), (shape, k)
+    al = gx.retrace(cont, t, False)
+    assert _steps_list(al._steps) == o.alignment() and al.score == o.score
