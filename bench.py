@@ -140,7 +140,7 @@ def load_traffic(workload: str):
     return None, None
 
 
-def load_valu(workload: str):
+def load_valu(workload: str, twin: bool = False):
     """VALU issue profile of this workload's fill (profiles/valu_fill_*.json,
     made by tools/gpu_valu.sh + tools/valu_summary.py): VALU instructions per
     cell (SQ_INSTS_VALU), the shader clock under this load and the VALU
@@ -155,8 +155,8 @@ def load_valu(workload: str):
                 if "ceiling" not in v:
                     continue
                 for case in ("planes", "noplanes"):
-                    if v.get(case, {}).get("workload") == workload:
-                        c = v[case]
+                    c = v.get(case, {})
+                    if c.get("workload") == workload and ("fill_pk_kernel" in c.get("kernel", "")) == twin:
                         return {"valu_insts_per_cell": c["valu_insts_per_cell"],
                                 "valu_issue_frac": c["valu_issue_frac"], "clock_ghz": c["clock_ghz"],
                                 "peak_tops": c["valu_lane_ops_peak_tops"],
@@ -443,13 +443,15 @@ def main():
     fill_bytes = bytes_per_cell * cells_rank
     achieved = fill_bytes / (avg_fill_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(workload)
-    valu = load_valu(workload)
+    twin = bool(finfo.get("twin"))
+    kname = "gx::fill_pk_kernel (twin fill)" if twin else "gx::fill_kernel"
+    valu = load_valu(workload, twin)
     hbm = {"bound": "hbm", "achieved": round(achieved, 1) if keep_planes else None,
            "peak": PEAK_HBM_GBS, "unit": "GB/s",
            "frac": round(achieved / PEAK_HBM_GBS, 4) if keep_planes else None,
            "frac_of_measured_copy_ceiling": round(achieved / MEASURED_HBM_GBS, 4) if keep_planes else None,
            "traffic": traffic, "traffic_source": traffic_src,
-           "kernel": "gx::fill_kernel", "fill_ms_avg": round(avg_fill_ms, 3),
+           "kernel": kname, "fill_ms_avg": round(avg_fill_ms, 3),
            "algorithmic_bytes_per_cell": bytes_per_cell,
            "algorithmic_bytes_per_launch": fill_bytes}
     if valu is not None and keep_planes and bytes_per_cell == 3:
@@ -459,10 +461,11 @@ def main():
         ach = valu["valu_insts_per_cell"] * cells_rank / (avg_fill_ms * 1e-3) / 1e12
         roofline = {"bound": "valu", "achieved": round(ach, 3), "peak": valu["peak_tops"], "unit": "TOP/s",
                     "frac": round(ach / valu["peak_tops"], 4), "traffic": traffic, "traffic_source": traffic_src,
-                    "kernel": "gx::fill_kernel", "fill_ms_avg": round(avg_fill_ms, 3),
+                    "kernel": kname, "fill_ms_avg": round(avg_fill_ms, 3),
                     "algorithmic_ops_per_cell": valu["valu_insts_per_cell"],
                     "algorithmic_ops_per_launch": round(valu["valu_insts_per_cell"] * cells_rank),
-                    "ops": "int32 VALU lane-operations (wave64 VALU instructions x 64)",
+                    "ops": "VALU lane-operations (wave64 VALU instructions x 64; a packed 16-bit twin "
+                           "instruction updates two pairs' cells)",
                     "peak_basis": f"1024 SIMDs x 64 lanes x {valu['clock_ghz']} GHz / {valu['cpi_fill_mix']} cycles "
                                   f"per wave64 VALU instruction at the fill's mix (tools/valu_probe.hip)",
                     "source": valu["source"], "hbm": hbm}
@@ -480,7 +483,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if args.workload == "allvsall" else "weak",
         "vs_baseline": None,
-        "dtype": "int32",
+        "dtype": "int16x2 (two pairs per register, exact, relative to int32 block bases)" if twin else "int32",
         "data": "synthetic" if args.workload == "synthetic" else "reference FASTA data (tests/golden)",
         "config": {"workload": workload, "pairs_per_gpu": P, "seq_len": L if args.workload == "synthetic" else None,
                    "cells_per_step": total_cells, "parallelism": f"pairs sharded over {world} GPU(s)"},

@@ -632,7 +632,7 @@ static hipError_t enqueue_plane_sums(gx_context* ctx, const FillJob& job, const 
 // of a W-strip band lies within D (192 (k + 1) + 16) + 2 (|a| + |smax| + |smin|)
 // of its base, D = max |V''(i,j) - V''(i',j')| over neighbours = max(|a - g|,
 // |U - g|) (the range proof of d8_planes_ok).  Returns the widest admissible
-// band width <= W_want from {4, 8, 15}, or 0 when the twin fill does not apply
+// band width <= W_want from {3, 4, 7, 8, 15}, or 0 when the twin fill does not apply
 // (shape, mode, scores, GX_TWIN=0).
 static int twin_width(const std::vector<PairHost>& ph, const Scores32& sc, int is_local, bool track, bool lcs, int lay,
                       bool planes, bool d8, int W_want) {
@@ -645,8 +645,8 @@ static int twin_width(const std::vector<PairHost>& ph, const Scores32& sc, int i
     const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
     const long long U = std::max(0LL, smax - a);
     const long long D = std::max(std::llabs(a - g), std::llabs(U - g));
-    for (int W : {15, 8, 4}) {
-        if (W > W_want && W != 4) continue;
+    for (int W : {15, 8, 7, 4, 3}) {
+        if (W > W_want && W != 3) continue;
         const long long bound = D * (192LL * W + 16) + 2 * (std::llabs(a) + std::llabs(smax) + std::llabs(smin)) + 64;
         if (bound < 30000) return W;
     }
@@ -822,7 +822,10 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     HIPCHK(hipMemsetAsync(job.progress.p, 0, std::max<size_t>(prog_elems, 1) * sizeof(int), ctx->stream));
     HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, ctx->stream));
     HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), ctx->stream));
-    const int grid = std::min(bands, fill_grid_cap(ctx->device));
+    // twin workgroups: as many per CU as fit 16 waves (the twin kernels hold
+    // up to 128 VGPRs: 4 waves per SIMD)
+    const int per_cu = (twin && !getenv("GX_FILL_GRID")) ? std::max(1, 16 / (Wf + 1)) : 1;
+    const int grid = std::min(bands, fill_grid_cap(ctx->device) * per_cu);
     const auto h_launch = std::chrono::steady_clock::now();
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].fb : ctx->ev0, eve = slot >= 0 ? ctx->slots[slot].fe : ctx->ev1;
     HIPCHK(hipEventRecord(evb, ctx->stream));

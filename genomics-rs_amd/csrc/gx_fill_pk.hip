@@ -20,7 +20,7 @@
 //     need converting; the blocks it pushes carry that same base;
 //   * the I/O wave converts the band's bottom row back to int32 for HBM.
 // The host admits a launch only when the worst-case spread of a band's values
-// around the inherited bases stays below 2^15 (gx_api.cpp twin_ok).
+// around the inherited bases stays below 2^15 (gx_api.cpp twin_width).
 // Comparisons and max are exact on values within 2^15 of each other, so the
 // codes, landing columns, planes and results equal the int32 fill's.
 #include "gx_device.h"
@@ -629,10 +629,10 @@ static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int ntw
     return hipErrorInvalidValue;
 }
 
-// Twin launch: W from {4, 8, 15}; planes: 0 none, 1 compact.
+// Twin launch: W from {3, 4, 7, 8, 15}; planes: 0 none, 1 compact.
 hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int ntwins, int total_bands, int* d_counter,
                           PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
-    return launch_pk_w<4, 8, 15>(W, planes, d_pairs, ntwins, total_bands, d_counter, d_pres, sc, grid, st);
+    return launch_pk_w<3, 4, 7, 8, 15>(W, planes, d_pairs, ntwins, total_bands, d_counter, d_pres, sc, grid, st);
 }
 
 }  // namespace gx

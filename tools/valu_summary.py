@@ -4,7 +4,10 @@ fill's VALU instructions per cell, and how close it runs to the VALU issue
 ceiling MEASURED on this chip (tools/valu_probe.hip), with and without score
 planes.
 
-    python tools/valu_summary.py gpurun_out/valu_<tag> <tag> [profiles/isa_mix_fill_*.json]
+    python tools/valu_summary.py gpurun_out/valu_<tag> <tag> [profiles/isa_mix_*.json] [waves per SIMD]
+
+(the twin fill, gx_fill_pk.hip: profiles/isa_mix_twin_r02.json at its 8-strip
+bands' 9 waves per CU, ~2 per SIMD)
 
 Ceiling.  valu_probe times independent streams of one instruction form at 1,
 2, 4 and 8 waves per SIMD over the whole chip (kernel wall time x clock x
@@ -36,7 +39,7 @@ def counters(d):
     for kname, ctr, avg, dur in c.execute(
             "select kernel_name, counter_name, avg(value), avg(duration) from counters_collection "
             "group by kernel_name, counter_name"):
-        if "fill_kernel" in kname:
+        if "fill_kernel" in kname or "fill_pk_kernel" in kname:
             out.setdefault(kname, {"duration_ns": dur})[ctr] = avg
     k = max(out, key=lambda n: out[n]["duration_ns"])   # the batch fill: the longest fill launch
     return k, out[k]
@@ -65,14 +68,15 @@ def main():
         probe = json.load(f)
     with open(mix_path) as f:
         mix = json.load(f)
-    cpi_dual, cpi_rest, dual_names = probe_cpi(probe)
+    waves = int(sys.argv[4]) if len(sys.argv) > 4 else FILL_WAVES_PER_SIMD
+    cpi_dual, cpi_rest, dual_names = probe_cpi(probe, waves)
     n_dual = sum(n for op, n in mix["valu"].items() if op.replace("_e32", "").replace("_e64", "") in dual_names)
     f_dual = n_dual / mix["valu_total"]
     cpi = f_dual * cpi_dual + (1 - f_dual) * cpi_rest
     res = {"source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CU_CYCLES SQ_CYCLES SQ_WAVE_CYCLES "
                      "SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE, bench.py --steps 2 "
                      "--warmup 1 (tools/gpu_valu.sh); ceiling from tools/valu_probe.hip",
-           "ceiling": {"waves_per_simd": FILL_WAVES_PER_SIMD, "cpi_dual_rate_ops": round(cpi_dual, 3),
+           "ceiling": {"waves_per_simd": waves, "cpi_dual_rate_ops": round(cpi_dual, 3),
                        "cpi_other_ops": round(cpi_rest, 3), "dual_rate_forms": sorted(dual_names),
                        "dual_rate_fraction_of_fill_valu": round(f_dual, 4),
                        "cpi_fill_mix": round(cpi, 3), "isa_mix": os.path.relpath(mix_path, ROOT),
@@ -91,6 +95,7 @@ def main():
             "duration_ms": round(dur * 1e3, 3),
             "clock_ghz": round(clk / 1e9, 3),
             "valu_insts_per_cell": round(insts * 64 / cells, 2),
+            "valu_insts_per_cell_note": "wave64 instructions x 64 lanes / cells (a packed twin instruction covers two cells)",
             "salu_insts_per_cell": round(v["SQ_INSTS_SALU"] * 64 / cells, 2),
             "valu_issue_frac": round(insts * cpi / (cyc * SIMDS), 4),
             "valu_issue_frac_at_4_cycles": round(insts * 4 / (cyc * SIMDS), 4),
