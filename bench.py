@@ -124,16 +124,17 @@ def _cpu_model():
     return "unknown"
 
 
-def load_traffic(workload: str):
+def load_traffic(workload: str, twin: bool = False):
     """HBM bytes per fill launch from the committed PMC profile of this
-    workload (profiles/pmc_fill_*.json, made by tools/pmc_traffic.py)."""
+    workload and fill kernel (profiles/pmc_fill_*.json, made by
+    tools/gpu_profile.sh + tools/rocpd_summary.py)."""
     for name in sorted(os.listdir(os.path.join(ROOT, "profiles")), reverse=True) if os.path.isdir(
             os.path.join(ROOT, "profiles")) else []:
         if name.startswith("pmc_fill") and name.endswith(".json"):
             try:
                 with open(os.path.join(ROOT, "profiles", name)) as f:
                     d = json.load(f)
-                if d.get("workload") == workload:
+                if d.get("workload") == workload and ("fill_pk_kernel" in d.get("kernel", "")) == twin:
                     return d.get("hbm_bytes_per_launch"), name
             except Exception:
                 continue
@@ -442,9 +443,9 @@ def main():
         workload = f"synthetic {L}x{L} DNA pairs (SplitMix64), {P} per GPU, {mode_s}"
     fill_bytes = bytes_per_cell * cells_rank
     achieved = fill_bytes / (avg_fill_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic(workload)
     twin = bool(finfo.get("twin"))
     kname = "gx::fill_pk_kernel (twin fill)" if twin else "gx::fill_kernel"
+    traffic, traffic_src = load_traffic(workload, twin)
     valu = load_valu(workload, twin)
     hbm = {"bound": "hbm", "achieved": round(achieved, 1) if keep_planes else None,
            "peak": PEAK_HBM_GBS, "unit": "GB/s",

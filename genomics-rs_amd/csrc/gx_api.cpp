@@ -1688,19 +1688,24 @@ static double chunk_budget(gx_context* ctx) {
 }
 
 // Contiguous [begin, end) ranges of the pairs, each within the budget (a pair
-// larger than the budget runs alone).
+// larger than the budget runs alone).  A chunk holding more than one pair ends
+// after an even count when it can, so that equal-shape pairs keep their twin
+// (run_fill pairs 2q with 2q+1).
 static std::vector<std::pair<size_t, size_t>> plan_chunks(gx_context* ctx, const std::vector<PairHost>& ph,
                                                           double plane_bpc) {
     const double budget = chunk_budget(ctx);
     std::vector<std::pair<size_t, size_t>> out;
+    auto bytes = [&](size_t p) { return (ph[p].n && ph[p].m) ? pair_device_bytes(ph[p].n, ph[p].m, plane_bpc) : 0.0; };
     size_t b = 0;
     double acc = 0;
     for (size_t p = 0; p < ph.size(); ++p) {
-        const double x = (ph[p].n && ph[p].m) ? pair_device_bytes(ph[p].n, ph[p].m, plane_bpc) : 0.0;
+        const double x = bytes(p);
         if (p > b && acc + x > budget) {
-            out.emplace_back(b, p);
-            b = p;
-            acc = 0;
+            size_t e = p;
+            if ((e - b) % 2 && e - b > 2) --e;   // even chunk: pair p-1 moves to the next chunk
+            out.emplace_back(b, e);
+            b = e;
+            acc = e < p ? bytes(e) : 0.0;
         }
         acc += x;
     }

@@ -60,7 +60,7 @@ def main():
             if name == "FETCH_SIZE" and "WRITE_SIZE" in pmc:
                 if kname == pmc["WRITE_SIZE"]["kernel"]:
                     pmc[name] = {"kernel": kname, "launches": n, "avg_kib": avg, "avg_duration_ns": dur}
-            elif "fill_kernel" in kname and (name not in pmc or avg > pmc[name]["avg_kib"]):
+            elif ("fill_kernel" in kname or "fill_pk_kernel" in kname) and (name not in pmc or avg > pmc[name]["avg_kib"]):
                 pmc[name] = {"kernel": kname, "launches": n, "avg_kib": avg, "avg_duration_ns": dur}
     with open(os.path.join(src, "bench.json")) as f:
         bench = json.loads(f.read().strip().splitlines()[-1])
