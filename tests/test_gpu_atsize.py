@@ -103,7 +103,8 @@ def _host_fold(table, n, m, chunk=1024):
         w = (iw + jw[None, :])[:, 1:]
         for k in range(3):
             v = table.rows(k, r0, rows)[:, 1:].view(np.uint64)
-            sums[k] = sums[k] + np.sum(v * w, dtype=np.uint64)
+            with np.errstate(over="ignore"):   # the checksum wraps mod 2^64 by design
+                sums[k] = sums[k] + np.sum(v * w, dtype=np.uint64)
     return [int(x) for x in sums]
 
 
