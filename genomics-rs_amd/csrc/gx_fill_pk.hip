@@ -55,11 +55,13 @@ __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(d) : "v"(m), "v"(a), "v"(b));
     return d;
 }
-// code bit-planes: each half shifted left by one, the sign mask's low bit shifted in
-__device__ __forceinline__ uint32_t pcode(uint32_t c, uint32_t m) {
-    const uint32_t t = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u2, c) << (u2){1, 1});
+// Code bit-planes, kept negated: with N = -C (mod 2^16 per half) and the
+// sign mask m = -bit, C' = 2C + bit becomes N' = 2N + m -- one v_pk_mad_u16
+// (a shift and a masked or on C).  The code words are negated back once per
+// 16 steps, when they are stored.
+__device__ __forceinline__ uint32_t pcode(uint32_t n, uint32_t m) {
     uint32_t d;
-    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(d) : "v"(m), "s"(0x00010001u), "v"(t));
+    asm("v_pk_mad_u16 %0, %1, 2, %2 op_sel_hi:[1,0,1]" : "=v"(d) : "v"(n), "v"(m));
     return d;
 }
 // 0 where the two bytes match, 1 elsewhere (per half)
@@ -122,7 +124,7 @@ struct PkScores {
 // One row of a lane, both pairs: the cell left of the one being computed.
 struct RowPk {
     uint32_t I, SD, Dd, SMp, SMtl;   // insert, max(sub, delete), delete successor, score_max + sm'', SMp(i-1, j-1)
-    uint32_t cI, cD;                 // code bit-planes (16 steps, one per half)
+    uint32_t cI, cD;                 // code bit-planes, negated (16 steps, one per half; pcode)
     uint32_t E, Etl;                 // landing columns (int16 per half)
 };
 struct LanePk {
@@ -420,8 +422,9 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
         {   // code words of both pairs: codes[strip][t/16][lane][row-in-lane]
             typedef unsigned v2u __attribute__((ext_vector_type(2)));
             typedef __attribute__((address_space(1))) v2u gv2u;
-            const v2u c0 = {(st.a.cD << 16) | (st.a.cI & 0xFFFFu), (st.b.cD << 16) | (st.b.cI & 0xFFFFu)};
-            const v2u c1 = {(st.a.cD & 0xFFFF0000u) | (st.a.cI >> 16), (st.b.cD & 0xFFFF0000u) | (st.b.cI >> 16)};
+            const uint32_t aI = psub(0, st.a.cI), aD = psub(0, st.a.cD), bI = psub(0, st.b.cI), bD = psub(0, st.b.cD);
+            const v2u c0 = {(aD << 16) | (aI & 0xFFFFu), (bD << 16) | (bI & 0xFFFFu)};
+            const v2u c1 = {(aD & 0xFFFF0000u) | (aI >> 16), (bD & 0xFFFF0000u) | (bI >> 16)};
             const size_t wo = ((size_t)(t0 >> 4) * kWave + lane) * kRowsPerLane;
             *(gv2u*)(w.codes[0] + wo) = c0;
             *(gv2u*)(w.codes[1] + wo) = c1;

@@ -1,5 +1,6 @@
 # GPU box: interleaved timing of environment settings over "P|flags" cases.
 #   gpurun -- 'bash tools/gpu_envab.sh "GX_FILL_GRID=1024 GX_FILL_GRID=256" "8| 16|" 3'
+# (settings joined by commas within one variant; flags joined by commas within one case)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -10,7 +11,7 @@ for r in $(seq 1 "$R"); do
   for C in $2; do
     for E in $1; do
       P=${C%%|*}; F=${C#*|}
-      env ${E//,/ } timeout -k 10 300 python bench.py --pairs-per-gpu $P --steps 4 --warmup 1 --no-cpu-baseline $F \
+      env ${E//,/ } timeout -k 10 300 python bench.py --pairs-per-gpu $P --steps 4 --warmup 1 --no-cpu-baseline ${F//,/ } \
           > "$O/b.json" 2>> "$O/err.log" || { echo BENCH_FAIL $E $C; tail -20 "$O/err.log"; exit 1; }
       python3 - "$E" "$C" >> "$O/ab.tsv" <<'PY'
 import json, sys
