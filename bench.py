@@ -84,9 +84,10 @@ def cpu_baseline(s1: bytes, s2: bytes, target_s: float, is_local: bool):
         path = oracle.LIB_PATH
         kind_note = "gcc -O3 -march=x86-64-v3"
     try:
-        os.sched_setaffinity(0, {sorted(os.sched_getaffinity(0))[0]})
+        allowed = os.sched_getaffinity(0)
+        os.sched_setaffinity(0, {sorted(allowed)[0]})
     except Exception:
-        pass
+        allowed = None
     # grow the sample until one run takes >= half the target (the per-row cost
     # falls as rows share pages of the column-major table, so extrapolating
     # from a few rows would overshoot); the touched part of the table stays
@@ -100,6 +101,11 @@ def cpu_baseline(s1: bytes, s2: bytes, target_s: float, is_local: bool):
         if dt >= target_s / 2 or rows >= max_rows:
             break
         rows = int(min(max_rows, rows * min(8.0, max(2.0, target_s / max(dt, 1e-3)))))
+    if allowed:
+        try:
+            os.sched_setaffinity(0, allowed)
+        except Exception:
+            pass
     return {
         "value": round(cells / dt / 1e9, 6),
         "unit": "GCUPS",
@@ -166,6 +172,59 @@ def load_valu(workload: str, twin: bool = False):
             except Exception:
                 continue
     return None
+
+
+def cpu_baseline_parallel(pairs, threads: int, target_s: float, is_local: bool):
+    """The same reference-layout restatement on `threads` host cores at once,
+    one independent pair per thread (the batch shape the GPU runs; the
+    reference's own CLI aligns one pair at a time): each thread fills the first
+    R rows of its pair, R sized so all tables stay under ~48 GB, timed
+    wall-clock.  ctypes releases the GIL for the duration of each fill."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test/measurement infrastructure, CPU baseline only
+    import tempfile
+    import threading
+    path = os.path.join(tempfile.mkdtemp(prefix="gx_cpu_"), "liboracle_native.so")
+    try:
+        oracle.build(native=True, out=path)
+    except Exception:
+        oracle.build()
+        path = oracle.LIB_PATH
+    threads = max(1, min(threads, len(pairs)))
+    cpus = sorted(os.sched_getaffinity(0))[:threads]
+    threads = len(cpus)
+    m = max(len(b) for _, b in pairs[:threads])
+    max_rows = int(48e9 / threads / (48 * (m + 1)))
+    rows = 64
+    while True:
+        res = [None] * threads
+
+        def work(k):
+            try:
+                os.sched_setaffinity(0, {cpus[k]})   # this thread only (Linux: per-thread affinity)
+            except Exception:
+                pass
+            a, b = pairs[k]
+            res[k] = oracle.ref_layout_fill_rows(a, b, min(rows, len(a) + 1), SCORES, is_local, lib_path=path)[0]
+
+        ts = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
+        t0 = time.perf_counter()
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        dt = time.perf_counter() - t0
+        if dt >= target_s / 2 or rows >= max_rows:
+            break
+        rows = int(min(max_rows, rows * min(8.0, max(2.0, target_s / max(dt, 1e-3)))))
+    cells = sum(res)
+    return {
+        "value": round(cells / dt / 1e9, 6), "unit": "GCUPS", "cores": threads, "kind": "port",
+        "sample": f"the cpu_baseline restatement on {threads} cores at once, one synthetic pair per core "
+                  f"(pairs 0-{threads - 1}), first {rows - 1} interior rows x {m} columns each; {cells} cells in "
+                  f"{dt:.2f} s wall",
+        "seconds": round(dt, 3),
+    }
 
 
 def fasta_pair(gx, which: str):
@@ -336,6 +395,8 @@ def main():
     ap.add_argument("--local", action="store_true", help="Smith-Waterman mode (default: global NW)")
     ap.add_argument("--no-planes", action="store_true", help="score+traceback only (not the headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="cores of the all-cores CPU baseline (the GPU box's CPU share is 16; 1 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="skip the parity pass against the oracle digests")
     ap.add_argument("--workload", choices=["synthetic", "allvsall", "covid", "brca2"], default="synthetic",
@@ -554,6 +615,9 @@ def main():
                                              "(SURVEY.md 8(d))"}
         else:
             out["cpu_baseline"] = cpu_baseline(pairs[0][0], pairs[0][1], args.cpu_seconds, args.local)
+            if args.cpu_threads > 1:
+                out["cpu_baseline_all_cores"] = cpu_baseline_parallel(pairs, args.cpu_threads, args.cpu_seconds / 2,
+                                                                      args.local)
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()
