@@ -626,28 +626,38 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // matches_at_max, algo.rs:258-262, 279); lcs: also keep the LCS plane.
 static hipError_t enqueue_plane_sums(gx_context* ctx, const FillJob& job, const Scores32& sc, unsigned long long* out);
 
-// The twin fill (gx_fill_pk.hip): two pairs of equal shape per band, one in
-// each 16-bit half.  Its values are kept relative to bases that a band's
+// The twin fill (gx_fill_pk.hip): two pairs per band, one in each 16-bit
+// half.  Its values are kept relative to bases that a band's
 // strips inherit from its top row (see the file header); a value of strip k
 // of a W-strip band lies within D (192 (k + 1) + 16) + 2 (|a| + |smax| + |smin|)
 // of its base, D = max |V''(i,j) - V''(i',j')| over neighbours = max(|a - g|,
 // |U - g|) (the range proof of d8_planes_ok).  Returns the widest admissible
 // band width <= W_want from {3, 4, 7, 8, 15}, or 0 when the twin fill does not apply
-// (shape, mode, scores, GX_TWIN=0).
+// (shape, mode, scores, GX_TWIN=0; run_fill also skips it for short queues).
+// Pairs 2q and 2q+1 form twin q whatever
+// their shapes: the sweep covers the larger n and m, the shorter pair's state
+// stays at its last column (its values beyond lie in the row above's range,
+// but the bound takes the column difference anyway); an odd last pair is
+// twinned with itself (run_fill's phantom descriptor).
 static int twin_width(const std::vector<PairHost>& ph, const Scores32& sc, int is_local, bool track, bool lcs, int lay,
                       bool planes, bool d8, int W_want) {
     if (const char* e = getenv("GX_TWIN"); e && !strcmp(e, "0")) return 0;
     if (lay != 0 || is_local || track || lcs || (planes && !d8) || sc.g > 0 || sc.h > 0) return 0;
-    if (ph.empty() || ph.size() % 2) return 0;
-    for (size_t q = 0; q + 1 < ph.size(); q += 2)
-        if (ph[q].n != ph[q + 1].n || ph[q].m != ph[q + 1].m || ph[q].m + 80 > 32000) return 0;
+    if (ph.empty()) return 0;
+    long long dm = 0;
+    for (size_t q = 0; q < ph.size(); q += 2) {
+        const PairHost& x = ph[q];
+        const PairHost& y = q + 1 < ph.size() ? ph[q + 1] : ph[q];
+        if (!x.n || !x.m || !y.n || !y.m || std::max(x.m, y.m) + 80 > 32000) return 0;
+        dm = std::max(dm, std::llabs((long long)x.m - (long long)y.m));
+    }
     const long long g = sc.g, a = (long long)sc.h + sc.g;
     const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
     const long long U = std::max(0LL, smax - a);
     const long long D = std::max(std::llabs(a - g), std::llabs(U - g));
     for (int W : {15, 8, 7, 4, 3}) {
         if (W > W_want && W != 3) continue;
-        const long long bound = D * (192LL * W + 16) + 2 * (std::llabs(a) + std::llabs(smax) + std::llabs(smin)) + 64;
+        const long long bound = D * (192LL * W + 16 + dm) + 2 * (std::llabs(a) + std::llabs(smax) + std::llabs(smin)) + 64;
         if (bound < 30000) return W;
     }
     return 0;
@@ -692,6 +702,16 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         if (const char* e = getenv("GX_BAND_WAVES")) wt_want = atoi(e);
         else wt_want = fill_band_waves(false, total_strips / 2, fill_grid_cap(ctx->device), lay, min_strips);
         Wt = twin_width(ph, sc, is_local, track, lcs, lay, planes, d8, wt_want);
+        // auto: only queues of >= 2.5 rounds of scalar bands (a twin band is
+        // ~1.3x slower per step, so short queues lose parallelism: 30k pairs,
+        // fill ms scalar/twin: 4 pairs 7.2/9.7, 8 9.9/10.0, 16 14.4/15.4, 32
+        // 24.7/22.0, all-vs-all 34.5/29.5, 80 53.0/47.2); GX_TWIN=1 forces it
+        const char* e = getenv("GX_TWIN");
+        if (Wt && !(e && !strcmp(e, "1"))) {
+            long long scalar_bands = 0;
+            for (const PairHost& h : ph) scalar_bands += ceil_div(ceil_div((int)h.n, SR), W);
+            if (2 * scalar_bands < 5LL * fill_grid_cap(ctx->device)) Wt = 0;
+        }
     }
     const bool twin = Wt > 0;
     job.twin = twin;
@@ -711,16 +731,23 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         const int n = (int)ph[p].n, m = (int)ph[p].m;
         PairDev& d = job.pd[p];
         d.n = n; d.m = m;
-        d.strips = ceil_div(n, SR);
+        // the shape the pair is laid out for: its own, or its twin's larger n and m
+        int ns = n, ms = m;
+        if (twin) {
+            const PairHost& x = ph[p & ~(size_t)1];
+            const PairHost& y = (p | 1) < P ? ph[p | 1] : x;
+            ns = (int)std::max(x.n, y.n); ms = (int)std::max(x.m, y.m);
+        }
+        d.strips = ceil_div(ns, SR);
         d.bands = ceil_div(d.strips, Wf);
         // steps per strip: layout 0, lane 63 pushes column m at step m + 63; layout 1, column m at step m - 1
-        const int T = lay ? m + 1 : m + kWave;
+        const int T = lay ? ms + 1 : ms + kWave;
         d.t16 = ceil_div(T, 16);
         d.t4 = d.t16 * 4;
         d.band_base = bands;
         d.strip_base = strips;
-        d.feed_stride = (int)align_up((size_t)m + 1 + 64, 16);
-        d.skel_stride = (int)align_up((size_t)m + 1, 64);
+        d.feed_stride = (int)align_up((size_t)ms + 1 + 64, 16);
+        d.skel_stride = (int)align_up((size_t)ms + 1, 64);
         const bool second = twin && (p & 1);   // the twin's second pair: its bands, feed and skeleton are the first's
         if (!second) bands += d.bands;
         strips += d.strips;
@@ -749,7 +776,10 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     if ((rc = pool_get(ctx, std::max<size_t>(feed_recs, 1) * sizeof(Rec), &job.feed))) return rc;
     if ((rc = pool_get(ctx, std::max<size_t>(prog_elems, 1) * sizeof(int), &job.progress))) return rc;
     if ((rc = pool_get(ctx, std::max(strips, 1) * sizeof(StripRes), &job.sres))) return rc;
-    if ((rc = pool_get(ctx, P * sizeof(PairRes), &job.pres))) return rc;
+    // an odd twin launch ends with a phantom descriptor: the last pair again,
+    // its twin in the other half (same buffers, same bytes written twice)
+    const size_t Pd = P + (twin && (P & 1) ? 1 : 0);
+    if ((rc = pool_get(ctx, Pd * sizeof(PairRes), &job.pres))) return rc;
     // band queue order, stored after the pair descriptors: band-major ("round"
     // order: band 0 of every pair, then band 1, ...; a band's predecessor in its
     // pair is always dequeued before it, so a waiting band is never waiting on
@@ -776,7 +806,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         }
     }
     const size_t ord_bytes = align_up(order.size() * sizeof(int), 16);   // keeps the PairRes staging 16-B aligned
-    if ((rc = pool_get(ctx, P * sizeof(PairDev) + ord_bytes, &job.pairs))) return rc;
+    if ((rc = pool_get(ctx, Pd * sizeof(PairDev) + ord_bytes, &job.pairs))) return rc;
     if ((rc = pool_get(ctx, 64, &job.counter))) return rc;
     // -- chars upload
     const uint8_t* cbase = chars_dev;
@@ -813,15 +843,16 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         for (size_t p = 0; p < P; ++p) job.pd[p].trace = (StripTrace*)trace.p + job.pd[p].strip_base;
     }
     // descriptors in (and results out) through pinned staging, laid out [PairDev x P | PairRes x P | status]
-    const size_t pin_bytes = P * (sizeof(PairDev) + sizeof(PairRes)) + ord_bytes + 2 * sizeof(int);
+    const size_t pin_bytes = Pd * sizeof(PairDev) + P * sizeof(PairRes) + ord_bytes + 2 * sizeof(int);
     char* pin = (char*)(slot >= 0 ? pinned_grow(ctx->slots[slot].fpin, pin_bytes) : io_pinned(ctx, pin_bytes));
     if (!pin) return fail(GX_ENOMEM, "pinned staging buffer");
     memcpy(pin, job.pd.data(), P * sizeof(PairDev));
-    if (!order.empty()) memcpy(pin + P * sizeof(PairDev), order.data(), order.size() * sizeof(int));
-    HIPCHK(hipMemcpyAsync(job.pairs.p, pin, P * sizeof(PairDev) + ord_bytes, hipMemcpyHostToDevice, ctx->stream));
+    if (Pd > P) memcpy(pin + P * sizeof(PairDev), &job.pd[P - 1], sizeof(PairDev));
+    if (!order.empty()) memcpy(pin + Pd * sizeof(PairDev), order.data(), order.size() * sizeof(int));
+    HIPCHK(hipMemcpyAsync(job.pairs.p, pin, Pd * sizeof(PairDev) + ord_bytes, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemsetAsync(job.progress.p, 0, std::max<size_t>(prog_elems, 1) * sizeof(int), ctx->stream));
     HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, ctx->stream));
-    HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), ctx->stream));
+    HIPCHK(hipMemsetAsync(job.pres.p, 0, Pd * sizeof(PairRes), ctx->stream));
     // twin workgroups: as many per CU as fit 16 waves (the twin kernels hold
     // up to 128 VGPRs: 4 waves per SIMD)
     const int per_cu = (twin && !getenv("GX_FILL_GRID")) ? std::max(1, 16 / (Wf + 1)) : 1;
@@ -830,7 +861,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].fb : ctx->ev0, eve = slot >= 0 ? ctx->slots[slot].fe : ctx->ev1;
     HIPCHK(hipEventRecord(evb, ctx->stream));
     if (bands > 0 && twin)
-        HIPCHK(launch_fill_pk(Wf, planes ? 1 : 0, (const PairDev*)job.pairs.p, (int)(P / 2), bands, (int*)job.counter.p,
+        HIPCHK(launch_fill_pk(Wf, planes ? 1 : 0, (const PairDev*)job.pairs.p, (int)(Pd / 2), bands, (int*)job.counter.p,
                               (PairRes*)job.pres.p, scl, grid, ctx->stream));
     else if (bands > 0)
         HIPCHK(launch_fill(W, lay, is_local != 0, planes ? (d8 ? 2 : 1) : 0, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
@@ -847,8 +878,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                                (PairRes*)job.pres.p, ctx->stream));
     job.res.assign(P, PairRes{});
     int status[2] = {0, 0};
-    PairRes* pin_res = (PairRes*)(pin + P * sizeof(PairDev) + ord_bytes);
-    int* pin_status = (int*)(pin + P * (sizeof(PairDev) + sizeof(PairRes)) + ord_bytes);
+    PairRes* pin_res = (PairRes*)(pin + Pd * sizeof(PairDev) + ord_bytes);
+    int* pin_status = (int*)(pin + Pd * sizeof(PairDev) + P * sizeof(PairRes) + ord_bytes);
     HIPCHK(hipMemcpyAsync(pin_res, job.pres.p, P * sizeof(PairRes), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipMemcpyAsync(pin_status, job.counter.p, sizeof status, hipMemcpyDeviceToHost, ctx->stream));
     job.pin_res = pin_res;

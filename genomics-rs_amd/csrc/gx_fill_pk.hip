@@ -133,10 +133,11 @@ struct LanePk {
 };
 
 // algo.rs:222-268 on the shifted values, both pairs at once; MASKED keeps
-// the lanes outside columns 1..m unchanged.
+// the lanes outside columns 1..m unchanged, per pair (a twin's two pairs may
+// differ in length: the shorter one's state stays at its last column).
 template <bool MASKED>
 __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const uint32_t sm_in, const uint32_t e_up,
-                                        const uint32_t c2, const uint32_t c1, const bool act, const PkScores& k,
+                                        const uint32_t c2, const uint32_t c1, const uint32_t act, const PkScores& k,
                                         uint32_t& oI, uint32_t& oD, uint32_t& oS, uint32_t& oIold) {
     const uint32_t In = pmax(st.I, padds(st.SD, k.h));            // max(I, max(S,D) + h)   (algo.rs:231-236)
     const uint32_t Sn = pmad(pmis(c1, c2), k.dsm, st.SMtl);        // SM(i-1,j-1) + s''       (algo.rs:245-248)
@@ -153,9 +154,9 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
     const uint32_t cDn = pcode(st.cD, m2);
     const uint32_t SMpn = padds(SMn, k.smp);
     oI = In; oD = Dn; oS = Sn; oIold = st.I;
-    if (MASKED) {
-        st.I = act ? In : st.I; st.SD = act ? SDn : st.SD; st.Dd = act ? Ddn : st.Dd; st.SMp = act ? SMpn : st.SMp;
-        st.E = act ? En : st.E;
+    if (MASKED) {   // act: 0xFFFF in each half whose pair has this column
+        st.I = bfi(act, In, st.I); st.SD = bfi(act, SDn, st.SD); st.Dd = bfi(act, Ddn, st.Dd);
+        st.SMp = bfi(act, SMpn, st.SMp); st.E = bfi(act, En, st.E);
     } else {
         st.I = In; st.SD = SDn; st.Dd = Ddn; st.SMp = SMpn; st.E = En;
     }
@@ -165,15 +166,17 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
 }
 
 template <bool MASKED>
-__device__ __forceinline__ void dp_step_pk(LanePk& st, const Rec& r, const int t, const int lane, const int m,
-                                           const uint32_t c1a, const uint32_t c1b, const PkScores& k,
+__device__ __forceinline__ void dp_step_pk(LanePk& st, const Rec& r, const int t, const int lane, const int m0,
+                                           const int m1, const uint32_t c1a, const uint32_t c1b, const PkScores& k,
                                            uint32_t (&oI)[2], uint32_t (&oD)[2], uint32_t (&oS)[2],
                                            uint32_t (&oL)[2]) {
     const uint32_t dd_in = (uint32_t)shr1(r.dd, (int)st.b.Dd);
     const uint32_t sm_in = (uint32_t)shr1(r.sm, (int)st.b.SMp);
     const uint32_t c2 = (uint32_t)shr1(r.c2, (int)st.c2c);
     const uint32_t e_in = (uint32_t)shr1((int)pk2(t + 1, t + 1), (int)st.b.E);   // lane 0: its own column
-    const bool act = MASKED ? (unsigned)(t - lane) < (unsigned)m : true;
+    const uint32_t act = MASKED ? ((unsigned)(t - lane) < (unsigned)m0 ? 0xFFFFu : 0u) |
+                                      ((unsigned)(t - lane) < (unsigned)m1 ? 0xFFFF0000u : 0u)
+                                : ~0u;
     cell_pk<MASKED>(st.a, dd_in, sm_in, e_in, c2, c1a, act, k, oI[0], oD[0], oS[0], oL[0]);
     cell_pk<MASKED>(st.b, st.a.Dd, st.a.SMp, st.a.E, c2, c1b, act, k, oI[1], oD[1], oS[1], oL[1]);
     st.c2c = c2;
@@ -222,7 +225,8 @@ struct WavePk {
     uint32_t skel_voff;
     uint32_t scratch;
     uint32_t cnt_addr;
-    int m, lane;
+    int m, lane;                                      // m: the twin's columns (the longer pair's)
+    int m0, m1;                                       // each pair's own columns
     uint32_t c1a, c1b;
     int B0, B1;                                       // current bases (wave-uniform)
 };
@@ -242,39 +246,39 @@ __device__ __forceinline__ void group4_pk(LanePk& st, Rec (&nxt)[4], WavePk& w, 
     if (MASKED) {
         auto sko = [&](int c) { return (c >= 0 && c <= w.m) ? w.skel_voff + 4u * (uint32_t)c : kSkelOff; };
         push63_pk<4 * G4 + 0>(out_base, st, lane63_mask(push_on && col0 >= 0 && col0 <= w.m));
-        dp_step_pk<true>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, k, bI[0], bD[0], bS[0], bL[0]);
+        dp_step_pk<true>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[0], bD[0], bS[0], bL[0]);
         if (PLANES) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
         skel_store(w.skel_rsrc, sko(col0 + 1), (int)st.b.E);
         push63_pk<4 * G4 + 1>(out_base, st, lane63_mask(push_on && col0 + 1 >= 0 && col0 + 1 <= w.m));
-        dp_step_pk<true>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, k, bI[1], bD[1], bS[1], bL[1]);
+        dp_step_pk<true>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[1], bD[1], bS[1], bL[1]);
         if (PLANES) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
         skel_store(w.skel_rsrc, sko(col0 + 2), (int)st.b.E);
         push63_pk<4 * G4 + 2>(out_base, st, lane63_mask(push_on && col0 + 2 >= 0 && col0 + 2 <= w.m));
-        dp_step_pk<true>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, k, bI[2], bD[2], bS[2], bL[2]);
+        dp_step_pk<true>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[2], bD[2], bS[2], bL[2]);
         if (PLANES) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
         skel_store(w.skel_rsrc, sko(col0 + 3), (int)st.b.E);
         push63_pk<4 * G4 + 3>(out_base, st, lane63_mask(push_on && col0 + 3 >= 0 && col0 + 3 <= w.m));
         if (push_on && col0 + 3 >= 0 && col0 <= w.m) lds_store_lane0(w.wcnt_out, min(col0 + 3, w.m) + 1);
-        dp_step_pk<true>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, k, bI[3], bD[3], bS[3], bL[3]);
+        dp_step_pk<true>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[3], bD[3], bS[3], bL[3]);
         if (PLANES) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
         skel_store(w.skel_rsrc, sko(col0 + 4), (int)st.b.E);
     } else {
         const uint32_t pa = push_on && w.lane == kWave - 1 ? out_base : w.scratch;
         push_all_pk<4 * G4 + 0>(pa, st);
-        dp_step_pk<false>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, k, bI[0], bD[0], bS[0], bL[0]);
+        dp_step_pk<false>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[0], bD[0], bS[0], bL[0]);
         if (PLANES) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
         const uint32_t e0 = st.b.E;
         push_all_pk<4 * G4 + 1>(pa, st);
-        dp_step_pk<false>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, k, bI[1], bD[1], bS[1], bL[1]);
+        dp_step_pk<false>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[1], bD[1], bS[1], bL[1]);
         if (PLANES) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
         const uint32_t e1 = st.b.E;
         push_all_pk<4 * G4 + 2>(pa, st);
-        dp_step_pk<false>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, k, bI[2], bD[2], bS[2], bL[2]);
+        dp_step_pk<false>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[2], bD[2], bS[2], bL[2]);
         if (PLANES) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
         const uint32_t e2 = st.b.E;
         push_all_pk<4 * G4 + 3>(pa, st);
         publish_all(w.cnt_addr, col0 + 3 + 1);
-        dp_step_pk<false>(st, cur[3], t + 3, w.lane, w.m, w.c1a, w.c1b, k, bI[3], bD[3], bS[3], bL[3]);
+        dp_step_pk<false>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[3], bD[3], bS[3], bL[3]);
         if (PLANES) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
         skel_store4(w.skel_rsrc, w.skel_voff + 4u * (uint32_t)(col0 + 1), (int)e0, (int)e1, (int)e2, (int)st.b.E);
     }
@@ -342,9 +346,11 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
                                 lds_int* rcnt_in, lds_int* wcnt_out, lds_int* rcnt_out, lds_int* base_in,
                                 lds_int* base_out, const bool has_consumer, PairRes* pres0, PairRes* pres1,
                                 int* status, const uint32_t scratch_base) {
-    const int n = P0.n, m = P0.m;
+    // a twin's pairs may differ in shape: the sweep covers the longer's rows
+    // and columns (the host lays both out for that shape); each pair keeps
+    // its own characters, column masks and end cell
+    const int m = max(P0.m, P1.m), mmin = min(P0.m, P1.m);
     const int ia = s * kStripRows + kRowsPerLane * lane + 1;
-    const bool ok_a = ia <= n, ok_b = ia + 1 <= n;
     WavePk w;
     {
         const size_t strip_planes = (size_t)s * P0.t4 * kGroupInts;   // bytes per compact plane per strip
@@ -364,9 +370,9 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
     w.skel_voff = lane == kWave - 1 ? 0u : kSkelOff;
     w.scratch = scratch_base + 4u * (uint32_t)lane;
     w.cnt_addr = (has_consumer && lane == kWave - 1) ? lds_addr((const void*)wcnt_out) : w.scratch;
-    w.m = m; w.lane = lane;
-    w.c1a = pk2(ok_a ? (int)P0.c1[ia - 1] : 0x100, ok_a ? (int)P1.c1[ia - 1] : 0x100);
-    w.c1b = pk2(ok_b ? (int)P0.c1[ia] : 0x100, ok_b ? (int)P1.c1[ia] : 0x100);
+    w.m = m; w.lane = lane; w.m0 = P0.m; w.m1 = P1.m;
+    w.c1a = pk2(ia <= P0.n ? (int)P0.c1[ia - 1] : 0x100, ia <= P1.n ? (int)P1.c1[ia - 1] : 0x100);
+    w.c1b = pk2(ia + 1 <= P0.n ? (int)P0.c1[ia] : 0x100, ia + 1 <= P1.n ? (int)P1.c1[ia] : 0x100);
 
     // column 0 of the row above: its bases and record (published with the ring's first counter)
     wait_ge(wcnt_in, min(4, m) + 1, status);
@@ -415,7 +421,7 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
             base_out[2 * kk + 1] = w.B1;
         }
         const size_t sb_off = (size_t)(t0 >> 2) * kGroupInts;
-        const bool full = (t0 >= kWave) && (t0 + kSub - 1 <= m - 1);
+        const bool full = (t0 >= kWave) && (t0 + kSub - 1 <= mmin - 1);
         const uint32_t out_base = lds_addr(ring_out + ring_slot(t0 - (kWave - 1)));
         if (full) sub_block_pk<PLANES, false>(st, nxt, w, k, t0, out_base, has_consumer, sb_off);
         else sub_block_pk<PLANES, true>(st, nxt, w, k, t0, out_base, has_consumer, sb_off);
@@ -431,11 +437,16 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
         }
         lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
     }
-    // cell (n, m) of both pairs: score_max (shifted, absolute) and landing column
-    const bool fa = ok_a && ia == n, fb = ok_b && ia + 1 == n;
-    if (fa || fb) {
+    // cell (n, m) of each pair: score_max (shifted, absolute) and landing
+    // column (a shorter pair's lanes stopped at its own last column)
+    if (ia == P0.n || ia + 1 == P0.n) {
+        const bool fa = ia == P0.n;
         const uint32_t sm = psubs(fa ? st.a.SMp : st.b.SMp, k.smp), e = fa ? st.a.E : st.b.E;
         pres0->end_SM = lo16(sm) + w.B0; pres0->end_E = lo16(e);
+    }
+    if (ia == P1.n || ia + 1 == P1.n) {
+        const bool fa = ia == P1.n;
+        const uint32_t sm = psubs(fa ? st.a.SMp : st.b.SMp, k.smp), e = fa ? st.a.E : st.b.E;
         pres1->end_SM = hi16(sm) + w.B1; pres1->end_E = hi16(e);
     }
 }
@@ -453,7 +464,7 @@ __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, c
                            const PkScores& k, Rec* ring0, const Rec* ringW, lds_int* wcnt0, lds_int* rcnt0,
                            lds_int* wcntW, lds_int* rcntW, lds_int* base0, lds_int* baseW, const bool do_out,
                            int* status) {
-    const int m = P0.m;
+    const int m = max(P0.m, P1.m);   // the twin's columns; a shorter pair's columns beyond its own never match
     constexpr int CH = 16;
     int in_next = 0, out_next = 0;
     RecW* feed = reinterpret_cast<RecW*>(P0.feed);
@@ -480,7 +491,7 @@ __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, c
                         else {
                             dd0 = dd1 = 2 * sc.h;
                             sm0 = sm1 = sc.h + smp;
-                            c2 = (int)pk2(P0.c2[j - 1], P1.c2[j - 1]);
+                            c2 = (int)pk2(j <= P0.m ? (int)P0.c2[j - 1] : 0x200, j <= P1.m ? (int)P1.c2[j - 1] : 0x200);
                         }
                     } else {
                         const gu64* q = (const gu64*)(feed_in + j);

@@ -237,6 +237,7 @@ def test_chunks_keep_twins(gx, ctx, monkeypatch):
     pdb = (1024 + 128) * (1024 + 64) * 3.25 + 64 * (1024 + 64) * (1024 // 64 + 2) / 8 + 65536   # pair_device_bytes
     monkeypatch.setenv("GX_CHUNK_BYTES", str(5.5 * pdb))
     monkeypatch.setenv("GX_LAYOUT", "0")
+    monkeypatch.setenv("GX_TWIN", "1")   # 4-pair chunks: a short queue would take the scalar fill
     cases = _synth(1024)[:40]
     pairs = [_synth_pair(c["k"], 1024) for c in cases]
     info = _staged_check(gx, ctx, pairs, cases, steps=1)

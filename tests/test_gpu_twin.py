@@ -38,6 +38,13 @@ def _twin_pairs(seed, shapes, per_shape=2, alphas=(b"ACGT", b"AC", b"ACGTN", b"A
     return pairs
 
 
+@pytest.fixture(autouse=True)
+def _force_twin(monkeypatch):
+    """The batches here are small: force the twin fill (by default it runs
+    only for band queues of >= 2.5 rounds, gx_api.cpp run_fill)."""
+    monkeypatch.setenv("GX_TWIN", "1")
+
+
 @pytest.fixture(params=sorted(LAUNCH))
 def launch(request, monkeypatch):
     for k, v in LAUNCH[request.param].items():
@@ -127,3 +134,37 @@ def test_twin_table_planes(gx, ctx, oracle, monkeypatch, shape):
         assert np.array_equal(t.plane(k), o.planes[k]), (shape, k)
     al = gx.retrace(cont, t, False)
     assert _steps_list(al._steps) == o.alignment() and al.score == o.score
+
+
+MIXED = [((129, 300), (300, 129)), ((1, 1), (5, 9)), ((1, 300), (300, 1)), ((700, 257), (640, 300)),
+         ((64, 63), (63, 64)), ((1000, 77), (999, 80)), ((257, 256), (128, 1000))]
+
+
+@pytest.mark.parametrize("odd", [False, True])
+def test_twin_mixed_shapes(gx, ctx, oracle, monkeypatch, odd):
+    """Twins of different shapes (the sweep covers the larger n and m, the
+    shorter pair stops at its own last column) and an odd count (the last
+    pair twinned with itself): every alignment, score and plane checksum."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    rng = random.Random(17 + odd)
+    shapes = [s for tw in MIXED for s in tw] + ([(333, 222)] if odd else [])
+    pairs = [(bytes(rng.choice(b"ACGT") for _ in range(n)), bytes(rng.choice(b"ACGT") for _ in range(m)))
+             for n, m in shapes]
+    out = gx.align_batch(pairs, gx.Scores(*CONFIG_SCORES), False, ctx=ctx, max_cell=False)
+    assert ctx.fill_info()["twin"] == 1
+    for (a, b), (steps, r) in zip(pairs, out):
+        o = oracle.align(a, b, CONFIG_SCORES)
+        assert _steps_list(steps) == o.alignment(), (len(a), len(b))
+        assert (r.score, r.matches, r.mismatches, r.gap_extensions, r.opening_gaps) == \
+               (o.score, o.matches, o.mismatches, o.gap_extensions, o.opening_gaps)
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=2, plane_sums=True)
+    info = ctx.fill_info()
+    assert info["twin"] == 1 and info["plane_bytes_per_cell"] == 3, info
+    sums = st.plane_sums()
+    for p, (a, b) in enumerate(pairs):
+        o = oracle.align_lean(a, b, CONFIG_SCORES)
+        for k in range(2):
+            assert [int(x) for x in sums[k, p]] == o.extra["plane_sums"], (p, len(a), len(b), k)
+        assert res[p].score == o.score
+        assert _steps_list(st.steps(p)) == o.alignment(), (p, len(a), len(b))
