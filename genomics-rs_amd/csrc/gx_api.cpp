@@ -1719,12 +1719,13 @@ static double chunk_budget(gx_context* ctx) {
 }
 
 // Contiguous [begin, end) ranges of the pairs, each within the budget (a pair
-// larger than the budget runs alone).  A chunk holding more than one pair ends
-// after an even count when it can, so that equal-shape pairs keep their twin
-// (run_fill pairs 2q with 2q+1).
-static std::vector<std::pair<size_t, size_t>> plan_chunks(gx_context* ctx, const std::vector<PairHost>& ph,
-                                                          double plane_bpc) {
-    const double budget = chunk_budget(ctx);
+// larger than the budget runs alone), balanced: the fewest chunks the budget
+// allows, each near total / chunks (1024 x 16k: 4 x 256 pairs, not 3 x 330 +
+// 34, whose short last chunk would lose the twin fill and leave CUs idle).
+// A chunk holding more than one pair ends after an even count when it can, so
+// that pairs keep their twin (run_fill pairs 2q with 2q+1).
+static std::vector<std::pair<size_t, size_t>> plan_chunks_within(const std::vector<PairHost>& ph, double plane_bpc,
+                                                                 double budget) {
     std::vector<std::pair<size_t, size_t>> out;
     auto bytes = [&](size_t p) { return (ph[p].n && ph[p].m) ? pair_device_bytes(ph[p].n, ph[p].m, plane_bpc) : 0.0; };
     size_t b = 0;
@@ -1741,6 +1742,23 @@ static std::vector<std::pair<size_t, size_t>> plan_chunks(gx_context* ctx, const
         acc += x;
     }
     out.emplace_back(b, ph.size());
+    return out;
+}
+static std::vector<std::pair<size_t, size_t>> plan_chunks(gx_context* ctx, const std::vector<PairHost>& ph,
+                                                          double plane_bpc) {
+    const double budget = chunk_budget(ctx);
+    auto out = plan_chunks_within(ph, plane_bpc, budget);
+    if (out.size() > 1) {
+        double total = 0;
+        for (size_t p = 0; p < ph.size(); ++p)
+            total += (ph[p].n && ph[p].m) ? pair_device_bytes(ph[p].n, ph[p].m, plane_bpc) : 0.0;
+        // the same number of chunks with a smaller target, if the greedy split allows it
+        for (double f : {1.0, 1.02, 1.05, 1.1}) {
+            const double target = std::min(budget, f * total / (double)out.size());
+            auto bal = plan_chunks_within(ph, plane_bpc, target);
+            if (bal.size() <= out.size()) return bal;
+        }
+    }
     return out;
 }
 

@@ -126,7 +126,9 @@ __device__ __forceinline__ void put_byte(uint32_t& acc, int a, int b) {
             : "+v"(acc) : "v"(a), "v"(b));
 }
 __device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t v) {
-#ifndef GX_DIAG_NO_PLANES
+#if defined(GX_DIAG_SINK_PLANES)
+    asm volatile("" ::"v"(v));   // (timing only) the bytes are computed, not stored
+#elif !defined(GX_DIAG_NO_PLANES)
     __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)voff, 0, GX_PLANE_AUX);
 #endif
 }
