@@ -99,7 +99,8 @@ def _allvsall_job(job):
     assert r.status == 0
     return {"i": i, "j": j, "n": len(a), "m": len(b), "score": r.score,
             "stats": [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps],
-            "n_steps": int(len(r.choices)), "alignment_sha256": alignment_digest(r.choices, r.steps_i, r.steps_j)}
+            "n_steps": int(len(r.choices)), "alignment_sha256": alignment_digest(r.choices, r.steps_i, r.steps_j),
+            "plane_sums": [int(x) for x in r.extra["plane_sums"]]}
 
 
 def allvsall_cases(workers: int):

@@ -167,3 +167,26 @@ def test_all_vs_all_two_ranks_on_one_gpu():
     pairs, recs = _golden_result(g)
     for rank, prs, records, names in out:
         assert prs == pairs and records == recs and names == g["names"], rank
+
+
+@pytest.mark.parametrize("twin", ["auto", "off"])
+def test_all_vs_all_planes_match_oracle(gx, ctx, monkeypatch, twin):
+    """The 55 comparison pairs at size through the staged path with compact
+    score planes: every pair's I/D/S plane checksums (the weighted sums of
+    make_golden.py) and alignment.  By default the batch takes the twin fill,
+    whose twins here differ in shape; "off" pins the scalar fill."""
+    if twin == "off":
+        monkeypatch.setenv("GX_TWIN", "0")
+    g = _golden()
+    cont = _container(gx)
+    seqs = [s.sequence.encode() for s in cont.sequences]
+    pairs = [(seqs[c["i"]], seqs[c["j"]]) for c in g["cases"]]
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, _ = st.run(gx.Scores(*g["scores"]), False, keep_planes=True, steps=1, plane_sums=True)
+    info = ctx.fill_info()
+    assert info["plane_bytes_per_cell"] == 3 and info["twin"] == (1 if twin == "auto" else 0), info
+    sums = st.plane_sums()
+    for p, c in enumerate(g["cases"]):
+        assert [int(x) for x in sums[0, p]] == c["plane_sums"], (c["i"], c["j"])
+        assert res[p].score == c["score"] and res[p].n_steps == c["n_steps"]
+        assert _digest(st.steps(p)) == c["alignment_sha256"], (c["i"], c["j"])
