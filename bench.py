@@ -63,6 +63,49 @@ def synth_pair(k: int, length: int):
             splitmix64_bases(0x5EED0002 + 0x10000 * k, length))
 
 
+def related_pair(k: int, length: int):
+    """SURVEY.md 8(d) M1 "related" variant: s1 = synthetic pair k's s1; s2 =
+    s1 with ~10 % substitutions and ~1 % indels of length 1-10, drawn from a
+    SplitMix64 stream seeded 0x5EED0003 + 0x10000 k.  Per position of s1: u =
+    top 53 bits of the next draw; u < 0.01: an indel (next draw y: length 1 +
+    y % 10; bit 32 of y set: delete that many bases of s1, else insert that
+    many random bases before the current one); u < 0.11: substitute a
+    different base ("ACGT"[(b + 1 + y % 3) % 4]); else copy."""
+    s1 = splitmix64_bases(0x5EED0001 + 0x10000 * k, length)
+    state = (0x5EED0003 + 0x10000 * k) & 0xFFFFFFFFFFFFFFFF
+    M = 0xFFFFFFFFFFFFFFFF
+
+    def draw():
+        nonlocal state
+        state = (state + 0x9E3779B97F4A7C15) & M
+        z = state
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return z ^ (z >> 31)
+
+    code = {65: 0, 67: 1, 71: 2, 84: 3}
+    out = bytearray()
+    i = 0
+    p_indel, p_sub = int(0.01 * 2 ** 53), int(0.11 * 2 ** 53)
+    while i < length:
+        u = draw() >> 11
+        if u < p_indel:
+            y = draw()
+            n = 1 + y % 10
+            if (y >> 32) & 1:
+                i += n
+                continue
+            for _ in range(n):
+                out.append(b"ACGT"[draw() >> 62])
+            out.append(s1[i])
+        elif u < p_sub:
+            out.append(b"ACGT"[(code[s1[i]] + 1 + draw() % 3) % 4])
+        else:
+            out.append(s1[i])
+        i += 1
+    return s1, bytes(out)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -264,10 +307,11 @@ def plane_desc(bytes_per_cell: int) -> str:
     return f"score planes (int32, {bytes_per_cell} B/cell) + traceback"
 
 
-def rank_pairs(rank: int, pairs_per_rank: int, length: int):
+def rank_pairs(rank: int, pairs_per_rank: int, length: int, related: bool = False):
     """Weak-scaling shard: rank r aligns synthetic pairs r*P .. r*P+P-1 (no
     data-path collective; every rank generates its own inputs)."""
-    return [synth_pair(rank * pairs_per_rank + p, length) for p in range(pairs_per_rank)]
+    gen = related_pair if related else synth_pair
+    return [gen(rank * pairs_per_rank + p, length) for p in range(pairs_per_rank)]
 
 
 def combine_over_ranks(dist, elapsed: float, rows, device: str):
@@ -304,13 +348,13 @@ def alignment_sha256(steps) -> str:
     return h.hexdigest()
 
 
-def verify_against_golden(staged, scores, is_local, keep_planes, rank: int, P: int, L: int):
+def verify_against_golden(staged, scores, is_local, keep_planes, rank: int, P: int, L: int, related: bool = False):
     """Parity of the benchmarked launch itself: one more (untimed) pass of
     the same staged batch with on-device plane checksums; every pair that has
     an oracle digest (tests/golden/synthetic_L{L}.json: score, statistics,
     alignment sha256, the three plane checksums) must match it bit for bit.
     Raises on any difference.  Returns (pairs checked, source)."""
-    path = os.path.join(ROOT, "tests", "golden", f"synthetic_L{L}.json")
+    path = os.path.join(ROOT, "tests", "golden", f"synthetic_related_L{L}.json" if related else f"synthetic_L{L}.json")
     if is_local or not os.path.exists(path):
         return 0, None
     with open(path) as f:
@@ -405,6 +449,9 @@ def main():
                          "Covid_Wuhan x Covid_USA-CA4 global; brca2: config 3, the Human x Mouse BRCA2 cds pair "
                          "local (one copy per rank)")
     ap.add_argument("--planes", action="store_true", help="allvsall: also write the score planes")
+    ap.add_argument("--related", action="store_true",
+                    help="synthetic: the SURVEY 8(d) M1 related variant (s2 = s1 with ~10%% substitutions and ~1%% "
+                         "indels; a long non-trivial traceback)")
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="1 GPU only: time every rank's shard of an N-GPU run in turn and print the predicted "
                          "N-GPU step time and scaling efficiency (not the headline line)")
@@ -450,7 +497,7 @@ def main():
         keep_planes = not args.no_planes
         args.single_pair_steps = 0
     else:
-        pairs = rank_pairs(rank, P, L)
+        pairs = rank_pairs(rank, P, L, args.related)
         keep_planes = not args.no_planes
     staged = gx.StagedPairs(pairs, ctx=ctx)             # inputs resident in HBM
     cells_rank = sum(len(a) * len(b) for a, b in pairs)
@@ -501,7 +548,9 @@ def main():
     elif args.workload == "brca2":
         workload = f"Human x Mouse BRCA2 cds ({len(pairs[0][0])}x{len(pairs[0][1])}), one pair per GPU, {mode_s}"
     else:
-        workload = f"synthetic {L}x{L} DNA pairs (SplitMix64), {P} per GPU, {mode_s}"
+        workload = (f"synthetic related {L}-nt DNA pairs (SplitMix64 s1, s2 = s1 with ~10% substitutions and ~1% "
+                    f"indels), {P} per GPU, {mode_s}") if args.related else \
+                   f"synthetic {L}x{L} DNA pairs (SplitMix64), {P} per GPU, {mode_s}"
     fill_bytes = bytes_per_cell * cells_rank
     achieved = fill_bytes / (avg_fill_ms * 1e-3) / 1e9
     twin = bool(finfo.get("twin"))
@@ -556,7 +605,7 @@ def main():
         "traceback_us_pair0": int(np.mean(tb_us)),
     }
     if args.workload == "synthetic" and not args.no_verify:
-        checked, src = verify_against_golden(staged, scores, args.local, keep_planes, rank, P, L)
+        checked, src = verify_against_golden(staged, scores, args.local, keep_planes, rank, P, L, args.related)
         if dist is not None:
             import torch
             t = torch.tensor([checked], dtype=torch.int64, device="cuda")
@@ -608,7 +657,7 @@ def main():
                               "fill_ms_avg": round(float(np.mean(f1)), 3), "steps": args.single_pair_steps}
         del one
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if len(pairs[0][1]) > 30000:
+        if len(pairs[0][1]) > 40000:
             # the reference layout needs (n+1)(m+1) x 48 B (197 GB at 64k)
             out["cpu_baseline"] = {"value": None, "unit": "GCUPS", "cores": 1, "kind": "port",
                                    "sample": "N/A: the reference-layout table of one pair exceeds host memory "

@@ -141,6 +141,49 @@ def synth_pair(k: int, length: int):
             splitmix64_bases(0x5EED0002 + 0x10000 * k, length))
 
 
+def related_pair(k: int, length: int):
+    """SURVEY.md 8(d) M1 "related" variant: s1 = synthetic pair k's s1; s2 =
+    s1 with ~10 % substitutions and ~1 % indels of length 1-10, drawn from a
+    SplitMix64 stream seeded 0x5EED0003 + 0x10000 k.  Per position of s1: u =
+    top 53 bits of the next draw; u < 0.01: an indel (next draw y: length 1 +
+    y % 10; bit 32 of y set: delete that many bases of s1, else insert that
+    many random bases before the current one); u < 0.11: substitute a
+    different base ("ACGT"[(b + 1 + y % 3) % 4]); else copy."""
+    s1 = splitmix64_bases(0x5EED0001 + 0x10000 * k, length)
+    state = (0x5EED0003 + 0x10000 * k) & 0xFFFFFFFFFFFFFFFF
+    M = 0xFFFFFFFFFFFFFFFF
+
+    def draw():
+        nonlocal state
+        state = (state + 0x9E3779B97F4A7C15) & M
+        z = state
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return z ^ (z >> 31)
+
+    code = {65: 0, 67: 1, 71: 2, 84: 3}
+    out = bytearray()
+    i = 0
+    p_indel, p_sub = int(0.01 * 2 ** 53), int(0.11 * 2 ** 53)
+    while i < length:
+        u = draw() >> 11
+        if u < p_indel:
+            y = draw()
+            n = 1 + y % 10
+            if (y >> 32) & 1:
+                i += n
+                continue
+            for _ in range(n):
+                out.append(b"ACGT"[draw() >> 62])
+            out.append(s1[i])
+        elif u < p_sub:
+            out.append(b"ACGT"[(code[s1[i]] + 1 + draw() % 3) % 4])
+        else:
+            out.append(s1[i])
+        i += 1
+    return s1, bytes(out)
+
+
 # Synthetic batches digested by --synthetic: BASELINE configs[1]'s shape (the
 # bench's own 30k pairs, rank 0's 80 at N = 1) and configs[4] (1024 x 1k, and
 # samples of the 4k / 16k / 64k batches).
@@ -148,8 +191,8 @@ SYNTH_SETS = {30000: 80, 1024: 1024, 4096: 64, 16384: 8, 65536: 1}
 
 
 def _synth_job(job):
-    length, k = job
-    a, b = synth_pair(k, length)
+    length, k = job[:2]
+    a, b = (related_pair if len(job) > 2 and job[2] else synth_pair)(k, length)
     r = o.align_lean(a, b, CONFIG, is_local=False)
     assert r.status == 0
     return length, {"k": k, "n": len(a), "m": len(b), "score": r.score,
@@ -158,9 +201,11 @@ def _synth_job(job):
                     "plane_sums": [str(x) for x in r.extra["plane_sums"]]}
 
 
-def synthetic_cases(workers: int, lengths):
+def synthetic_cases(workers: int, lengths, related: bool = False):
+    """Oracle digests of the synthetic batches (related: the SURVEY 8(d) M1
+    "related" variant, s2 derived from s1, 80 pairs at 30k)."""
     from multiprocessing import Pool
-    jobs = [(L, k) for L in lengths for k in range(SYNTH_SETS[L])]
+    jobs = [(L, k, related) for L in lengths for k in range(SYNTH_SETS[L])]
     jobs.sort(key=lambda x: -x[0])
     out = {L: [] for L in lengths}
     with Pool(workers) as pool:
@@ -170,9 +215,13 @@ def synthetic_cases(workers: int, lengths):
                 print(f"synthetic L={L} k={rec['k']} done ({n_done}/{len(jobs)})", flush=True)
     for L in lengths:
         out[L].sort(key=lambda c: c["k"])
-        with open(os.path.join(HERE, f"synthetic_L{L}.json"), "w") as f:
-            json.dump({"_source": "tests/golden/make_golden.py --synthetic (oracle_align_lean, global, config.toml "
-                                  "scores; pair k = splitmix64 seeds 0x5EED0001/2 + 0x10000 k, bench.py synth_pair)",
+        name = f"synthetic_related_L{L}.json" if related else f"synthetic_L{L}.json"
+        src = ("tests/golden/make_golden.py --related (oracle_align_lean, global, config.toml scores; pair k = "
+               "related_pair(k): s1 of synthetic pair k, s2 derived with seed 0x5EED0003 + 0x10000 k)") if related else \
+              ("tests/golden/make_golden.py --synthetic (oracle_align_lean, global, config.toml "
+               "scores; pair k = splitmix64 seeds 0x5EED0001/2 + 0x10000 k, bench.py synth_pair)")
+        with open(os.path.join(HERE, name), "w") as f:
+            json.dump({"_source": src,
                        "length": L, "scores": list(CONFIG), "cases": out[L]}, f, indent=0)
 
 
@@ -182,9 +231,13 @@ def main():
     ap.add_argument("--allvsall", action="store_true")
     ap.add_argument("--synthetic", type=str, default=None,
                     help="comma-separated lengths of SYNTH_SETS to digest, or 'all'")
+    ap.add_argument("--related", action="store_true", help="the related 30k batch (SURVEY 8(d) M1 variant)")
     ap.add_argument("--workers", type=int, default=7)
     args = ap.parse_args()
     o.build()
+    if args.related:
+        synthetic_cases(args.workers, [30000], related=True)
+        return
     if args.synthetic:
         lengths = sorted(SYNTH_SETS) if args.synthetic == "all" else [int(x) for x in args.synthetic.split(",")]
         synthetic_cases(args.workers, lengths)

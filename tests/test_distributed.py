@@ -173,3 +173,15 @@ def test_combine_over_ranks_ragged_shares():
     assert all(p.exitcode == 0 for p in procs)
     for rank, t, gathered in out:
         assert t == 0.5 and gathered == [[(0, 0, 7), (0, 1, 7)], [(1, 0, 7)]]
+
+
+def test_related_pair_generators_agree():
+    """bench.py and tests/golden/make_golden.py generate the same related pairs
+    (SURVEY 8(d) M1 variant), whose digests the bench checks itself against."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_golden
+    for k in (0, 5):
+        a, b = bench.related_pair(k, 3000)
+        assert (a, b) == make_golden.related_pair(k, 3000)
+        assert a == bench.synth_pair(k, 3000)[0] and a != b and abs(len(a) - len(b)) < 300

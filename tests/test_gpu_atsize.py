@@ -242,3 +242,23 @@ def test_chunks_keep_twins(gx, ctx, monkeypatch):
     pairs = [_synth_pair(c["k"], 1024) for c in cases]
     info = _staged_check(gx, ctx, pairs, cases, steps=1)
     assert info["chunks"] == 10 and info["twin"] == 1, info
+
+
+@pytest.mark.parametrize("twin", ["1", "0"])
+def test_related_30k_batch(gx, ctx, monkeypatch, twin):
+    """SURVEY 8(d) M1's related variant (s2 = s1 with ~10 % substitutions and
+    ~1 % indels, so the path winds through the whole table and the pair
+    lengths differ): eight pairs through the staged launch with planes, with
+    and without the twin fill, against the oracle's digests
+    (tests/golden/synthetic_related_L30000.json)."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_golden
+    monkeypatch.setenv("GX_TWIN", twin)
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    with open(os.path.join(GOLDEN, "synthetic_related_L30000.json")) as f:
+        cases = json.load(f)["cases"][:8]
+    pairs = [make_golden.related_pair(c["k"], 30000) for c in cases]
+    assert any(len(a) != len(b) for a, b in pairs)
+    info = _staged_check(gx, ctx, pairs, cases, steps=2)
+    assert info["twin"] == int(twin), info
