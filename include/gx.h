@@ -207,9 +207,10 @@ int gx_fill_info(const gx_context* ctx, int* layout, int* band_waves, int* plane
  * as contiguous chunks of pairs through the same device buffers
  * (GX_CHUNK_BYTES overrides the per-chunk byte budget).  Measurement only. */
 int gx_batch_chunks(const gx_context* ctx);
-/* 1 when the last fill launch on ctx was the twin fill (two pairs of equal
- * shape per band, packed 16-bit arithmetic), else 0.
- * Measurement only (GX_TWIN=0 disables it). */
+/* 1 when the last fill launch on ctx was the twin fill (two pairs per band,
+ * one per 16-bit half, packed arithmetic), else 0.
+ * Measurement only (GX_TWIN=0 disables it, GX_TWIN=1 forces it where the
+ * range bound admits it; by default deep band queues take it). */
 int gx_fill_twin(const gx_context* ctx);
 /* Score-plane bytes per cell a batch launch (layout 0, no max tracking)
  * writes with these scores: 3 when the compact format's range proof holds
