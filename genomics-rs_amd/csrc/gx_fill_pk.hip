@@ -1,5 +1,5 @@
-// gx_fill_pk.hip -- the twin fill: two independent pairs of the same shape
-// (n, m) swept by one band of waves, one pair in each 16-bit half of every
+// gx_fill_pk.hip -- the twin fill: two independent pairs (laid out for the
+// larger n and m of the two) swept by one band of waves, one pair in each 16-bit half of every
 // register (VOP3P packed arithmetic: one v_pk_max_i16 / v_pk_add_u16 /
 // v_pk_mad_u16 computes the same cell of both pairs).  Specialised to the
 // batch path's untracked global fill on the anti-diagonal layout (layout 0,

@@ -1,5 +1,5 @@
 """GPU parity of the twin fill (genomics-rs_amd/csrc/gx_fill_pk.hip): batches
-whose pairs come in equal shapes run two pairs per band, one in each 16-bit
+run two pairs per band (of equal or different shapes), one in each 16-bit
 half of every register, with values kept relative to per-block bases.  Every
 result -- alignment, statistics, the compact score planes -- must equal the
 oracle's, on shapes around the strip and band edges, with bands queued for
