@@ -168,3 +168,27 @@ def test_twin_mixed_shapes(gx, ctx, oracle, monkeypatch, odd):
             assert [int(x) for x in sums[k, p]] == o.extra["plane_sums"], (p, len(a), len(b), k)
         assert res[p].score == o.score
         assert _steps_list(st.steps(p)) == o.alignment(), (p, len(a), len(b))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_twin_random_batches(gx, ctx, oracle, monkeypatch, seed):
+    """Randomised twin batches: random shapes (1-700 x 1-700, odd and even
+    counts), alphabets and admissible scores, band widths and grids; every
+    alignment, score and plane checksum against the oracle."""
+    rng = random.Random(1000 + seed)
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    monkeypatch.setenv("GX_BAND_WAVES", rng.choice(["3", "4", "7", "8", "15"]))
+    monkeypatch.setenv("GX_FILL_GRID", rng.choice(["1", "2", "5", "64"]))
+    scores = rng.choice([CONFIG_SCORES, (1, -2, -2, -5), (2, -3, -1, -4), (1, -1, 0, -3), (3, -2, -2, -2)])
+    al = rng.choice([b"ACGT", b"AC", b"ACGTN", b"ACDEFGHIKLMNPQRSTVWY"])
+    shapes = [(rng.randint(1, 700), rng.randint(1, 700)) for _ in range(rng.randint(2, 9))]
+    pairs = [(bytes(rng.choice(al) for _ in range(n)), bytes(rng.choice(al) for _ in range(m))) for n, m in shapes]
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, _ = st.run(gx.Scores(*scores), False, keep_planes=True, steps=1, plane_sums=True)
+    info = ctx.fill_info()
+    sums = st.plane_sums()
+    for p, (a, b) in enumerate(pairs):
+        o = oracle.align_lean(a, b, scores)
+        assert [int(x) for x in sums[0, p]] == o.extra["plane_sums"], (seed, p, len(a), len(b), info)
+        assert res[p].score == o.score, (seed, p)
+        assert _steps_list(st.steps(p)) == o.alignment(), (seed, p)
