@@ -302,6 +302,8 @@ def allvsall_share(gx, rank: int, world: int):
 
 
 def plane_desc(bytes_per_cell: int) -> str:
+    if bytes_per_cell == 2:
+        return "score planes (exact per-cell 16-bit codes of the three differences, 2 B/cell) + traceback"
     if bytes_per_cell == 3:
         return "score planes (exact per-cell byte differences, 3 B/cell) + traceback"
     return f"score planes (int32, {bytes_per_cell} B/cell) + traceback"

@@ -549,6 +549,20 @@ static bool d8_planes_ok(const Scores32& sc, int is_local) {
     return lo >= -128 && hi <= 127;
 }
 
+// Twin plane codes (gx_fill_pk.hip w16_code): x_I - g in [0, U - a - g] must
+// fit 4 unsigned bits, x_S in [smin - U, smax - 2a] 5 signed bits and x_D in
+// [2a - U, U - 2a] 7 signed bits (the bounds of d8_planes_ok); the default
+// scores give [0, 14], [-9, 13], [-19, 19].  GX_PLANES_W16=0 keeps the byte
+// format.
+static bool w16_ok(const Scores32& sc) {
+    if (sc.g > 0 || sc.h > 0 || getenv("GX_PLANES32")) return false;
+    if (const char* e = getenv("GX_PLANES_W16"); e && !strcmp(e, "0")) return false;
+    const long long g = sc.g, a = (long long)sc.h + sc.g;
+    const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
+    const long long U = std::max(0LL, smax - a);
+    return U - a - g <= 15 && smin - U >= -16 && smax - 2 * a <= 15 && 2 * a - U >= -64 && U - 2 * a <= 63;
+}
+
 struct PairHost {
     const uint8_t* s1;   // original bytes (traceback labels, sequence.rs:113 with rev=false)
     const uint8_t* s2;
@@ -595,6 +609,8 @@ struct FillJob {
     bool d8 = false;                    // compact byte planes (d8_planes_ok)
     bool shift = false;                 // values kept as V - (i + j) g (Scores32.shift)
     bool twin = false;                  // the twin fill (gx_fill_pk.hip): pairs 2q, 2q+1 share every band
+    bool w16 = false;                   // twin plane codes, 2 B per cell (w16_ok; batches only)
+    bool table = false;                 // an alignment table (exportable planes: never the twin codes)
     int g = 0;
     double fill_ms = 0.0;
     // the int64 fill (gx_wide.hip): its own buffers and results
@@ -715,12 +731,14 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     }
     const bool twin = Wt > 0;
     job.twin = twin;
+    const bool w16 = twin && planes && !job.table && w16_ok(sc);
+    job.w16 = w16;
     ctx->last_twin = twin ? 1 : 0;
     const int Wf = twin ? Wt : W;   // band width of the launch
     const size_t plane_esz = d8 ? 1 : sizeof(int32_t);
     job.W = Wf;
     ctx->last_lay = lay; ctx->last_W = Wf;
-    ctx->last_pbytes = planes ? (int)(plane_esz * 3) : 0;
+    ctx->last_pbytes = planes ? (w16 ? 2 : (int)(plane_esz * 3)) : 0;
     const size_t P = ph.size();
     job.pd.assign(P, PairDev{});
     // -- sizes
@@ -753,7 +771,12 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         strips += d.strips;
         c1o[p] = chars_bytes; chars_bytes += align_up(n, 64);
         c2o[p] = chars_bytes; chars_bytes += align_up(m, 64);
-        po[p] = plane_elems; plane_elems += (size_t)d.strips * d.t4 * (lay ? kGroupInts1 : kGroupInts);
+        if (w16) {   // one code plane per twin, shared by its two pairs
+            po[p] = second ? po[p - 1] : plane_elems;
+            if (!second) plane_elems += (size_t)d.strips * d.t4 * kTwinGroupBytes;
+        } else {
+            po[p] = plane_elems; plane_elems += (size_t)d.strips * d.t4 * (lay ? kGroupInts1 : kGroupInts);
+        }
         co[p] = code_elems; code_elems += (size_t)d.strips * d.t16 * SR;
         so[p] = second ? so[p - 1] : skel_elems;
         if (!second) skel_elems += (size_t)d.strips * d.skel_stride;
@@ -766,7 +789,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     job.total_bands = bands;
     job.total_strips = strips;
     int rc;
-    const int nplanes = lcs ? 4 : 3;
+    const int nplanes = w16 ? 1 : lcs ? 4 : 3;
     if (!chars_dev) {
         if ((rc = pool_get(ctx, chars_bytes, &job.chars))) return rc;
     }
@@ -827,8 +850,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         uint8_t* pl = (uint8_t*)job.planes.p;
         auto plane_at = [&](int k) { return (int32_t*)(pl + (k * plane_elems + po[p]) * plane_esz); };
         d.pI = planes ? plane_at(0) : nullptr;
-        d.pD = planes ? plane_at(1) : nullptr;
-        d.pS = planes ? plane_at(2) : nullptr;
+        d.pD = (planes && !w16) ? plane_at(1) : nullptr;
+        d.pS = (planes && !w16) ? plane_at(2) : nullptr;
         d.pL = (planes && lcs) ? plane_at(3) : nullptr;
         d.codes = codes ? (uint32_t*)job.codes.p + co[p] : nullptr;
         d.skel = (int*)job.skel.p + so[p];
@@ -861,7 +884,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].fb : ctx->ev0, eve = slot >= 0 ? ctx->slots[slot].fe : ctx->ev1;
     HIPCHK(hipEventRecord(evb, ctx->stream));
     if (bands > 0 && twin)
-        HIPCHK(launch_fill_pk(Wf, planes ? 1 : 0, (const PairDev*)job.pairs.p, (int)(Pd / 2), bands, (int*)job.counter.p,
+        HIPCHK(launch_fill_pk(Wf, planes ? (w16 ? 2 : 1) : 0, (const PairDev*)job.pairs.p, (int)(Pd / 2), bands, (int*)job.counter.p,
                               (PairRes*)job.pres.p, scl, grid, ctx->stream));
     else if (bands > 0)
         HIPCHK(launch_fill(W, lay, is_local != 0, planes ? (d8 ? 2 : 1) : 0, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
@@ -1386,6 +1409,7 @@ extern "C" int gx_alignment_table(gx_context* ctx, const uint8_t* s1, size_t n, 
     const bool planes = (flags & (GX_TABLE_PLANES | GX_TABLE_MATCHES)) != 0;
     const bool lcs = (flags & GX_TABLE_MATCHES) != 0;
     if (n >= 1 && m >= 1) {
+        t->job.table = true;   // exportable planes: the per-pair formats only
         rc = wide ? run_fill_wide(ctx, proc, ph, t->hs, is_local, planes, matches_at_max != nullptr, lcs, t->job)
                   : run_fill(ctx, proc, ph, t->sc, is_local, planes, matches_at_max != nullptr, lcs, t->job);
         if (rc) { job_release(ctx, t->job); delete t; return rc; }
@@ -1531,7 +1555,8 @@ static hipError_t enqueue_plane_sums(gx_context* ctx, const FillJob& job, const 
                                      unsigned long long* out) {
     int max_strips = 0;
     for (const PairDev& d : job.pd) max_strips = std::max(max_strips, d.strips);
-    return launch_plane_sums((const PairDev*)job.pairs.p, (int)job.pd.size(), max_strips, job.lay, job.d8 ? 2 : 1,
+    return launch_plane_sums((const PairDev*)job.pairs.p, (int)job.pd.size(), max_strips, job.lay,
+                             job.w16 ? 3 : job.d8 ? 2 : 1,
                              sc.h, sc.g, sc.floor_, job.shift ? sc.g : 0, out, ctx->stream);
 }
 

@@ -121,6 +121,17 @@ struct PkScores {
     uint32_t h, smp, dsm;
 };
 
+// Twin plane code (PLANES == 2, 2 B per cell): the three differences of a
+// cell in one 16-bit word, code = x_I + 16 x_S + 512 x_D (mod 2^16), x_I in
+// [0, 15] (shifted: I'' - I''(j-1)), x_S = S - I in [-16, 15], x_D = D - I in
+// [-64, 63] (gx_api.cpp w16_ok checks the ranges); both pairs' codes of a
+// cell in one dword, as the halves already hold them.  Two v_pk_mad_u16 and
+// three v_pk_sub_i16 per two cells (the byte format: three SDWA per cell).
+__device__ __forceinline__ uint32_t w16_code(uint32_t I, uint32_t D, uint32_t S, uint32_t Iold) {
+    const uint32_t xI = psub(I, Iold), xS = psub(S, I), xD = psub(D, I);
+    return pmad(xD, 0x02000200u, pmad(xS, 0x00100010u, xI));
+}
+
 // One row of a lane, both pairs: the cell left of the one being computed.
 struct RowPk {
     uint32_t I, SD, Dd, SMp, SMtl;   // insert, max(sub, delete), delete successor, score_max + sm'', SMp(i-1, j-1)
@@ -241,48 +252,72 @@ __device__ __forceinline__ void group4_pk(LanePk& st, Rec (&nxt)[4], WavePk& w, 
     asm volatile("" ::: "memory");
     read4_pk(nxt, w.ring_in + ring_slot(t + 5));
     uint32_t bI[4][2], bD[4][2], bS[4][2], bL[4][2];
-    uint32_t xI[2][2], xS[2][2], xD[2][2];   // compact plane dwords [pair][row], filled step by step
+    uint32_t xI[2][2], xS[2][2], xD[2][2];   // compact plane dwords [pair][row], filled step by step (PLANES 1)
+    uint32_t wc[2][4];                        // twin plane codes [row][step] (PLANES 2)
     const int col0 = t - (kWave - 1);
     if (MASKED) {
         auto sko = [&](int c) { return (c >= 0 && c <= w.m) ? w.skel_voff + 4u * (uint32_t)c : kSkelOff; };
         push63_pk<4 * G4 + 0>(out_base, st, lane63_mask(push_on && col0 >= 0 && col0 <= w.m));
         dp_step_pk<true>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[0], bD[0], bS[0], bL[0]);
-        if (PLANES) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
+        if (PLANES == 1) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
+        if (PLANES == 2) { wc[0][0] = w16_code(bI[0][0], bD[0][0], bS[0][0], bL[0][0]);
+                           wc[1][0] = w16_code(bI[0][1], bD[0][1], bS[0][1], bL[0][1]); }
         skel_store(w.skel_rsrc, sko(col0 + 1), (int)st.b.E);
         push63_pk<4 * G4 + 1>(out_base, st, lane63_mask(push_on && col0 + 1 >= 0 && col0 + 1 <= w.m));
         dp_step_pk<true>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[1], bD[1], bS[1], bL[1]);
-        if (PLANES) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
+        if (PLANES == 1) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
+        if (PLANES == 2) { wc[0][1] = w16_code(bI[1][0], bD[1][0], bS[1][0], bL[1][0]);
+                           wc[1][1] = w16_code(bI[1][1], bD[1][1], bS[1][1], bL[1][1]); }
         skel_store(w.skel_rsrc, sko(col0 + 2), (int)st.b.E);
         push63_pk<4 * G4 + 2>(out_base, st, lane63_mask(push_on && col0 + 2 >= 0 && col0 + 2 <= w.m));
         dp_step_pk<true>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[2], bD[2], bS[2], bL[2]);
-        if (PLANES) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
+        if (PLANES == 1) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
+        if (PLANES == 2) { wc[0][2] = w16_code(bI[2][0], bD[2][0], bS[2][0], bL[2][0]);
+                           wc[1][2] = w16_code(bI[2][1], bD[2][1], bS[2][1], bL[2][1]); }
         skel_store(w.skel_rsrc, sko(col0 + 3), (int)st.b.E);
         push63_pk<4 * G4 + 3>(out_base, st, lane63_mask(push_on && col0 + 3 >= 0 && col0 + 3 <= w.m));
         if (push_on && col0 + 3 >= 0 && col0 <= w.m) lds_store_lane0(w.wcnt_out, min(col0 + 3, w.m) + 1);
         dp_step_pk<true>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[3], bD[3], bS[3], bL[3]);
-        if (PLANES) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
+        if (PLANES == 1) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
+        if (PLANES == 2) { wc[0][3] = w16_code(bI[3][0], bD[3][0], bS[3][0], bL[3][0]);
+                           wc[1][3] = w16_code(bI[3][1], bD[3][1], bS[3][1], bL[3][1]); }
         skel_store(w.skel_rsrc, sko(col0 + 4), (int)st.b.E);
     } else {
         const uint32_t pa = push_on && w.lane == kWave - 1 ? out_base : w.scratch;
         push_all_pk<4 * G4 + 0>(pa, st);
         dp_step_pk<false>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[0], bD[0], bS[0], bL[0]);
-        if (PLANES) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
+        if (PLANES == 1) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
+        if (PLANES == 2) { wc[0][0] = w16_code(bI[0][0], bD[0][0], bS[0][0], bL[0][0]);
+                           wc[1][0] = w16_code(bI[0][1], bD[0][1], bS[0][1], bL[0][1]); }
         const uint32_t e0 = st.b.E;
         push_all_pk<4 * G4 + 1>(pa, st);
         dp_step_pk<false>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[1], bD[1], bS[1], bL[1]);
-        if (PLANES) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
+        if (PLANES == 1) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
+        if (PLANES == 2) { wc[0][1] = w16_code(bI[1][0], bD[1][0], bS[1][0], bL[1][0]);
+                           wc[1][1] = w16_code(bI[1][1], bD[1][1], bS[1][1], bL[1][1]); }
         const uint32_t e1 = st.b.E;
         push_all_pk<4 * G4 + 2>(pa, st);
         dp_step_pk<false>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[2], bD[2], bS[2], bL[2]);
-        if (PLANES) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
+        if (PLANES == 1) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
+        if (PLANES == 2) { wc[0][2] = w16_code(bI[2][0], bD[2][0], bS[2][0], bL[2][0]);
+                           wc[1][2] = w16_code(bI[2][1], bD[2][1], bS[2][1], bL[2][1]); }
         const uint32_t e2 = st.b.E;
         push_all_pk<4 * G4 + 3>(pa, st);
         publish_all(w.cnt_addr, col0 + 3 + 1);
         dp_step_pk<false>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[3], bD[3], bS[3], bL[3]);
-        if (PLANES) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
+        if (PLANES == 1) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
+        if (PLANES == 2) { wc[0][3] = w16_code(bI[3][0], bD[3][0], bS[3][0], bL[3][0]);
+                           wc[1][3] = w16_code(bI[3][1], bD[3][1], bS[3][1], bL[3][1]); }
         skel_store4(w.skel_rsrc, w.skel_voff + 4u * (uint32_t)(col0 + 1), (int)e0, (int)e1, (int)e2, (int)st.b.E);
     }
-    if (PLANES) {
+    if (PLANES == 2) {
+        // twin plane codes: per strip [group][row][lane][step] dwords (2 KB a group)
+        const uint32_t v = (uint32_t)G4 * kTwinGroupBytes + (uint32_t)w.lane * 16u;
+        const auto r = rsrc_of(w.pI[0] + sb_off * (kTwinGroupBytes / kGroupInts), 4 * kTwinGroupBytes);
+        bstore4(r, v, make_int4((int)wc[0][0], (int)wc[0][1], (int)wc[0][2], (int)wc[0][3]));
+        bstore4(r, v + kTwinGroupBytes / 2, make_int4((int)wc[1][0], (int)wc[1][1], (int)wc[1][2], (int)wc[1][3]));
+    }
+    if (PLANES == 1) {
         // compact planes of both pairs (bytes_step): x_I = I - I(j-1) (shifted:
         // x_I - g), x_S = S - I, x_D = D - I, one byte per cell
         constexpr int kSubBytes = kSub / 4 * kGroupInts;
@@ -353,13 +388,14 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
     const int ia = s * kStripRows + kRowsPerLane * lane + 1;
     WavePk w;
     {
-        const size_t strip_planes = (size_t)s * P0.t4 * kGroupInts;   // bytes per compact plane per strip
+        // bytes per compact plane per strip (PLANES 2: the twin's one code plane, 2 KB a group)
+        const size_t strip_planes = (size_t)s * P0.t4 * (PLANES == 2 ? kTwinGroupBytes : kGroupInts);
         w.pI[0] = PLANES ? (uint8_t*)P0.pI + strip_planes : nullptr;
-        w.pD[0] = PLANES ? (uint8_t*)P0.pD + strip_planes : nullptr;
-        w.pS[0] = PLANES ? (uint8_t*)P0.pS + strip_planes : nullptr;
-        w.pI[1] = PLANES ? (uint8_t*)P1.pI + strip_planes : nullptr;
-        w.pD[1] = PLANES ? (uint8_t*)P1.pD + strip_planes : nullptr;
-        w.pS[1] = PLANES ? (uint8_t*)P1.pS + strip_planes : nullptr;
+        w.pD[0] = PLANES == 1 ? (uint8_t*)P0.pD + strip_planes : nullptr;
+        w.pS[0] = PLANES == 1 ? (uint8_t*)P0.pS + strip_planes : nullptr;
+        w.pI[1] = PLANES == 1 ? (uint8_t*)P1.pI + strip_planes : nullptr;
+        w.pD[1] = PLANES == 1 ? (uint8_t*)P1.pD + strip_planes : nullptr;
+        w.pS[1] = PLANES == 1 ? (uint8_t*)P1.pS + strip_planes : nullptr;
         w.codes[0] = P0.codes + (size_t)s * P0.t16 * kWave * kRowsPerLane;
         w.codes[1] = P1.codes + (size_t)s * P0.t16 * kWave * kRowsPerLane;
     }
@@ -630,7 +666,10 @@ template <int W0, int... Ws>
 static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int ntwins, int total_bands, int* d_counter,
                               PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
     if (W == W0) {
-        if (planes)
+        if (planes == 2)
+            hipLaunchKernelGGL((fill_pk_kernel<W0, 2>), dim3(grid), dim3((W0 + 1) * kWave), 0, st, d_pairs, ntwins,
+                               total_bands, d_counter, d_pres, sc);
+        else if (planes)
             hipLaunchKernelGGL((fill_pk_kernel<W0, 1>), dim3(grid), dim3((W0 + 1) * kWave), 0, st, d_pairs, ntwins,
                                total_bands, d_counter, d_pres, sc);
         else
@@ -643,7 +682,8 @@ static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int ntw
     return hipErrorInvalidValue;
 }
 
-// Twin launch: W from {3, 4, 7, 8, 15}; planes: 0 none, 1 compact.
+// Twin launch: W from {3, 4, 7, 8, 15}; planes: 0 none, 1 compact bytes per
+// pair (3 B/cell), 2 twin codes (2 B/cell).
 hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int ntwins, int total_bands, int* d_counter,
                           PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
     return launch_pk_w<3, 4, 7, 8, 15>(W, planes, d_pairs, ntwins, total_bands, d_counter, d_pres, sc, grid, st);

@@ -35,6 +35,9 @@ constexpr int kStripRows = kWave * kRowsPerLane;   // 128 rows per strip
 // Plane layout (ints): plane[strip][t/4][row-in-lane][lane][t%4]; one 4-step
 // group of one row is 1 KiB contiguous per wave.
 constexpr int kGroupInts = kRowsPerLane * kWave * 4;
+// twin plane codes (gx_fill_pk.hip PLANES 2): one 2-B code per cell, both
+// pairs of a twin in one dword; a 4-step group of a strip = [row][lane][step]
+constexpr int kTwinGroupBytes = kRowsPerLane * kWave * 4 * 4;
 // Column-step layout (layout 1): 64-row strips, lane l owns row 64s + l + 1,
 // step t = column t + 1 for every lane (no skew); planes
 // plane[strip][t/4][lane][t%4] (1 KiB per wave per plane every 4 columns),

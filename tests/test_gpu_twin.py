@@ -64,14 +64,17 @@ def test_twin_batch_alignments(gx, ctx, oracle, launch):
                (o.score, o.matches, o.mismatches, o.gap_extensions, o.opening_gaps)
 
 
-def test_twin_staged_planes(gx, ctx, oracle, launch):
+@pytest.mark.parametrize("fmt", ["codes", "bytes"])
+def test_twin_staged_planes(gx, ctx, oracle, launch, monkeypatch, fmt):
     """The staged, pipelined path with compact planes through the twin fill:
     every pass's plane checksums and the last pass's alignments."""
+    if fmt == "bytes":
+        monkeypatch.setenv("GX_PLANES_W16", "0")
     pairs = _twin_pairs(11, SHAPES, per_shape=4)
     st = gx.StagedPairs(pairs, ctx=ctx)
     res, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=3, plane_sums=True)
     info = ctx.fill_info()
-    assert info["twin"] == 1 and info["plane_bytes_per_cell"] == 3, info
+    assert info["twin"] == 1 and info["plane_bytes_per_cell"] == (2 if fmt == "codes" else 3), info
     sums = st.plane_sums()
     for p, (a, b) in enumerate(pairs):
         o = oracle.align_lean(a, b, CONFIG_SCORES)
@@ -160,7 +163,7 @@ def test_twin_mixed_shapes(gx, ctx, oracle, monkeypatch, odd):
     st = gx.StagedPairs(pairs, ctx=ctx)
     res, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=2, plane_sums=True)
     info = ctx.fill_info()
-    assert info["twin"] == 1 and info["plane_bytes_per_cell"] == 3, info
+    assert info["twin"] == 1 and info["plane_bytes_per_cell"] == 2, info
     sums = st.plane_sums()
     for p, (a, b) in enumerate(pairs):
         o = oracle.align_lean(a, b, CONFIG_SCORES)
