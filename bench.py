@@ -567,8 +567,8 @@ def main():
            "kernel": kname, "fill_ms_avg": round(avg_fill_ms, 3),
            "algorithmic_bytes_per_cell": bytes_per_cell,
            "algorithmic_bytes_per_launch": fill_bytes}
-    if valu is not None and keep_planes and bytes_per_cell == 3:
-        # compact planes: the fill is bound by VALU issue, not HBM -- lane-ops
+    if valu is not None and keep_planes and bytes_per_cell in (2, 3):
+        # compact planes / twin codes: the fill is bound by VALU issue, not HBM -- lane-ops
         # per launch (VALU/cell x cells, SQ_INSTS_VALU profile) over the live
         # fill time, against the probe-measured ceiling at the fill's mix
         ach = valu["valu_insts_per_cell"] * cells_rank / (avg_fill_ms * 1e-3) / 1e12
@@ -617,7 +617,19 @@ def main():
                          "fields": "score, statistics, alignment sha256" + (", I/D/S plane checksums" if keep_planes
                                                                             else ""),
                          "source": src, "pass": "one extra untimed pass of the same staged launch"}
-    if world == 1 and keep_planes and bytes_per_cell == 3 and args.int32_steps > 0:
+    if world == 1 and keep_planes and bytes_per_cell == 2 and args.no_plane_steps > 0:
+        # the same batch with the per-pair byte planes (3 B/cell, the table format)
+        os.environ["GX_PLANES_W16"] = "0"
+        try:
+            staged.run(scores, args.local, True)
+            _, fms3 = staged.run(scores, args.local, True, steps=args.no_plane_steps)
+            fi3 = ctx.fill_info()
+        finally:
+            del os.environ["GX_PLANES_W16"]
+        out["byte_planes"] = {"fill_ms_avg": round(fms3, 3),
+                              "fill_gcups_per_gpu": round(cells_rank / (fms3 * 1e-3) / 1e9, 3),
+                              "steps": args.no_plane_steps, "fill_launch": fi3}
+    if world == 1 and keep_planes and bytes_per_cell in (2, 3) and args.int32_steps > 0:
         # the same batch with int32 score planes (12 B/cell, the HBM-bound
         # format of SURVEY 8(d)); batches beyond the free HBM run in chunks
         os.environ["GX_PLANES32"] = "1"
