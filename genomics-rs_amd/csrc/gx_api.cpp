@@ -733,6 +733,9 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     job.twin = twin;
     const bool w16 = twin && planes && !job.table && w16_ok(sc);
     job.w16 = w16;
+    // small-alphabet twins: the match test through a penalty table (cell_pk);
+    // the byte-plane twin (tables) keeps the plain test
+    const bool twin_tbl = twin && tbl && (!planes || w16) && sc.sm >= sc.smm && sc.sm - sc.smm <= 255;
     ctx->last_twin = twin ? 1 : 0;
     const int Wf = twin ? Wt : W;   // band width of the launch
     const size_t plane_esz = d8 ? 1 : sizeof(int32_t);
@@ -880,11 +883,14 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     // up to 128 VGPRs: 4 waves per SIMD)
     const int per_cu = (twin && !getenv("GX_FILL_GRID")) ? std::max(1, 16 / (Wf + 1)) : 1;
     const int grid = std::min(bands, fill_grid_cap(ctx->device) * per_cu);
+    if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug"))
+        fprintf(stderr, "[gx DEBUG] fill launch: P=%zu layout=%d W=%d twin=%d plane_bytes=%d tbl=%d grid=%d bands=%d\n", P,
+                lay, Wf, twin ? 1 : 0, ctx->last_pbytes, (twin ? twin_tbl : tbl) ? 1 : 0, grid, bands);
     const auto h_launch = std::chrono::steady_clock::now();
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].fb : ctx->ev0, eve = slot >= 0 ? ctx->slots[slot].fe : ctx->ev1;
     HIPCHK(hipEventRecord(evb, ctx->stream));
     if (bands > 0 && twin)
-        HIPCHK(launch_fill_pk(Wf, planes ? (w16 ? 2 : 1) : 0, (const PairDev*)job.pairs.p, (int)(Pd / 2), bands, (int*)job.counter.p,
+        HIPCHK(launch_fill_pk(Wf, (planes ? (w16 ? 2 : 1) : 0) + (twin_tbl ? 4 : 0), (const PairDev*)job.pairs.p, (int)(Pd / 2), bands, (int*)job.counter.p,
                               (PairRes*)job.pres.p, scl, grid, ctx->stream));
     else if (bands > 0)
         HIPCHK(launch_fill(W, lay, is_local != 0, planes ? (d8 ? 2 : 1) : 0, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,

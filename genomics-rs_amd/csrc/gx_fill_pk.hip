@@ -127,6 +127,20 @@ struct PkScores {
 // [-64, 63] (gx_api.cpp w16_ok checks the ranges); both pairs' codes of a
 // cell in one dword, as the halves already hold them.  Two v_pk_mad_u16 and
 // three v_pk_sub_i16 per two cells (the byte format: three SDWA per cell).
+// Small-alphabet twins (TBL, the launch's <= 4 symbols in Scores32.sym): a
+// row's penalty table (byte k: 0 if c1 is symbol k, else s_match -
+// s_mismatch, in [0, 255]) and a column's selector for v_perm_b32.
+__device__ __forceinline__ uint32_t penalty_table(int c1, const Scores32& sc) {
+    const uint32_t pen = (uint32_t)(sc.sm - sc.smm) & 0xFFu;
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t |= (c1 == sc.sym[k] ? 0u : pen) << (8 * k);
+    return t;
+}
+__device__ __forceinline__ uint32_t perm_selector(int code0, int code1) {
+    return (uint32_t)code0 | 0x0C00u | ((uint32_t)(4 + code1) << 16) | 0x0C000000u;
+}
+
 __device__ __forceinline__ uint32_t w16_code(uint32_t I, uint32_t D, uint32_t S, uint32_t Iold) {
     const uint32_t xI = psub(I, Iold), xS = psub(S, I), xD = psub(D, I);
     return pmad(xD, 0x02000200u, pmad(xS, 0x00100010u, xI));
@@ -146,12 +160,18 @@ struct LanePk {
 // algo.rs:222-268 on the shifted values, both pairs at once; MASKED keeps
 // the lanes outside columns 1..m unchanged, per pair (a twin's two pairs may
 // differ in length: the shorter one's state stays at its last column).
-template <bool MASKED>
+template <bool MASKED, bool TBL>
 __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const uint32_t sm_in, const uint32_t e_up,
-                                        const uint32_t c2, const uint32_t c1, const uint32_t act, const PkScores& k,
+                                        const uint32_t c2, const uint32_t c1, const uint32_t c1h, const uint32_t act,
+                                        const PkScores& k,
                                         uint32_t& oI, uint32_t& oD, uint32_t& oS, uint32_t& oIold) {
     const uint32_t In = pmax(st.I, padds(st.SD, k.h));            // max(I, max(S,D) + h)   (algo.rs:231-236)
-    const uint32_t Sn = pmad(pmis(c1, c2), k.dsm, st.SMtl);        // SM(i-1,j-1) + s''       (algo.rs:245-248)
+    // SM(i-1,j-1) + s''  (algo.rs:245-248).  TBL: c1/c1h are the row's penalty
+    // tables of the two pairs (byte k: 0 if the row's char is symbol k, else
+    // s_match - s_mismatch) and c2 the column's selector (pair 0's symbol in
+    // byte 0, 4 + pair 1's in byte 2, zero bytes between): one v_perm_b32
+    // reads both penalties (xor + min + mad without the table)
+    const uint32_t Sn = TBL ? psub(st.SMtl, __builtin_amdgcn_perm(c1h, c1, c2)) : pmad(pmis(c1, c2), k.dsm, st.SMtl);
     const uint32_t Dn = dd_in;                                     // (algo.rs:238-243, from the row above)
     const uint32_t IS = pmax(In, Sn);
     const uint32_t SMn = pmax(IS, Dn);
@@ -176,9 +196,10 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
     st.Etl = e_up;
 }
 
-template <bool MASKED>
+template <bool MASKED, bool TBL>
 __device__ __forceinline__ void dp_step_pk(LanePk& st, const Rec& r, const int t, const int lane, const int m0,
-                                           const int m1, const uint32_t c1a, const uint32_t c1b, const PkScores& k,
+                                           const int m1, const uint32_t c1a, const uint32_t c1b, const uint32_t c1ah,
+                                           const uint32_t c1bh, const PkScores& k,
                                            uint32_t (&oI)[2], uint32_t (&oD)[2], uint32_t (&oS)[2],
                                            uint32_t (&oL)[2]) {
     const uint32_t dd_in = (uint32_t)shr1(r.dd, (int)st.b.Dd);
@@ -188,8 +209,8 @@ __device__ __forceinline__ void dp_step_pk(LanePk& st, const Rec& r, const int t
     const uint32_t act = MASKED ? ((unsigned)(t - lane) < (unsigned)m0 ? 0xFFFFu : 0u) |
                                       ((unsigned)(t - lane) < (unsigned)m1 ? 0xFFFF0000u : 0u)
                                 : ~0u;
-    cell_pk<MASKED>(st.a, dd_in, sm_in, e_in, c2, c1a, act, k, oI[0], oD[0], oS[0], oL[0]);
-    cell_pk<MASKED>(st.b, st.a.Dd, st.a.SMp, st.a.E, c2, c1b, act, k, oI[1], oD[1], oS[1], oL[1]);
+    cell_pk<MASKED, TBL>(st.a, dd_in, sm_in, e_in, c2, c1a, c1ah, act, k, oI[0], oD[0], oS[0], oL[0]);
+    cell_pk<MASKED, TBL>(st.b, st.a.Dd, st.a.SMp, st.a.E, c2, c1b, c1bh, act, k, oI[1], oD[1], oS[1], oL[1]);
     st.c2c = c2;
 }
 
@@ -238,7 +259,8 @@ struct WavePk {
     uint32_t cnt_addr;
     int m, lane;                                      // m: the twin's columns (the longer pair's)
     int m0, m1;                                       // each pair's own columns
-    uint32_t c1a, c1b;
+    uint32_t c1a, c1b;                                // rows A, B: both pairs' chars (TBL: pair 0's penalty tables)
+    uint32_t c1ah, c1bh;                              // TBL: pair 1's penalty tables
     int B0, B1;                                       // current bases (wave-uniform)
 };
 
@@ -258,66 +280,66 @@ __device__ __forceinline__ void group4_pk(LanePk& st, Rec (&nxt)[4], WavePk& w, 
     if (MASKED) {
         auto sko = [&](int c) { return (c >= 0 && c <= w.m) ? w.skel_voff + 4u * (uint32_t)c : kSkelOff; };
         push63_pk<4 * G4 + 0>(out_base, st, lane63_mask(push_on && col0 >= 0 && col0 <= w.m));
-        dp_step_pk<true>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[0], bD[0], bS[0], bL[0]);
-        if (PLANES == 1) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
-        if (PLANES == 2) { wc[0][0] = w16_code(bI[0][0], bD[0][0], bS[0][0], bL[0][0]);
+        dp_step_pk<true, (PLANES & 4) != 0>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[0], bD[0], bS[0], bL[0]);
+        if ((PLANES & 3) == 1) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
+        if ((PLANES & 3) == 2) { wc[0][0] = w16_code(bI[0][0], bD[0][0], bS[0][0], bL[0][0]);
                            wc[1][0] = w16_code(bI[0][1], bD[0][1], bS[0][1], bL[0][1]); }
         skel_store(w.skel_rsrc, sko(col0 + 1), (int)st.b.E);
         push63_pk<4 * G4 + 1>(out_base, st, lane63_mask(push_on && col0 + 1 >= 0 && col0 + 1 <= w.m));
-        dp_step_pk<true>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[1], bD[1], bS[1], bL[1]);
-        if (PLANES == 1) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
-        if (PLANES == 2) { wc[0][1] = w16_code(bI[1][0], bD[1][0], bS[1][0], bL[1][0]);
+        dp_step_pk<true, (PLANES & 4) != 0>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[1], bD[1], bS[1], bL[1]);
+        if ((PLANES & 3) == 1) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
+        if ((PLANES & 3) == 2) { wc[0][1] = w16_code(bI[1][0], bD[1][0], bS[1][0], bL[1][0]);
                            wc[1][1] = w16_code(bI[1][1], bD[1][1], bS[1][1], bL[1][1]); }
         skel_store(w.skel_rsrc, sko(col0 + 2), (int)st.b.E);
         push63_pk<4 * G4 + 2>(out_base, st, lane63_mask(push_on && col0 + 2 >= 0 && col0 + 2 <= w.m));
-        dp_step_pk<true>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[2], bD[2], bS[2], bL[2]);
-        if (PLANES == 1) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
-        if (PLANES == 2) { wc[0][2] = w16_code(bI[2][0], bD[2][0], bS[2][0], bL[2][0]);
+        dp_step_pk<true, (PLANES & 4) != 0>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[2], bD[2], bS[2], bL[2]);
+        if ((PLANES & 3) == 1) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
+        if ((PLANES & 3) == 2) { wc[0][2] = w16_code(bI[2][0], bD[2][0], bS[2][0], bL[2][0]);
                            wc[1][2] = w16_code(bI[2][1], bD[2][1], bS[2][1], bL[2][1]); }
         skel_store(w.skel_rsrc, sko(col0 + 3), (int)st.b.E);
         push63_pk<4 * G4 + 3>(out_base, st, lane63_mask(push_on && col0 + 3 >= 0 && col0 + 3 <= w.m));
         if (push_on && col0 + 3 >= 0 && col0 <= w.m) lds_store_lane0(w.wcnt_out, min(col0 + 3, w.m) + 1);
-        dp_step_pk<true>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[3], bD[3], bS[3], bL[3]);
-        if (PLANES == 1) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
-        if (PLANES == 2) { wc[0][3] = w16_code(bI[3][0], bD[3][0], bS[3][0], bL[3][0]);
+        dp_step_pk<true, (PLANES & 4) != 0>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[3], bD[3], bS[3], bL[3]);
+        if ((PLANES & 3) == 1) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
+        if ((PLANES & 3) == 2) { wc[0][3] = w16_code(bI[3][0], bD[3][0], bS[3][0], bL[3][0]);
                            wc[1][3] = w16_code(bI[3][1], bD[3][1], bS[3][1], bL[3][1]); }
         skel_store(w.skel_rsrc, sko(col0 + 4), (int)st.b.E);
     } else {
         const uint32_t pa = push_on && w.lane == kWave - 1 ? out_base : w.scratch;
         push_all_pk<4 * G4 + 0>(pa, st);
-        dp_step_pk<false>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[0], bD[0], bS[0], bL[0]);
-        if (PLANES == 1) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
-        if (PLANES == 2) { wc[0][0] = w16_code(bI[0][0], bD[0][0], bS[0][0], bL[0][0]);
+        dp_step_pk<false, (PLANES & 4) != 0>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[0], bD[0], bS[0], bL[0]);
+        if ((PLANES & 3) == 1) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
+        if ((PLANES & 3) == 2) { wc[0][0] = w16_code(bI[0][0], bD[0][0], bS[0][0], bL[0][0]);
                            wc[1][0] = w16_code(bI[0][1], bD[0][1], bS[0][1], bL[0][1]); }
         const uint32_t e0 = st.b.E;
         push_all_pk<4 * G4 + 1>(pa, st);
-        dp_step_pk<false>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[1], bD[1], bS[1], bL[1]);
-        if (PLANES == 1) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
-        if (PLANES == 2) { wc[0][1] = w16_code(bI[1][0], bD[1][0], bS[1][0], bL[1][0]);
+        dp_step_pk<false, (PLANES & 4) != 0>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[1], bD[1], bS[1], bL[1]);
+        if ((PLANES & 3) == 1) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
+        if ((PLANES & 3) == 2) { wc[0][1] = w16_code(bI[1][0], bD[1][0], bS[1][0], bL[1][0]);
                            wc[1][1] = w16_code(bI[1][1], bD[1][1], bS[1][1], bL[1][1]); }
         const uint32_t e1 = st.b.E;
         push_all_pk<4 * G4 + 2>(pa, st);
-        dp_step_pk<false>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[2], bD[2], bS[2], bL[2]);
-        if (PLANES == 1) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
-        if (PLANES == 2) { wc[0][2] = w16_code(bI[2][0], bD[2][0], bS[2][0], bL[2][0]);
+        dp_step_pk<false, (PLANES & 4) != 0>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[2], bD[2], bS[2], bL[2]);
+        if ((PLANES & 3) == 1) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
+        if ((PLANES & 3) == 2) { wc[0][2] = w16_code(bI[2][0], bD[2][0], bS[2][0], bL[2][0]);
                            wc[1][2] = w16_code(bI[2][1], bD[2][1], bS[2][1], bL[2][1]); }
         const uint32_t e2 = st.b.E;
         push_all_pk<4 * G4 + 3>(pa, st);
         publish_all(w.cnt_addr, col0 + 3 + 1);
-        dp_step_pk<false>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, k, bI[3], bD[3], bS[3], bL[3]);
-        if (PLANES == 1) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
-        if (PLANES == 2) { wc[0][3] = w16_code(bI[3][0], bD[3][0], bS[3][0], bL[3][0]);
+        dp_step_pk<false, (PLANES & 4) != 0>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[3], bD[3], bS[3], bL[3]);
+        if ((PLANES & 3) == 1) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
+        if ((PLANES & 3) == 2) { wc[0][3] = w16_code(bI[3][0], bD[3][0], bS[3][0], bL[3][0]);
                            wc[1][3] = w16_code(bI[3][1], bD[3][1], bS[3][1], bL[3][1]); }
         skel_store4(w.skel_rsrc, w.skel_voff + 4u * (uint32_t)(col0 + 1), (int)e0, (int)e1, (int)e2, (int)st.b.E);
     }
-    if (PLANES == 2) {
+    if ((PLANES & 3) == 2) {
         // twin plane codes: per strip [group][row][lane][step] dwords (2 KB a group)
         const uint32_t v = (uint32_t)G4 * kTwinGroupBytes + (uint32_t)w.lane * 16u;
         const auto r = rsrc_of(w.pI[0] + sb_off * (kTwinGroupBytes / kGroupInts), 4 * kTwinGroupBytes);
         bstore4(r, v, make_int4((int)wc[0][0], (int)wc[0][1], (int)wc[0][2], (int)wc[0][3]));
         bstore4(r, v + kTwinGroupBytes / 2, make_int4((int)wc[1][0], (int)wc[1][1], (int)wc[1][2], (int)wc[1][3]));
     }
-    if (PLANES == 1) {
+    if ((PLANES & 3) == 1) {
         // compact planes of both pairs (bytes_step): x_I = I - I(j-1) (shifted:
         // x_I - g), x_S = S - I, x_D = D - I, one byte per cell
         constexpr int kSubBytes = kSub / 4 * kGroupInts;
@@ -389,13 +411,13 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
     WavePk w;
     {
         // bytes per compact plane per strip (PLANES 2: the twin's one code plane, 2 KB a group)
-        const size_t strip_planes = (size_t)s * P0.t4 * (PLANES == 2 ? kTwinGroupBytes : kGroupInts);
-        w.pI[0] = PLANES ? (uint8_t*)P0.pI + strip_planes : nullptr;
-        w.pD[0] = PLANES == 1 ? (uint8_t*)P0.pD + strip_planes : nullptr;
-        w.pS[0] = PLANES == 1 ? (uint8_t*)P0.pS + strip_planes : nullptr;
-        w.pI[1] = PLANES == 1 ? (uint8_t*)P1.pI + strip_planes : nullptr;
-        w.pD[1] = PLANES == 1 ? (uint8_t*)P1.pD + strip_planes : nullptr;
-        w.pS[1] = PLANES == 1 ? (uint8_t*)P1.pS + strip_planes : nullptr;
+        const size_t strip_planes = (size_t)s * P0.t4 * ((PLANES & 3) == 2 ? kTwinGroupBytes : kGroupInts);
+        w.pI[0] = (PLANES & 3) ? (uint8_t*)P0.pI + strip_planes : nullptr;
+        w.pD[0] = (PLANES & 3) == 1 ? (uint8_t*)P0.pD + strip_planes : nullptr;
+        w.pS[0] = (PLANES & 3) == 1 ? (uint8_t*)P0.pS + strip_planes : nullptr;
+        w.pI[1] = (PLANES & 3) == 1 ? (uint8_t*)P1.pI + strip_planes : nullptr;
+        w.pD[1] = (PLANES & 3) == 1 ? (uint8_t*)P1.pD + strip_planes : nullptr;
+        w.pS[1] = (PLANES & 3) == 1 ? (uint8_t*)P1.pS + strip_planes : nullptr;
         w.codes[0] = P0.codes + (size_t)s * P0.t16 * kWave * kRowsPerLane;
         w.codes[1] = P1.codes + (size_t)s * P0.t16 * kWave * kRowsPerLane;
     }
@@ -407,8 +429,16 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
     w.scratch = scratch_base + 4u * (uint32_t)lane;
     w.cnt_addr = (has_consumer && lane == kWave - 1) ? lds_addr((const void*)wcnt_out) : w.scratch;
     w.m = m; w.lane = lane; w.m0 = P0.m; w.m1 = P1.m;
-    w.c1a = pk2(ia <= P0.n ? (int)P0.c1[ia - 1] : 0x100, ia <= P1.n ? (int)P1.c1[ia - 1] : 0x100);
-    w.c1b = pk2(ia + 1 <= P0.n ? (int)P0.c1[ia] : 0x100, ia + 1 <= P1.n ? (int)P1.c1[ia] : 0x100);
+    if constexpr ((PLANES & 4) != 0) {   // TBL: penalty tables of rows A, B per pair
+        w.c1a = penalty_table(ia <= P0.n ? (int)P0.c1[ia - 1] : 0x100, sc);
+        w.c1ah = penalty_table(ia <= P1.n ? (int)P1.c1[ia - 1] : 0x100, sc);
+        w.c1b = penalty_table(ia + 1 <= P0.n ? (int)P0.c1[ia] : 0x100, sc);
+        w.c1bh = penalty_table(ia + 1 <= P1.n ? (int)P1.c1[ia] : 0x100, sc);
+    } else {
+        w.c1a = pk2(ia <= P0.n ? (int)P0.c1[ia - 1] : 0x100, ia <= P1.n ? (int)P1.c1[ia - 1] : 0x100);
+        w.c1b = pk2(ia + 1 <= P0.n ? (int)P0.c1[ia] : 0x100, ia + 1 <= P1.n ? (int)P1.c1[ia] : 0x100);
+        w.c1ah = w.c1bh = 0;
+    }
 
     // column 0 of the row above: its bases and record (published with the ring's first counter)
     wait_ge(wcnt_in, min(4, m) + 1, status);
@@ -496,6 +526,7 @@ struct __attribute__((aligned(16))) RecW {
 // I/O wave of a twin band: ring 0 from row 0 (analytic) or the previous
 // band's bottom row (absolute -> relative to the bases it picks per block);
 // ring W to HBM (relative -> absolute with the last strip's bases).
+template <bool TBL>
 __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, const int lane, const Scores32& sc,
                            const PkScores& k, Rec* ring0, const Rec* ringW, lds_int* wcnt0, lds_int* rcnt0,
                            lds_int* wcntW, lds_int* rcntW, lds_int* base0, lds_int* baseW, const bool do_out,
@@ -527,7 +558,11 @@ __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, c
                         else {
                             dd0 = dd1 = 2 * sc.h;
                             sm0 = sm1 = sc.h + smp;
-                            c2 = (int)pk2(j <= P0.m ? (int)P0.c2[j - 1] : 0x200, j <= P1.m ? (int)P1.c2[j - 1] : 0x200);
+                            if (TBL)   // the column's v_perm_b32 selector (cell_pk)
+                                c2 = (int)perm_selector(j <= P0.m ? sym_code(P0.c2[j - 1], sc) : 0,
+                                                        j <= P1.m ? sym_code(P1.c2[j - 1], sc) : 0);
+                            else
+                                c2 = (int)pk2(j <= P0.m ? (int)P0.c2[j - 1] : 0x200, j <= P1.m ? (int)P1.c2[j - 1] : 0x200);
                         }
                     } else {
                         const gu64* q = (const gu64*)(feed_in + j);
@@ -654,7 +689,7 @@ __global__ __launch_bounds__((W + 1) * kWave, (W + 1 + 3) / 4) void fill_pk_kern
                                         lds_addr(push_scratch[wave]));
             }
         } else {
-            io_wave_pk(P0, P1, lb, lane, sc, k, rings[0], rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0],
+            io_wave_pk<(PLANES & 4) != 0>(P0, P1, lb, lane, sc, k, rings[0], rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0],
                        (lds_int*)&wcnt[W], (lds_int*)&rcnt[W], (lds_int*)bases[0], (lds_int*)bases[W],
                        lb + 1 < P0.bands, band_counter + 1);
         }
@@ -666,15 +701,17 @@ template <int W0, int... Ws>
 static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int ntwins, int total_bands, int* d_counter,
                               PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
     if (W == W0) {
-        if (planes == 2)
-            hipLaunchKernelGGL((fill_pk_kernel<W0, 2>), dim3(grid), dim3((W0 + 1) * kWave), 0, st, d_pairs, ntwins,
-                               total_bands, d_counter, d_pres, sc);
-        else if (planes)
-            hipLaunchKernelGGL((fill_pk_kernel<W0, 1>), dim3(grid), dim3((W0 + 1) * kWave), 0, st, d_pairs, ntwins,
-                               total_bands, d_counter, d_pres, sc);
-        else
-            hipLaunchKernelGGL((fill_pk_kernel<W0, 0>), dim3(grid), dim3((W0 + 1) * kWave), 0, st, d_pairs, ntwins,
-                               total_bands, d_counter, d_pres, sc);
+#define GX_PK(PL) hipLaunchKernelGGL((fill_pk_kernel<W0, PL>), dim3(grid), dim3((W0 + 1) * kWave), 0, st, d_pairs, \
+                                     ntwins, total_bands, d_counter, d_pres, sc)
+        switch (planes) {
+            case 0: GX_PK(0); break;
+            case 1: GX_PK(1); break;
+            case 2: GX_PK(2); break;
+            case 4: GX_PK(4); break;
+            case 6: GX_PK(6); break;
+            default: return hipErrorInvalidValue;
+        }
+#undef GX_PK
         return hipGetLastError();
     }
     if constexpr (sizeof...(Ws) > 0) return launch_pk_w<Ws...>(W, planes, d_pairs, ntwins, total_bands, d_counter,
@@ -683,7 +720,8 @@ static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int ntw
 }
 
 // Twin launch: W from {3, 4, 7, 8, 15}; planes: 0 none, 1 compact bytes per
-// pair (3 B/cell), 2 twin codes (2 B/cell).
+// pair (3 B/cell), 2 twin codes (2 B/cell); + 4: small-alphabet score tables
+// (with none or twin codes: the batch launches).
 hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int ntwins, int total_bands, int* d_counter,
                           PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
     return launch_pk_w<3, 4, 7, 8, 15>(W, planes, d_pairs, ntwins, total_bands, d_counter, d_pres, sc, grid, st);
