@@ -4,7 +4,7 @@ blocks holding the compact-plane byte inserts), from a device-only assembly
 build of gx_kernels.hip:
 
     python tools/isa_mix.py [kernel-name-regex]   (default: the bench's W=15 compact-plane kernel)
-    python tools/isa_mix.py twin                  (the twin fill, gx_fill_pk.hip, W=8 with twin plane codes)
+    python tools/isa_mix.py twin                  (the twin fill, gx_fill_pk.hip, W=8, twin plane codes, score tables)
 
 Compiles to /tmp/gx_isa/ (about 2 minutes) unless GX_ISA_S names an existing .s.
 A twin group holds 16 cells per lane (4 steps x 2 rows x 2 pairs)."""
@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pat = sys.argv[1] if len(sys.argv) > 1 else r"_ZN2gx11fill_kernelILi15ELb0ELi2ELb1ELb0ELb0ELb1ELi0E"
 src, cells = "gx_kernels", 8
 if pat == "twin":
-    pat, src, cells = r"_ZN2gx14fill_pk_kernelILi8ELi2E", "gx_fill_pk", 16
+    pat, src, cells = r"_ZN2gx14fill_pk_kernelILi8ELi6E", "gx_fill_pk", 16
 s_path = os.environ.get("GX_ISA_S")
 if not s_path:
     os.makedirs("/tmp/gx_isa", exist_ok=True)
