@@ -215,7 +215,9 @@ int gx_fill_twin(const gx_context* ctx);
 /* Score-plane bytes per cell a batch launch (layout 0, no max tracking)
  * writes with these scores: 3 when the compact format's range proof holds
  * (global mode, g, h <= 0, differences within a signed byte), else 12; -1 on
- * invalid scores. */
+ * invalid scores.  An upper bound: a launch that takes the twin fill with
+ * its plane codes writes 2 (gx_fill_info reports the
+ * launch's own figure). */
 int gx_plane_bytes_per_cell(const gx_scores* scores, int is_local);
 
 /* ---- sequence.rs / config.rs mirrors ----------------------------------- */
