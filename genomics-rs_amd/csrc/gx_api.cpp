@@ -733,9 +733,11 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     job.twin = twin;
     const bool w16 = twin && planes && !job.table && w16_ok(sc);
     job.w16 = w16;
-    // small-alphabet twins: the match test through a penalty table (cell_pk);
+    // small-alphabet twins: the match test through score tables (cell_pk; the
+    // shifted scores must fit an unsigned byte);
     // the byte-plane twin (tables) keeps the plain test
-    const bool twin_tbl = twin && tbl && (!planes || w16) && sc.sm >= sc.smm && sc.sm - sc.smm <= 255;
+    const bool twin_tbl = twin && tbl && (!planes || w16) && scl.sm >= 0 && scl.sm <= 255 && scl.smm >= 0 &&
+                          scl.smm <= 255;
     ctx->last_twin = twin ? 1 : 0;
     const int Wf = twin ? Wt : W;   // band width of the launch
     const size_t plane_esz = d8 ? 1 : sizeof(int32_t);

@@ -128,13 +128,13 @@ struct PkScores {
 // cell in one dword, as the halves already hold them.  Two v_pk_mad_u16 and
 // three v_pk_sub_i16 per two cells (the byte format: three SDWA per cell).
 // Small-alphabet twins (TBL, the launch's <= 4 symbols in Scores32.sym): a
-// row's penalty table (byte k: 0 if c1 is symbol k, else s_match -
-// s_mismatch, in [0, 255]) and a column's selector for v_perm_b32.
-__device__ __forceinline__ uint32_t penalty_table(int c1, const Scores32& sc) {
-    const uint32_t pen = (uint32_t)(sc.sm - sc.smm) & 0xFFu;
+// row's score table (byte k: the shifted match score if c1 is symbol k, else
+// the shifted mismatch score, both in [0, 255]) and a column's selector for
+// v_perm_b32.
+__device__ __forceinline__ uint32_t score_table_pk(int c1, const Scores32& sc) {
     uint32_t t = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) t |= (c1 == sc.sym[k] ? 0u : pen) << (8 * k);
+    for (int k = 0; k < 4; ++k) t |= ((uint32_t)(c1 == sc.sym[k] ? sc.sm : sc.smm) & 0xFFu) << (8 * k);
     return t;
 }
 __device__ __forceinline__ uint32_t perm_selector(int code0, int code1) {
@@ -166,12 +166,13 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
                                         const PkScores& k,
                                         uint32_t& oI, uint32_t& oD, uint32_t& oS, uint32_t& oIold) {
     const uint32_t In = pmax(st.I, padds(st.SD, k.h));            // max(I, max(S,D) + h)   (algo.rs:231-236)
-    // SM(i-1,j-1) + s''  (algo.rs:245-248).  TBL: c1/c1h are the row's penalty
-    // tables of the two pairs (byte k: 0 if the row's char is symbol k, else
-    // s_match - s_mismatch) and c2 the column's selector (pair 0's symbol in
-    // byte 0, 4 + pair 1's in byte 2, zero bytes between): one v_perm_b32
-    // reads both penalties (xor + min + mad without the table)
-    const uint32_t Sn = TBL ? psub(st.SMtl, __builtin_amdgcn_perm(c1h, c1, c2)) : pmad(pmis(c1, c2), k.dsm, st.SMtl);
+    // SM(i-1,j-1) + s''  (algo.rs:245-248).  TBL: c1/c1h are the row's score
+    // tables of the two pairs (byte k: s_match'' if the row's char is symbol
+    // k, else s_mismatch''; SM is then kept without the s_match'' offset) and
+    // c2 the column's selector (pair 0's symbol in byte 0, 4 + pair 1's in
+    // byte 2, zero bytes between): one v_perm_b32 reads both scores (xor +
+    // min + mad, and the offset's add, without the table)
+    const uint32_t Sn = TBL ? padd(st.SMtl, __builtin_amdgcn_perm(c1h, c1, c2)) : pmad(pmis(c1, c2), k.dsm, st.SMtl);
     const uint32_t Dn = dd_in;                                     // (algo.rs:238-243, from the row above)
     const uint32_t IS = pmax(In, Sn);
     const uint32_t SMn = pmax(IS, Dn);
@@ -183,7 +184,7 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
     const uint32_t En = bfi(m2, e_up, E1);
     const uint32_t cIn = pcode(st.cI, m1);
     const uint32_t cDn = pcode(st.cD, m2);
-    const uint32_t SMpn = padds(SMn, k.smp);
+    const uint32_t SMpn = TBL ? SMn : padds(SMn, k.smp);           // TBL: no offset (k.smp = 0, the tables hold s'')
     oI = In; oD = Dn; oS = Sn; oIold = st.I;
     if (MASKED) {   // act: 0xFFFF in each half whose pair has this column
         st.I = bfi(act, In, st.I); st.SD = bfi(act, SDn, st.SD); st.Dd = bfi(act, Ddn, st.Dd);
@@ -429,11 +430,11 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
     w.scratch = scratch_base + 4u * (uint32_t)lane;
     w.cnt_addr = (has_consumer && lane == kWave - 1) ? lds_addr((const void*)wcnt_out) : w.scratch;
     w.m = m; w.lane = lane; w.m0 = P0.m; w.m1 = P1.m;
-    if constexpr ((PLANES & 4) != 0) {   // TBL: penalty tables of rows A, B per pair
-        w.c1a = penalty_table(ia <= P0.n ? (int)P0.c1[ia - 1] : 0x100, sc);
-        w.c1ah = penalty_table(ia <= P1.n ? (int)P1.c1[ia - 1] : 0x100, sc);
-        w.c1b = penalty_table(ia + 1 <= P0.n ? (int)P0.c1[ia] : 0x100, sc);
-        w.c1bh = penalty_table(ia + 1 <= P1.n ? (int)P1.c1[ia] : 0x100, sc);
+    if constexpr ((PLANES & 4) != 0) {   // TBL: score tables of rows A, B per pair
+        w.c1a = score_table_pk(ia <= P0.n ? (int)P0.c1[ia - 1] : 0x100, sc);
+        w.c1ah = score_table_pk(ia <= P1.n ? (int)P1.c1[ia - 1] : 0x100, sc);
+        w.c1b = score_table_pk(ia + 1 <= P0.n ? (int)P0.c1[ia] : 0x100, sc);
+        w.c1bh = score_table_pk(ia + 1 <= P1.n ? (int)P1.c1[ia] : 0x100, sc);
     } else {
         w.c1a = pk2(ia <= P0.n ? (int)P0.c1[ia - 1] : 0x100, ia <= P1.n ? (int)P1.c1[ia - 1] : 0x100);
         w.c1b = pk2(ia + 1 <= P0.n ? (int)P0.c1[ia] : 0x100, ia + 1 <= P1.n ? (int)P1.c1[ia] : 0x100);
@@ -539,7 +540,7 @@ __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, c
     RecW* feed_out = do_out ? feed + (size_t)lb * P0.feed_stride : nullptr;
     const int* prog_in = lb > 0 ? P0.progress + (size_t)(lb - 1) * kProgStride : nullptr;
     int* prog_out = do_out ? P0.progress + (size_t)lb * kProgStride : nullptr;
-    const int smp = sc.sm;              // sm'' (the launch's scores carry the shift's -2g, Scores32.shift)
+    const int smp = TBL ? 0 : sc.sm;    // sm'' (the launch's scores carry the shift's -2g, Scores32.shift); TBL: no offset
     unsigned idle = 0;
     int bprev0 = 0, bprev1 = 0;         // bases of the block before the current chunk's first column
     while (in_next <= m || (do_out && out_next <= m)) {
@@ -664,7 +665,9 @@ __global__ __launch_bounds__((W + 1) * kWave, (W + 1 + 3) / 4) void fill_pk_kern
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int lane = threadIdx.x & (kWave - 1);
     const int smp = sc.sm, smmp = sc.smm;   // s - 2g: the launch's scores carry the shift (Scores32.shift)
-    const PkScores k{pk2(sc.h, sc.h), pk2(smp, smp), pk2(smmp - smp, smmp - smp)};
+    // score_max is kept as SM + sm'' (TBL: as SM; its tables add the score)
+    const int off = (PLANES & 4) ? 0 : smp;
+    const PkScores k{pk2(sc.h, sc.h), pk2(off, off), pk2(smmp - smp, smmp - smp)};
     for (;;) {
         if (threadIdx.x == 0) band_sh = atomicAdd(band_counter, 1);
         if (threadIdx.x < W + 1) { wcnt[threadIdx.x] = 0; rcnt[threadIdx.x] = 0; }
