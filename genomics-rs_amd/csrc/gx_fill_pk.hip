@@ -236,8 +236,20 @@ __device__ __forceinline__ void push_all_pk(uint32_t vaddr, const LanePk& st) {
         : "memory");
 }
 
+// The fields load one by one (ds_read_b32, kept apart by empty asm): each
+// lands in a register of its own that the step's DPP move then writes in
+// place (lane 0 keeps the record), where a merged ds_read_b96 tuple cost a
+// v_mov per field to free the tuple for the next group's loads.
 __device__ __forceinline__ void read4_pk(Rec (&r)[4], const Rec* rin) {
-    r[0] = rin[0]; r[1] = rin[1]; r[2] = rin[2]; r[3] = rin[3];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        r[u].dd = rin[u].dd;
+        asm volatile("" ::: "memory");
+        r[u].sm = rin[u].sm;
+        asm volatile("" ::: "memory");
+        r[u].c2 = rin[u].c2;
+        asm volatile("" ::: "memory");
+    }
 }
 
 // Bases of a ring: slot 0 = column 0; slot 1 + (b mod kBaseSlots) = block b
