@@ -718,15 +718,20 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         if (const char* e = getenv("GX_BAND_WAVES")) wt_want = atoi(e);
         else wt_want = fill_band_waves(false, total_strips / 2, fill_grid_cap(ctx->device), lay, min_strips);
         Wt = twin_width(ph, sc, is_local, track, lcs, lay, planes, d8, wt_want);
-        // auto: only queues of >= 2.5 rounds of scalar bands (a twin band is
-        // ~1.3x slower per step, so short queues lose parallelism: 30k pairs,
-        // fill ms scalar/twin: 4 pairs 7.2/9.7, 8 9.9/10.0, 16 14.4/15.4, 32
-        // 24.7/22.0, all-vs-all 34.5/29.5, 80 53.0/47.2); GX_TWIN=1 forces it
+        // auto: the twin fill once its own bands fill the grid (a twin band
+        // is slower per step than a scalar one, so fewer bands than CUs
+        // leave it latency-bound).  30k pairs, fill ms scalar / twin (codes,
+        // tables): 4 pairs (158 twin bands) 7.2 / 8.8, 6 (237) 9.4 / 8.9,
+        // 8 9.96 / 8.9, 16 14.1 / 12.9, 24 19.2 / 17.4, all-vs-all and 80
+        // pairs far apart.  GX_TWIN=1 forces it.
         const char* e = getenv("GX_TWIN");
         if (Wt && !(e && !strcmp(e, "1"))) {
-            long long scalar_bands = 0;
-            for (const PairHost& h : ph) scalar_bands += ceil_div(ceil_div((int)h.n, SR), W);
-            if (2 * scalar_bands < 5LL * fill_grid_cap(ctx->device)) Wt = 0;
+            long long twin_bands = 0;
+            for (size_t q = 0; q < ph.size(); q += 2) {
+                const PairHost& y = q + 1 < ph.size() ? ph[q + 1] : ph[q];
+                twin_bands += ceil_div(ceil_div((int)std::max(ph[q].n, y.n), SR), Wt);
+            }
+            if (10 * twin_bands < 9LL * fill_grid_cap(ctx->device)) Wt = 0;
         }
     }
     const bool twin = Wt > 0;
