@@ -1584,7 +1584,9 @@ extern "C" int gx_table_plane_sums(const gx_table* t, uint64_t* sums) {
     std::lock_guard<std::mutex> lk(ctx->mu);
     HIPCHK(hipSetDevice(ctx->device));
     DevBuf buf;
-    int rc = pool_get(ctx, 3 * sizeof(unsigned long long), &buf);
+    // (a GX_TABLE_TWIN table holds the pair twice: room for both; pair 0's are returned)
+    const size_t np = t->job.wide ? 1 : std::max<size_t>(t->job.pd.size(), 1);
+    int rc = pool_get(ctx, 3 * np * sizeof(unsigned long long), &buf);
     if (rc) return rc;
     const WideDev* w = t->job.wide ? &t->job.wd[0] : nullptr;
     hipError_t e = w ? launch_wide_plane_sums((const int64_t*)w->pI, (const int64_t*)w->pD, (const int64_t*)w->pS,
