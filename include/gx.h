@@ -199,8 +199,9 @@ int gx_staged_steps(const gx_context* ctx, size_t pair, gx_step* steps, size_t c
 /* The last fill launch on ctx: its layout (0: anti-diagonal 128-row strips,
  * 1: column step over 64-row strips), band width (strips per workgroup) and
  * score-plane bytes written per cell (0: none, 12: int32 planes, 3: compact
- * planes -- per-cell byte differences, decoded exactly by the exports).  No
- * reference counterpart (measurement only). */
+ * planes -- per-cell byte differences, decoded exactly by the exports, 2:
+ * the twin fill's plane codes -- the three differences in one 16-bit word,
+ * DESIGN.md 4.4, batches only).  No reference counterpart (measurement only). */
 int gx_fill_info(const gx_context* ctx, int* layout, int* band_waves, int* plane_bytes_per_cell);
 /* Chunks of the last gx_run_staged(_steps) / gx_align_batch call: a batch
  * whose device footprint (planes, codes, skeleton) exceeds the free HBM runs
