@@ -195,3 +195,22 @@ def test_twin_random_batches(gx, ctx, oracle, monkeypatch, seed):
         assert [int(x) for x in sums[0, p]] == o.extra["plane_sums"], (seed, p, len(a), len(b), info)
         assert res[p].score == o.score, (seed, p)
         assert _steps_list(st.steps(p)) == o.alignment(), (seed, p)
+
+
+@pytest.mark.parametrize("m", [31920, 31921])
+def test_twin_column_limit(gx, ctx, oracle, monkeypatch, m):
+    """The twin fill's landing columns are int16 halves: twins up to 31,920
+    columns (every pair checked against the oracle), the scalar fill beyond."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    rng = random.Random(m)
+    shapes = [(200, m), (150, m - 7), (260, m - 1)]
+    pairs = [(bytes(rng.choice(b"ACGT") for _ in range(n)), bytes(rng.choice(b"ACGT") for _ in range(mm)))
+             for n, mm in shapes]
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=1, plane_sums=True)
+    assert ctx.fill_info()["twin"] == (1 if m <= 31920 else 0)
+    sums = st.plane_sums()
+    for p, (a, b) in enumerate(pairs):
+        o = oracle.align_lean(a, b, CONFIG_SCORES)
+        assert [int(x) for x in sums[0, p]] == o.extra["plane_sums"], (m, p)
+        assert res[p].score == o.score and _steps_list(st.steps(p)) == o.alignment(), (m, p)
