@@ -277,7 +277,9 @@ def _steps_array(alignment) -> np.ndarray:
 
 def plane_bytes_per_cell(scores: "Scores", is_local: bool) -> int:
     """Score-plane bytes per cell of a batch launch with these scores: 3
-    (compact byte differences) or 12 (int32 planes); gx_plane_bytes_per_cell."""
+    (compact byte differences) or 12 (int32 planes); gx_plane_bytes_per_cell.
+    An upper bound: a launch that takes the twin fill writes 2 (its plane
+    codes; Context.fill_info reports the launch's figure)."""
     r = lib().gx_plane_bytes_per_cell(ctypes.byref(scores.c()), int(is_local))
     if r < 0:
         raise GxError(3, "invalid scores")
