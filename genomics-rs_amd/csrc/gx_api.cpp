@@ -39,8 +39,8 @@ hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, 
                             int floor_, int gshift, int row0, int rows, hipStream_t st);
 hipError_t launch_plane_sums(const PairDev* d_pairs, int npairs, int max_strips, int lay, int mode, int h, int g,
                              int floor_, int gshift, unsigned long long* out, hipStream_t st);
-hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int ntwins, int total_bands, int* d_counter,
-                          PairRes* d_pres, Scores32 sc, int grid, hipStream_t st);
+hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int npairs, int ntwins, int total_bands,
+                          int* d_counter, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st);
 hipError_t launch_fill_wide(const WideDev* d_pairs, int npairs, WideScores sc, WideRes* d_res, int local, int track,
                             hipStream_t st);
 hipError_t launch_wide_plane_sums(const int64_t* pI, const int64_t* pD, const int64_t* pS, int n, int m,
@@ -650,20 +650,41 @@ static hipError_t enqueue_plane_sums(gx_context* ctx, const FillJob& job, const 
 // |U - g|) (the range proof of d8_planes_ok).  Returns the widest admissible
 // band width <= W_want from {3, 4, 7, 8, 15}, or 0 when the twin fill does not apply
 // (shape, mode, scores, GX_TWIN=0; run_fill also skips it for short queues).
-// Pairs 2q and 2q+1 form twin q whatever
-// their shapes: the sweep covers the larger n and m, the shorter pair's state
-// stays at its last column (its values beyond lie in the row above's range,
-// but the bound takes the column difference anyway); an odd last pair is
-// twinned with itself (run_fill's phantom descriptor).
-static int twin_width(const std::vector<PairHost>& ph, const Scores32& sc, int is_local, bool track, bool lcs, int lay,
-                      bool planes, bool d8, int W_want) {
+// The twins (twin_table) pair the batch's pairs by shape whatever their
+// order; the sweep covers the larger n and m of a twin, the shorter pair's
+// state stays at its last column (its values beyond lie in the row above's
+// range, but the bound takes the column difference anyway); an odd last pair
+// is twinned with itself.
+static std::vector<std::pair<int, int>> twin_table(const std::vector<PairHost>& ph) {
+    std::vector<int> idx(ph.size());
+    for (size_t p = 0; p < ph.size(); ++p) idx[p] = (int)p;
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) {
+        return ph[a].m != ph[b].m ? ph[a].m > ph[b].m : ph[a].n > ph[b].n;
+    });
+    // neighbours in that order, unless their column counts lie more than
+    // 1,024 apart (the admission bound's column margin): such a pair is
+    // twinned with itself
+    std::vector<std::pair<int, int>> tw;
+    for (size_t k = 0; k < idx.size();) {
+        if (k + 1 < idx.size() && ph[idx[k]].m - ph[idx[k + 1]].m <= 1024) {
+            tw.emplace_back(idx[k], idx[k + 1]);
+            k += 2;
+        } else {
+            tw.emplace_back(idx[k], idx[k]);
+            k += 1;
+        }
+    }
+    return tw;
+}
+static int twin_width(const std::vector<PairHost>& ph, const std::vector<std::pair<int, int>>& tw, const Scores32& sc,
+                      int is_local, bool track, bool lcs, int lay, bool planes, bool d8, int W_want) {
     if (const char* e = getenv("GX_TWIN"); e && !strcmp(e, "0")) return 0;
     if (lay != 0 || is_local || track || lcs || (planes && !d8) || sc.g > 0 || sc.h > 0) return 0;
     if (ph.empty()) return 0;
     long long dm = 0;
-    for (size_t q = 0; q < ph.size(); q += 2) {
-        const PairHost& x = ph[q];
-        const PairHost& y = q + 1 < ph.size() ? ph[q + 1] : ph[q];
+    for (const auto& t : tw) {
+        const PairHost& x = ph[t.first];
+        const PairHost& y = ph[t.second];
         if (!x.n || !x.m || !y.n || !y.m || std::max(x.m, y.m) + 80 > 32000) return 0;
         dm = std::max(dm, std::llabs((long long)x.m - (long long)y.m));
     }
@@ -713,11 +734,12 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     // twin fill: half as many band jobs (each carries two pairs); the band
     // width follows the usual rule on the twins' strips (GX_BAND_WAVES forces it)
     int Wt = 0;
+    const std::vector<std::pair<int, int>> tw = twin_table(ph);
     {
         int wt_want = 15;
         if (const char* e = getenv("GX_BAND_WAVES")) wt_want = atoi(e);
         else wt_want = fill_band_waves(false, total_strips / 2, fill_grid_cap(ctx->device), lay, min_strips);
-        Wt = twin_width(ph, sc, is_local, track, lcs, lay, planes, d8, wt_want);
+        Wt = twin_width(ph, tw, sc, is_local, track, lcs, lay, planes, d8, wt_want);
         // auto: the twin fill once its own bands fill the grid (a twin band
         // is slower per step than a scalar one, so fewer bands than CUs
         // leave it latency-bound).  30k pairs, fill ms scalar / twin (codes,
@@ -727,10 +749,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         const char* e = getenv("GX_TWIN");
         if (Wt && !(e && !strcmp(e, "1"))) {
             long long twin_bands = 0;
-            for (size_t q = 0; q < ph.size(); q += 2) {
-                const PairHost& y = q + 1 < ph.size() ? ph[q + 1] : ph[q];
-                twin_bands += ceil_div(ceil_div((int)std::max(ph[q].n, y.n), SR), Wt);
-            }
+            for (const auto& t : tw)
+                twin_bands += ceil_div(ceil_div((int)std::max(ph[t.first].n, ph[t.second].n), SR), Wt);
             if (10 * twin_bands < 9LL * fill_grid_cap(ctx->device)) Wt = 0;
         }
     }
@@ -755,6 +775,14 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     size_t chars_bytes = 0, plane_elems = 0, code_elems = 0, feed_recs = 0, prog_elems = 0, skel_elems = 0;
     std::vector<size_t> c1o(P), c2o(P), po(P), co(P), fo(P), gofs(P), so(P);
     int bands = 0, strips = 0;
+    // twins: each pair's mate and its half (the first of a twin is the low half)
+    std::vector<int> mate(P, -1), half(P, 0);
+    if (twin)
+        for (const auto& t : tw) {
+            mate[t.first] = t.second; mate[t.second] = t.first;
+            half[t.first] = 0;
+            if (t.second != t.first) half[t.second] = 1;
+        }
     for (size_t p = 0; p < P; ++p) {
         const int n = (int)ph[p].n, m = (int)ph[p].m;
         PairDev& d = job.pd[p];
@@ -762,9 +790,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         // the shape the pair is laid out for: its own, or its twin's larger n and m
         int ns = n, ms = m;
         if (twin) {
-            const PairHost& x = ph[p & ~(size_t)1];
-            const PairHost& y = (p | 1) < P ? ph[p | 1] : x;
-            ns = (int)std::max(x.n, y.n); ms = (int)std::max(x.m, y.m);
+            const PairHost& y = ph[mate[p]];
+            ns = (int)std::max(ph[p].n, y.n); ms = (int)std::max(ph[p].m, y.m);
         }
         d.strips = ceil_div(ns, SR);
         d.bands = ceil_div(d.strips, Wf);
@@ -772,30 +799,37 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         const int T = lay ? ms + 1 : ms + kWave;
         d.t16 = ceil_div(T, 16);
         d.t4 = d.t16 * 4;
-        d.band_base = bands;
         d.strip_base = strips;
         d.feed_stride = (int)align_up((size_t)ms + 1 + 64, 16);
         d.skel_stride = (int)align_up((size_t)ms + 1, 64);
-        const bool second = twin && (p & 1);   // the twin's second pair: its bands, feed and skeleton are the first's
-        if (!second) bands += d.bands;
+        d.twin_half = half[p];
         strips += d.strips;
         c1o[p] = chars_bytes; chars_bytes += align_up(n, 64);
         c2o[p] = chars_bytes; chars_bytes += align_up(m, 64);
-        if (w16) {   // one code plane per twin, shared by its two pairs
-            po[p] = second ? po[p - 1] : plane_elems;
-            if (!second) plane_elems += (size_t)d.strips * d.t4 * kTwinGroupBytes;
-        } else {
-            po[p] = plane_elems; plane_elems += (size_t)d.strips * d.t4 * (lay ? kGroupInts1 : kGroupInts);
-        }
+        if (!w16) { po[p] = plane_elems; plane_elems += (size_t)d.strips * d.t4 * (lay ? kGroupInts1 : kGroupInts); }
         co[p] = code_elems; code_elems += (size_t)d.strips * d.t16 * SR;
-        so[p] = second ? so[p - 1] : skel_elems;
-        if (!second) skel_elems += (size_t)d.strips * d.skel_stride;
-        // twin feed records are 32 B (gx_fill_pk.hip RecW): two Rec slots per column
-        fo[p] = second ? fo[p - 1] : feed_recs;
-        if (!second) feed_recs += (size_t)std::max(d.bands - 1, 0) * d.feed_stride * (twin ? 2 : 1);
-        gofs[p] = second ? gofs[p - 1] : prog_elems;
-        if (!second) prog_elems += (size_t)std::max(d.bands - 1, 0) * kProgStride;
+        if (!twin) {
+            d.band_base = bands;
+            bands += d.bands;
+            so[p] = skel_elems; skel_elems += (size_t)d.strips * d.skel_stride;
+            fo[p] = feed_recs; feed_recs += (size_t)std::max(d.bands - 1, 0) * d.feed_stride;
+            gofs[p] = prog_elems; prog_elems += (size_t)std::max(d.bands - 1, 0) * kProgStride;
+        }
     }
+    // a twin's bands, skeleton (both halves' landing columns), hand-off rows
+    // (32-B records, gx_fill_pk.hip RecW: two Rec slots per column) and code
+    // plane (w16) are shared by its two pairs
+    if (twin)
+        for (const auto& t : tw) {
+            PairDev& d = job.pd[t.first];
+            const size_t a = t.first, b = t.second;
+            d.band_base = bands; job.pd[b].band_base = bands;
+            bands += d.bands;
+            so[a] = so[b] = skel_elems; skel_elems += (size_t)d.strips * d.skel_stride;
+            fo[a] = fo[b] = feed_recs; feed_recs += (size_t)std::max(d.bands - 1, 0) * d.feed_stride * 2;
+            gofs[a] = gofs[b] = prog_elems; prog_elems += (size_t)std::max(d.bands - 1, 0) * kProgStride;
+            if (w16) { po[a] = po[b] = plane_elems; plane_elems += (size_t)d.strips * d.t4 * kTwinGroupBytes; }
+        }
     job.total_bands = bands;
     job.total_strips = strips;
     int rc;
@@ -809,10 +843,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     if ((rc = pool_get(ctx, std::max<size_t>(feed_recs, 1) * sizeof(Rec), &job.feed))) return rc;
     if ((rc = pool_get(ctx, std::max<size_t>(prog_elems, 1) * sizeof(int), &job.progress))) return rc;
     if ((rc = pool_get(ctx, std::max(strips, 1) * sizeof(StripRes), &job.sres))) return rc;
-    // an odd twin launch ends with a phantom descriptor: the last pair again,
-    // its twin in the other half (same buffers, same bytes written twice)
-    const size_t Pd = P + (twin && (P & 1) ? 1 : 0);
-    if ((rc = pool_get(ctx, Pd * sizeof(PairRes), &job.pres))) return rc;
+    if ((rc = pool_get(ctx, P * sizeof(PairRes), &job.pres))) return rc;
     // band queue order, stored after the pair descriptors: band-major ("round"
     // order: band 0 of every pair, then band 1, ...; a band's predecessor in its
     // pair is always dequeued before it, so a waiting band is never waiting on
@@ -821,12 +852,13 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     order.reserve(2 * (size_t)bands);
     {
         const char* bo = getenv("GX_BAND_ORDER");
-        if (twin) {   // band-major over the twins: entries (twin q, band)
+        if (twin) {   // band-major over the twins: entries (twin q, band), then the twin table
             int maxb = 0;
-            for (size_t p = 0; p < P; p += 2) maxb = std::max(maxb, job.pd[p].bands);
+            for (const auto& t : tw) maxb = std::max(maxb, job.pd[t.first].bands);
             for (int lb = 0; lb < maxb; ++lb)
-                for (size_t p = 0; p < P; p += 2)
-                    if (lb < job.pd[p].bands) { order.push_back((int)(p / 2)); order.push_back(lb); }
+                for (size_t q = 0; q < tw.size(); ++q)
+                    if (lb < job.pd[tw[q].first].bands) { order.push_back((int)q); order.push_back(lb); }
+            for (const auto& t : tw) { order.push_back(t.first); order.push_back(t.second); }
         } else if (bo && !strcmp(bo, "pair")) {
             for (size_t p = 0; p < P; ++p)
                 for (int lb = 0; lb < job.pd[p].bands; ++lb) { order.push_back((int)p); order.push_back(lb); }
@@ -839,7 +871,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         }
     }
     const size_t ord_bytes = align_up(order.size() * sizeof(int), 16);   // keeps the PairRes staging 16-B aligned
-    if ((rc = pool_get(ctx, Pd * sizeof(PairDev) + ord_bytes, &job.pairs))) return rc;
+    if ((rc = pool_get(ctx, P * sizeof(PairDev) + ord_bytes, &job.pairs))) return rc;
     if ((rc = pool_get(ctx, 64, &job.counter))) return rc;
     // -- chars upload
     const uint8_t* cbase = chars_dev;
@@ -876,16 +908,15 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         for (size_t p = 0; p < P; ++p) job.pd[p].trace = (StripTrace*)trace.p + job.pd[p].strip_base;
     }
     // descriptors in (and results out) through pinned staging, laid out [PairDev x P | PairRes x P | status]
-    const size_t pin_bytes = Pd * sizeof(PairDev) + P * sizeof(PairRes) + ord_bytes + 2 * sizeof(int);
+    const size_t pin_bytes = P * (sizeof(PairDev) + sizeof(PairRes)) + ord_bytes + 2 * sizeof(int);
     char* pin = (char*)(slot >= 0 ? pinned_grow(ctx->slots[slot].fpin, pin_bytes) : io_pinned(ctx, pin_bytes));
     if (!pin) return fail(GX_ENOMEM, "pinned staging buffer");
     memcpy(pin, job.pd.data(), P * sizeof(PairDev));
-    if (Pd > P) memcpy(pin + P * sizeof(PairDev), &job.pd[P - 1], sizeof(PairDev));
-    if (!order.empty()) memcpy(pin + Pd * sizeof(PairDev), order.data(), order.size() * sizeof(int));
-    HIPCHK(hipMemcpyAsync(job.pairs.p, pin, Pd * sizeof(PairDev) + ord_bytes, hipMemcpyHostToDevice, ctx->stream));
+    if (!order.empty()) memcpy(pin + P * sizeof(PairDev), order.data(), order.size() * sizeof(int));
+    HIPCHK(hipMemcpyAsync(job.pairs.p, pin, P * sizeof(PairDev) + ord_bytes, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemsetAsync(job.progress.p, 0, std::max<size_t>(prog_elems, 1) * sizeof(int), ctx->stream));
     HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, ctx->stream));
-    HIPCHK(hipMemsetAsync(job.pres.p, 0, Pd * sizeof(PairRes), ctx->stream));
+    HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), ctx->stream));
     // twin workgroups: as many per CU as fit 16 waves (the twin kernels hold
     // up to 128 VGPRs: 4 waves per SIMD)
     const int per_cu = (twin && !getenv("GX_FILL_GRID")) ? std::max(1, 16 / (Wf + 1)) : 1;
@@ -897,7 +928,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].fb : ctx->ev0, eve = slot >= 0 ? ctx->slots[slot].fe : ctx->ev1;
     HIPCHK(hipEventRecord(evb, ctx->stream));
     if (bands > 0 && twin)
-        HIPCHK(launch_fill_pk(Wf, (planes ? (w16 ? 2 : 1) : 0) + (twin_tbl ? 4 : 0), (const PairDev*)job.pairs.p, (int)(Pd / 2), bands, (int*)job.counter.p,
+        HIPCHK(launch_fill_pk(Wf, (planes ? (w16 ? 2 : 1) : 0) + (twin_tbl ? 4 : 0), (const PairDev*)job.pairs.p, (int)P, (int)tw.size(), bands, (int*)job.counter.p,
                               (PairRes*)job.pres.p, scl, grid, ctx->stream));
     else if (bands > 0)
         HIPCHK(launch_fill(W, lay, is_local != 0, planes ? (d8 ? 2 : 1) : 0, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
@@ -914,8 +945,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                                (PairRes*)job.pres.p, ctx->stream));
     job.res.assign(P, PairRes{});
     int status[2] = {0, 0};
-    PairRes* pin_res = (PairRes*)(pin + Pd * sizeof(PairDev) + ord_bytes);
-    int* pin_status = (int*)(pin + Pd * sizeof(PairDev) + P * sizeof(PairRes) + ord_bytes);
+    PairRes* pin_res = (PairRes*)(pin + P * sizeof(PairDev) + ord_bytes);
+    int* pin_status = (int*)(pin + P * (sizeof(PairDev) + sizeof(PairRes)) + ord_bytes);
     HIPCHK(hipMemcpyAsync(pin_res, job.pres.p, P * sizeof(PairRes), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipMemcpyAsync(pin_status, job.counter.p, sizeof status, hipMemcpyDeviceToHost, ctx->stream));
     job.pin_res = pin_res;
@@ -1238,7 +1269,7 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
         t.seg = (int*)seg.p + 4 * so[p];
         t.recs = (uint32_t*)recs.p + so[p] * SR;
         t.srows = SR;
-        t.skel_half = job.twin ? (int)(p & 1) : -1;
+        t.skel_half = job.twin ? job.pd[p].twin_half : -1;
         t.end_ij = (int*)cnt.p + 4 * p;
     }
     TbDev* pin_jobs = (TbDev*)(slot >= 0 ? pinned_grow(ctx->slots[slot].tjpin, P * sizeof(TbDev))

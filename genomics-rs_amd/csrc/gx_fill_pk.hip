@@ -662,12 +662,14 @@ __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, c
     }
 }
 
-// Twin fill: pairs 2q and 2q+1 of the launch share every band; queue entry b
-// of the order table = (twin q, band lb).
+// Twin fill: the two pairs of twin q share every band.  After the npairs
+// descriptors: the band queue (total_bands entries (twin q, band lb)), then
+// the twin table (ntwins entries (pair a, pair b); b == a twins a pair with
+// itself, both halves writing the same bytes).
 template <int W, int PLANES>
 __global__ __launch_bounds__((W + 1) * kWave, (W + 1 + 3) / 4) void fill_pk_kernel(
-    const PairDev* __restrict__ pairs, const int ntwins, const int total_bands, int* band_counter, PairRes* pres,
-    const Scores32 sc) {
+    const PairDev* __restrict__ pairs, const int npairs, const int ntwins, const int total_bands, int* band_counter,
+    PairRes* pres, const Scores32 sc) {
     __shared__ Rec rings[W + 1][kRing];
     __shared__ uint32_t push_scratch[W][kPushScratch];
     __shared__ int bases[W + 1][2 * (1 + kBaseSlots)];
@@ -686,10 +688,13 @@ __global__ __launch_bounds__((W + 1) * kWave, (W + 1 + 3) / 4) void fill_pk_kern
         __syncthreads();
         const int b = __builtin_amdgcn_readfirstlane(band_sh);
         if (b >= total_bands) return;
-        const int2 ob = reinterpret_cast<const int2*>(pairs + 2 * ntwins)[b];
+        const int2* queue = reinterpret_cast<const int2*>(pairs + npairs);
+        const int2 ob = queue[b];
         const int q = __builtin_amdgcn_readfirstlane(ob.x);
-        const PairDev& P0 = pairs[2 * q];
-        const PairDev& P1 = pairs[2 * q + 1];
+        const int2 tw = queue[total_bands + q];
+        const int pa = __builtin_amdgcn_readfirstlane(tw.x), pb = __builtin_amdgcn_readfirstlane(tw.y);
+        const PairDev& P0 = pairs[pa];
+        const PairDev& P1 = pairs[pb];
         const int lb = __builtin_amdgcn_readfirstlane(ob.y);
         const int s0 = lb * W;
         if (wave < W) {
@@ -700,7 +705,7 @@ __global__ __launch_bounds__((W + 1) * kWave, (W + 1 + 3) / 4) void fill_pk_kern
                 compute_wave_pk<PLANES>(P0, P1, s, lane, sc, k, rings[wave], rings[wave + 1], (lds_int*)&wcnt[wave],
                                         (lds_int*)&rcnt[wave], (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1],
                                         (lds_int*)bases[wave], (lds_int*)bases[wave + 1], has_consumer,
-                                        pres + 2 * q, pres + 2 * q + 1, band_counter + 1,
+                                        pres + pa, pres + pb, band_counter + 1,
                                         lds_addr(push_scratch[wave]));
             }
         } else {
@@ -713,11 +718,11 @@ __global__ __launch_bounds__((W + 1) * kWave, (W + 1 + 3) / 4) void fill_pk_kern
 }
 
 template <int W0, int... Ws>
-static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int ntwins, int total_bands, int* d_counter,
-                              PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
+static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int npairs, int ntwins, int total_bands,
+                              int* d_counter, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
     if (W == W0) {
 #define GX_PK(PL) hipLaunchKernelGGL((fill_pk_kernel<W0, PL>), dim3(grid), dim3((W0 + 1) * kWave), 0, st, d_pairs, \
-                                     ntwins, total_bands, d_counter, d_pres, sc)
+                                     npairs, ntwins, total_bands, d_counter, d_pres, sc)
         switch (planes) {
             case 0: GX_PK(0); break;
             case 1: GX_PK(1); break;
@@ -729,17 +734,18 @@ static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int ntw
 #undef GX_PK
         return hipGetLastError();
     }
-    if constexpr (sizeof...(Ws) > 0) return launch_pk_w<Ws...>(W, planes, d_pairs, ntwins, total_bands, d_counter,
-                                                               d_pres, sc, grid, st);
+    if constexpr (sizeof...(Ws) > 0) return launch_pk_w<Ws...>(W, planes, d_pairs, npairs, ntwins, total_bands,
+                                                               d_counter, d_pres, sc, grid, st);
     return hipErrorInvalidValue;
 }
 
 // Twin launch: W from {3, 4, 7, 8, 15}; planes: 0 none, 1 compact bytes per
 // pair (3 B/cell), 2 twin codes (2 B/cell); + 4: small-alphabet score tables
 // (with none or twin codes: the batch launches).
-hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int ntwins, int total_bands, int* d_counter,
-                          PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
-    return launch_pk_w<3, 4, 7, 8, 15>(W, planes, d_pairs, ntwins, total_bands, d_counter, d_pres, sc, grid, st);
+hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int npairs, int ntwins, int total_bands,
+                          int* d_counter, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
+    return launch_pk_w<3, 4, 7, 8, 15>(W, planes, d_pairs, npairs, ntwins, total_bands, d_counter, d_pres, sc, grid,
+                                       st);
 }
 
 }  // namespace gx

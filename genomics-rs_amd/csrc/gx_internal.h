@@ -127,6 +127,7 @@ struct PairDev {
     int* skel;           // [strips][skel_stride] landing column E of each strip's bottom row
     int feed_stride;
     int skel_stride;
+    int twin_half;       // twin fill: this pair's 16-bit half (0 low, 1 high) in its twin's shared buffers
 };
 
 struct TbDev {           // per-pair traceback job

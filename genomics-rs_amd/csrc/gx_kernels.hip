@@ -1516,7 +1516,7 @@ __global__ __launch_bounds__(64) void plane_sums_kernel(const PairDev* __restric
     const size_t gints = lay ? kGroupInts1 : kGroupInts;
     const size_t row0 = (size_t)s * d.t4 * gints + (lay ? (size_t)lane * 4 : (size_t)hh * kWave * 4 + (size_t)lane * 4);
     if (mode == 3) {   // twin plane codes (gx_fill_pk.hip w16_code): this pair's half of each dword
-        const int half = blockIdx.y & 1;   // pairs 2q, 2q+1 of the launch share twin q's code plane
+        const int half = d.twin_half;      // the twin's two pairs share its code plane
         const uint8_t* base = (const uint8_t*)d.pI + (size_t)s * d.t4 * kTwinGroupBytes +
                               (size_t)hh * (kTwinGroupBytes / 2) + (size_t)lane * 16;
         int I = max(h + i * g, floor_) + h;             // H(i, 0) + h, as the fill seeds it

@@ -214,3 +214,25 @@ def test_twin_column_limit(gx, ctx, oracle, monkeypatch, m):
         o = oracle.align_lean(a, b, CONFIG_SCORES)
         assert [int(x) for x in sums[0, p]] == o.extra["plane_sums"], (m, p)
         assert res[p].score == o.score and _steps_list(st.steps(p)) == o.alignment(), (m, p)
+
+
+def test_twin_pairs_by_shape(gx, ctx, oracle, monkeypatch):
+    """Twins are formed by shape, not by position: a batch alternating very
+    different lengths (adjacent pairs 60x apart in columns, beyond the
+    admission bound's column margin) still takes the twin fill, each twin
+    holding two pairs of near shapes; every result against the oracle."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    rng = random.Random(77)
+    shapes = []
+    for k in range(5):
+        shapes += [(150 + 7 * k, 6000 + 13 * k), (140 + 5 * k, 100 + 3 * k)]
+    pairs = [(bytes(rng.choice(b"ACGT") for _ in range(n)), bytes(rng.choice(b"ACGT") for _ in range(m)))
+             for n, m in shapes]
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=1, plane_sums=True)
+    assert ctx.fill_info()["twin"] == 1
+    sums = st.plane_sums()
+    for p, (a, b) in enumerate(pairs):
+        o = oracle.align_lean(a, b, CONFIG_SCORES)
+        assert [int(x) for x in sums[0, p]] == o.extra["plane_sums"], p
+        assert res[p].score == o.score and _steps_list(st.steps(p)) == o.alignment(), p
