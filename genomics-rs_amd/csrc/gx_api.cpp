@@ -752,6 +752,11 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
             for (const auto& t : tw)
                 twin_bands += ceil_div(ceil_div((int)std::max(ph[t.first].n, ph[t.second].n), SR), Wt);
             if (10 * twin_bands < 9LL * fill_grid_cap(ctx->device)) Wt = 0;
+            // a pair twinned with itself does a twin band's work for one pair:
+            // batches of mostly unmatched shapes stay on the scalar fill
+            size_t selfs = 0;
+            for (const auto& t : tw) selfs += t.first == t.second;
+            if (4 * selfs > tw.size() + 3) Wt = 0;
         }
     }
     const bool twin = Wt > 0;
