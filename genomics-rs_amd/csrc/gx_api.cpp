@@ -608,7 +608,7 @@ struct FillJob {
     bool planes_on = false, lcs_on = false, track_on = false;
     bool d8 = false;                    // compact byte planes (d8_planes_ok)
     bool shift = false;                 // values kept as V - (i + j) g (Scores32.shift)
-    bool twin = false;                  // the twin fill (gx_fill_pk.hip): pairs 2q, 2q+1 share every band
+    bool twin = false;                  // the twin fill (gx_fill_pk.hip): twin_table's pairs share every band
     bool w16 = false;                   // twin plane codes, 2 B per cell (w16_ok; batches only)
     bool table = false;                 // an alignment table (exportable planes: never the twin codes)
     int g = 0;
@@ -655,18 +655,40 @@ static hipError_t enqueue_plane_sums(gx_context* ctx, const FillJob& job, const 
 // state stays at its last column (its values beyond lie in the row above's
 // range, but the bound takes the column difference anyway); an odd last pair
 // is twinned with itself.
-static std::vector<std::pair<int, int>> twin_table(const std::vector<PairHost>& ph) {
+// The admission bound of a W-strip twin band whose twins' column counts
+// differ by up to dm: the largest |value - base| any state of the band can
+// reach (see the comment above twin_table).
+constexpr long long kTwinBoundLimit = 30000;   // < 2^15 with room for the derived offsets
+static long long twin_bound(const Scores32& sc, int W, long long dm) {
+    const long long g = sc.g, a = (long long)sc.h + sc.g;
+    const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
+    const long long U = std::max(0LL, smax - a);
+    const long long D = std::max(std::llabs(a - g), std::llabs(U - g));
+    return D * (192LL * W + 16 + dm) + 2 * (std::llabs(a) + std::llabs(smax) + std::llabs(smin)) + 64;
+}
+// Largest column gap between twins that keeps band width W admissible under
+// twin_width's bound (capped at 1,024): twin_table pairs no wider gaps, so one
+// ill-matched twin never narrows the band width of a whole batch.
+static long long twin_gap_cap(const Scores32& sc, int W) {
+    const long long g = sc.g, a = (long long)sc.h + sc.g;
+    const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
+    const long long U = std::max(0LL, smax - a);
+    const long long D = std::max({std::llabs(a - g), std::llabs(U - g), 1LL});
+    const long long rest = 30000 - 1 - 2 * (std::llabs(a) + std::llabs(smax) + std::llabs(smin)) - 64;
+    return std::max(0LL, std::min(1024LL, rest / D - 192LL * W - 16));
+}
+static std::vector<std::pair<int, int>> twin_table(const std::vector<PairHost>& ph, long long gap_cap = 1024) {
     std::vector<int> idx(ph.size());
     for (size_t p = 0; p < ph.size(); ++p) idx[p] = (int)p;
     std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) {
         return ph[a].m != ph[b].m ? ph[a].m > ph[b].m : ph[a].n > ph[b].n;
     });
     // neighbours in that order, unless their column counts lie more than
-    // 1,024 apart (the admission bound's column margin): such a pair is
+    // gap_cap apart (the admission bound's column margin): such a pair is
     // twinned with itself
     std::vector<std::pair<int, int>> tw;
     for (size_t k = 0; k < idx.size();) {
-        if (k + 1 < idx.size() && ph[idx[k]].m - ph[idx[k + 1]].m <= 1024) {
+        if (k + 1 < idx.size() && (long long)(ph[idx[k]].m - ph[idx[k + 1]].m) <= gap_cap) {
             tw.emplace_back(idx[k], idx[k + 1]);
             k += 2;
         } else {
@@ -688,14 +710,9 @@ static int twin_width(const std::vector<PairHost>& ph, const std::vector<std::pa
         if (!x.n || !x.m || !y.n || !y.m || std::max(x.m, y.m) + 80 > 32000) return 0;
         dm = std::max(dm, std::llabs((long long)x.m - (long long)y.m));
     }
-    const long long g = sc.g, a = (long long)sc.h + sc.g;
-    const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
-    const long long U = std::max(0LL, smax - a);
-    const long long D = std::max(std::llabs(a - g), std::llabs(U - g));
     for (int W : {15, 8, 7, 4, 3}) {
         if (W > W_want && W != 3) continue;
-        const long long bound = D * (192LL * W + 16 + dm) + 2 * (std::llabs(a) + std::llabs(smax) + std::llabs(smin)) + 64;
-        if (bound < 30000) return W;
+        if (twin_bound(sc, W, dm) < kTwinBoundLimit) return W;
     }
     return 0;
 }
@@ -734,11 +751,11 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     // twin fill: half as many band jobs (each carries two pairs); the band
     // width follows the usual rule on the twins' strips (GX_BAND_WAVES forces it)
     int Wt = 0;
-    const std::vector<std::pair<int, int>> tw = twin_table(ph);
+    int wt_want = 15;
+    if (const char* e = getenv("GX_BAND_WAVES")) wt_want = atoi(e);
+    else wt_want = fill_band_waves(false, total_strips / 2, fill_grid_cap(ctx->device), lay, min_strips);
+    const std::vector<std::pair<int, int>> tw = twin_table(ph, twin_gap_cap(sc, wt_want >= 15 ? 15 : wt_want >= 8 ? 8 : wt_want >= 7 ? 7 : wt_want >= 4 ? 4 : 3));
     {
-        int wt_want = 15;
-        if (const char* e = getenv("GX_BAND_WAVES")) wt_want = atoi(e);
-        else wt_want = fill_band_waves(false, total_strips / 2, fill_grid_cap(ctx->device), lay, min_strips);
         Wt = twin_width(ph, tw, sc, is_local, track, lcs, lay, planes, d8, wt_want);
         // auto: the twin fill once its own bands fill the grid (a twin band
         // is slower per step than a scalar one, so fewer bands than CUs
@@ -1798,8 +1815,8 @@ static double chunk_budget(gx_context* ctx) {
 // larger than the budget runs alone), balanced: the fewest chunks the budget
 // allows, each near total / chunks (1024 x 16k: 4 x 256 pairs, not 3 x 330 +
 // 34, whose short last chunk would lose the twin fill and leave CUs idle).
-// A chunk holding more than one pair ends after an even count when it can, so
-// that pairs keep their twin (run_fill pairs 2q with 2q+1).
+// (Twins are formed inside each chunk by twin_table, by shape, so a chunk's
+// pair count need not be even.)
 static std::vector<std::pair<size_t, size_t>> plan_chunks_within(const std::vector<PairHost>& ph, double plane_bpc,
                                                                  double budget) {
     std::vector<std::pair<size_t, size_t>> out;
@@ -1809,11 +1826,9 @@ static std::vector<std::pair<size_t, size_t>> plan_chunks_within(const std::vect
     for (size_t p = 0; p < ph.size(); ++p) {
         const double x = bytes(p);
         if (p > b && acc + x > budget) {
-            size_t e = p;
-            if ((e - b) % 2 && e - b > 2) --e;   // even chunk: pair p-1 moves to the next chunk
-            out.emplace_back(b, e);
-            b = e;
-            acc = e < p ? bytes(e) : 0.0;
+            out.emplace_back(b, p);
+            b = p;
+            acc = 0.0;
         }
         acc += x;
     }
@@ -2399,6 +2414,16 @@ extern "C" int gx_fill_info(const gx_context* ctx, int* layout, int* band_waves,
     if (band_waves) *band_waves = ctx->last_W;
     if (plane_bytes_per_cell) *plane_bytes_per_cell = ctx->last_pbytes;
     return GX_OK;
+}
+
+extern "C" int gx_twin_admission(const gx_scores* scores, int band_waves, int64_t col_gap, int64_t* bound) {
+    if (!scores || band_waves < 1 || col_gap < 0) return -1;
+    HostScores hs;
+    Scores32 sc;
+    if (check_scores(scores, 1, 1, &hs, &sc, 0, nullptr) != GX_OK) return -1;
+    const long long b = twin_bound(sc, band_waves, col_gap);
+    if (bound) *bound = b;
+    return (sc.g <= 0 && sc.h <= 0 && b < kTwinBoundLimit) ? 1 : 0;
 }
 
 extern "C" int gx_plane_bytes_per_cell(const gx_scores* scores, int is_local) {

@@ -201,6 +201,40 @@ __device__ __forceinline__ void lds_store_lane0(lds_int* p, int v) {
         : "memory");
 }
 
+// in-place inclusive prefix max over the 64 lanes (lanes without a DPP source
+// keep their value: old = INT_MIN is the identity of max)
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int dpp_max(int x) {
+    return max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, CTRL, RM, BM, false));
+}
+__device__ __forceinline__ int scan_max64(int x) {
+    x = dpp_max<0x111, 0xF, 0xF>(x);   // row_shr:1
+    x = dpp_max<0x112, 0xF, 0xF>(x);   // row_shr:2
+    x = dpp_max<0x114, 0xF, 0xF>(x);   // row_shr:4
+    x = dpp_max<0x118, 0xF, 0xF>(x);   // row_shr:8
+    x = dpp_max<0x142, 0xA, 0xF>(x);   // row_bcast:15 -> rows 1, 3
+    x = dpp_max<0x143, 0xC, 0xF>(x);   // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
+// Interleaved scans: independent chains side by side, so each DPP step's
+// latency (~14 cycles on a dependent chain, tools/dpp_probe.hip) is covered
+// by the other chain's step instead of wait states.
+template <int CTRL, int RM, int BM, int N>
+__device__ __forceinline__ void dpp_max_n(int (&x)[N]) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) x[q] = dpp_max<CTRL, RM, BM>(x[q]);
+}
+template <int N>
+__device__ __forceinline__ void scan_max64_n(int (&x)[N]) {
+    dpp_max_n<0x111, 0xF, 0xF>(x);
+    dpp_max_n<0x112, 0xF, 0xF>(x);
+    dpp_max_n<0x114, 0xF, 0xF>(x);
+    dpp_max_n<0x118, 0xF, 0xF>(x);
+    dpp_max_n<0x142, 0xA, 0xF>(x);
+    dpp_max_n<0x143, 0xC, 0xF>(x);
+}
+
 // Small-alphabet scoring (TBL): the host maps the job's <= 4 distinct
 // processed bytes to codes 0..3 (Scores32.sym); a row's table holds
 // score(c1, sym[k]) as signed byte k.

@@ -106,7 +106,7 @@ struct __attribute__((aligned(16))) StripTrace {
     long long t_q[kTraceQ];   // when the sweep passed k/8 of its steps (k = 1..7)
 };
 
-struct PairDev {
+struct __attribute__((aligned(16))) PairDev {   // 16-B multiple: the pinned staging puts PairRes (aligned 16) after P of these
     const uint8_t* c1;   // processed row chars, n   (is_match row operand)
     const uint8_t* c2;   // processed col chars, m
     int n, m;
@@ -129,6 +129,7 @@ struct PairDev {
     int skel_stride;
     int twin_half;       // twin fill: this pair's 16-bit half (0 low, 1 high) in its twin's shared buffers
 };
+static_assert(sizeof(PairDev) % 16 == 0, "PairDev staging keeps the PairRes that follow it 16-B aligned");
 
 struct TbDev {           // per-pair traceback job
     const uint32_t* codes;

@@ -74,7 +74,8 @@ EXPORTED = ["gx_last_error", "gx_version", "gx_context_create", "gx_context_dest
             "gx_alignment_table", "gx_table_info", "gx_table_export", "gx_table_export_plane", "gx_table_export_rows",
             "gx_table_plane_sums", "gx_retrace", "gx_table_free", "gx_align", "gx_align_batch", "gx_stage_pairs",
             "gx_run_staged", "gx_run_staged_steps", "gx_staged_plane_sums", "gx_staged_steps",
-            "gx_fill_info", "gx_batch_chunks", "gx_fill_twin", "gx_plane_bytes_per_cell", "gx_fasta_load",
+            "gx_fill_info", "gx_batch_chunks", "gx_fill_twin", "gx_plane_bytes_per_cell", "gx_twin_admission",
+            "gx_fasta_load",
             "gx_config_load", "gx_format_alignment", "gx_format_table"]
 
 _lib = None
@@ -120,6 +121,8 @@ def lib():
     L.gx_batch_chunks.argtypes = [vp]
     L.gx_fill_twin.argtypes = [vp]
     L.gx_plane_bytes_per_cell.argtypes = [ctypes.POINTER(CScores), ctypes.c_int]
+    L.gx_twin_admission.argtypes = [ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int64,
+                                    ctypes.POINTER(ctypes.c_int64)]
     L.gx_fasta_load.argtypes = [ctypes.c_char_p, vp, sz, vp, vp, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.gx_config_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(CScores)]
     L.gx_format_alignment.argtypes = [vp, sz, vp, sz, vp, sz, ctypes.POINTER(CResult), vp, sz, ctypes.POINTER(sz)]
@@ -284,6 +287,17 @@ def plane_bytes_per_cell(scores: "Scores", is_local: bool) -> int:
     if r < 0:
         raise GxError(3, "invalid scores")
     return r
+
+
+def twin_admission(scores: "Scores", band_waves: int, col_gap: int = 0) -> Tuple[bool, int]:
+    """The twin fill's int16 admission rule (gx_twin_admission): (admitted,
+    bound), bound = the largest |value - base| a band of `band_waves` strips
+    can reach when a twin's pairs differ by up to col_gap columns."""
+    b = ctypes.c_int64(0)
+    r = lib().gx_twin_admission(ctypes.byref(scores.c()), int(band_waves), int(col_gap), ctypes.byref(b))
+    if r < 0:
+        raise GxError(3, "invalid scores")
+    return bool(r), int(b.value)
 
 
 class Context:

@@ -221,6 +221,14 @@ int gx_fill_twin(const gx_context* ctx);
  * launch's own figure). */
 int gx_plane_bytes_per_cell(const gx_scores* scores, int is_local);
 
+/* The twin fill's int16 admission rule: *bound receives the
+ * largest |value - base| a band of `band_waves` strips can reach with these
+ * scores when a twin's two pairs differ by up to col_gap columns; returns 1
+ * when the twin fill admits the band (bound < 30,000 < 2^15), 0 when it does
+ * not, -1 on invalid scores.  Diagnostic (tests/test_twin_bound.py checks the
+ * rule against brute-force spreads).  No reference counterpart. */
+int gx_twin_admission(const gx_scores* scores, int band_waves, int64_t col_gap, int64_t* bound);
+
 /* ---- sequence.rs / config.rs mirrors ----------------------------------- */
 /* from_fasta (sequence.rs:45-95) on a file: records are appended to the
  * caller's buffers.  Returns GX_OK and sets *n_records; names/sequences are

@@ -237,8 +237,9 @@ def test_config5_1k_chunked(gx, ctx, monkeypatch):
 
 
 def test_chunks_keep_twins(gx, ctx, monkeypatch):
-    """A budget of 5.5 pairs: chunks end after an even count (4 pairs), so
-    the equal-shape pairs keep the twin fill in every chunk."""
+    """A budget of 5.5 pairs: 5-pair chunks; twin_table forms the twins by
+    shape inside each chunk (one pair twinned with itself per odd chunk), so
+    every chunk keeps the twin fill."""
     pdb = (1024 + 128) * (1024 + 64) * 3.25 + 64 * (1024 + 64) * (1024 // 64 + 2) / 8 + 65536   # pair_device_bytes
     monkeypatch.setenv("GX_CHUNK_BYTES", str(5.5 * pdb))
     monkeypatch.setenv("GX_LAYOUT", "0")
@@ -246,7 +247,7 @@ def test_chunks_keep_twins(gx, ctx, monkeypatch):
     cases = _synth(1024)[:40]
     pairs = [_synth_pair(c["k"], 1024) for c in cases]
     info = _staged_check(gx, ctx, pairs, cases, steps=1)
-    assert info["chunks"] == 10 and info["twin"] == 1, info
+    assert info["chunks"] == 8 and info["twin"] == 1, info
 
 
 @pytest.mark.parametrize("twin", ["1", "0"])

@@ -236,3 +236,97 @@ def test_twin_pairs_by_shape(gx, ctx, oracle, monkeypatch):
         o = oracle.align_lean(a, b, CONFIG_SCORES)
         assert [int(x) for x in sums[0, p]] == o.extra["plane_sums"], p
         assert res[p].score == o.score and _steps_list(st.steps(p)) == o.alignment(), p
+
+
+# ---- the int16 admission bound where it binds (gx_api.cpp twin_width) ------
+# Inputs that push the twin fill's values hardest (tests/test_twin_bound.py
+# measures their spreads against the rule on the CPU) at the widest scores
+# each band width admits; every plane cell of a table filled by the twin
+# kernel (GX_TABLE_TWIN), and the alignment, against the oracle.
+from test_twin_bound import _families  # noqa: E402
+
+BOUND_SCORES = [(CONFIG_SCORES, 15), ((1, -1, -1, -7), 15), ((1, -1, -1, -16), 8), ((2, -2, -1, -34), 4)]
+
+
+@pytest.mark.parametrize("scores,W", BOUND_SCORES)
+@pytest.mark.parametrize("family", ["all_mismatch", "all_match", "gap_rows", "gap_cols", "repeat"])
+def test_twin_bound_worst_inputs_table(gx, ctx, oracle, monkeypatch, scores, W, family):
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    monkeypatch.setenv("GX_TABLE_TWIN", "1")
+    monkeypatch.setenv("GX_BAND_WAVES", str(W))
+    monkeypatch.setenv("GX_NO_TABLE_PRINT", "1")
+    n, m = 128 * W * 2 + 300, 1400   # two full bands and a partial third
+    a, b = _families(n, m)[family]
+    cont = gx.SequenceContainer([gx.Sequence("a", a.decode()), gx.Sequence("b", b.decode())])
+    t, _ = gx.alignment_table(cont, gx.Scores(*scores), False, False, ctx=ctx, max_cell=False)
+    info = ctx.fill_info()
+    assert info["twin"] == 1 and info["band_waves"] == W, info
+    o = oracle.align(a, b, scores, want_planes=True)
+    for k in range(3):
+        assert np.array_equal(t.plane(k), o.planes[k]), (family, scores, k)
+    al = gx.retrace(cont, t, False)
+    assert _steps_list(al._steps) == o.alignment() and al.score == o.score
+
+
+@pytest.mark.parametrize("scores,W", BOUND_SCORES)
+def test_twin_bound_worst_inputs_batch(gx, ctx, oracle, monkeypatch, scores, W):
+    """The same inputs as a staged twin batch (twin plane codes where w16_ok
+    holds, else bytes), plus twins 1,024 columns apart where W <= 8 admits
+    them: plane checksums of every pass, scores and alignments."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    monkeypatch.setenv("GX_BAND_WAVES", str(W))
+    n, m = 128 * W * 2 + 300, 1400
+    pairs = list(_families(n, m).values())
+    if W <= 8:
+        rng = random.Random(W)
+        pairs += [(bytes(rng.choice(b"ACGT") for _ in range(n)), bytes(rng.choice(b"ACGT") for _ in range(mm)))
+                  for mm in (3000, 1976)]
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, _ = st.run(gx.Scores(*scores), False, keep_planes=True, steps=2, plane_sums=True)
+    info = ctx.fill_info()
+    assert info["twin"] == 1 and info["band_waves"] == W, info
+    sums = st.plane_sums()
+    for p, (a, b) in enumerate(pairs):
+        o = oracle.align_lean(a, b, scores)
+        for k in range(2):
+            assert [int(x) for x in sums[k, p]] == o.extra["plane_sums"], (scores, p, k)
+        assert res[p].score == o.score and _steps_list(st.steps(p)) == o.alignment(), (scores, p)
+
+
+def test_twin_bound_column_limit_worst(gx, ctx, oracle, monkeypatch):
+    """m = 31,920 (the int16 landing-column limit) with all-mismatch and
+    all-match rows: plane checksums, scores and alignments."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    m = 31920
+    pairs = [(b"A" * 200, b"C" * m), (b"A" * 150, b"A" * (m - 3)), (b"AC" * 130, b"CA" * (m // 2))]
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=1, plane_sums=True)
+    assert ctx.fill_info()["twin"] == 1
+    sums = st.plane_sums()
+    for p, (a, b) in enumerate(pairs):
+        o = oracle.align_lean(a, b, CONFIG_SCORES)
+        assert [int(x) for x in sums[0, p]] == o.extra["plane_sums"], p
+        assert res[p].score == o.score and _steps_list(st.steps(p)) == o.alignment(), p
+
+
+@pytest.mark.parametrize("kind", ["self_twins", "deep_equal"])
+def test_twin_auto_selection(gx, ctx, oracle, monkeypatch, kind):
+    """GX_TWIN unset: the automatic rules of run_fill.  A batch of mostly
+    unmatched shapes (column counts more than the gap cap apart, so every pair
+    would be twinned with itself) stays on the scalar fill; a deep batch of
+    equal shapes (>= 0.9 x CUs twin bands) takes the twin fill.  Results
+    against the oracle either way."""
+    monkeypatch.delenv("GX_TWIN", raising=False)
+    rng = random.Random(99)
+    if kind == "self_twins":
+        shapes = [(300 + 13 * k, 200 + 1500 * k) for k in range(8)]
+    else:
+        shapes = [(1500, 1500)] * 128
+    pairs = [(bytes(rng.choice(b"ACGT") for _ in range(n)), bytes(rng.choice(b"ACGT") for _ in range(m)))
+             for n, m in shapes]
+    out = gx.align_batch(pairs, gx.Scores(*CONFIG_SCORES), False, ctx=ctx, max_cell=False)
+    assert ctx.fill_info()["twin"] == (0 if kind == "self_twins" else 1), ctx.fill_info()
+    for (a, b), (steps, r) in zip(pairs, out):
+        o = oracle.align_lean(a, b, CONFIG_SCORES)
+        assert r.score == o.score and r.n_steps == len(o.choices)
+        assert _steps_list(steps) == o.alignment()
