@@ -32,13 +32,16 @@ hipError_t launch_fill(int W, int lay, bool local, int planes, bool track, bool 
                        hipStream_t st);
 hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d_sres, PairRes* d_pres,
                            hipStream_t st);
-hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipStream_t st);
+hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, bool w16, hipStream_t st);
 hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, int gshift, int row0,
                          int rows, hipStream_t st);
 hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, int n, int m, int t4, int h, int g,
                             int floor_, int gshift, int row0, int rows, hipStream_t st);
 hipError_t launch_plane_sums(const PairDev* d_pairs, int npairs, int max_strips, int lay, int mode, int h, int g,
                              int floor_, int gshift, unsigned long long* out, hipStream_t st);
+hipError_t launch_fill_cs2(int W, bool local, bool planes, bool tbl, const PairDev* d_pairs, int npairs,
+                           int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
+                           hipStream_t st);
 hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int npairs, int ntwins, int total_bands,
                           int* d_counter, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st);
 hipError_t launch_fill_wide(const WideDev* d_pairs, int npairs, WideScores sc, WideRes* d_res, int local, int track,
@@ -563,6 +566,26 @@ static bool w16_ok(const Scores32& sc) {
     return U - a - g <= 15 && smin - U >= -16 && smax - 2 * a <= 15 && 2 * a - U >= -64 && U - 2 * a <= 63;
 }
 
+// The split column step (gx_cs2.hip) replaces layout 1's one-wave strips for
+// untracked fills; GX_CS2=0 keeps the one-wave kernel.  Band width: the
+// narrowest instantiated width whose bands fit the grid (W = 2: every compute
+// wave of a CU on its own SIMD), else 7-strip bands queued for workgroups
+// (GX_BAND_WAVES forces an instantiated width).
+static bool cs2_enabled() {
+    const char* e = getenv("GX_CS2");
+    return !(e && !strcmp(e, "0"));
+}
+static int cs2_band_waves(int total_strips, int grid_cap) {
+    static constexpr int kCs2Widths[] = {1, 2, 3, 4, 7};
+    if (const char* e = getenv("GX_BAND_WAVES")) {
+        const int w = atoi(e);
+        for (int x : kCs2Widths) if (x == w) return w;
+    }
+    for (int x : {2, 3, 4})
+        if (ceil_div(total_strips, x) <= grid_cap) return x;
+    return 7;
+}
+
 struct PairHost {
     const uint8_t* s1;   // original bytes (traceback labels, sequence.rs:113 with rev=false)
     const uint8_t* s2;
@@ -610,6 +633,7 @@ struct FillJob {
     bool shift = false;                 // values kept as V - (i + j) g (Scores32.shift)
     bool twin = false;                  // the twin fill (gx_fill_pk.hip): twin_table's pairs share every band
     bool w16 = false;                   // twin plane codes, 2 B per cell (w16_ok; batches only)
+    bool nocodes = false;               // w16 without code words: the traceback derives them from the planes
     bool table = false;                 // an alignment table (exportable planes: never the twin codes)
     int g = 0;
     double fill_ms = 0.0;
@@ -731,12 +755,17 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     track = track || lcs;
     int min_strips = INT_MAX;
     for (const PairHost& h : ph) min_strips = std::min(min_strips, ceil_div((int)h.n, SR));
-    const int W = fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device), lay, min_strips);
+    // the split column step (gx_cs2.hip): layout 1's formats, each strip on a
+    // core and a side wave; untracked fills (global or local)
+    const bool cs2 = lay == 1 && !track && cs2_enabled();
+    const int W = cs2 ? cs2_band_waves(total_strips, fill_grid_cap(ctx->device))
+                      : fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device), lay, min_strips);
     job.lay = lay;
-    // layout-0 untracked global fills keep every value as V - (i + j) g (one
-    // add less per recurrence, gx_kernels.hip cell); the sub scores carry -2g
+    // layout-0 untracked global fills and the split column step keep every
+    // value as V - (i + j) g (one add less per recurrence, gx_kernels.hip
+    // cell; the local floor becomes -(i + j) g); the sub scores carry -2g
     Scores32 scl = sc;
-    const bool shift = lay == 0 && !is_local && !track;
+    const bool shift = (lay == 0 && !is_local && !track) || cs2;
     scl.shift = shift ? 1 : 0;
     if (shift) { scl.sm = sc.sm - 2 * sc.g; scl.smm = sc.smm - 2 * sc.g; }
     job.shift = shift; job.g = sc.g;
@@ -780,6 +809,11 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     job.twin = twin;
     const bool w16 = twin && planes && !job.table && w16_ok(sc);
     job.w16 = w16;
+    // with twin plane codes the fill stores no code words (0.25 B/cell less):
+    // the traceback rebuilds the words of the path's strips from the planes
+    // (tb_w16_codes_kernel); GX_TWIN_CODES=1 keeps them
+    const char* tce = getenv("GX_TWIN_CODES");
+    job.nocodes = w16 && !(tce && !strcmp(tce, "1"));
     // small-alphabet twins: the match test through score tables (cell_pk; the
     // shifted scores must fit an unsigned byte);
     // the byte-plane twin (tables) keeps the plain test
@@ -789,7 +823,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     const int Wf = twin ? Wt : W;   // band width of the launch
     const size_t plane_esz = d8 ? 1 : sizeof(int32_t);
     job.W = Wf;
-    ctx->last_lay = lay; ctx->last_W = Wf;
+    ctx->last_lay = cs2 ? 2 : lay; ctx->last_W = Wf;
     ctx->last_pbytes = planes ? (w16 ? 2 : (int)(plane_esz * 3)) : 0;
     const size_t P = ph.size();
     job.pd.assign(P, PairDev{});
@@ -950,8 +984,12 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].fb : ctx->ev0, eve = slot >= 0 ? ctx->slots[slot].fe : ctx->ev1;
     HIPCHK(hipEventRecord(evb, ctx->stream));
     if (bands > 0 && twin)
-        HIPCHK(launch_fill_pk(Wf, (planes ? (w16 ? 2 : 1) : 0) + (twin_tbl ? 4 : 0), (const PairDev*)job.pairs.p, (int)P, (int)tw.size(), bands, (int*)job.counter.p,
+        HIPCHK(launch_fill_pk(Wf, (planes ? (w16 ? 2 : 1) : 0) + (twin_tbl ? 4 : 0) + (job.nocodes ? 8 : 0),
+                              (const PairDev*)job.pairs.p, (int)P, (int)tw.size(), bands, (int*)job.counter.p,
                               (PairRes*)job.pres.p, scl, grid, ctx->stream));
+    else if (bands > 0 && cs2)
+        HIPCHK(launch_fill_cs2(W, is_local != 0, planes, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
+                               (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, ctx->stream));
     else if (bands > 0)
         HIPCHK(launch_fill(W, lay, is_local != 0, planes ? (d8 ? 2 : 1) : 0, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
                            (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, ctx->stream));
@@ -1293,6 +1331,9 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
         t.srows = SR;
         t.skel_half = job.twin ? job.pd[p].twin_half : -1;
         t.end_ij = (int*)cnt.p + 4 * p;
+        t.w16 = job.nocodes ? (const uint8_t*)d.pI : nullptr;   // the twin's code plane (shared by its pairs)
+        t.w16_half = d.twin_half;
+        t.t4 = d.t4;
     }
     TbDev* pin_jobs = (TbDev*)(slot >= 0 ? pinned_grow(ctx->slots[slot].tjpin, P * sizeof(TbDev))
                                          : io_pinned(ctx, P * sizeof(TbDev)));
@@ -1302,7 +1343,7 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     if (e == hipSuccess) e = hipMemsetAsync(seg.p, 0, std::max<size_t>(stot, 1) * 4 * sizeof(int), ctx->stream);
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].tb : ctx->ev1, eve = slot >= 0 ? ctx->slots[slot].te : ctx->ev2;
     if (e == hipSuccess) e = hipEventRecord(evb, ctx->stream);
-    if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, max_strips, ctx->stream);
+    if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, max_strips, job.nocodes, ctx->stream);
     if (e == hipSuccess) e = hipEventRecord(eve, ctx->stream);
     // one pinned host block: c | sg | hr
     const size_t nc = 4 * P, nsg = 4 * std::max<size_t>(stot, 1), nhr = std::max<size_t>(stot, 1) * SR;
@@ -2212,6 +2253,73 @@ extern "C" int gx_align_batch(gx_context* ctx, const uint8_t* const* s1, const s
             }
         }
     }
+    return GX_OK;
+}
+
+// Many independent pairs over several GPUs (one context each): the pairs are
+// shared out by longest-processing-time on n * m cells (the heaviest pair to
+// the least-loaded context), and each share runs as one gx_align_batch on its
+// own host thread -- no device-to-device traffic, the shares are independent.
+// The reference's multi-worker driver is the rayon pool over all pairs of
+// compare (main.rs:245-261); this is its multi-GPU counterpart.
+static std::vector<std::vector<size_t>> lpt_shares(const size_t* n, const size_t* m, size_t npairs, int parts) {
+    std::vector<size_t> order(npairs);
+    for (size_t p = 0; p < npairs; ++p) order[p] = p;
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+        return (double)n[a] * (double)m[a] > (double)n[b] * (double)m[b];
+    });
+    std::vector<std::vector<size_t>> bins((size_t)parts);
+    std::vector<double> load((size_t)parts, 0.0);
+    for (size_t p : order) {
+        size_t b = 0;
+        for (size_t k = 1; k < bins.size(); ++k)
+            if (load[k] < load[b]) b = k;
+        bins[b].push_back(p);
+        load[b] += (double)n[p] * (double)m[p] + (double)(n[p] + m[p]);
+    }
+    for (auto& b : bins) std::sort(b.begin(), b.end());
+    return bins;
+}
+
+extern "C" int gx_align_batch_multi(gx_context* const* ctxs, int nctx, const uint8_t* const* s1, const size_t* n,
+                                    const uint8_t* const* s2, const size_t* m, size_t npairs,
+                                    const gx_scores* scores, int is_local, uint32_t flags, gx_step* const* steps,
+                                    const size_t* caps, gx_result* out) {
+    if (!ctxs || nctx < 1 || !s1 || !n || !s2 || !m || !out) return fail(GX_EINVAL, "NULL argument");
+    for (int k = 0; k < nctx; ++k)
+        if (!ctxs[k]) return fail(GX_EINVAL, "NULL context");
+    if (nctx == 1)
+        return gx_align_batch(ctxs[0], s1, n, s2, m, npairs, scores, is_local, flags, steps, caps, out);
+    const auto bins = lpt_shares(n, m, npairs, nctx);
+    std::vector<int> rc((size_t)nctx, GX_OK);
+    std::vector<std::string> err((size_t)nctx);
+    std::vector<std::thread> th;
+    for (int k = 0; k < nctx; ++k) {
+        if (bins[(size_t)k].empty()) continue;
+        th.emplace_back([&, k] {
+            const auto& b = bins[(size_t)k];
+            const size_t q = b.size();
+            std::vector<const uint8_t*> a1(q), a2(q);
+            std::vector<size_t> an(q), am(q), acap(q);
+            std::vector<gx_step*> ast(q, nullptr);
+            std::vector<gx_result> ares(q);
+            for (size_t x = 0; x < q; ++x) {
+                const size_t p = b[x];
+                a1[x] = s1[p]; a2[x] = s2[p]; an[x] = n[p]; am[x] = m[p];
+                ast[x] = steps ? steps[p] : nullptr;
+                acap[x] = caps ? caps[p] : 0;
+            }
+            rc[(size_t)k] = gx_align_batch(ctxs[k], a1.data(), an.data(), a2.data(), am.data(), q, scores, is_local,
+                                           flags, steps ? ast.data() : nullptr, caps ? acap.data() : nullptr,
+                                           ares.data());
+            if (rc[(size_t)k]) err[(size_t)k] = g_err;   // g_err is thread-local
+            else
+                for (size_t x = 0; x < q; ++x) out[b[x]] = ares[x];
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int k = 0; k < nctx; ++k)
+        if (rc[(size_t)k]) return fail(rc[(size_t)k], "context " + std::to_string(k) + ": " + err[(size_t)k]);
     return GX_OK;
 }
 

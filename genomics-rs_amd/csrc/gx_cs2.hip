@@ -36,6 +36,10 @@
 
 namespace gx {
 
+#ifndef GX_CS2_ASM
+#define GX_CS2_ASM 1   // 0: the core's cross-lane moves through update_dpp builtins (compiler-fused)
+#endif
+
 // core -> side staging: one group = In, S, D of 4 columns for every lane
 // (a lane's 4 columns of one value are one ds_write_b128 / ds_read_b128)
 struct SideGrp {
@@ -60,14 +64,30 @@ __device__ __forceinline__ void cs2_push(uint32_t vaddr, int dd, int sm, int c2)
 // psm = SM''(i0, j - 1).  fl = -(i + j) g (local floor, shifted).
 template <bool LOCAL, bool TBL>
 __device__ __forceinline__ void cs2_core_step(int& I, int& SDh, int& SM, const int psm, const int fl, const Rec& r,
-                                              const int c1v, const Scores32& sc, int& oI, int& oS, int& oD,
-                                              int& dd_out) {
+                                              const int c1v, const Scores32& sc, const int hv, int& oI, int& oS,
+                                              int& oD, int& dd_out) {
     const int scv = TBL ? __builtin_amdgcn_sbfe(c1v, r.c2, 8) : (r.c2 == c1v ? sc.sm : sc.smm);
     const int In = LOCAL ? max3i(I, SDh, fl) : max(I, SDh);
+#if GX_CS2_ASM
+    // the two cross-lane moves fused with their adds (v_add_u32_dpp, lane 0
+    // keeps the destination's value: the ring's input set beforehand), one
+    // VALU op each on the column's dependent chain instead of a v_mov_dpp,
+    // its old-value copy and the add; the s_nop covers the DPP read-after-
+    // VALU-write hazard, which the compiler does not track into inline asm
+    int Sn = psm + scv;                             // lane 0: SM''(i0, j-1) + s''
+    asm("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
+        : "+v"(Sn) : "v"(SM), "v"(scv));
+    const int IS = max(In, Sn);
+    const int Y = IS + sc.h;
+    int Z = r.dd;                                   // lane 0: D''(i0 + 1, j)
+    asm("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
+        : "+v"(Z) : "v"(IS), "v"(hv));            // lane l: IS''(l-1) + h
+#else
     const int Sn = shr1(psm, SM) + scv;             // lane 0: SM''(i0, j-1) from the ring
     const int IS = max(In, Sn);
     const int Y = IS + sc.h;
     int Z = shr1(r.dd, Y);                          // lane 0: D''(i0 + 1, j); lane l: IS''(l-1) + h
+#endif
     Z = scan_max64(Z);
     const int Dn = LOCAL ? max(Z, fl) : Z;
     SM = max(IS, Dn);
@@ -81,29 +101,30 @@ __device__ __forceinline__ void cs2_core_step(int& I, int& SDh, int& SM, const i
 // the same ring protocol as layout 1's cs_group4 -- observe the producer's
 // counter, read the next group's records speculatively, compute, re-read
 // after a wait if the counter did not cover them.
-template <bool LOCAL, bool TBL, int KSB, int G>
+template <bool LOCAL, bool TBL, int KSB, bool TAIL, int G>
 __device__ __forceinline__ void cs2_core_group(int& I, int& SDh, int& SM, int& psm, int& fl, Rec (&cur)[4],
                                                Rec (&nxt)[4], const int t0, const int m, const int c1v,
                                                const Scores32& sc, const Rec* ring_in, lds_int* wcnt_in,
                                                SideGrp* sb, const int lane, const uint32_t pa, const uint32_t scr,
-                                               const uint32_t cnt_addr, int* status) {
+                                               const uint32_t cnt_addr, const int hv, int* status) {
     constexpr int kSBG = KSB / 4;
     const int t = t0 + 4 * G;
-    const int need = min(t + 8, m) + 1;
+    const int need = TAIL ? min(t + 8, m) + 1 : t + 9;
     const int seen = *wcnt_in;
     asm volatile("" ::: "memory");
-    nxt[0] = ring_in[ring_slot(t + 5)]; nxt[1] = ring_in[ring_slot(t + 6)];
-    nxt[2] = ring_in[ring_slot(t + 7)]; nxt[3] = ring_in[ring_slot(t + 8)];
+    // the next group's 4 records: slots (t + 20 .. t + 23) mod kRing, one
+    // aligned block of 4 (t is a multiple of 4)
+    const Rec* const nb = ring_in + ring_slot(t + 5);
+    nxt[0] = nb[0]; nxt[1] = nb[1]; nxt[2] = nb[2]; nxt[3] = nb[3];
     int oI[4], oS[4], oD[4];
-    const bool tail = t + 4 > m;
 #pragma unroll
     for (int U = 0; U < 4; ++U) {
         int dd;
-        cs2_core_step<LOCAL, TBL>(I, SDh, SM, psm, fl, cur[U], c1v, sc, oI[U], oS[U], oD[U], dd);
+        cs2_core_step<LOCAL, TBL>(I, SDh, SM, psm, fl, cur[U], c1v, sc, hv, oI[U], oS[U], oD[U], dd);
         psm = cur[U].sm;
         if (LOCAL) fl -= sc.g;
         // lane 63's record of column t + U + 1 (none past column m)
-        const uint32_t a = (tail && t + U + 1 > m) ? scr : pa;
+        const uint32_t a = (TAIL && t + U + 1 > m) ? scr : pa;
         if (U == 0) cs2_push<4 * G + 0>(a, dd, SM, cur[U].c2);
         if (U == 1) cs2_push<4 * G + 1>(a, dd, SM, cur[U].c2);
         if (U == 2) cs2_push<4 * G + 2>(a, dd, SM, cur[U].c2);
@@ -115,17 +136,16 @@ __device__ __forceinline__ void cs2_core_group(int& I, int& SDh, int& SM, int& p
     g.v[2][lane] = make_int4(oD[0], oD[1], oD[2], oD[3]);
     // the records and staging of columns .. t + 4 are written (one wave's DS
     // operations execute in order): publish to the strip below and the side
-    publish_all(cnt_addr, min(t + 5, m + 1));
+    publish_all(cnt_addr, TAIL ? min(t + 5, m + 1) : t + 5);
     if (__builtin_amdgcn_readfirstlane(seen) < need) {
         wait_ge(wcnt_in, need, status);
-        nxt[0] = ring_in[ring_slot(t + 5)]; nxt[1] = ring_in[ring_slot(t + 6)];
-        nxt[2] = ring_in[ring_slot(t + 7)]; nxt[3] = ring_in[ring_slot(t + 8)];
+        nxt[0] = nb[0]; nxt[1] = nb[1]; nxt[2] = nb[2]; nxt[3] = nb[3];
     }
     __builtin_amdgcn_sched_barrier(0);
 }
 
 template <bool LOCAL, bool TBL, int KSB>
-__device__ void cs2_core(const PairDev& P, const int s, const int lane, const Scores32& sc, const Rec* ring_in,
+__device__ __forceinline__ void cs2_core(const PairDev& P, const int s, const int lane, const Scores32& sc, const Rec* ring_in,
                          Rec* ring_out, lds_int* wcnt_in, lds_int* rcnt_in, lds_int* wcnt_out, lds_int* rcnt_out,
                          lds_int* scnt, SideGrp* sb, const bool has_consumer, int* status, const uint32_t scratch) {
     const int n = P.n, m = P.m;
@@ -156,16 +176,25 @@ __device__ void cs2_core(const PairDev& P, const int s, const int lane, const Sc
         ra[2] = ring_in[ring_slot(3)]; ra[3] = ring_in[ring_slot(4)];
     }
     const uint32_t scr = scratch + 4u * (uint32_t)lane;
+    int hv = sc.h;                                  // (a VGPR: the DPP add's second operand)
+    asm volatile("" : "+v"(hv));
     for (int t0 = 0; t0 < m; t0 += kSub) {
         const int last_col = min(t0 + kSub, m);
         if (has_consumer && last_col >= kRing) wait_ge(rcnt_out, last_col - kRing + 1, status);
         if (t0 + 17 - KSB > 0) wait_ge(scnt, min(t0 + 17 - KSB, m + 1), status);   // staging slots free
         const uint32_t out_base = lds_addr(ring_out + ring_slot(t0 + 1));
         const uint32_t pa = has_consumer && lane == kWave - 1 ? out_base : scr;
-        cs2_core_group<LOCAL, TBL, KSB, 0>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, status);
-        cs2_core_group<LOCAL, TBL, KSB, 1>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, status);
-        cs2_core_group<LOCAL, TBL, KSB, 2>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, status);
-        cs2_core_group<LOCAL, TBL, KSB, 3>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, status);
+        if (t0 + kSub <= m) {
+            cs2_core_group<LOCAL, TBL, KSB, false, 0>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
+            cs2_core_group<LOCAL, TBL, KSB, false, 1>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
+            cs2_core_group<LOCAL, TBL, KSB, false, 2>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
+            cs2_core_group<LOCAL, TBL, KSB, false, 3>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
+        } else {
+            cs2_core_group<LOCAL, TBL, KSB, true, 0>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
+            cs2_core_group<LOCAL, TBL, KSB, true, 1>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
+            cs2_core_group<LOCAL, TBL, KSB, true, 2>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
+            cs2_core_group<LOCAL, TBL, KSB, true, 3>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
+        }
         lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
     }
 }
@@ -173,11 +202,14 @@ __device__ void cs2_core(const PairDev& P, const int s, const int lane, const Sc
 // The side wave's per-column work: retrace priority bits and the landing
 // column (gx_internal.h; keys (lane + 1) << 24 | (E + 64), a delete cell
 // takes the nearest non-delete lane above, or the top boundary column j).
-// Ep = E + 64 of (i, j - 1) on entry, of (i, j) on return.
+// Ek = the scanned key of (i, j - 1) on entry, of (i, j) on return: E + 64 in
+// its low 24 bits, the source lane above them (the skeleton and the results
+// keep it; readers mask it off).  The lane field is replaced by one v_bfi_b32
+// when the next key is built, so no mask sits on the chain.
 __device__ __forceinline__ void cs2_side_bits(const int In, const int Sn, const int Dn, const int t, const int kl,
-                                              int& Ep, uint32_t& cI, uint32_t& cD) {
+                                              const uint32_t low24, int& Ek, uint32_t& cI, uint32_t& cD) {
     const int IS = max(In, Sn);
-    const int etl = shr1(t + 64, Ep);               // lane 0: (i0, j - 1) on the boundary -> E = j - 1
+    const int etl = shr1(t + 64, Ek);               // lane 0: (i0, j - 1) on the boundary -> E = j - 1
     const int dkey = t + 65;                        // delete with no non-delete lane above: E = j
     int key;
     unsigned long long m1, m2, k1, k2;
@@ -188,21 +220,70 @@ __device__ __forceinline__ void cs2_side_bits(const int In, const int Sn, const 
         "v_cmp_gt_i32 %[m2], %[dn], %[is]\n\t"
         "v_cndmask_b32 %[key], %[etl], %[el], %[m1]\n\t"
         "v_addc_co_u32 %[ci], %[k1], %[ci], %[ci], %[m1]\n\t"
-        "v_or_b32 %[key], %[key], %[kl]\n\t"
+        "v_bfi_b32 %[key], %[lo], %[key], %[kl]\n\t"
         "v_addc_co_u32 %[cd], %[k2], %[cd], %[cd], %[m2]\n\t"
         "v_cndmask_b32 %[key], %[key], %[dk], %[m2]"
         : [key] "=&v"(key), [ci] "+v"(cI), [cd] "+v"(cD), [m1] "=&s"(m1), [m2] "=&s"(m2), [k1] "=&s"(k1),
           [k2] "=&s"(k2)
-        : [in] "v"(In), [sn] "v"(Sn), [dn] "v"(Dn), [is] "v"(IS), [etl] "v"(etl), [el] "v"(Ep), [kl] "v"(kl),
-          [dk] "v"(dkey));
-    Ep = scan_max64(key) & 0xFFFFFF;
+        : [in] "v"(In), [sn] "v"(Sn), [dn] "v"(Dn), [is] "v"(IS), [etl] "v"(etl), [el] "v"(Ek), [kl] "v"(kl),
+          [dk] "v"(dkey), [lo] "s"(low24));
+    Ek = scan_max64(key);
+}
+
+// Per-strip state of the side wave.
+struct Cs2Side {
+    int Ep;                 // scanned key of (i, j - 1): E + 64 in the low 24 bits (landing column, gx_internal.h)
+    int e_last;             // the key of the column before the current group (skeleton)
+    uint32_t cI, cD;        // code bit-planes of the current 16-column word
+    int fl;                 // local: floor'' = -(i + j) g of the next column
+    int lbest, lstep, lE;   // local: last max of the row (unshifted), its step and landing column
+    int fin_sm, fin_E;      // score_max'' and E + 64 of cell (i, m)
+};
+
+// One 4-column group of the side wave (columns t + 1 .. t + 4).
+template <bool LOCAL, bool PLANES, int KSB, bool TAIL>
+__device__ __forceinline__ void cs2_side_group(Cs2Side& st, const int t, const int m, const int lane, const int kl,
+                                               const Scores32& sc, lds_int* wcnt_core, const uint32_t scnt_addr,
+                                               const SideGrp* sb, const __amdgpu_buffer_rsrc_t& rI,
+                                               const __amdgpu_buffer_rsrc_t& rD, const __amdgpu_buffer_rsrc_t& rS,
+                                               const __amdgpu_buffer_rsrc_t& skel_rsrc, const uint32_t skel_voff,
+                                               int* status) {
+    constexpr int kSBG = KSB / 4;
+    wait_ge(wcnt_core, TAIL ? min(t + 5, m + 1) : t + 5, status);
+    const SideGrp& g = sb[(t >> 2) & (kSBG - 1)];
+    const int4 vI = g.v[0][lane], vS = g.v[1][lane], vD = g.v[2][lane];
+    publish_all(scnt_addr, TAIL ? min(t + 5, m + 1) : t + 5);   // (after the reads: in-order DS execution)
+    const int aI[4] = {vI.x, vI.y, vI.z, vI.w}, aS[4] = {vS.x, vS.y, vS.z, vS.w}, aD[4] = {vD.x, vD.y, vD.z, vD.w};
+    int e[4];
+#pragma unroll
+    for (int U = 0; U < 4; ++U) {
+        cs2_side_bits(aI[U], aS[U], aD[U], t + U, kl, 0xFFFFFFu, st.Ep, st.cI, st.cD);
+        e[U] = st.Ep;
+        if (LOCAL) {
+            // H(i, j) = SM'' - fl'' (unshifted); the last max of the row wins ties
+            const int H = max(max(aI[U], aS[U]), aD[U]) - st.fl;
+            const bool nl = (!TAIL || t + U < m) && H >= st.lbest;
+            st.lbest = nl ? H : st.lbest; st.lstep = nl ? t + U : st.lstep; st.lE = nl ? st.Ep : st.lE;
+            st.fl -= sc.g;
+        }
+        if (TAIL && t + U == m - 1) { st.fin_sm = max(max(aI[U], aS[U]), aD[U]); st.fin_E = st.Ep; }
+    }
+    if (PLANES) {
+        const uint32_t v = (uint32_t)lane * 16u + (uint32_t)(t >> 2) * (uint32_t)kGroupInts1 * 4u;
+        bstore4(rI, v, vI);
+        bstore4(rD, v, vD);
+        bstore4(rS, v, vS);
+    }
+    // skeleton: lane 63's E + 64 of columns t .. t + 3 (16-B aligned)
+    skel_store4(skel_rsrc, skel_voff + 4u * (uint32_t)t, st.e_last, e[0], e[1], e[2]);
+    st.e_last = e[3];
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 template <bool LOCAL, bool PLANES, int KSB>
-__device__ void cs2_side(const PairDev& P, const int s, const int lane, const Scores32& sc, lds_int* wcnt_core,
-                         lds_int* scnt, const SideGrp* sb, const bool has_consumer, StripRes* sres, PairRes* pres,
-                         int* status) {
-    constexpr int kSBG = KSB / 4;
+__device__ __forceinline__ void cs2_side(const PairDev& P, const int s, const int lane, const Scores32& sc,
+                                         lds_int* wcnt_core, lds_int* scnt, const SideGrp* sb,
+                                         const bool has_consumer, StripRes* sres, PairRes* pres, int* status) {
     const int n = P.n, m = P.m;
     const int i = s * kWave + lane + 1;
     const bool ok = i <= n;
@@ -220,69 +301,44 @@ __device__ void cs2_side(const PairDev& P, const int s, const int lane, const Sc
     const uint32_t skel_voff = lane == kWave - 1 ? 0u : kSkelOff;
     const uint32_t scnt_addr = lds_addr((const void*)scnt);
     const int kl = (lane + 1) << 24;
-    int Ep = 63 - lane;                             // column 0: E = -(lane + 1) (+ 64)
-    int e_last = Ep;                                // E + 64 of the column before the group (skeleton)
-    uint32_t cI = 0, cD = 0;
-    // local: floor'' and the last max of the row (algo.rs:310-322, unshifted values)
-    int fl = LOCAL ? -(i + 1) * sc.g : 0;
-    int lbest = ok ? INT_MIN : INT_MAX, lstep = 0, lE = 0;
-    int fin_sm = 0, fin_E = 0;
+    Cs2Side st;
+    st.Ep = 63 - lane;                              // column 0: E = -(lane + 1) (+ 64)
+    st.e_last = st.Ep;
+    st.cI = 0; st.cD = 0;
+    st.fl = LOCAL ? -(i + 1) * sc.g : 0;
+    st.lbest = ok ? INT_MIN : INT_MAX; st.lstep = 0; st.lE = 0;
+    st.fin_sm = 0; st.fin_E = 0;
     for (int t0 = 0; t0 < m; t0 += kSub) {
+        if (t0 + kSub <= m) {
 #pragma unroll
-        for (int G = 0; G < 4; ++G) {
-            const int t = t0 + 4 * G;
-            wait_ge(wcnt_core, min(t + 5, m + 1), status);
-            const SideGrp& g = sb[(t >> 2) & (kSBG - 1)];
-            const int4 vI = g.v[0][lane], vS = g.v[1][lane], vD = g.v[2][lane];
-            publish_all(scnt_addr, min(t + 5, m + 1));   // (after the reads: in-order DS execution)
-            const int aI[4] = {vI.x, vI.y, vI.z, vI.w}, aS[4] = {vS.x, vS.y, vS.z, vS.w},
-                      aD[4] = {vD.x, vD.y, vD.z, vD.w};
-            const bool tail = t + 4 > m;
-            int e[4];
+            for (int G = 0; G < 4; ++G)
+                cs2_side_group<LOCAL, PLANES, KSB, false>(st, t0 + 4 * G, m, lane, kl, sc, wcnt_core, scnt_addr, sb,
+                                                          rI, rD, rS, skel_rsrc, skel_voff, status);
+        } else {
 #pragma unroll
-            for (int U = 0; U < 4; ++U) {
-                cs2_side_bits(aI[U], aS[U], aD[U], t + U, kl, Ep, cI, cD);
-                e[U] = Ep;
-                if (LOCAL) {
-                    // H(i, j) = SM'' - fl'' (unshifted); the last max of the row wins ties
-                    const int H = max(max(aI[U], aS[U]), aD[U]) - fl;
-                    const bool act = !tail || t + U < m;
-                    const bool nl = act && H >= lbest;
-                    lbest = nl ? H : lbest; lstep = nl ? t + U : lstep; lE = nl ? Ep : lE;
-                    fl -= sc.g;
-                }
-                if (tail && t + U == m - 1) { fin_sm = max(max(aI[U], aS[U]), aD[U]); fin_E = Ep; }
-            }
-            if (PLANES) {
-                const uint32_t v = (uint32_t)lane * 16u + (uint32_t)(t >> 2) * (uint32_t)kGroupInts1 * 4u;
-                bstore4(rI, v, vI);
-                bstore4(rD, v, vD);
-                bstore4(rS, v, vS);
-            }
-            // skeleton: lane 63's E + 64 of columns t .. t + 3 (16-B aligned)
-            skel_store4(skel_rsrc, skel_voff + 4u * (uint32_t)t, e_last, e[0], e[1], e[2]);
-            e_last = e[3];
-            __builtin_amdgcn_sched_barrier(0);
+            for (int G = 0; G < 4; ++G)
+                cs2_side_group<LOCAL, PLANES, KSB, true>(st, t0 + 4 * G, m, lane, kl, sc, wcnt_core, scnt_addr, sb,
+                                                         rI, rD, rS, skel_rsrc, skel_voff, status);
         }
-        gstore1(codes + (size_t)(t0 >> 4) * kWave + lane, (cD << 16) | (cI & 0xFFFFu));
+        gstore1(codes + (size_t)(t0 >> 4) * kWave + lane, (st.cD << 16) | (st.cI & 0xFFFFu));
     }
     // the last group's fourth column (16 ceil(m / 16): stored only if it is m)
-    skel_store(skel_rsrc, skel_voff + 4u * (uint32_t)((m + 15) & ~15), e_last);
+    skel_store(skel_rsrc, skel_voff + 4u * (uint32_t)((m + 15) & ~15), st.e_last);
     if (LOCAL) {
-        const int lb = ok ? lbest : INT_MIN;
+        const int lb = ok ? st.lbest : INT_MIN;
         int lmx = lb;
         for (int off = 32; off > 0; off >>= 1) lmx = max(lmx, __shfl_xor(lmx, off));
         const unsigned long long lmask = __ballot(ok && lb == lmx);
         const int ll = lmask ? (63 - __clzll((long long)lmask)) : 0;
-        const int l_step = __shfl(lstep, ll), l_E = __shfl(lE, ll);
+        const int l_step = __shfl(st.lstep, ll), l_E = __shfl(st.lE, ll);
         if (lane == 0) {
             StripRes r;
             r.best = INT_MIN; r.bi = 0; r.bj = 0; r.bl = 0;
-            r.lbest = lmx; r.li = s * kWave + ll + 1; r.lj = l_step + 1; r.lE = l_E - 64;
+            r.lbest = lmx; r.li = s * kWave + ll + 1; r.lj = l_step + 1; r.lE = (l_E & 0xFFFFFF) - 64;
             sres[P.strip_base + s] = r;
         }
     }
-    if (ok && i == n) { pres->end_SM = fin_sm; pres->end_E = fin_E - 64; }
+    if (ok && i == n) { pres->end_SM = st.fin_sm; pres->end_E = (st.fin_E & 0xFFFFFF) - 64; }
 }
 
 template <int W, bool LOCAL, bool PLANES, bool TBL>

@@ -144,6 +144,12 @@ struct TbDev {           // per-pair traceback job
     int* seg;              // out: [strips][4] {entry_i, entry_j, records, active} per strip on the path
     uint32_t* recs;        // out: [strips][kStripRows] one record per row, (insert run << 2) | kind
     int* end_ij;           // out: [4] {i, j} where the walk leaves the interior, first strip, rounds
+    // twin fill without code words (gx_fill_pk.hip, twin plane codes): the
+    // traceback derives the code words of the strips on the path from the
+    // plane codes first (tb_w16_codes_kernel); nullptr: the fill wrote them
+    const uint8_t* w16;    // the twin's code plane (strip 0), [strip][t/4][row-in-lane][lane][t%4] dwords
+    int w16_half;          // this pair's 16-bit half of each dword
+    int t4;                // 4-step groups per strip
 };
 
 // ---- wide (int64) fill (gx_wide.hip): jobs outside the exact-int32 range --

@@ -1229,10 +1229,56 @@ __global__ void tb_chase_kernel(const TbDev* __restrict__ jobs) {
             J.seg[4 * s + 0] = (s + 1) * SR; J.seg[4 * s + 1] = E; J.seg[4 * s + 3] = 1;
             E = ((gcint*)J.skel)[(size_t)s * J.skel_stride + E];
             if (J.skel_half >= 0) E = (int)(short)((unsigned)E >> (16 * J.skel_half));   // twin fill (gx_fill_pk.hip)
-            if (SR == kStripRows1) E -= 64;                        // layout 1 stores E + 64
+            if (SR == kStripRows1) E = (E & 0xFFFFFF) - 64;        // layout 1 stores E + 64 (the split column step
+                                                                   // keeps the key's lane field above it)
         }
     }
     J.end_ij[0] = i; J.end_ij[1] = j; J.end_ij[2] = first;
+}
+
+// Code words of the strips on the path from the twin plane codes (DESIGN.md
+// 4.4), for a twin fill that stored no code words.  A cell's plane code holds
+// x_S = S - I and x_D = D - I, and the retrace priority S > I > D
+// (algo.rs:351-400) is "insert beats sub" = x_S < 0 and "delete beats both" =
+// x_D > max(0, x_S).  The path crosses strip s between its entry column
+// (seg[s], the bottom row) and the entry column of the strip above (or where
+// it leaves the interior), so only the words holding those columns of each
+// row are rebuilt; the walk (tb_strip_kernel) never uses a word outside them
+// once its rows have converged (every path cell lies in that range).  One
+// block of 128 threads per strip, one thread per row.
+__global__ __launch_bounds__(128) void tb_w16_codes_kernel(const TbDev* __restrict__ jobs) {
+    const TbDev J = jobs[blockIdx.y];
+    const int s = blockIdx.x;
+    if (!J.w16 || s >= J.strips) return;
+    const int* seg = J.seg;
+    if (!((gcint*)seg)[4 * s + 3]) return;                     // not on the path
+    const int j_hi = ((gcint*)seg)[4 * s + 1];
+    int j_lo = (s > 0 && ((gcint*)seg)[4 * (s - 1) + 3]) ? ((gcint*)seg)[4 * (s - 1) + 1] : ((gcint*)J.end_ij)[1];
+    j_lo = max(j_lo, 1);
+    const int rho = threadIdx.x, lane = rho >> 1, hh = rho & 1;
+    const int q_lo = (j_lo - 1 + lane) >> 4, q_hi = min((j_hi - 1 + lane) >> 4, J.t16 - 1);
+    const uint8_t* base = J.w16 + (size_t)s * J.t4 * kTwinGroupBytes + (size_t)hh * (kTwinGroupBytes / 2) +
+                          (size_t)lane * 16;
+    const int sh = 16 * J.w16_half;
+    guint* const out = (guint*)(J.codes + (size_t)s * J.t16 * kStripRows + rho);
+    for (int q = q_lo; q <= q_hi; ++q) {
+        uint32_t cI = 0, cD = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const uint4 w4 = *(const uint4*)(base + (size_t)(4 * q + g) * kTwinGroupBytes);
+            const uint32_t wk[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t code = (wk[k] >> sh) & 0xFFFFu;
+                const uint32_t r = code >> 4;                               // x_S + 32 x_D (mod 2^12)
+                const int xS = (int)(r << 27) >> 27;                        // 5-bit signed
+                const int xD = (int)(((r - (uint32_t)xS) >> 5) << 25) >> 25;   // 7-bit signed
+                cI = (cI << 1) | (uint32_t)(xS < 0);
+                cD = (cD << 1) | (uint32_t)(xD > max(0, xS));
+            }
+        }
+        out[(size_t)q * kStripRows] = (cD << 16) | cI;
+    }
 }
 
 __global__ __launch_bounds__(64) void tb_strip_kernel(const TbDev* __restrict__ jobs) {
@@ -1570,10 +1616,15 @@ hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d
     return hipGetLastError();
 }
 
-hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, hipStream_t st) {
+hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, bool w16, hipStream_t st) {
     hipLaunchKernelGGL(tb_chase_kernel, dim3(njobs), dim3(64), 0, st, d_jobs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (w16) {   // code words of the path's strips from the twin plane codes
+        hipLaunchKernelGGL(tb_w16_codes_kernel, dim3(max_strips, njobs), dim3(kStripRows), 0, st, d_jobs);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(tb_strip_kernel, dim3(max_strips, njobs), dim3(64), 0, st, d_jobs);
     return hipGetLastError();
 }

@@ -72,7 +72,8 @@ STEP_DTYPE = np.dtype([("choice", "u1"), ("pad", "u1", (7,)), ("i", "<u8"), ("j"
 # exported symbols (include/gx.h) -- checked by tests/test_abi.py
 EXPORTED = ["gx_last_error", "gx_version", "gx_context_create", "gx_context_destroy", "gx_context_trim",
             "gx_alignment_table", "gx_table_info", "gx_table_export", "gx_table_export_plane", "gx_table_export_rows",
-            "gx_table_plane_sums", "gx_retrace", "gx_table_free", "gx_align", "gx_align_batch", "gx_stage_pairs",
+            "gx_table_plane_sums", "gx_retrace", "gx_table_free", "gx_align", "gx_align_batch", "gx_align_batch_multi",
+            "gx_stage_pairs",
             "gx_run_staged", "gx_run_staged_steps", "gx_staged_plane_sums", "gx_staged_steps",
             "gx_fill_info", "gx_batch_chunks", "gx_fill_twin", "gx_plane_bytes_per_cell", "gx_twin_admission",
             "gx_fasta_load",
@@ -112,6 +113,8 @@ def lib():
                            ctypes.c_uint32, vp, sz, ctypes.POINTER(CResult)]
     L.gx_align_batch.argtypes = [vp, vp, vp, vp, vp, sz, ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_uint32,
                                  vp, vp, vp]
+    L.gx_align_batch_multi.argtypes = [vp, ctypes.c_int, vp, vp, vp, vp, sz, ctypes.POINTER(CScores), ctypes.c_int,
+                                       ctypes.c_uint32, vp, vp, vp]
     L.gx_stage_pairs.argtypes = [vp, vp, vp, vp, vp, sz]
     L.gx_run_staged.argtypes = [vp, ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int, ctypes.c_uint32, vp,
                                 ctypes.POINTER(ctypes.c_double)]
@@ -551,6 +554,27 @@ def align_batch(pairs: Seq[Tuple[bytes, bytes]], scores: Scores, is_local: bool,
         st = steps_arr[p][: res[p].n_steps] if with_steps else None
         out.append((st, res[p]))
     return out
+
+
+def align_batch_multi(pairs: Seq[Tuple[bytes, bytes]], scores: Scores, is_local: bool, ctxs: Seq[Context],
+                      with_steps: bool = True, max_cell: bool = True):
+    """align_batch over several GPUs (gx_align_batch_multi): one context per
+    device, the pairs shared out by longest-processing-time on n*m cells, one
+    host thread per context -> list of (steps, CResult) in pair order."""
+    P = len(pairs)
+    keep = [(_buf(a), _buf(b)) for a, b in pairs]
+    s1p = (ctypes.c_void_p * P)(*[k[0][1] for k in keep])
+    s2p = (ctypes.c_void_p * P)(*[k[1][1] for k in keep])
+    n = (ctypes.c_size_t * P)(*[len(a) for a, _ in pairs])
+    m = (ctypes.c_size_t * P)(*[len(b) for _, b in pairs])
+    res = (CResult * P)()
+    steps_arr = [np.zeros(len(a) + len(b) + 2, STEP_DTYPE) for a, b in pairs] if with_steps else None
+    stp = (ctypes.c_void_p * P)(*[s.ctypes.data for s in steps_arr]) if with_steps else None
+    caps = (ctypes.c_size_t * P)(*[s.size for s in steps_arr]) if with_steps else None
+    cp = (ctypes.c_void_p * len(ctxs))(*[c.ptr.value for c in ctxs])
+    _check(lib().gx_align_batch_multi(cp, len(ctxs), s1p, n, s2p, m, P, ctypes.byref(scores.c()), int(is_local),
+                                      GX_ALIGN_MAX_CELL if max_cell else 0, stp, caps, res))
+    return [(steps_arr[p][: res[p].n_steps] if with_steps else None, res[p]) for p in range(P)]
 
 
 class StagedPairs:

@@ -172,6 +172,16 @@ int gx_align_batch(gx_context* ctx, const uint8_t* const* s1, const size_t* n, c
                    const size_t* m, size_t npairs, const gx_scores* scores, int is_local, uint32_t flags,
                    gx_step* const* steps, const size_t* caps, gx_result* out);
 
+/* The same over several GPUs: ctxs[0..nctx-1] are contexts created with
+ * gx_context_create (one per device; two contexts on one device are allowed).
+ * The pairs are shared out by longest-processing-time on n[p] * m[p] cells and
+ * each share runs as one gx_align_batch on its own host thread; results land
+ * at their pair's index.  SURVEY.md 8(b)'s gx_align_batch(..., ndev) shape; the
+ * reference's multi-worker driver is the rayon pool of main.rs:245-261. */
+int gx_align_batch_multi(gx_context* const* ctxs, int nctx, const uint8_t* const* s1, const size_t* n,
+                         const uint8_t* const* s2, const size_t* m, size_t npairs, const gx_scores* scores,
+                         int is_local, uint32_t flags, gx_step* const* steps, const size_t* caps, gx_result* out);
+
 /* ---- device-resident benchmarking path ---------------------------------
  * Stage one pair per slot in HBM once (gx_stage_pairs), then run the hot
  * path (fill with score planes + traceback) on the staged inputs with no

@@ -190,3 +190,25 @@ def test_all_vs_all_planes_match_oracle(gx, ctx, monkeypatch, twin):
         assert [int(x) for x in sums[0, p]] == c["plane_sums"], (c["i"], c["j"])
         assert res[p].score == c["score"] and res[p].n_steps == c["n_steps"]
         assert _digest(st.steps(p)) == c["alignment_sha256"], (c["i"], c["j"])
+
+
+@pytest.mark.parametrize("nctx", [2, 4])
+def test_align_batch_multi_contexts_on_one_gpu(gx, nctx, monkeypatch):
+    """gx_align_batch_multi (the C ABI's multi-GPU batch: LPT shares, one host
+    thread and context per device) with `nctx` contexts mapped onto device 0
+    (GX_DEVICE_MAP=0,0,..): all 55 comparison pairs' scores, statistics and
+    alignment digests against the oracle's."""
+    monkeypatch.setenv("GX_DEVICE_MAP", ",".join(["0"] * nctx))
+    g = _golden()
+    seqs = [s.sequence.encode() for s in _container(gx).sequences]
+    ctxs = [gx.Context(gx.device_for_rank(k)) for k in range(nctx)]
+    try:
+        out = gx.align_batch_multi([(seqs[c["i"]], seqs[c["j"]]) for c in g["cases"]], gx.Scores(*g["scores"]),
+                                   False, ctxs, max_cell=False)
+    finally:
+        for c in ctxs:
+            c.close()
+    for c, (steps, r) in zip(g["cases"], out):
+        assert [r.score, r.matches, r.mismatches, r.gap_extensions, r.opening_gaps, r.n_steps] == \
+               [c["score"]] + c["stats"] + [c["n_steps"]], (c["i"], c["j"])
+        assert _digest(steps) == c["alignment_sha256"], (c["i"], c["j"])
