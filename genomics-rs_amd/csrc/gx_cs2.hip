@@ -109,7 +109,7 @@ __device__ __forceinline__ void cs2_core_group(int& I, int& SDh, int& SM, int& p
                                                const uint32_t cnt_addr, const int hv, int* status) {
     constexpr int kSBG = KSB / 4;
     const int t = t0 + 4 * G;
-    const int need = TAIL ? min(t + 8, m) + 1 : t + 9;
+    const int need = min(t + 8, m) + 1;             // (the next group may be past column m)
     const int seen = *wcnt_in;
     asm volatile("" ::: "memory");
     // the next group's 4 records: slots (t + 20 .. t + 23) mod kRing, one
@@ -166,7 +166,12 @@ __device__ __forceinline__ void cs2_core(const PairDev& P, const int s, const in
         lds_wait();
         if (lane == 0) *wcnt_out = 1;
     }
-    wait_ge(wcnt_in, min(4, m) + 1, status);
+    StripTrace* const trace = P.trace;   // GX_TRACE_FILE diagnostics (tools/trace_summary.py)
+    long long tr_start = 0, tr_first = 0, clk_first = 0;
+    long long tr_q[kTraceQ] = {};
+    if (trace) tr_start = __builtin_amdgcn_s_memrealtime();
+    const unsigned tr_win0 = wait_ge(wcnt_in, min(4, m) + 1, status);
+    if (trace) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
     Rec ra[4], rb[4];
     int psm;
     {
@@ -180,8 +185,14 @@ __device__ __forceinline__ void cs2_core(const PairDev& P, const int s, const in
     asm volatile("" : "+v"(hv));
     for (int t0 = 0; t0 < m; t0 += kSub) {
         const int last_col = min(t0 + kSub, m);
+        if (trace) {
+            const int q = (int)((long long)t0 * (kTraceQ + 1) / (m + 1)) - 1;
+            if (q >= 0 && q < kTraceQ && tr_q[q] == 0) tr_q[q] = __builtin_amdgcn_s_memrealtime();
+        }
         if (has_consumer && last_col >= kRing) wait_ge(rcnt_out, last_col - kRing + 1, status);
-        if (t0 + 17 - KSB > 0) wait_ge(scnt, min(t0 + 17 - KSB, m + 1), status);   // staging slots free
+        // staging slots free: group g reuses the slot of group g - KSB/4, so the
+        // sub-block's last group needs the side past column 4 (g - KSB/4) + 4
+        if (t0 + 12 >= KSB) wait_ge(scnt, min(t0 + 17 - KSB, m + 1), status);
         const uint32_t out_base = lds_addr(ring_out + ring_slot(t0 + 1));
         const uint32_t pa = has_consumer && lane == kWave - 1 ? out_base : scr;
         if (t0 + kSub <= m) {
@@ -196,6 +207,14 @@ __device__ __forceinline__ void cs2_core(const PairDev& P, const int s, const in
             cs2_core_group<LOCAL, TBL, KSB, true, 3>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
         }
         lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
+    }
+    if (trace && lane == 0) {
+        StripTrace tr;
+        tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
+        tr.wait_in = (int)tr_win0; tr.wait_out = 0;
+        tr.clk = __builtin_amdgcn_s_memtime() - clk_first;
+        for (int q = 0; q < kTraceQ; ++q) tr.t_q[q] = tr_q[q];
+        trace[s] = tr;
     }
 }
 
@@ -309,7 +328,8 @@ __device__ __forceinline__ void cs2_side(const PairDev& P, const int s, const in
     st.lbest = ok ? INT_MIN : INT_MAX; st.lstep = 0; st.lE = 0;
     st.fin_sm = 0; st.fin_E = 0;
     for (int t0 = 0; t0 < m; t0 += kSub) {
-        if (t0 + kSub <= m) {
+        // the sub-block holding column m always runs as a tail (the end cell is taken there)
+        if (t0 + kSub < m) {
 #pragma unroll
             for (int G = 0; G < 4; ++G)
                 cs2_side_group<LOCAL, PLANES, KSB, false>(st, t0 + 4 * G, m, lane, kl, sc, wcnt_core, scnt_addr, sb,
@@ -349,7 +369,7 @@ __global__ __launch_bounds__((2 * W + 1) * kWave) void fill_cs2_kernel(const Pai
     constexpr int KSB = W <= 4 ? 32 : 16;
     __shared__ Rec rings[W + 1][kRing];
     __shared__ SideGrp sbuf[W][KSB / 4];
-    __shared__ uint32_t push_scratch[W][kWave];
+    __shared__ uint32_t push_scratch[W][kPushScratch];   // lanes 0-62's pushes: 4 B per lane + the record offsets
     __shared__ int wcnt[W + 1];
     __shared__ int rcnt[W + 1];
     __shared__ int scnt[W];

@@ -33,10 +33,14 @@ __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::
 // turns a non-zero status into GX_EHIP.
 constexpr unsigned kSpinLimit = 1u << 25;
 
+// A wave that has spun 2^12 times also checks the status word: once any
+// wave of the launch has timed out, every other waiting wave gives up at once
+// and the grid drains in about one spin limit instead of one per wait.
 __device__ __forceinline__ unsigned wait_ge(lds_int* p, int v, int* status) {
     unsigned it = 0;
     for (; *p < v; ++it) {
         if (it > kSpinLimit) { __hip_atomic_store((gint*)status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
+        if ((it & 4095u) == 4095u && __hip_atomic_load((gint*)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
         __builtin_amdgcn_s_sleep(1);
     }
     asm volatile("" ::: "memory");

@@ -39,6 +39,19 @@ __device__ __forceinline__ uint32_t as_u(s2 x) { return __builtin_bit_cast(uint3
 __device__ __forceinline__ uint32_t pmax(uint32_t a, uint32_t b) {
     return as_u(__builtin_elementwise_max(as_s2(a), as_s2(b)));
 }
+// Values are held in offset binary (each half + 0x8000, "biased"): the
+// admission bound keeps every value within 30,000 of its base, so a biased
+// half lies in [2768, 62768] and adding a small non-negative constant (a
+// score-table byte) or subtracting one (|h|) never carries or borrows across
+// the halves -- those adds run as one 32-bit v_add_u32 / v_sub_u32, a
+// dual-rate VOP2 form (~2.4 cycles per wave64 at two waves per SIMD against
+// ~4.6 for a VOP3P v_pk_add, profiles/valu_probe_r02k.json).  Comparisons
+// of biased halves are unsigned (v_pk_max_u16); differences are unbiased.
+constexpr uint32_t kBias2 = 0x80008000u;
+typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pmaxu(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b)));
+}
 __device__ __forceinline__ uint32_t padd(uint32_t a, uint32_t b) { return as_u(as_s2(a) + as_s2(b)); }
 __device__ __forceinline__ uint32_t padds(uint32_t a, uint32_t b) { return padd(a, b); }
 __device__ __forceinline__ uint32_t psub(uint32_t a, uint32_t b) { return as_u(as_s2(a) - as_s2(b)); }
@@ -118,7 +131,7 @@ __device__ __forceinline__ void bytes_step(uint32_t (&xI)[2][2], uint32_t (&xS)[
 
 // Packed scores (both halves equal): h, sm'' = s_match - 2g, dsm = (s_mismatch - 2g) - sm''
 struct PkScores {
-    uint32_t h, smp, dsm;
+    uint32_t nh, smp, dsm;   // -h (>= 0) in both halves, the score_max offset, the mismatch - match delta
 };
 
 // Twin plane code (PLANES == 2, 2 B per cell): the three differences of a
@@ -165,19 +178,19 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
                                         const uint32_t c2, const uint32_t c1, const uint32_t c1h, const uint32_t act,
                                         const PkScores& k,
                                         uint32_t& oI, uint32_t& oD, uint32_t& oS, uint32_t& oIold) {
-    const uint32_t In = pmax(st.I, padds(st.SD, k.h));            // max(I, max(S,D) + h)   (algo.rs:231-236)
+    const uint32_t In = pmaxu(st.I, st.SD - k.nh);                // max(I, max(S,D) + h)   (algo.rs:231-236)
     // SM(i-1,j-1) + s''  (algo.rs:245-248).  TBL: c1/c1h are the row's score
     // tables of the two pairs (byte k: s_match'' if the row's char is symbol
     // k, else s_mismatch''; SM is then kept without the s_match'' offset) and
     // c2 the column's selector (pair 0's symbol in byte 0, 4 + pair 1's in
     // byte 2, zero bytes between): one v_perm_b32 reads both scores (xor +
     // min + mad, and the offset's add, without the table)
-    const uint32_t Sn = TBL ? padd(st.SMtl, __builtin_amdgcn_perm(c1h, c1, c2)) : pmad(pmis(c1, c2), k.dsm, st.SMtl);
+    const uint32_t Sn = TBL ? st.SMtl + __builtin_amdgcn_perm(c1h, c1, c2) : pmad(pmis(c1, c2), k.dsm, st.SMtl);
     const uint32_t Dn = dd_in;                                     // (algo.rs:238-243, from the row above)
-    const uint32_t IS = pmax(In, Sn);
-    const uint32_t SMn = pmax(IS, Dn);
-    const uint32_t SDn = pmax(Sn, Dn);
-    const uint32_t Ddn = pmax(padds(IS, k.h), Dn);                 // D(i+1, j)
+    const uint32_t IS = pmaxu(In, Sn);
+    const uint32_t SMn = pmaxu(IS, Dn);
+    const uint32_t SDn = pmaxu(Sn, Dn);
+    const uint32_t Ddn = pmaxu(IS - k.nh, Dn);                     // D(i+1, j)
     // retrace priority S > I > D (algo.rs:351-400): m1 = I beats S, m2 = D beats both
     const uint32_t m1 = psign(psub(Sn, In)), m2 = psign(psub(IS, Dn));
     const uint32_t E1 = bfi(m1, st.E, st.Etl);
@@ -402,10 +415,10 @@ __device__ __forceinline__ void sub_block_pk(LanePk& st, Rec (&nxt)[4], WavePk& 
 // H(i, 0) = h + i g -> h; I = H + h (compact planes' seed) -> 2h;
 // delete successor (row i+1) -> h; relative to the bases (B0, B1).
 __device__ __forceinline__ void init_row_pk(RowPk& rs, const Scores32& sc, int B0, int B1, const PkScores& k) {
-    rs.I = pk2(2 * sc.h - B0, 2 * sc.h - B1);
-    rs.SD = pk2(sc.h - B0, sc.h - B1);
-    rs.Dd = pk2(sc.h - B0, sc.h - B1);
-    rs.SMp = padds(pk2(sc.h - B0, sc.h - B1), k.smp);
+    rs.I = pk2(2 * sc.h - B0, 2 * sc.h - B1) ^ kBias2;
+    rs.SD = pk2(sc.h - B0, sc.h - B1) ^ kBias2;
+    rs.Dd = pk2(sc.h - B0, sc.h - B1) ^ kBias2;
+    rs.SMp = padds(pk2(sc.h - B0, sc.h - B1) ^ kBias2, k.smp);
     rs.SMtl = 0;
     rs.cI = 0; rs.cD = 0;
 }
@@ -521,12 +534,12 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
     if (ia == P0.n || ia + 1 == P0.n) {
         const bool fa = ia == P0.n;
         const uint32_t sm = psubs(fa ? st.a.SMp : st.b.SMp, k.smp), e = fa ? st.a.E : st.b.E;
-        pres0->end_SM = lo16(sm) + w.B0; pres0->end_E = lo16(e);
+        pres0->end_SM = lo16(sm ^ kBias2) + w.B0; pres0->end_E = lo16(e);
     }
     if (ia == P1.n || ia + 1 == P1.n) {
         const bool fa = ia == P1.n;
         const uint32_t sm = psubs(fa ? st.a.SMp : st.b.SMp, k.smp), e = fa ? st.a.E : st.b.E;
-        pres1->end_SM = hi16(sm) + w.B1; pres1->end_E = hi16(e);
+        pres1->end_SM = hi16(sm ^ kBias2) + w.B1; pres1->end_E = hi16(e);
     }
 }
 
@@ -608,8 +621,8 @@ __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, c
                     // lane 0 (column 16 c0) belongs to the previous block (or column 0)
                     const int u0 = lane == 0 ? bprev0 : nb0, u1 = lane == 0 ? bprev1 : nb1;
                     Rec r;
-                    r.dd = (int)pk2(dd0 - u0, dd1 - u1);
-                    r.sm = (int)pk2(sm0 - u0, sm1 - u1);
+                    r.dd = (int)(pk2(dd0 - u0, dd1 - u1) ^ kBias2);   // (biased halves)
+                    r.sm = (int)(pk2(sm0 - u0, sm1 - u1) ^ kBias2);
                     r.c2 = c2;
                     r.l = 0;
                     ring0[ring_slot(j)] = r;
@@ -631,11 +644,11 @@ __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, c
                     const int kk = j == 0 ? 0 : 1 + (((j - 1) >> 4) & (kBaseSlots - 1));
                     const int2 b = make_int2(baseW[2 * kk], baseW[2 * kk + 1]);
                     const unsigned long long a =
-                        (unsigned long long)(unsigned)(lo16((uint32_t)r.dd) + b.x) |
-                        ((unsigned long long)(unsigned)(hi16((uint32_t)r.dd) + b.y) << 32);
+                        (unsigned long long)(unsigned)(lo16((uint32_t)r.dd ^ kBias2) + b.x) |
+                        ((unsigned long long)(unsigned)(hi16((uint32_t)r.dd ^ kBias2) + b.y) << 32);
                     const unsigned long long bb =
-                        (unsigned long long)(unsigned)(lo16((uint32_t)r.sm) + b.x) |
-                        ((unsigned long long)(unsigned)(hi16((uint32_t)r.sm) + b.y) << 32);
+                        (unsigned long long)(unsigned)(lo16((uint32_t)r.sm ^ kBias2) + b.x) |
+                        ((unsigned long long)(unsigned)(hi16((uint32_t)r.sm ^ kBias2) + b.y) << 32);
                     gu64* q = (gu64*)(feed_out + j);
                     __hip_atomic_store(q, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(q + 1, bb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -681,7 +694,7 @@ __global__ __launch_bounds__((W + 1) * kWave, (W + 1 + 3) / 4) void fill_pk_kern
     const int smp = sc.sm, smmp = sc.smm;   // s - 2g: the launch's scores carry the shift (Scores32.shift)
     // score_max is kept as SM + sm'' (TBL: as SM; its tables add the score)
     const int off = (PLANES & 4) ? 0 : smp;
-    const PkScores k{pk2(sc.h, sc.h), pk2(off, off), pk2(smmp - smp, smmp - smp)};
+    const PkScores k{pk2(-sc.h, -sc.h), pk2(off, off), pk2(smmp - smp, smmp - smp)};
     for (;;) {
         if (threadIdx.x == 0) band_sh = atomicAdd(band_counter, 1);
         if (threadIdx.x < W + 1) { wcnt[threadIdx.x] = 0; rcnt[threadIdx.x] = 0; }

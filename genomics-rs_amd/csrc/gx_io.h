@@ -111,7 +111,9 @@ __device__ void io_wave(const PairDev& P, const int lb, const int lane, const Sc
             }
         }
         if (moved) idle = 0;
-        else if (++idle > kSpinLimit) {
+        else if (++idle > kSpinLimit ||
+                 ((idle & 4095u) == 4095u &&
+                  __hip_atomic_load((gint*)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
             __hip_atomic_store((gint*)status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
         } else {
