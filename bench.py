@@ -283,6 +283,50 @@ def fasta_pair(gx, which: str):
     return cont.sequences[0].sequence.encode(), cont.sequences[1].sequence.encode()
 
 
+def config_record(gx, ctx, which: str, steps: int):
+    """BASELINE configs 2 (Covid_Wuhan x Covid_USA-CA4, global) and 3 (Human x
+    Mouse BRCA2, local): the reference's align call (main.rs:143-150), one pair
+    per call, resident in HBM, with int32 score planes and traceback, `steps`
+    timed passes (bench.py's own clock), then one untimed pass with device
+    plane checksums compared with tests/golden/large_digests.json (score,
+    statistics, alignment sha256, the three plane checksums)."""
+    a, b = fasta_pair(gx, which)
+    local = which == "brca2"
+    scores = gx.Scores(*SCORES)
+    st = gx.StagedPairs([(a, b)], ctx=ctx)
+    st.run(scores, local, True)
+    t0 = time.perf_counter()
+    res, fms = st.run(scores, local, True, steps=steps)
+    el = time.perf_counter() - t0
+    finfo = ctx.fill_info()
+    cells = len(a) * len(b)
+    out = {"workload": f"{'Covid_Wuhan x Covid_USA-CA4' if which == 'covid' else 'Human x Mouse BRCA2 cds'} "
+                       f"({len(a)}x{len(b)}), {'local SW' if local else 'global NW'}, scores {SCORES}, "
+                       f"{plane_desc(finfo['plane_bytes_per_cell'])} + traceback",
+           "gcups": round(cells * steps / el / 1e9, 3), "ms_per_step": round(el / steps * 1e3, 3),
+           "fill_ms_avg": round(fms, 3), "fill_gcups": round(cells / (fms * 1e-3) / 1e9, 3), "steps": steps,
+           "fill_launch": finfo}
+    bpc = finfo["plane_bytes_per_cell"]
+    ach = bpc * cells / (fms * 1e-3) / 1e9
+    out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                       "frac": round(ach / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_cell": bpc,
+                       "note": "a single pair is latency-bound (the strip chain), not HBM-bound; DESIGN.md 6.6"}
+    with open(os.path.join(ROOT, "tests", "golden", "large_digests.json")) as f:
+        gold = {c["name"]: c for c in json.load(f)["cases"]}
+    g = gold["brca2/local" if local else "covid_wuhan_usa/global"]
+    res, _ = st.run(scores, local, True, plane_sums=True)
+    sums = [int(x) for x in st.plane_sums()[0, 0]]
+    r = res[0]
+    ok = (r.score == g["score"] and [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps] == g["stats"]
+          and r.n_steps == g["n_steps"] and alignment_sha256(st.steps(0)) == g["alignment_sha256"]
+          and sums == [int(x) for x in g["plane_sums"]])
+    if not ok:
+        raise RuntimeError(f"{which}: result differs from tests/golden/large_digests.json")
+    out["parity"] = {"bit_exact": True, "fields": "score, statistics, alignment sha256, I/D/S plane checksums",
+                     "source": "tests/golden/large_digests.json (oracle)"}
+    return out
+
+
 def allvsall_share(gx, rank: int, world: int):
     """BASELINE config 4: rank r's longest-processing-time share of the 45
     pairs i<j of the comparison_data genomes (files in name order, the same
@@ -457,6 +501,9 @@ def main():
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="1 GPU only: time every rank's shard of an N-GPU run in turn and print the predicted "
                          "N-GPU step time and scaling efficiency (not the headline line)")
+    ap.add_argument("--config-steps", type=int, default=5,
+                    help="synthetic, 1 GPU: also time BASELINE configs 2 and 3 (the single-pair align calls) "
+                         "with this many steps (0: skip)")
     ap.add_argument("--single-pair-steps", type=int, default=5,
                     help="also time BASELINE config 2's shape alone (one pair, latency), 1 GPU only; 0 = skip")
     ap.add_argument("--int32-steps", type=int, default=2,
@@ -670,6 +717,10 @@ def main():
                               "ms_per_step": round(e1 / args.single_pair_steps * 1e3, 3),
                               "fill_ms_avg": round(float(np.mean(f1)), 3), "steps": args.single_pair_steps}
         del one
+    if world == 1 and args.workload == "synthetic" and args.config_steps > 0:
+        # BASELINE configs 2 and 3, the drop-in single-pair align calls, timed here
+        out["config2"] = config_record(gx, ctx, "covid", args.config_steps)
+        out["config3"] = config_record(gx, ctx, "brca2", args.config_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if len(pairs[0][1]) > 40000:
             # the reference layout needs (n+1)(m+1) x 48 B (197 GB at 64k)

@@ -1517,8 +1517,12 @@ extern "C" int gx_alignment_table(gx_context* ctx, const uint8_t* s1, size_t n, 
     const bool lcs = (flags & GX_TABLE_MATCHES) != 0;
     if (n >= 1 && m >= 1) {
         t->job.table = true;   // exportable planes: the per-pair formats only
+        SmallAlpha alpha;      // (the batch paths' small-alphabet score table)
+        alpha.add(t->c1.data(), n);
+        alpha.add(t->c2.data(), m);
         rc = wide ? run_fill_wide(ctx, proc, ph, t->hs, is_local, planes, matches_at_max != nullptr, lcs, t->job)
-                  : run_fill(ctx, proc, ph, t->sc, is_local, planes, matches_at_max != nullptr, lcs, t->job);
+                  : run_fill(ctx, proc, ph, t->sc, is_local, planes, matches_at_max != nullptr, lcs, t->job, nullptr,
+                             nullptr, nullptr, &alpha);
         if (rc) { job_release(ctx, t->job); delete t; return rc; }
     } else {
         t->job.res.assign(1, PairRes{});

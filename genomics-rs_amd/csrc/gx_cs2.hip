@@ -31,6 +31,7 @@
 // steps per column each) instead of the sum of both instruction streams.
 // A band of W strips = W core + W side + 1 I/O wave (gx_io.h); W = 2 puts
 // every compute wave of a CU on its own SIMD.
+#include <stdlib.h>
 #include "gx_device.h"
 #include "gx_io.h"
 
@@ -47,47 +48,49 @@ struct SideGrp {
 };
 
 // lane 63's record of column j for the strip below: {dd, sm, c2} (Rec), or
-// the lane's scratch slot (full exec, no branch)
+// the lane's scratch slot (full exec, no branch).  Plain LDS stores, not
+// inline asm: the compiler may then schedule them into the dependent chain's
+// DPP wait states (a volatile asm statement ends a scheduling region); the
+// ring counter's publish (publish_all, a memory-clobbering asm) keeps them
+// before it.
+typedef __attribute__((address_space(3))) Rec lds_rec;
 template <int U>
 __device__ __forceinline__ void cs2_push(uint32_t vaddr, int dd, int sm, int c2) {
-    asm volatile(
-        "ds_write2_b32 %0, %1, %2 offset0:%4 offset1:%5\n\t"
-        "ds_write_b32 %0, %3 offset:%6"
-        :
-        : "v"(vaddr), "v"(dd), "v"(sm), "v"(c2), "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8)
-        : "memory");
+    lds_rec* r = (lds_rec*)(uintptr_t)vaddr + U;
+    r->dd = dd; r->sm = sm; r->c2 = c2;
 }
 
 // One column of the core recurrence for the 64 rows of the strip.
 // State (cell (i, j-1)): I = I'', SDh = max(S, D)'' + h, SM = score_max''.
 // r = ring record of column j (dd = D''(i0 + 1, j), sm = SM''(i0, j), c2);
 // psm = SM''(i0, j - 1).  fl = -(i + j) g (local floor, shifted).
-template <bool LOCAL, bool TBL>
+template <bool LOCAL, bool TBL, bool ASM = GX_CS2_ASM>
 __device__ __forceinline__ void cs2_core_step(int& I, int& SDh, int& SM, const int psm, const int fl, const Rec& r,
                                               const int c1v, const Scores32& sc, const int hv, int& oI, int& oS,
                                               int& oD, int& dd_out) {
     const int scv = TBL ? __builtin_amdgcn_sbfe(c1v, r.c2, 8) : (r.c2 == c1v ? sc.sm : sc.smm);
     const int In = LOCAL ? max3i(I, SDh, fl) : max(I, SDh);
-#if GX_CS2_ASM
+    int Sn, IS, Y, Z;
+    if constexpr (ASM) {
     // the two cross-lane moves fused with their adds (v_add_u32_dpp, lane 0
     // keeps the destination's value: the ring's input set beforehand), one
     // VALU op each on the column's dependent chain instead of a v_mov_dpp,
     // its old-value copy and the add; the s_nop covers the DPP read-after-
     // VALU-write hazard, which the compiler does not track into inline asm
-    int Sn = psm + scv;                             // lane 0: SM''(i0, j-1) + s''
+    Sn = psm + scv;                                 // lane 0: SM''(i0, j-1) + s''
     asm("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
         : "+v"(Sn) : "v"(SM), "v"(scv));
-    const int IS = max(In, Sn);
-    const int Y = IS + sc.h;
-    int Z = r.dd;                                   // lane 0: D''(i0 + 1, j)
+    IS = max(In, Sn);
+    Y = IS + sc.h;
+    Z = r.dd;                                       // lane 0: D''(i0 + 1, j)
     asm("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
         : "+v"(Z) : "v"(IS), "v"(hv));            // lane l: IS''(l-1) + h
-#else
-    const int Sn = shr1(psm, SM) + scv;             // lane 0: SM''(i0, j-1) from the ring
-    const int IS = max(In, Sn);
-    const int Y = IS + sc.h;
-    int Z = shr1(r.dd, Y);                          // lane 0: D''(i0 + 1, j); lane l: IS''(l-1) + h
-#endif
+    } else {
+    Sn = shr1(psm, SM) + scv;                       // lane 0: SM''(i0, j-1) from the ring
+    IS = max(In, Sn);
+    Y = IS + sc.h;
+    Z = shr1(r.dd, Y);                              // lane 0: D''(i0 + 1, j); lane l: IS''(l-1) + h
+    }
     Z = scan_max64(Z);
     const int Dn = LOCAL ? max(Z, fl) : Z;
     SM = max(IS, Dn);
@@ -101,50 +104,59 @@ __device__ __forceinline__ void cs2_core_step(int& I, int& SDh, int& SM, const i
 // the same ring protocol as layout 1's cs_group4 -- observe the producer's
 // counter, read the next group's records speculatively, compute, re-read
 // after a wait if the counter did not cover them.
-template <bool LOCAL, bool TBL, int KSB, bool TAIL, int G>
+template <bool LOCAL, bool TBL, int KSB, bool TAIL, int G, int DIAG>
 __device__ __forceinline__ void cs2_core_group(int& I, int& SDh, int& SM, int& psm, int& fl, Rec (&cur)[4],
                                                Rec (&nxt)[4], const int t0, const int m, const int c1v,
                                                const Scores32& sc, const Rec* ring_in, lds_int* wcnt_in,
                                                SideGrp* sb, const int lane, const uint32_t pa, const uint32_t scr,
-                                               const uint32_t cnt_addr, const int hv, int* status) {
+                                               const uint32_t cnt_addr, const int hv, unsigned& twin,
+                                               int* status) {
     constexpr int kSBG = KSB / 4;
     const int t = t0 + 4 * G;
     const int need = min(t + 8, m) + 1;             // (the next group may be past column m)
-    const int seen = *wcnt_in;
+    const int seen = DIAG == 7 ? 0 : *wcnt_in;
     asm volatile("" ::: "memory");
     // the next group's 4 records: slots (t + 20 .. t + 23) mod kRing, one
     // aligned block of 4 (t is a multiple of 4)
     const Rec* const nb = ring_in + ring_slot(t + 5);
-    nxt[0] = nb[0]; nxt[1] = nb[1]; nxt[2] = nb[2]; nxt[3] = nb[3];
+    if (DIAG < 4) { nxt[0] = nb[0]; nxt[1] = nb[1]; nxt[2] = nb[2]; nxt[3] = nb[3]; }
     int oI[4], oS[4], oD[4];
 #pragma unroll
     for (int U = 0; U < 4; ++U) {
         int dd;
-        cs2_core_step<LOCAL, TBL>(I, SDh, SM, psm, fl, cur[U], c1v, sc, hv, oI[U], oS[U], oD[U], dd);
+        if (DIAG == 2) {   // (timing only: no recurrence, the side alone sets the pace)
+            oI[U] = I + cur[U].dd; oS[U] = SDh + cur[U].sm; oD[U] = SM; dd = oI[U]; SM = oS[U];
+        } else
+            cs2_core_step<LOCAL, TBL, DIAG == 6 ? false : bool(GX_CS2_ASM)>(I, SDh, SM, psm, fl, cur[U], c1v, sc, hv,
+                                                                            oI[U], oS[U], oD[U], dd);
         psm = cur[U].sm;
         if (LOCAL) fl -= sc.g;
         // lane 63's record of column t + U + 1 (none past column m)
         const uint32_t a = (TAIL && t + U + 1 > m) ? scr : pa;
+        if (DIAG == 8) { asm volatile("" :: "v"(dd), "v"(SM)); continue; }
         if (U == 0) cs2_push<4 * G + 0>(a, dd, SM, cur[U].c2);
         if (U == 1) cs2_push<4 * G + 1>(a, dd, SM, cur[U].c2);
         if (U == 2) cs2_push<4 * G + 2>(a, dd, SM, cur[U].c2);
         if (U == 3) cs2_push<4 * G + 3>(a, dd, SM, cur[U].c2);
     }
     SideGrp& g = sb[(t >> 2) & (kSBG - 1)];
-    g.v[0][lane] = make_int4(oI[0], oI[1], oI[2], oI[3]);
-    g.v[1][lane] = make_int4(oS[0], oS[1], oS[2], oS[3]);
-    g.v[2][lane] = make_int4(oD[0], oD[1], oD[2], oD[3]);
+    if (DIAG >= 3) {   // (timing only: nothing staged; keeps the values alive)
+        asm volatile("" :: "v"(oI[0] ^ oI[1] ^ oI[2] ^ oI[3] ^ oS[0] ^ oS[1] ^ oS[2] ^ oS[3] ^ oD[0] ^ oD[1] ^ oD[2] ^ oD[3]));
+    } else {
+        g.v[0][lane] = make_int4(oI[0], oI[1], oI[2], oI[3]);
+        g.v[1][lane] = make_int4(oS[0], oS[1], oS[2], oS[3]);
+        g.v[2][lane] = make_int4(oD[0], oD[1], oD[2], oD[3]);
+    }
     // the records and staging of columns .. t + 4 are written (one wave's DS
     // operations execute in order): publish to the strip below and the side
-    publish_all(cnt_addr, TAIL ? min(t + 5, m + 1) : t + 5);
-    if (__builtin_amdgcn_readfirstlane(seen) < need) {
-        wait_ge(wcnt_in, need, status);
+    if (DIAG != 7) publish_all(cnt_addr, TAIL ? min(t + 5, m + 1) : t + 5);
+    if (DIAG < 4 && __builtin_amdgcn_readfirstlane(seen) < need) {
+        twin += wait_ge(wcnt_in, need, status) + 1;
         nxt[0] = nb[0]; nxt[1] = nb[1]; nxt[2] = nb[2]; nxt[3] = nb[3];
     }
-    __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool LOCAL, bool TBL, int KSB>
+template <bool LOCAL, bool TBL, int KSB, int DIAG>
 __device__ __forceinline__ void cs2_core(const PairDev& P, const int s, const int lane, const Scores32& sc, const Rec* ring_in,
                          Rec* ring_out, lds_int* wcnt_in, lds_int* rcnt_in, lds_int* wcnt_out, lds_int* rcnt_out,
                          lds_int* scnt, SideGrp* sb, const bool has_consumer, int* status, const uint32_t scratch) {
@@ -181,6 +193,22 @@ __device__ __forceinline__ void cs2_core(const PairDev& P, const int s, const in
         ra[2] = ring_in[ring_slot(3)]; ra[3] = ring_in[ring_slot(4)];
     }
     const uint32_t scr = scratch + 4u * (uint32_t)lane;
+    unsigned tr_wait_in = 0, tr_wait_sb = 0;       // wait iterations (diagnostics)
+    if (DIAG == 9) {   // (timing only: the recurrence alone in registers, m columns)
+        int acc = 0;
+        const int x0 = psm;
+        for (int t0 = 0; t0 < m; t0 += kSub) {
+#pragma unroll
+            for (int u = 0; u < kSub; ++u) {
+                Rec r{x0 + u, x0 - u, (u & 3) * 8, 0};
+                int a0, a1, a2, dd;
+                cs2_core_step<LOCAL, TBL>(I, SDh, SM, psm, fl, r, c1v, sc, sc.h, a0, a1, a2, dd);
+                acc ^= dd ^ a0 ^ a1 ^ a2;
+            }
+        }
+        if (acc == 0x7FFFFFFF) ring_out[0].dd = acc;
+        return;
+    }
     int hv = sc.h;                                  // (a VGPR: the DPP add's second operand)
     asm volatile("" : "+v"(hv));
     for (int t0 = 0; t0 < m; t0 += kSub) {
@@ -192,29 +220,33 @@ __device__ __forceinline__ void cs2_core(const PairDev& P, const int s, const in
         if (has_consumer && last_col >= kRing) wait_ge(rcnt_out, last_col - kRing + 1, status);
         // staging slots free: group g reuses the slot of group g - KSB/4, so the
         // sub-block's last group needs the side past column 4 (g - KSB/4) + 4
-        if (t0 + 12 >= KSB) wait_ge(scnt, min(t0 + 17 - KSB, m + 1), status);
+        if (DIAG < 5 && t0 + 12 >= KSB) tr_wait_sb += wait_ge(scnt, min(t0 + 17 - KSB, m + 1), status);
         const uint32_t out_base = lds_addr(ring_out + ring_slot(t0 + 1));
         const uint32_t pa = has_consumer && lane == kWave - 1 ? out_base : scr;
         if (t0 + kSub <= m) {
-            cs2_core_group<LOCAL, TBL, KSB, false, 0>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
-            cs2_core_group<LOCAL, TBL, KSB, false, 1>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
-            cs2_core_group<LOCAL, TBL, KSB, false, 2>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
-            cs2_core_group<LOCAL, TBL, KSB, false, 3>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
+            cs2_core_group<LOCAL, TBL, KSB, false, 0, DIAG>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, tr_wait_in, status);
+            cs2_core_group<LOCAL, TBL, KSB, false, 1, DIAG>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, tr_wait_in, status);
+            cs2_core_group<LOCAL, TBL, KSB, false, 2, DIAG>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, tr_wait_in, status);
+            cs2_core_group<LOCAL, TBL, KSB, false, 3, DIAG>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, tr_wait_in, status);
         } else {
-            cs2_core_group<LOCAL, TBL, KSB, true, 0>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
-            cs2_core_group<LOCAL, TBL, KSB, true, 1>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
-            cs2_core_group<LOCAL, TBL, KSB, true, 2>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
-            cs2_core_group<LOCAL, TBL, KSB, true, 3>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, status);
+            cs2_core_group<LOCAL, TBL, KSB, true, 0, DIAG>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, tr_wait_in, status);
+            cs2_core_group<LOCAL, TBL, KSB, true, 1, DIAG>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, tr_wait_in, status);
+            cs2_core_group<LOCAL, TBL, KSB, true, 2, DIAG>(I, SDh, SM, psm, fl, ra, rb, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, tr_wait_in, status);
+            cs2_core_group<LOCAL, TBL, KSB, true, 3, DIAG>(I, SDh, SM, psm, fl, rb, ra, t0, m, c1v, sc, ring_in, wcnt_in, sb, lane, pa, scr, cnt_addr, hv, tr_wait_in, status);
         }
         lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
     }
     if (trace && lane == 0) {
         StripTrace tr;
         tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
-        tr.wait_in = (int)tr_win0; tr.wait_out = 0;
+        tr.wait_in = (int)(tr_win0 + tr_wait_in); tr.wait_out = (int)tr_wait_sb;
         tr.clk = __builtin_amdgcn_s_memtime() - clk_first;
-        for (int q = 0; q < kTraceQ; ++q) tr.t_q[q] = tr_q[q];
-        trace[s] = tr;
+        for (int q = 0; q < kTraceQ - 1; ++q) tr.t_q[q] = tr_q[q];
+        // (t_q[kTraceQ - 1] belongs to the side wave: its own wait iterations)
+        long long* d = &trace[s].t_start;
+        d[0] = tr.t_start; d[1] = tr.t_first; d[2] = tr.t_end;
+        trace[s].wait_in = tr.wait_in; trace[s].wait_out = tr.wait_out; trace[s].clk = tr.clk;
+        for (int q = 0; q < kTraceQ - 1; ++q) trace[s].t_q[q] = tr.t_q[q];
     }
 }
 
@@ -228,24 +260,16 @@ __device__ __forceinline__ void cs2_core(const PairDev& P, const int s, const in
 __device__ __forceinline__ void cs2_side_bits(const int In, const int Sn, const int Dn, const int t, const int kl,
                                               const uint32_t low24, int& Ek, uint32_t& cI, uint32_t& cD) {
     const int IS = max(In, Sn);
+    const bool m1 = In > Sn, m2 = Dn > IS;          // insert beats sub; delete beats both
+    // the landing-column chain (depends on the previous column's Ek only
+    // through etl and the select): builtins, so that the compiler fills its
+    // DPP wait states with the independent compares and code bits
     const int etl = shr1(t + 64, Ek);               // lane 0: (i0, j - 1) on the boundary -> E = j - 1
     const int dkey = t + 65;                        // delete with no non-delete lane above: E = j
-    int key;
-    unsigned long long m1, m2, k1, k2;
-    // one asm block: each compare feeds its code bit (v_addc shift-in) and its
-    // select, so no mask stays alive (layout 1's cs_step does the same)
-    asm volatile(
-        "v_cmp_gt_i32 %[m1], %[in], %[sn]\n\t"
-        "v_cmp_gt_i32 %[m2], %[dn], %[is]\n\t"
-        "v_cndmask_b32 %[key], %[etl], %[el], %[m1]\n\t"
-        "v_addc_co_u32 %[ci], %[k1], %[ci], %[ci], %[m1]\n\t"
-        "v_bfi_b32 %[key], %[lo], %[key], %[kl]\n\t"
-        "v_addc_co_u32 %[cd], %[k2], %[cd], %[cd], %[m2]\n\t"
-        "v_cndmask_b32 %[key], %[key], %[dk], %[m2]"
-        : [key] "=&v"(key), [ci] "+v"(cI), [cd] "+v"(cD), [m1] "=&s"(m1), [m2] "=&s"(m2), [k1] "=&s"(k1),
-          [k2] "=&s"(k2)
-        : [in] "v"(In), [sn] "v"(Sn), [dn] "v"(Dn), [is] "v"(IS), [etl] "v"(etl), [el] "v"(Ek), [kl] "v"(kl),
-          [dk] "v"(dkey), [lo] "s"(low24));
+    int key = (int)((((uint32_t)(m1 ? Ek : etl)) & low24) | (uint32_t)kl);
+    key = m2 ? dkey : key;
+    cI = cI + cI + (m1 ? 1u : 0u);
+    cD = cD + cD + (m2 ? 1u : 0u);
     Ek = scan_max64(key);
 }
 
@@ -260,18 +284,19 @@ struct Cs2Side {
 };
 
 // One 4-column group of the side wave (columns t + 1 .. t + 4).
-template <bool LOCAL, bool PLANES, int KSB, bool TAIL>
+template <bool LOCAL, bool PLANES, int KSB, bool TAIL, int DIAG>
 __device__ __forceinline__ void cs2_side_group(Cs2Side& st, const int t, const int m, const int lane, const int kl,
                                                const Scores32& sc, lds_int* wcnt_core, const uint32_t scnt_addr,
                                                const SideGrp* sb, const __amdgpu_buffer_rsrc_t& rI,
                                                const __amdgpu_buffer_rsrc_t& rD, const __amdgpu_buffer_rsrc_t& rS,
                                                const __amdgpu_buffer_rsrc_t& skel_rsrc, const uint32_t skel_voff,
-                                               int* status) {
+                                               unsigned& twait, int* status) {
     constexpr int kSBG = KSB / 4;
-    wait_ge(wcnt_core, TAIL ? min(t + 5, m + 1) : t + 5, status);
+    twait += wait_ge(wcnt_core, TAIL ? min(t + 5, m + 1) : t + 5, status);
     const SideGrp& g = sb[(t >> 2) & (kSBG - 1)];
     const int4 vI = g.v[0][lane], vS = g.v[1][lane], vD = g.v[2][lane];
     publish_all(scnt_addr, TAIL ? min(t + 5, m + 1) : t + 5);   // (after the reads: in-order DS execution)
+    if (DIAG == 1 || DIAG >= 3) return;   // (timing only: the side consumes, the core alone sets the pace)
     const int aI[4] = {vI.x, vI.y, vI.z, vI.w}, aS[4] = {vS.x, vS.y, vS.z, vS.w}, aD[4] = {vD.x, vD.y, vD.z, vD.w};
     int e[4];
 #pragma unroll
@@ -296,10 +321,9 @@ __device__ __forceinline__ void cs2_side_group(Cs2Side& st, const int t, const i
     // skeleton: lane 63's E + 64 of columns t .. t + 3 (16-B aligned)
     skel_store4(skel_rsrc, skel_voff + 4u * (uint32_t)t, st.e_last, e[0], e[1], e[2]);
     st.e_last = e[3];
-    __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool LOCAL, bool PLANES, int KSB>
+template <bool LOCAL, bool PLANES, int KSB, int DIAG>
 __device__ __forceinline__ void cs2_side(const PairDev& P, const int s, const int lane, const Scores32& sc,
                                          lds_int* wcnt_core, lds_int* scnt, const SideGrp* sb,
                                          const bool has_consumer, StripRes* sres, PairRes* pres, int* status) {
@@ -327,18 +351,19 @@ __device__ __forceinline__ void cs2_side(const PairDev& P, const int s, const in
     st.fl = LOCAL ? -(i + 1) * sc.g : 0;
     st.lbest = ok ? INT_MIN : INT_MAX; st.lstep = 0; st.lE = 0;
     st.fin_sm = 0; st.fin_E = 0;
+    unsigned twait = 0;
     for (int t0 = 0; t0 < m; t0 += kSub) {
         // the sub-block holding column m always runs as a tail (the end cell is taken there)
         if (t0 + kSub < m) {
 #pragma unroll
             for (int G = 0; G < 4; ++G)
-                cs2_side_group<LOCAL, PLANES, KSB, false>(st, t0 + 4 * G, m, lane, kl, sc, wcnt_core, scnt_addr, sb,
-                                                          rI, rD, rS, skel_rsrc, skel_voff, status);
+                cs2_side_group<LOCAL, PLANES, KSB, false, DIAG>(st, t0 + 4 * G, m, lane, kl, sc, wcnt_core, scnt_addr, sb,
+                                                          rI, rD, rS, skel_rsrc, skel_voff, twait, status);
         } else {
 #pragma unroll
             for (int G = 0; G < 4; ++G)
-                cs2_side_group<LOCAL, PLANES, KSB, true>(st, t0 + 4 * G, m, lane, kl, sc, wcnt_core, scnt_addr, sb,
-                                                         rI, rD, rS, skel_rsrc, skel_voff, status);
+                cs2_side_group<LOCAL, PLANES, KSB, true, DIAG>(st, t0 + 4 * G, m, lane, kl, sc, wcnt_core, scnt_addr, sb,
+                                                         rI, rD, rS, skel_rsrc, skel_voff, twait, status);
         }
         gstore1(codes + (size_t)(t0 >> 4) * kWave + lane, (st.cD << 16) | (st.cI & 0xFFFFu));
     }
@@ -359,9 +384,10 @@ __device__ __forceinline__ void cs2_side(const PairDev& P, const int s, const in
         }
     }
     if (ok && i == n) { pres->end_SM = st.fin_sm; pres->end_E = (st.fin_E & 0xFFFFFF) - 64; }
+    if (P.trace && lane == 0) P.trace[s].t_q[kTraceQ - 1] = (long long)twait;   // diagnostics
 }
 
-template <int W, bool LOCAL, bool PLANES, bool TBL>
+template <int W, bool LOCAL, bool PLANES, bool TBL, int DIAG = 0>
 __global__ __launch_bounds__((2 * W + 1) * kWave) void fill_cs2_kernel(const PairDev* __restrict__ pairs,
                                                                        const int npairs, const int total_bands,
                                                                        int* band_counter, StripRes* sres,
@@ -388,19 +414,21 @@ __global__ __launch_bounds__((2 * W + 1) * kWave) void fill_cs2_kernel(const Pai
         const PairDev& P = pairs[p];
         const int lb = __builtin_amdgcn_readfirstlane(ob.y);
         const int s0 = lb * W;
-        if (wave < 2 * W) {
+        if (DIAG >= 5 && wave >= W && wave < 2 * W) {
+            // (timing only: the core waves and the I/O wave alone -- no side)
+        } else if (wave < 2 * W) {
             const int k = wave < W ? wave : wave - W;
             const int s = s0 + k;
             if (s < P.strips) {
                 const bool last_in_band = k == W - 1;
                 const bool has_consumer = last_in_band ? (lb + 1 < P.bands) : (s + 1 < P.strips);
                 if (wave < W)
-                    cs2_core<LOCAL, TBL, KSB>(P, s, lane, sc, rings[k], rings[k + 1], (lds_int*)&wcnt[k],
+                    cs2_core<LOCAL, TBL, KSB, DIAG>(P, s, lane, sc, rings[k], rings[k + 1], (lds_int*)&wcnt[k],
                                               (lds_int*)&rcnt[k], (lds_int*)&wcnt[k + 1], (lds_int*)&rcnt[k + 1],
                                               (lds_int*)&scnt[k], sbuf[k], has_consumer, band_counter + 1,
                                               lds_addr(push_scratch[k]));
                 else
-                    cs2_side<LOCAL, PLANES, KSB>(P, s, lane, sc, (lds_int*)&wcnt[k + 1], (lds_int*)&scnt[k],
+                    cs2_side<LOCAL, PLANES, KSB, DIAG>(P, s, lane, sc, (lds_int*)&wcnt[k + 1], (lds_int*)&scnt[k],
                                                  sbuf[k], has_consumer, sres, pres + p, band_counter + 1);
             }
         } else {
@@ -415,6 +443,31 @@ __global__ __launch_bounds__((2 * W + 1) * kWave) void fill_cs2_kernel(const Pai
 template <int W, bool LOCAL, bool PLANES, bool TBL>
 static hipError_t launch_cs2_t(const PairDev* d_pairs, int npairs, int total_bands, int* d_counter, StripRes* d_sres,
                                PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
+    // GX_CS2_DIAG (timing diagnostics, wrong results): 1 = the side only
+    // consumes the staging, 2 = the core skips the recurrence, 3 = 1 and the
+    // core stages nothing, 4 = 3 and the core reads no ring records, 5 = 4 with
+    // the side waves idle (the core wave and the I/O wave alone on the CU); 6, 7, 8 = 5
+    // with the builtin DPP moves, without the counters, without the pushes
+    if constexpr (W == 2 && !LOCAL && PLANES && TBL) {
+        if (const char* e = getenv("GX_CS2_DIAG"); e && atoi(e) >= 1 && atoi(e) <= 9) {
+#define GX_CS2_DG(D) hipLaunchKernelGGL((fill_cs2_kernel<W, LOCAL, PLANES, TBL, D>), dim3(grid), \
+                                        dim3((2 * W + 1) * kWave), 0, st, d_pairs, npairs, total_bands, d_counter, \
+                                        d_sres, d_pres, sc)
+            switch (atoi(e)) {
+                case 1: GX_CS2_DG(1); break;
+                case 2: GX_CS2_DG(2); break;
+                case 3: GX_CS2_DG(3); break;
+                case 4: GX_CS2_DG(4); break;
+                case 5: GX_CS2_DG(5); break;
+                case 6: GX_CS2_DG(6); break;
+                case 7: GX_CS2_DG(7); break;
+                case 8: GX_CS2_DG(8); break;
+                default: GX_CS2_DG(9); break;
+            }
+#undef GX_CS2_DG
+            return hipGetLastError();
+        }
+    }
     hipLaunchKernelGGL((fill_cs2_kernel<W, LOCAL, PLANES, TBL>), dim3(grid), dim3((2 * W + 1) * kWave), 0, st, d_pairs,
                        npairs, total_bands, d_counter, d_sres, d_pres, sc);
     return hipGetLastError();

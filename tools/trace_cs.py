@@ -16,7 +16,13 @@ G = os.path.join(ROOT, "tests", "golden")
 out = os.path.join(ROOT, "gpurun_out")
 os.makedirs(out, exist_ok=True)
 ctx = gx.Context(0)
-cases = [("covid", os.path.join(G, "comparison_data", "Covid_Wuhan.fasta"),
+import random  # noqa: E402
+rng = random.Random(3)
+syn = os.path.join(out, "syn64.fasta")
+with open(syn, "w") as f:
+    f.write(">a\n" + "".join(rng.choice("ACGT") for _ in range(64)) + "\n>b\n" +
+            "".join(rng.choice("ACGT") for _ in range(30000)) + "\n")
+cases = [("syn64", syn, None, False), ("covid", os.path.join(G, "comparison_data", "Covid_Wuhan.fasta"),
           os.path.join(G, "comparison_data", "Covid_USA-CA4.fasta"), False),
          ("brca2", os.path.join(G, "fasta", "Human-Mouse-BRCA2-cds.fasta"), None, True)]
 tag = os.environ.get("GX_TRACE_TAG", "")
@@ -38,3 +44,11 @@ for name, f1, f2, local in cases:
     print(name, len(c.sequences[0].sequence), len(c.sequences[1].sequence), "fill_us", al.fill_us,
           "retrace_us", al.retrace_us, ctx.fill_info(), flush=True)
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "trace_summary.py"), path])
+    import csv
+    rows = list(csv.DictReader(open(path)))
+    m = len(c.sequences[1].sequence)
+    for k in sorted(set([0, 1, len(rows) // 2, len(rows) - 1])):
+        r = rows[k]
+        dur = (int(r["t_end"]) - int(r["t_first"])) / 100.0
+        print(f"  strip {k}: {dur:.0f} us = {dur * 1000 / m:.1f} ns/col, clk/col {int(r['clk']) / m:.0f}, "
+              f"core input waits {r['wait_in']}, core staging waits {r['wait_out']}, side waits {r['q7']}")
