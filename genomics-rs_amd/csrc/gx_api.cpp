@@ -571,9 +571,15 @@ static bool w16_ok(const Scores32& sc) {
 // narrowest instantiated width whose bands fit the grid (W = 2: every compute
 // wave of a CU on its own SIMD), else 7-strip bands queued for workgroups
 // (GX_BAND_WAVES forces an instantiated width).
-static bool cs2_enabled() {
+// The split column step (gx_cs2.hip) by default for local fills only: on a
+// 30k global pair its two-wave strips in two-strip bands lose to layout 1's
+// one-wave strips in four-strip bands (more band hand-offs through HBM,
+// 5.33 vs 4.53 ms; BRCA2 local 1.76 vs 1.79 ms, profiles/r03a_bench.json).
+// GX_CS2=1 / 0 forces it on / off.
+static bool cs2_enabled(int is_local) {
     const char* e = getenv("GX_CS2");
-    return !(e && !strcmp(e, "0"));
+    if (e && *e) return strcmp(e, "0") != 0;
+    return is_local != 0;
 }
 static int cs2_band_waves(int total_strips, int grid_cap) {
     static constexpr int kCs2Widths[] = {1, 2, 3, 4, 7};
@@ -757,7 +763,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     for (const PairHost& h : ph) min_strips = std::min(min_strips, ceil_div((int)h.n, SR));
     // the split column step (gx_cs2.hip): layout 1's formats, each strip on a
     // core and a side wave; untracked fills (global or local)
-    const bool cs2 = lay == 1 && !track && cs2_enabled();
+    const bool cs2 = lay == 1 && !track && cs2_enabled(is_local);
     const int W = cs2 ? cs2_band_waves(total_strips, fill_grid_cap(ctx->device))
                       : fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device), lay, min_strips);
     job.lay = lay;

@@ -31,12 +31,14 @@ LAUNCH_SHAPES = {"auto": {},
                  "w15_grid2": {"GX_LAYOUT": "0", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "2"},
                  # the pair-major band queue of earlier versions (the default is band-major)
                  "pair_order": {"GX_LAYOUT": "0", "GX_BAND_ORDER": "pair", "GX_FILL_GRID": "3"},
-                 # layout 1: column-step fill over 64-row strips (gx_internal.h), by
-                 # default the split core + side waves (gx_cs2.hip); one-band bands
-                 # queued on a 2-workgroup grid (every hand-off through HBM)
-                 "cs": {"GX_LAYOUT": "1"}, "cs_w7": {"GX_LAYOUT": "1", "GX_BAND_WAVES": "7"},
-                 "cs_w1_grid2": {"GX_LAYOUT": "1", "GX_BAND_WAVES": "1", "GX_FILL_GRID": "2"},
-                 # layout 1's one-wave strips (GX_CS2=0)
+                 # layout 1: column-step fill over 64-row strips (gx_internal.h), as
+                 # the split core + side waves (gx_cs2.hip, GX_CS2=1; the default for
+                 # local fills); one-band bands queued on a 2-workgroup grid (every
+                 # hand-off through HBM)
+                 "cs": {"GX_LAYOUT": "1", "GX_CS2": "1"},
+                 "cs_w7": {"GX_LAYOUT": "1", "GX_CS2": "1", "GX_BAND_WAVES": "7"},
+                 "cs_w1_grid2": {"GX_LAYOUT": "1", "GX_CS2": "1", "GX_BAND_WAVES": "1", "GX_FILL_GRID": "2"},
+                 # layout 1's one-wave strips (GX_CS2=0; the default for global fills)
                  "cs1": {"GX_LAYOUT": "1", "GX_CS2": "0"},
                  "cs1_w15_grid2": {"GX_LAYOUT": "1", "GX_CS2": "0", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "2"}}
 

@@ -47,7 +47,7 @@ for name, f1, f2, local in cases:
     import csv
     rows = list(csv.DictReader(open(path)))
     m = len(c.sequences[1].sequence)
-    for k in sorted(set([0, 1, len(rows) // 2, len(rows) - 1])):
+    for k in sorted(set(k for k in (0, 1, len(rows) // 2, len(rows) - 1) if 0 <= k < len(rows))):
         r = rows[k]
         dur = (int(r["t_end"]) - int(r["t_first"])) / 100.0
         print(f"  strip {k}: {dur:.0f} us = {dur * 1000 / m:.1f} ns/col, clk/col {int(r['clk']) / m:.0f}, "
