@@ -32,7 +32,7 @@ hipError_t launch_fill(int W, int lay, bool local, int planes, bool track, bool 
                        hipStream_t st);
 hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d_sres, PairRes* d_pres,
                            hipStream_t st);
-hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, bool w16, hipStream_t st);
+hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, bool w16, bool seq, hipStream_t st);
 hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, int gshift, int row0,
                          int rows, hipStream_t st);
 hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, int n, int m, int t4, int h, int g,
@@ -640,6 +640,7 @@ struct FillJob {
     bool twin = false;                  // the twin fill (gx_fill_pk.hip): twin_table's pairs share every band
     bool w16 = false;                   // twin plane codes, 2 B per cell (w16_ok; batches only)
     bool nocodes = false;               // w16 without code words: the traceback derives them from the planes
+    bool noskel = false;                // nocodes without landing columns: the traceback walks the strips in sequence
     bool table = false;                 // an alignment table (exportable planes: never the twin codes)
     int g = 0;
     double fill_ms = 0.0;
@@ -820,6 +821,12 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     // (tb_w16_codes_kernel); GX_TWIN_CODES=1 keeps them
     const char* tce = getenv("GX_TWIN_CODES");
     job.nocodes = w16 && !(tce && !strcmp(tce, "1"));
+    // ... and no landing columns either (a quarter of the twin cell's VALU):
+    // the traceback then walks the strips one after another, each entered
+    // where the one below left it (tb_seq_kernel); GX_TWIN_SKEL=1 keeps the
+    // skeleton and the parallel strip walks
+    const char* tse = getenv("GX_TWIN_SKEL");
+    job.noskel = job.nocodes && !(tse && !strcmp(tse, "1"));
     // small-alphabet twins: the match test through score tables (cell_pk; the
     // shifted scores must fit an unsigned byte);
     // the byte-plane twin (tables) keeps the plain test
@@ -990,7 +997,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].fb : ctx->ev0, eve = slot >= 0 ? ctx->slots[slot].fe : ctx->ev1;
     HIPCHK(hipEventRecord(evb, ctx->stream));
     if (bands > 0 && twin)
-        HIPCHK(launch_fill_pk(Wf, (planes ? (w16 ? 2 : 1) : 0) + (twin_tbl ? 4 : 0) + (job.nocodes ? 8 : 0),
+        HIPCHK(launch_fill_pk(Wf, (planes ? (w16 ? 2 : 1) : 0) + (twin_tbl ? 4 : 0) + (job.nocodes ? 8 : 0) +
+                                  (job.noskel ? 16 : 0),
                               (const PairDev*)job.pairs.p, (int)P, (int)tw.size(), bands, (int*)job.counter.p,
                               (PairRes*)job.pres.p, scl, grid, ctx->stream));
     else if (bands > 0 && cs2)
@@ -1349,7 +1357,7 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     if (e == hipSuccess) e = hipMemsetAsync(seg.p, 0, std::max<size_t>(stot, 1) * 4 * sizeof(int), ctx->stream);
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].tb : ctx->ev1, eve = slot >= 0 ? ctx->slots[slot].te : ctx->ev2;
     if (e == hipSuccess) e = hipEventRecord(evb, ctx->stream);
-    if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, max_strips, job.nocodes, ctx->stream);
+    if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, max_strips, job.nocodes, job.noskel, ctx->stream);
     if (e == hipSuccess) e = hipEventRecord(eve, ctx->stream);
     // one pinned host block: c | sg | hr
     const size_t nc = 4 * P, nsg = 4 * std::max<size_t>(stot, 1), nhr = std::max<size_t>(stot, 1) * SR;

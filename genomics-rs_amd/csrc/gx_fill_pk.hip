@@ -173,7 +173,7 @@ struct LanePk {
 // algo.rs:222-268 on the shifted values, both pairs at once; MASKED keeps
 // the lanes outside columns 1..m unchanged, per pair (a twin's two pairs may
 // differ in length: the shorter one's state stays at its last column).
-template <bool MASKED, bool TBL, bool CODES>
+template <bool MASKED, bool TBL, bool CODES, bool NOE = false>
 __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const uint32_t sm_in, const uint32_t e_up,
                                         const uint32_t c2, const uint32_t c1, const uint32_t c1h, const uint32_t act,
                                         const PkScores& k,
@@ -192,25 +192,30 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
     const uint32_t SDn = pmaxu(Sn, Dn);
     const uint32_t Ddn = pmaxu(IS - k.nh, Dn);                     // D(i+1, j)
     // retrace priority S > I > D (algo.rs:351-400): m1 = I beats S, m2 = D beats both
-    const uint32_t m1 = psign(psub(Sn, In)), m2 = psign(psub(IS, Dn));
-    const uint32_t E1 = bfi(m1, st.E, st.Etl);
-    const uint32_t En = bfi(m2, e_up, E1);
+    // (NOE: no landing columns -- the twin fill without a skeleton, whose
+    // traceback walks the strips in sequence, tb_seq_kernel; with no code
+    // words either, neither mask is needed)
+    const uint32_t m1 = (CODES || !NOE) ? psign(psub(Sn, In)) : 0u, m2 = (CODES || !NOE) ? psign(psub(IS, Dn)) : 0u;
+    const uint32_t E1 = NOE ? 0u : bfi(m1, st.E, st.Etl);
+    const uint32_t En = NOE ? 0u : bfi(m2, e_up, E1);
     const uint32_t cIn = CODES ? pcode(st.cI, m1) : 0u;   // (no code words: the traceback derives
     const uint32_t cDn = CODES ? pcode(st.cD, m2) : 0u;   // them from the plane codes, tb_w16_codes_kernel)
     const uint32_t SMpn = TBL ? SMn : padds(SMn, k.smp);           // TBL: no offset (k.smp = 0, the tables hold s'')
     oI = In; oD = Dn; oS = Sn; oIold = st.I;
     if (MASKED) {   // act: 0xFFFF in each half whose pair has this column
         st.I = bfi(act, In, st.I); st.SD = bfi(act, SDn, st.SD); st.Dd = bfi(act, Ddn, st.Dd);
-        st.SMp = bfi(act, SMpn, st.SMp); st.E = bfi(act, En, st.E);
+        st.SMp = bfi(act, SMpn, st.SMp);
+        if (!NOE) st.E = bfi(act, En, st.E);
     } else {
-        st.I = In; st.SD = SDn; st.Dd = Ddn; st.SMp = SMpn; st.E = En;
+        st.I = In; st.SD = SDn; st.Dd = Ddn; st.SMp = SMpn;
+        if (!NOE) st.E = En;
     }
     if (CODES) { st.cI = cIn; st.cD = cDn; }
     st.SMtl = sm_in;
-    st.Etl = e_up;
+    if (!NOE) st.Etl = e_up;
 }
 
-template <bool MASKED, bool TBL, bool CODES>
+template <bool MASKED, bool TBL, bool CODES, bool NOE = false>
 __device__ __forceinline__ void dp_step_pk(LanePk& st, const Rec& r, const int t, const int lane, const int m0,
                                            const int m1, const uint32_t c1a, const uint32_t c1b, const uint32_t c1ah,
                                            const uint32_t c1bh, const PkScores& k,
@@ -219,12 +224,12 @@ __device__ __forceinline__ void dp_step_pk(LanePk& st, const Rec& r, const int t
     const uint32_t dd_in = (uint32_t)shr1(r.dd, (int)st.b.Dd);
     const uint32_t sm_in = (uint32_t)shr1(r.sm, (int)st.b.SMp);
     const uint32_t c2 = (uint32_t)shr1(r.c2, (int)st.c2c);
-    const uint32_t e_in = (uint32_t)shr1((int)pk2(t + 1, t + 1), (int)st.b.E);   // lane 0: its own column
+    const uint32_t e_in = NOE ? 0u : (uint32_t)shr1((int)pk2(t + 1, t + 1), (int)st.b.E);   // lane 0: its own column
     const uint32_t act = MASKED ? ((unsigned)(t - lane) < (unsigned)m0 ? 0xFFFFu : 0u) |
                                       ((unsigned)(t - lane) < (unsigned)m1 ? 0xFFFF0000u : 0u)
                                 : ~0u;
-    cell_pk<MASKED, TBL, CODES>(st.a, dd_in, sm_in, e_in, c2, c1a, c1ah, act, k, oI[0], oD[0], oS[0], oL[0]);
-    cell_pk<MASKED, TBL, CODES>(st.b, st.a.Dd, st.a.SMp, st.a.E, c2, c1b, c1bh, act, k, oI[1], oD[1], oS[1], oL[1]);
+    cell_pk<MASKED, TBL, CODES, NOE>(st.a, dd_in, sm_in, e_in, c2, c1a, c1ah, act, k, oI[0], oD[0], oS[0], oL[0]);
+    cell_pk<MASKED, TBL, CODES, NOE>(st.b, st.a.Dd, st.a.SMp, st.a.E, c2, c1b, c1bh, act, k, oI[1], oD[1], oS[1], oL[1]);
     st.c2c = c2;
 }
 
@@ -306,57 +311,58 @@ __device__ __forceinline__ void group4_pk(LanePk& st, Rec (&nxt)[4], WavePk& w, 
     if (MASKED) {
         auto sko = [&](int c) { return (c >= 0 && c <= w.m) ? w.skel_voff + 4u * (uint32_t)c : kSkelOff; };
         push63_pk<4 * G4 + 0>(out_base, st, lane63_mask(push_on && col0 >= 0 && col0 <= w.m));
-        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[0], bD[0], bS[0], bL[0]);
+        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[0], bD[0], bS[0], bL[0]);
         if ((PLANES & 3) == 1) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
         if ((PLANES & 3) == 2) { wc[0][0] = w16_code(bI[0][0], bD[0][0], bS[0][0], bL[0][0]);
                            wc[1][0] = w16_code(bI[0][1], bD[0][1], bS[0][1], bL[0][1]); }
-        skel_store(w.skel_rsrc, sko(col0 + 1), (int)st.b.E);
+        if ((PLANES & 16) == 0) skel_store(w.skel_rsrc, sko(col0 + 1), (int)st.b.E);
         push63_pk<4 * G4 + 1>(out_base, st, lane63_mask(push_on && col0 + 1 >= 0 && col0 + 1 <= w.m));
-        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[1], bD[1], bS[1], bL[1]);
+        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[1], bD[1], bS[1], bL[1]);
         if ((PLANES & 3) == 1) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
         if ((PLANES & 3) == 2) { wc[0][1] = w16_code(bI[1][0], bD[1][0], bS[1][0], bL[1][0]);
                            wc[1][1] = w16_code(bI[1][1], bD[1][1], bS[1][1], bL[1][1]); }
-        skel_store(w.skel_rsrc, sko(col0 + 2), (int)st.b.E);
+        if ((PLANES & 16) == 0) skel_store(w.skel_rsrc, sko(col0 + 2), (int)st.b.E);
         push63_pk<4 * G4 + 2>(out_base, st, lane63_mask(push_on && col0 + 2 >= 0 && col0 + 2 <= w.m));
-        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[2], bD[2], bS[2], bL[2]);
+        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[2], bD[2], bS[2], bL[2]);
         if ((PLANES & 3) == 1) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
         if ((PLANES & 3) == 2) { wc[0][2] = w16_code(bI[2][0], bD[2][0], bS[2][0], bL[2][0]);
                            wc[1][2] = w16_code(bI[2][1], bD[2][1], bS[2][1], bL[2][1]); }
-        skel_store(w.skel_rsrc, sko(col0 + 3), (int)st.b.E);
+        if ((PLANES & 16) == 0) skel_store(w.skel_rsrc, sko(col0 + 3), (int)st.b.E);
         push63_pk<4 * G4 + 3>(out_base, st, lane63_mask(push_on && col0 + 3 >= 0 && col0 + 3 <= w.m));
         if (push_on && col0 + 3 >= 0 && col0 <= w.m) lds_store_lane0(w.wcnt_out, min(col0 + 3, w.m) + 1);
-        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[3], bD[3], bS[3], bL[3]);
+        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[3], bD[3], bS[3], bL[3]);
         if ((PLANES & 3) == 1) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
         if ((PLANES & 3) == 2) { wc[0][3] = w16_code(bI[3][0], bD[3][0], bS[3][0], bL[3][0]);
                            wc[1][3] = w16_code(bI[3][1], bD[3][1], bS[3][1], bL[3][1]); }
-        skel_store(w.skel_rsrc, sko(col0 + 4), (int)st.b.E);
+        if ((PLANES & 16) == 0) skel_store(w.skel_rsrc, sko(col0 + 4), (int)st.b.E);
     } else {
         const uint32_t pa = push_on && w.lane == kWave - 1 ? out_base : w.scratch;
         push_all_pk<4 * G4 + 0>(pa, st);
-        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[0], bD[0], bS[0], bL[0]);
+        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[0], bD[0], bS[0], bL[0]);
         if ((PLANES & 3) == 1) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
         if ((PLANES & 3) == 2) { wc[0][0] = w16_code(bI[0][0], bD[0][0], bS[0][0], bL[0][0]);
                            wc[1][0] = w16_code(bI[0][1], bD[0][1], bS[0][1], bL[0][1]); }
         const uint32_t e0 = st.b.E;
         push_all_pk<4 * G4 + 1>(pa, st);
-        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[1], bD[1], bS[1], bL[1]);
+        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[1], bD[1], bS[1], bL[1]);
         if ((PLANES & 3) == 1) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
         if ((PLANES & 3) == 2) { wc[0][1] = w16_code(bI[1][0], bD[1][0], bS[1][0], bL[1][0]);
                            wc[1][1] = w16_code(bI[1][1], bD[1][1], bS[1][1], bL[1][1]); }
         const uint32_t e1 = st.b.E;
         push_all_pk<4 * G4 + 2>(pa, st);
-        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[2], bD[2], bS[2], bL[2]);
+        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[2], bD[2], bS[2], bL[2]);
         if ((PLANES & 3) == 1) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
         if ((PLANES & 3) == 2) { wc[0][2] = w16_code(bI[2][0], bD[2][0], bS[2][0], bL[2][0]);
                            wc[1][2] = w16_code(bI[2][1], bD[2][1], bS[2][1], bL[2][1]); }
         const uint32_t e2 = st.b.E;
         push_all_pk<4 * G4 + 3>(pa, st);
         publish_all(w.cnt_addr, col0 + 3 + 1);
-        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[3], bD[3], bS[3], bL[3]);
+        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[3], bD[3], bS[3], bL[3]);
         if ((PLANES & 3) == 1) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
         if ((PLANES & 3) == 2) { wc[0][3] = w16_code(bI[3][0], bD[3][0], bS[3][0], bL[3][0]);
                            wc[1][3] = w16_code(bI[3][1], bD[3][1], bS[3][1], bL[3][1]); }
-        skel_store4(w.skel_rsrc, w.skel_voff + 4u * (uint32_t)(col0 + 1), (int)e0, (int)e1, (int)e2, (int)st.b.E);
+        if ((PLANES & 16) == 0)
+            skel_store4(w.skel_rsrc, w.skel_voff + 4u * (uint32_t)(col0 + 1), (int)e0, (int)e1, (int)e2, (int)st.b.E);
     }
     if ((PLANES & 3) == 2) {
         // twin plane codes: per strip [group][row][lane][step] dwords (2 KB a group)
@@ -534,12 +540,12 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
     if (ia == P0.n || ia + 1 == P0.n) {
         const bool fa = ia == P0.n;
         const uint32_t sm = psubs(fa ? st.a.SMp : st.b.SMp, k.smp), e = fa ? st.a.E : st.b.E;
-        pres0->end_SM = lo16(sm ^ kBias2) + w.B0; pres0->end_E = lo16(e);
+        pres0->end_SM = lo16(sm ^ kBias2) + w.B0; pres0->end_E = (PLANES & 16) ? 0 : lo16(e);
     }
     if (ia == P1.n || ia + 1 == P1.n) {
         const bool fa = ia == P1.n;
         const uint32_t sm = psubs(fa ? st.a.SMp : st.b.SMp, k.smp), e = fa ? st.a.E : st.b.E;
-        pres1->end_SM = hi16(sm ^ kBias2) + w.B1; pres1->end_E = hi16(e);
+        pres1->end_SM = hi16(sm ^ kBias2) + w.B1; pres1->end_E = (PLANES & 16) ? 0 : hi16(e);
     }
 }
 
@@ -744,6 +750,8 @@ static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int npa
             case 6: GX_PK(6); break;
             case 10: GX_PK(10); break;   // twin codes, no code words
             case 14: GX_PK(14); break;
+            case 26: GX_PK(26); break;   // twin codes, no code words, no skeleton (tb_seq_kernel)
+            case 30: GX_PK(30); break;
             default: return hipErrorInvalidValue;
         }
 #undef GX_PK

@@ -1246,6 +1246,38 @@ __global__ void tb_chase_kernel(const TbDev* __restrict__ jobs) {
 // row are rebuilt; the walk (tb_strip_kernel) never uses a word outside them
 // once its rows have converged (every path cell lies in that range).  One
 // block of 128 threads per strip, one thread per row.
+// The code word (cD << 16 | cI, first step in bit 15) of 16 steps of one row
+// from its four 4-step groups of twin plane codes (this pair's half `sh`).
+__device__ __forceinline__ uint32_t w16_word_of(const uint4 (&w4)[4], const int sh) {
+    uint32_t cI = 0, cD = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const uint32_t wk[4] = {w4[g].x, w4[g].y, w4[g].z, w4[g].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t code = (wk[k] >> sh) & 0xFFFFu;
+            const uint32_t r = code >> 4;                               // x_S + 32 x_D (mod 2^12)
+            const int xS = (int)(r << 27) >> 27;                        // 5-bit signed
+            const int xD = (int)(((r - (uint32_t)xS) >> 5) << 25) >> 25;   // 7-bit signed
+            cI = (cI << 1) | (uint32_t)(xS < 0);
+            cD = (cD << 1) | (uint32_t)(xD > max(0, xS));
+        }
+    }
+    return (cD << 16) | cI;
+}
+// Address of row rho's 4-step group G of strip s in the twin code plane.
+__device__ __forceinline__ const uint4* w16_group(const TbDev& J, int s, int G, int rho) {
+    return (const uint4*)(J.w16 + ((size_t)s * J.t4 + G) * kTwinGroupBytes + (size_t)(rho & 1) * (kTwinGroupBytes / 2) +
+                          (size_t)(rho >> 1) * 16);
+}
+// Code word q of row rho of strip s, derived from the twin plane codes.
+__device__ __forceinline__ uint32_t w16_word(const TbDev& J, int s, int q, int rho) {
+    uint4 w4[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) w4[g] = *w16_group(J, s, 4 * q + g, rho);
+    return w16_word_of(w4, 16 * J.w16_half);
+}
+
 __global__ __launch_bounds__(128) void tb_w16_codes_kernel(const TbDev* __restrict__ jobs) {
     const TbDev J = jobs[blockIdx.y];
     const int s = blockIdx.x;
@@ -1262,23 +1294,93 @@ __global__ __launch_bounds__(128) void tb_w16_codes_kernel(const TbDev* __restri
     const int sh = 16 * J.w16_half;
     guint* const out = (guint*)(J.codes + (size_t)s * J.t16 * kStripRows + rho);
     for (int q = q_lo; q <= q_hi; ++q) {
-        uint32_t cI = 0, cD = 0;
+        uint4 w4[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const uint4 w4 = *(const uint4*)(base + (size_t)(4 * q + g) * kTwinGroupBytes);
-            const uint32_t wk[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t code = (wk[k] >> sh) & 0xFFFFu;
-                const uint32_t r = code >> 4;                               // x_S + 32 x_D (mod 2^12)
-                const int xS = (int)(r << 27) >> 27;                        // 5-bit signed
-                const int xD = (int)(((r - (uint32_t)xS) >> 5) << 25) >> 25;   // 7-bit signed
-                cI = (cI << 1) | (uint32_t)(xS < 0);
-                cD = (cD << 1) | (uint32_t)(xD > max(0, xS));
+        for (int g = 0; g < 4; ++g) w4[g] = *(const uint4*)(base + (size_t)(4 * q + g) * kTwinGroupBytes);
+        out[(size_t)q * kStripRows] = w16_word_of(w4, sh);
+    }
+}
+
+// One 64-row block of a strip's walk (tb_strip_kernel, tb_seq_kernel).  The
+// path enters the block at lane R (row-in-block), column ce; win holds words
+// q0 .. q0 + WIN - 1 of every lane's row.  Writes the records of the rows it
+// covers (from the entry row upwards) at recs[nrec ..], advances nrec, and
+// returns the lane where the walk leaves the strip or the interior (-1: it
+// goes on in the block above, entered at its lane 63 at column nj of lane 0).
+// Per lane: nj = the column after its row's last move, run_end = the row's
+// insert run reached column 0.  W16: words outside the window are derived
+// from the twin plane codes (no code words in HBM).
+template <int WIN, bool W16>
+__device__ __forceinline__ int tb_walk_block(const TbDev& J, const int ss, const int vb, const int vb_top, const int R,
+                                             const int ce, const int q0, const lu32* win, lint* ltbl, const int lane,
+                                             guint* recs, int& nrec, int& nj, bool& run_end) {
+    gcu32* const codes = (gcu32*)J.codes;
+    const int rho = tb_rho(J, vb, lane);
+    const int lo_t = tb_lot(J, rho);  // step of column 1 on this row
+    {   // per lane: nearest non-insert step strictly below each window word (branch-free)
+        int run = -1;
+#pragma unroll 8
+        for (int x = 0; x < WIN; ++x) {
+            ltbl[x * kWave + lane] = run;
+            const uint32_t w = win[x * kWave + lane];
+            const uint32_t m = ((w >> 16) | ~w) & 0xFFFFu;
+            const int k = 15 - (int)__builtin_ctz(m | 0x10000u);
+            const int cand = ((16 * (q0 + x) + k) << 1) | (int)((w >> ((31 - k) & 31)) & 1u);
+            run = m ? cand : run;
+        }
+    }
+    const bool act = lane <= R;
+    const bool top_row = vb == vb_top && lane == 0;   // its move leaves the strip
+    int g = ce - (R - lane);          // diagonal guess of this row's entry column
+    int rec = 0;
+    bool end = true;
+    nj = 0; run_end = false;
+    for (;;) {
+        const bool valid = act && g >= 1;
+        const int t_in = g - 1 + lo_t;
+        const int x = (t_in >> 4) - q0;
+        const int xc = min(max(x, 0), WIN - 1);
+        const uint32_t w = win[xc * kWave + lane];
+        const int tb = ltbl[xc * kWave + lane];
+        const uint32_t nonI = ((w >> 16) | ~w) & ((0xFFFFu << (15 - (t_in & 15))) & 0xFFFFu);
+        const int kw = 15 - (int)__builtin_ctz(nonI | 0x10000u);
+        int tf = nonI ? (t_in & ~15) + kw : (tb >> 1);
+        int del = nonI ? (int)((w >> ((31 - kw) & 31)) & 1u) : (tb & 1);
+        const bool need_scan = valid && (x < 0 || (!nonI && tb < 0 && 16 * q0 > lo_t));
+        if (__builtin_amdgcn_ballot_w64(need_scan)) {
+            if (need_scan) {          // below the window (rare): scan the HBM words
+                int t = x < 0 ? t_in : 16 * q0 - 1;
+                tf = -1; del = 0;
+                while (t >= lo_t) {
+                    const uint32_t wg = W16 ? w16_word(J, ss, t >> 4, rho) : codes[tb_word(J, ss, t >> 4, rho)];
+                    const uint32_t ng = ((wg >> 16) | ~wg) & ((0xFFFFu << (15 - (t & 15))) & 0xFFFFu);
+                    if (ng) {
+                        tf = (t & ~15) + (15 - __builtin_ctz(ng));
+                        del = (wg >> (31 - (tf & 15))) & 1u;
+                        break;
+                    }
+                    t = (t & ~15) - 1;
+                }
             }
         }
-        out[(size_t)q * kStripRows] = (cD << 16) | cI;
+        run_end = valid && tf < lo_t;     // (i, g..1) all insert: the walk leaves at (i, 0)
+        nj = tf - lo_t + del;             // del ? tf-lo_t+1 : tf-lo_t
+        end = !valid || run_end || nj < 1 || top_row;
+        rec = run_end ? ((g << 2) | 1) : (((t_in - tf) << 2) | (del << 1));
+        // next guess: the exit column of the lane above; the top lane's entry is fixed
+        const int prop = end ? 0 : nj;
+        int gn = __builtin_amdgcn_update_dpp(0, prop, 0x130 /* wave_shl:1 */, 0xF, 0xF, false);
+        gn = lane == R ? ce : gn;
+        if (__builtin_amdgcn_ballot_w64(act && gn != g) == 0) break;
+        g = gn;
     }
+    // the path covers lanes R down to the first lane (from the top) where it ends
+    const unsigned long long em = __builtin_amdgcn_ballot_w64(act && end);
+    const int E = em ? 63 - __builtin_clzll(em) : -1;
+    const int lo = E >= 0 ? E : 0;
+    if (act && lane >= lo) recs[nrec + (R - lane)] = (uint32_t)rec;
+    nrec += R - lo + 1;
+    return E;
 }
 
 __global__ __launch_bounds__(64) void tb_strip_kernel(const TbDev* __restrict__ jobs) {
@@ -1293,7 +1395,6 @@ __global__ __launch_bounds__(64) void tb_strip_kernel(const TbDev* __restrict__ 
     const int i0 = __builtin_amdgcn_readfirstlane(((gcint*)J.seg)[4 * ss + 0]);
     const int j0 = __builtin_amdgcn_readfirstlane(((gcint*)J.seg)[4 * ss + 1]);
     guint* const recs = (guint*)(J.recs + (size_t)ss * J.srows);
-    gcu32* const codes = (gcu32*)J.codes;
     lint* const ltbl = (lint*)(uintptr_t)lds_addr(tbl);
     const int vb_top = J.srows == kStripRows ? 2 * ss : ss;   // the strip's top block
     int vb = (i0 - 1) / kTbRows;          // current block
@@ -1308,72 +1409,10 @@ __global__ __launch_bounds__(64) void tb_strip_kernel(const TbDev* __restrict__ 
         // the block above (if in this strip) is entered at its lane 63, no further right than ce
         const int q_n = vb > vb_top ? tb_q0(ce - 1 + tb_lot(J, tb_rho(J, vb - 1, kTbRows - 1))) : 0;
         if (vb > vb_top) tb_prefetch(tbuf[cb ^ 1], J, vb - 1, q_n, lane);
-        const int q0 = q_c;
         const lu32* win = (const lu32*)(uintptr_t)lds_addr(tbuf[cb]);
-        const int rho = tb_rho(J, vb, lane);
-        const int lo_t = tb_lot(J, rho);  // step of column 1 on this row
-        {   // per lane: nearest non-insert step strictly below each window word (branch-free)
-            int run = -1;
-#pragma unroll 8
-            for (int x = 0; x < kTbWin; ++x) {
-                ltbl[x * kWave + lane] = run;
-                const uint32_t w = win[x * kWave + lane];
-                const uint32_t m = ((w >> 16) | ~w) & 0xFFFFu;
-                const int k = 15 - (int)__builtin_ctz(m | 0x10000u);
-                const int cand = ((16 * (q0 + x) + k) << 1) | (int)((w >> ((31 - k) & 31)) & 1u);
-                run = m ? cand : run;
-            }
-        }
-        const bool act = lane <= R;
-        const bool top_row = vb == vb_top && lane == 0;   // its move leaves the strip
-        int g = ce - (R - lane);          // diagonal guess of this row's entry column
-        int rec = 0, nj = 0;
-        bool end = true, run_end = false;
-        for (;;) {
-            const bool valid = act && g >= 1;
-            const int t_in = g - 1 + lo_t;
-            const int x = (t_in >> 4) - q0;
-            const int xc = min(max(x, 0), kTbWin - 1);
-            const uint32_t w = win[xc * kWave + lane];
-            const int tb = ltbl[xc * kWave + lane];
-            const uint32_t nonI = ((w >> 16) | ~w) & ((0xFFFFu << (15 - (t_in & 15))) & 0xFFFFu);
-            const int kw = 15 - (int)__builtin_ctz(nonI | 0x10000u);
-            int tf = nonI ? (t_in & ~15) + kw : (tb >> 1);
-            int del = nonI ? (int)((w >> ((31 - kw) & 31)) & 1u) : (tb & 1);
-            const bool need_scan = valid && (x < 0 || (!nonI && tb < 0 && 16 * q0 > lo_t));
-            if (__builtin_amdgcn_ballot_w64(need_scan)) {
-                if (need_scan) {          // below the window (rare): scan the HBM words
-                    int t = x < 0 ? t_in : 16 * q0 - 1;
-                    tf = -1; del = 0;
-                    while (t >= lo_t) {
-                        const uint32_t wg = codes[tb_word(J, ss, t >> 4, rho)];
-                        const uint32_t ng = ((wg >> 16) | ~wg) & ((0xFFFFu << (15 - (t & 15))) & 0xFFFFu);
-                        if (ng) {
-                            tf = (t & ~15) + (15 - __builtin_ctz(ng));
-                            del = (wg >> (31 - (tf & 15))) & 1u;
-                            break;
-                        }
-                        t = (t & ~15) - 1;
-                    }
-                }
-            }
-            run_end = valid && tf < lo_t;     // (i, g..1) all insert: the walk leaves at (i, 0)
-            nj = tf - lo_t + del;             // del ? tf-lo_t+1 : tf-lo_t
-            end = !valid || run_end || nj < 1 || top_row;
-            rec = run_end ? ((g << 2) | 1) : (((t_in - tf) << 2) | (del << 1));
-            // next guess: the exit column of the lane above; the top lane's entry is fixed
-            const int prop = end ? 0 : nj;
-            int gn = __builtin_amdgcn_update_dpp(0, prop, 0x130 /* wave_shl:1 */, 0xF, 0xF, false);
-            gn = lane == R ? ce : gn;
-            if (__builtin_amdgcn_ballot_w64(act && gn != g) == 0) break;
-            g = gn;
-        }
-        // the path covers lanes R down to the first lane (from the top) where it ends
-        const unsigned long long em = __builtin_amdgcn_ballot_w64(act && end);
-        const int E = em ? 63 - __builtin_clzll(em) : -1;
-        const int lo = E >= 0 ? E : 0;
-        if (act && lane >= lo) recs[nrec + (R - lane)] = (uint32_t)rec;
-        nrec += R - lo + 1;
+        int nj;
+        bool run_end;
+        const int E = tb_walk_block<kTbWin, false>(J, ss, vb, vb_top, R, ce, q_c, win, ltbl, lane, recs, nrec, nj, run_end);
         if (E >= 0) break;                // the walk leaves the strip (or the interior) here
         ce = __builtin_amdgcn_readlane(nj, 0);
         vb -= 1;
@@ -1382,6 +1421,108 @@ __global__ __launch_bounds__(64) void tb_strip_kernel(const TbDev* __restrict__ 
         q_c = q_n;
     }
     if (lane == 0) ((gint*)J.seg)[4 * ss + 2] = nrec;
+}
+
+// The walk of a twin fill that kept no landing columns (gx_fill_pk.hip,
+// PLANES 16: no skeleton) and no code words: the strips are walked in
+// sequence from the start cell, each entered where the one below left it
+// (what tb_chase_kernel's hops through the skeleton give the parallel strip
+// walks), the code words of each 64-row block's window derived from the
+// plane codes.  One workgroup per pair: wave 0 walks block k (the
+// tb_strip_kernel block walk, its window in LDS) while kSqHelp helper waves
+// derive block k + 1's window (kSqWin words a row ending at block k's entry
+// column: the path only moves left) into the other LDS buffer, so a block
+// costs about the larger of the walk and one window's loads + derivation
+// instead of their sum.  Writes the same seg / recs / end_ij as
+// tb_chase_kernel + tb_strip_kernel, so the host's labelling is unchanged.
+// Layout 0 only.
+constexpr int kSqWin = 12;
+constexpr int kSqHelp = 4;
+struct SqCtl {
+    int s, vb, R, ce, q0, done, end_i, end_j;
+};
+// words q0 .. q0 + kSqWin - 1 of block vb's rows (strip vb / 2), derived by
+// the kSqHelp helper waves: helper h takes words h, h + kSqHelp, ... (all its
+// loads in flight at once)
+static_assert(kSqWin % kSqHelp == 0, "helper word split");
+__device__ __forceinline__ void tb_seq_window(const TbDev& J, const int vb, const int q0, uint32_t* buf, const int hw,
+                                              const int lane) {
+    typedef __attribute__((address_space(3))) uint32_t lu32w;
+    lu32w* const lw = (lu32w*)(uintptr_t)lds_addr(buf);
+    const int s = vb >> 1, rho = tb_rho(J, vb, lane), sh = 16 * J.w16_half;
+    constexpr int kPer = kSqWin / kSqHelp;
+    uint4 w4[kPer][4];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        const int q = min(q0 + hw + u * kSqHelp, J.t16 - 1);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) w4[u][g] = *w16_group(J, s, 4 * q + g, rho);
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) lw[(hw + u * kSqHelp) * kWave + lane] = w16_word_of(w4[u], sh);
+}
+__global__ __launch_bounds__((1 + kSqHelp) * kWave) void tb_seq_kernel(const TbDev* __restrict__ jobs) {
+    __shared__ uint32_t wbuf[2][kSqWin * kWave];
+    __shared__ int tbl[kSqWin * kWave];
+    __shared__ SqCtl ctl;
+    const TbDev J = jobs[blockIdx.x];
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int i = J.start_i, j = J.start_j;
+    if (i < 1 || j < 1) {
+        if (threadIdx.x == 0) { J.end_ij[0] = i; J.end_ij[1] = j; J.end_ij[2] = -1; }
+        return;
+    }
+    const int first = (i - 1) / J.srows;
+    // block 0 of the walk: its window from every wave
+    int vb = (i - 1) / kTbRows, R = (i - 1) % kTbRows, ce = j;
+    int q0 = max(((ce - 1 + tb_lot(J, tb_rho(J, vb, R))) >> 4) - (kSqWin - 1), 0);
+    if (wave > 0) tb_seq_window(J, vb, q0, wbuf[0], wave - 1, lane);
+    if (threadIdx.x == 0) { J.seg[4 * first + 0] = i; J.seg[4 * first + 1] = j; J.seg[4 * first + 3] = 1; }
+    lint* const ltbl = (lint*)(uintptr_t)lds_addr(tbl);
+    int s = first, nrec = 0, cb = 0;
+    int end_i = -1, end_j = -1;
+    __syncthreads();
+    for (int guard = 0; guard <= 2 * J.strips + 2; ++guard) {
+        // the next block in the walk is always vb - 1 (the strip above once vb
+        // is its strip's top block); its window ends at this block's entry
+        const int qn = vb > 0 ? max(((ce - 1 + tb_lot(J, tb_rho(J, vb - 1, kTbRows - 1))) >> 4) - (kSqWin - 1), 0) : 0;
+        if (wave > 0) {
+            if (vb > 0) tb_seq_window(J, vb - 1, qn, wbuf[cb ^ 1], wave - 1, lane);
+        } else {
+            const int vb_top = 2 * s;
+            guint* const recs = (guint*)(J.recs + (size_t)s * J.srows);
+            int nj;
+            bool run_end;
+            const int E = tb_walk_block<kSqWin, true>(J, s, vb, vb_top, R, ce, q0, (const lu32*)(uintptr_t)lds_addr(wbuf[cb]),
+                                                      ltbl, lane, recs, nrec, nj, run_end);
+            int done = 0;
+            if (E < 0) {                  // on into the block above, in this strip
+                ce = __builtin_amdgcn_readlane(nj, 0);
+            } else {
+                if (lane == 0) J.seg[4 * s + 2] = nrec;
+                const int iE = vb * kTbRows + E + 1;   // the row where this strip's walk ends
+                const int njE = __builtin_amdgcn_readlane(nj, E);
+                if (__builtin_amdgcn_readlane((int)run_end, E)) { end_i = iE; end_j = 0; done = 1; }   // inserts to (iE, 0)
+                else if (E == 0 && vb == vb_top && njE >= 1 && s >= 1) {
+                    // the top row's move enters strip s - 1 at its bottom row
+                    s -= 1; ce = njE; nrec = 0;
+                    if (lane == 0) { J.seg[4 * s + 0] = iE - 1; J.seg[4 * s + 1] = njE; J.seg[4 * s + 3] = 1; }
+                } else { end_i = iE - 1; end_j = njE; done = 1; }   // row 0 or column 0
+            }
+            if (lane == 0) { ctl.s = s; ctl.ce = ce; ctl.done = done; ctl.end_i = end_i; ctl.end_j = end_j; }
+        }
+        __syncthreads();
+        if (ctl.done) break;
+        s = ctl.s; ce = ctl.ce;
+        vb -= 1; R = kTbRows - 1; q0 = qn; cb ^= 1;
+        __syncthreads();   // (ctl read by every wave before wave 0 writes it again)
+    }
+    if (threadIdx.x == 0) {
+        end_i = ctl.done ? ctl.end_i : -1;
+        end_j = ctl.done ? ctl.end_j : -1;
+        J.end_ij[0] = end_i; J.end_ij[1] = end_j; J.end_ij[2] = end_i < 0 ? -1 : first;
+    }
 }
 
 // Plane checksums of every pair of a fill launch, decoded from the planes as
@@ -1616,7 +1757,11 @@ hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d
     return hipGetLastError();
 }
 
-hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, bool w16, hipStream_t st) {
+hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, bool w16, bool seq, hipStream_t st) {
+    if (seq) {   // no skeleton: the strips walked in sequence (twin plane codes only)
+        hipLaunchKernelGGL(tb_seq_kernel, dim3(njobs), dim3((1 + kSqHelp) * kWave), 0, st, d_jobs);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(tb_chase_kernel, dim3(njobs), dim3(64), 0, st, d_jobs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
