@@ -1430,6 +1430,9 @@ static int tb_collect(gx_context* ctx, int slot, size_t P, TbOut& out) {
         out.end_j[p] = out.c[4 * p + 1];
         if (out.end_i[p] < 0) return fail(GX_EHIP, "traceback: landing column out of range (incomplete fill)");
     }
+    if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug") && P)
+        fprintf(stderr, "[gx DEBUG] traceback %.3f ms; pair 0 diag word %u (%u cycles per block, %u walking)\n", ms,
+                (unsigned)out.c[3], (unsigned)out.c[3] >> 16, (unsigned)out.c[3] & 0xFFFFu);
     return GX_OK;
 }
 

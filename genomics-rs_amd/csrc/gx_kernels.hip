@@ -1435,7 +1435,11 @@ __global__ __launch_bounds__(64) void tb_strip_kernel(const TbDev* __restrict__ 
 // costs about the larger of the walk and one window's loads + derivation
 // instead of their sum.  Writes the same seg / recs / end_ij as
 // tb_chase_kernel + tb_strip_kernel, so the host's labelling is unchanged.
-// Layout 0 only.
+// The walk, not the windows, sets the pace (~22k cycles a block: on gapped
+// paths the fixed point needs about one round per row; a walker doing the
+// rows one by one on scalar values ran at ~650 cycles a row, a lone wave's
+// issue latency), so the host overlaps it with the next fill (gx_api.cpp
+// batch_core_steps).  Layout 0 only.
 constexpr int kSqWin = 12;
 constexpr int kSqHelp = 4;
 struct SqCtl {
@@ -1482,6 +1486,8 @@ __global__ __launch_bounds__((1 + kSqHelp) * kWave) void tb_seq_kernel(const TbD
     lint* const ltbl = (lint*)(uintptr_t)lds_addr(tbl);
     int s = first, nrec = 0, cb = 0;
     int end_i = -1, end_j = -1;
+    long long clk0 = __builtin_amdgcn_s_memtime(), walk_clk = 0;   // (diagnostics: end_ij[3])
+    int nblk = 0;
     __syncthreads();
     for (int guard = 0; guard <= 2 * J.strips + 2; ++guard) {
         // the next block in the walk is always vb - 1 (the strip above once vb
@@ -1494,8 +1500,11 @@ __global__ __launch_bounds__((1 + kSqHelp) * kWave) void tb_seq_kernel(const TbD
             guint* const recs = (guint*)(J.recs + (size_t)s * J.srows);
             int nj;
             bool run_end;
+            const long long w0 = __builtin_amdgcn_s_memtime();
             const int E = tb_walk_block<kSqWin, true>(J, s, vb, vb_top, R, ce, q0, (const lu32*)(uintptr_t)lds_addr(wbuf[cb]),
                                                       ltbl, lane, recs, nrec, nj, run_end);
+            walk_clk += __builtin_amdgcn_s_memtime() - w0;
+            ++nblk;
             int done = 0;
             if (E < 0) {                  // on into the block above, in this strip
                 ce = __builtin_amdgcn_readlane(nj, 0);
@@ -1522,6 +1531,9 @@ __global__ __launch_bounds__((1 + kSqHelp) * kWave) void tb_seq_kernel(const TbD
         end_i = ctl.done ? ctl.end_i : -1;
         end_j = ctl.done ? ctl.end_j : -1;
         J.end_ij[0] = end_i; J.end_ij[1] = end_j; J.end_ij[2] = end_i < 0 ? -1 : first;
+        // cycles per block: all (high 16 bits) and the walk's (low 16)
+        const long long all = (__builtin_amdgcn_s_memtime() - clk0) / max(nblk, 1), wk = walk_clk / max(nblk, 1);
+        J.end_ij[3] = (int)((min(all, 65535LL) << 16) | min(wk, 65535LL));
     }
 }
 

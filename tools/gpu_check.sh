@@ -7,6 +7,6 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout
 rc=$?
 echo "pytest rc=$rc"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline --config-steps 0 --int32-steps 0 \
+GX_LOG=${BENCH_LOG:-} timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --no-cpu-baseline --config-steps 0 --int32-steps 0 \
     --no-plane-steps 0 --single-pair-steps 0 > "$O/bench.json" 2> "$O/bench.err"
 echo "bench rc=$?"
