@@ -729,8 +729,12 @@ static std::vector<std::pair<int, int>> twin_table(const std::vector<PairHost>& 
     }
     return tw;
 }
+// long_ok: the launch will be the twin fill without landing columns (twin
+// plane codes, no code words, no skeleton): no int16 column quantity is
+// left, so the 31,920-column limit of the int16 landing columns is lifted.
 static int twin_width(const std::vector<PairHost>& ph, const std::vector<std::pair<int, int>>& tw, const Scores32& sc,
-                      int is_local, bool track, bool lcs, int lay, bool planes, bool d8, int W_want) {
+                      int is_local, bool track, bool lcs, int lay, bool planes, bool d8, int W_want,
+                      bool long_ok = false) {
     if (const char* e = getenv("GX_TWIN"); e && !strcmp(e, "0")) return 0;
     if (lay != 0 || is_local || track || lcs || (planes && !d8) || sc.g > 0 || sc.h > 0) return 0;
     if (ph.empty()) return 0;
@@ -738,7 +742,8 @@ static int twin_width(const std::vector<PairHost>& ph, const std::vector<std::pa
     for (const auto& t : tw) {
         const PairHost& x = ph[t.first];
         const PairHost& y = ph[t.second];
-        if (!x.n || !x.m || !y.n || !y.m || std::max(x.m, y.m) + 80 > 32000) return 0;
+        if (!x.n || !x.m || !y.n || !y.m) return 0;
+        if (std::max(x.m, y.m) + 80 > 32000 && !long_ok) return 0;
         dm = std::max(dm, std::llabs((long long)x.m - (long long)y.m));
     }
     for (int W : {15, 8, 7, 4, 3}) {
@@ -792,7 +797,11 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     else wt_want = fill_band_waves(false, total_strips / 2, fill_grid_cap(ctx->device), lay, min_strips);
     const std::vector<std::pair<int, int>> tw = twin_table(ph, twin_gap_cap(sc, wt_want >= 15 ? 15 : wt_want >= 8 ? 8 : wt_want >= 7 ? 7 : wt_want >= 4 ? 4 : 3));
     {
-        Wt = twin_width(ph, tw, sc, is_local, track, lcs, lay, planes, d8, wt_want);
+        const char* tce0 = getenv("GX_TWIN_CODES");
+        const char* tse0 = getenv("GX_TWIN_SKEL");
+        const bool long_ok = planes && !job.table && w16_ok(sc) && !(tce0 && !strcmp(tce0, "1")) &&
+                             !(tse0 && !strcmp(tse0, "1"));   // (the noskel rule below)
+        Wt = twin_width(ph, tw, sc, is_local, track, lcs, lay, planes, d8, wt_want, long_ok);
         // auto: the twin fill once its own bands fill the grid (a twin band
         // is slower per step than a scalar one, so fewer bands than CUs
         // leave it latency-bound).  30k pairs, fill ms scalar / twin (codes,

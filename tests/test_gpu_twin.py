@@ -197,18 +197,24 @@ def test_twin_random_batches(gx, ctx, oracle, monkeypatch, seed):
         assert _steps_list(st.steps(p)) == o.alignment(), (seed, p)
 
 
-@pytest.mark.parametrize("m", [31920, 31921])
-def test_twin_column_limit(gx, ctx, oracle, monkeypatch, m):
-    """The twin fill's landing columns are int16 halves: twins up to 31,920
-    columns (every pair checked against the oracle), the scalar fill beyond."""
+@pytest.mark.parametrize("skel", ["noskel", "skel"])
+@pytest.mark.parametrize("m", [31920, 31921, 65536])
+def test_twin_column_limit(gx, ctx, oracle, monkeypatch, m, skel):
+    """With a skeleton the twin fill's landing columns are int16 halves: twins
+    up to 31,920 columns, the scalar fill beyond.  Without one (the default
+    with twin plane codes: no landing columns, the traceback walks the strips
+    in sequence) the twin fill has no column limit: 65,536 columns.  Every
+    pair checked against the oracle (plane checksums, score, alignment)."""
     monkeypatch.setenv("GX_LAYOUT", "0")
+    if skel == "skel":
+        monkeypatch.setenv("GX_TWIN_SKEL", "1")
     rng = random.Random(m)
     shapes = [(200, m), (150, m - 7), (260, m - 1)]
     pairs = [(bytes(rng.choice(b"ACGT") for _ in range(n)), bytes(rng.choice(b"ACGT") for _ in range(mm)))
              for n, mm in shapes]
     st = gx.StagedPairs(pairs, ctx=ctx)
     res, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=1, plane_sums=True)
-    assert ctx.fill_info()["twin"] == (1 if m <= 31920 else 0)
+    assert ctx.fill_info()["twin"] == (1 if m <= 31920 or skel == "noskel" else 0)
     sums = st.plane_sums()
     for p, (a, b) in enumerate(pairs):
         o = oracle.align_lean(a, b, CONFIG_SCORES)
@@ -293,11 +299,12 @@ def test_twin_bound_worst_inputs_batch(gx, ctx, oracle, monkeypatch, scores, W):
         assert res[p].score == o.score and _steps_list(st.steps(p)) == o.alignment(), (scores, p)
 
 
-def test_twin_bound_column_limit_worst(gx, ctx, oracle, monkeypatch):
-    """m = 31,920 (the int16 landing-column limit) with all-mismatch and
+@pytest.mark.parametrize("m", [31920, 65536])
+def test_twin_bound_column_limit_worst(gx, ctx, oracle, monkeypatch, m):
+    """m = 31,920 (the int16 landing-column limit of a twin fill with a
+    skeleton) and 65,536 (the fill without one) with all-mismatch and
     all-match rows: plane checksums, scores and alignments."""
     monkeypatch.setenv("GX_LAYOUT", "0")
-    m = 31920
     pairs = [(b"A" * 200, b"C" * m), (b"A" * 150, b"A" * (m - 3)), (b"AC" * 130, b"CA" * (m // 2))]
     st = gx.StagedPairs(pairs, ctx=ctx)
     res, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=1, plane_sums=True)
