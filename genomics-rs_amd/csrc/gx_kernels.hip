@@ -1435,11 +1435,14 @@ __global__ __launch_bounds__(64) void tb_strip_kernel(const TbDev* __restrict__ 
 // costs about the larger of the walk and one window's loads + derivation
 // instead of their sum.  Writes the same seg / recs / end_ij as
 // tb_chase_kernel + tb_strip_kernel, so the host's labelling is unchanged.
-// The walk, not the windows, sets the pace (~22k cycles a block: on gapped
-// paths the fixed point needs about one round per row; a walker doing the
-// rows one by one on scalar values ran at ~650 cycles a row, a lone wave's
-// issue latency), so the host overlaps it with the next fill (gx_api.cpp
-// batch_core_steps).  Layout 0 only.
+// The walk, not the windows, sets the pace: ~22k cycles a block (on gapped
+// paths the fixed point needs about one ~340-cycle round per row).  Walkers
+// doing the rows one by one on wave-uniform values were slower still: ~650
+// cycles a row with the window in LDS read a row ahead, ~565 with a
+// per-row "nearest non-insert" table in LDS, ~475 with the window transposed
+// into registers (row r's words in the lanes of Wr[r], two v_readlane a row)
+// -- a lone wave's instruction latency, not the memory, sets a row's cost.
+// Layout 0 only.
 constexpr int kSqWin = 12;
 constexpr int kSqHelp = 4;
 struct SqCtl {
