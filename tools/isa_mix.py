@@ -4,7 +4,7 @@ blocks holding the compact-plane byte inserts), from a device-only assembly
 build of gx_kernels.hip:
 
     python tools/isa_mix.py [kernel-name-regex]   (default: the bench's W=15 compact-plane kernel)
-    python tools/isa_mix.py twin                  (the twin fill, gx_fill_pk.hip, W=8, twin plane codes, score tables)
+    python tools/isa_mix.py twin                  (the twin fill, gx_fill_pk.hip, W=8, twin plane codes, score tables, no code words, no skeleton: PLANES 30)
 
 Compiles to /tmp/gx_isa/ (about 2 minutes) unless GX_ISA_S names an existing .s.
 A twin group holds 16 cells per lane (4 steps x 2 rows x 2 pairs)."""
@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pat = sys.argv[1] if len(sys.argv) > 1 else r"_ZN2gx11fill_kernelILi15ELb0ELi2ELb1ELb0ELb0ELb1ELi0E"
 src, cells = "gx_kernels", 8
 if pat == "twin":
-    pat, src, cells = r"_ZN2gx14fill_pk_kernelILi8ELi6E", "gx_fill_pk", 16
+    pat, src, cells = r"_ZN2gx14fill_pk_kernelILi8ELi30E", "gx_fill_pk", 16
 s_path = os.environ.get("GX_ISA_S")
 if not s_path:
     os.makedirs("/tmp/gx_isa", exist_ok=True)
@@ -59,5 +59,5 @@ if steady:
         with open(os.environ["GX_ISA_JSON"], "w") as f:
             json.dump({"kernel": m.group(1), "block": steady[-1][0], "cells_per_lane": cells, "valu": valu,
                        "valu_total": sum(valu.values()),
-                       "dual_rate": sum(n for op, n in valu.items() if op in ("v_add_u32_e32", "v_sub_u32_e32")),
+                       "dual_rate": sum(n for op, n in valu.items() if op in ("v_add_u32_e32", "v_sub_u32_e32", "v_subrev_u32_e32")),
                        "source": f"tools/isa_mix.py (steady-state 4-step group: {cells} cells per lane)"}, f, indent=1)

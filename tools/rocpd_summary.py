@@ -36,8 +36,14 @@ def main():
     out_dir = os.path.join(ROOT, "profiles")
     os.makedirs(out_dir, exist_ok=True)
 
-    c = one_db(os.path.join(src, "kt"))
-    rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
+    ks = glob.glob(os.path.join(src, "kt", "**", "*kernel_stats.csv"), recursive=True)
+    if ks:   # (tools/gpu_evidence.sh: the kernel-trace pass writes csv)
+        with open(ks[0]) as f:
+            rows = [(r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]) / 1e3, float(r["AverageNs"]) / 1e3,
+                     float(r["Percentage"])) for r in csv.DictReader(f)]   # (ns -> us, as top_kernels)
+    else:
+        c = one_db(os.path.join(src, "kt"))
+        rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
     stats = os.path.join(out_dir, f"{tag}_kernel_stats.csv")
     with open(stats, "w", newline="") as f:
         w = csv.writer(f)
@@ -62,7 +68,8 @@ def main():
                     pmc[name] = {"kernel": kname, "launches": n, "avg_kib": avg, "avg_duration_ns": dur}
             elif ("fill_kernel" in kname or "fill_pk_kernel" in kname) and (name not in pmc or avg > pmc[name]["avg_kib"]):
                 pmc[name] = {"kernel": kname, "launches": n, "avg_kib": avg, "avg_duration_ns": dur}
-    with open(os.path.join(src, "bench.json")) as f:
+    bj = os.path.join(src, "bench.json")
+    with open(bj if os.path.exists(bj) else os.path.join(src, "kt_bench.json")) as f:
         bench = json.loads(f.read().strip().splitlines()[-1])
     workload = bench["config"]["workload"]
     wr = pmc["WRITE_SIZE"]["avg_kib"] * 1024

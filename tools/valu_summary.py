@@ -70,7 +70,8 @@ def main():
         mix = json.load(f)
     waves = int(sys.argv[4]) if len(sys.argv) > 4 else FILL_WAVES_PER_SIMD
     cpi_dual, cpi_rest, dual_names = probe_cpi(probe, waves)
-    n_dual = sum(n for op, n in mix["valu"].items() if op.replace("_e32", "").replace("_e64", "") in dual_names)
+    n_dual = sum(n for op, n in mix["valu"].items()
+                 if op.replace("_e32", "").replace("_e64", "").replace("subrev", "sub") in dual_names)
     f_dual = n_dual / mix["valu_total"]
     cpi = f_dual * cpi_dual + (1 - f_dual) * cpi_rest
     res = {"source": "rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CU_CYCLES SQ_CYCLES SQ_WAVE_CYCLES "
@@ -81,7 +82,8 @@ def main():
                        "dual_rate_fraction_of_fill_valu": round(f_dual, 4),
                        "cpi_fill_mix": round(cpi, 3), "isa_mix": os.path.relpath(mix_path, ROOT),
                        "probe": "valu_probe (chip wall time x clock x SIMDs / instructions)"}}
-    for case in ("planes", "noplanes"):
+    cases = [c for c in ("planes", "noplanes") if os.path.isdir(os.path.join(src, c))]
+    for case in cases:
         k, v = counters(os.path.join(src, case))
         with open(os.path.join(src, f"{case}.json")) as f:
             bench = json.loads(f.read().strip().splitlines()[-1])
@@ -111,7 +113,7 @@ def main():
     with open(p, "w") as f:
         json.dump(res, f, indent=1)
     print("cpi", res["ceiling"])
-    for case in ("planes", "noplanes"):
+    for case in cases:
         r = res[case]
         print(case, r["duration_ms"], "ms", r["clock_ghz"], "GHz VALU/cell", r["valu_insts_per_cell"],
               "issue", r["valu_issue_frac"], "dual", r["dual_issued_fraction"], "ceiling GCUPS",
