@@ -154,9 +154,12 @@ __device__ __forceinline__ uint32_t perm_selector(int code0, int code1) {
     return (uint32_t)code0 | 0x0C00u | ((uint32_t)(4 + code1) << 16) | 0x0C000000u;
 }
 
+// Stored negated: -code = 527 I + I(j-1) - 16 S - 512 D (mod 2^16), three
+// v_pk_mad_u16 on the cell's values directly instead of three differences and
+// two mads; the offset-binary bias cancels (527 + 1 - 16 - 512 = 0).  The
+// decoders (gx_kernels.hip w16_word_of, plane_sums_kernel) negate it back.
 __device__ __forceinline__ uint32_t w16_code(uint32_t I, uint32_t D, uint32_t S, uint32_t Iold) {
-    const uint32_t xI = psub(I, Iold), xS = psub(S, I), xD = psub(D, I);
-    return pmad(xD, 0x02000200u, pmad(xS, 0x00100010u, xI));
+    return pmad(D, 0xFE00FE00u, pmad(S, 0xFFF0FFF0u, pmad(I, 0x020F020Fu, Iold)));
 }
 
 // One row of a lane, both pairs: the cell left of the one being computed.

@@ -1255,7 +1255,7 @@ __device__ __forceinline__ uint32_t w16_word_of(const uint4 (&w4)[4], const int 
         const uint32_t wk[4] = {w4[g].x, w4[g].y, w4[g].z, w4[g].w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t code = (wk[k] >> sh) & 0xFFFFu;
+            const uint32_t code = (0u - (wk[k] >> sh)) & 0xFFFFu;   // (stored negated, gx_fill_pk.hip w16_code)
             const uint32_t r = code >> 4;                               // x_S + 32 x_D (mod 2^12)
             const int xS = (int)(r << 27) >> 27;                        // 5-bit signed
             const int xD = (int)(((r - (uint32_t)xS) >> 5) << 25) >> 25;   // 7-bit signed
@@ -1584,7 +1584,7 @@ __global__ __launch_bounds__(64) void plane_sums_kernel(const PairDev* __restric
             for (int k = 0; k < 4; ++k) {
                 const int j = 4 * q + k - l + 1;
                 if (!row_ok || j < 1 || j > d.m) continue;
-                const uint32_t code = (wk[k] >> (16 * half)) & 0xFFFFu;
+                const uint32_t code = (0u - (wk[k] >> (16 * half))) & 0xFFFFu;   // (stored negated, w16_code)
                 const int xI = (int)(code & 15u);
                 const uint32_t r = code >> 4;                       // x_S + 32 x_D (mod 2^12)
                 const int xS = (int)(r << 27) >> 27;                // 5-bit signed
