@@ -1949,7 +1949,9 @@ static int label_batch(gx_context* ctx, const std::vector<PairHost>& ph, const H
     };
     // the calling thread plus up to 11 pool workers (the box gives a process
     // 16 CPUs; the HIP runtime's threads and the caller's keep the rest)
-    const size_t nthreads = std::min<size_t>({P, (size_t)std::max(1u, std::thread::hardware_concurrency()), 12});
+    size_t cap = 12;
+    if (const char* e = getenv("GX_LABEL_THREADS"); e && atoi(e) > 0) cap = (size_t)atoi(e);
+    const size_t nthreads = std::min<size_t>({P, (size_t)std::max(1u, std::thread::hardware_concurrency()), cap});
     if (nthreads <= 1) {
         for (size_t p = 0; p < P; ++p) label_one(p);
     } else {
