@@ -201,6 +201,8 @@ struct gx_context {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t cstream = nullptr;   // pipelined path: traceback record copies (D2H) off the fill stream
+    hipStream_t stream2 = nullptr;   // overlapped batches (batch_core_overlap): the second group's fills
+    hipStream_t tstream = nullptr;   // ... and the walks
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     std::mutex mu;
     std::vector<DevBuf> free_list;
@@ -223,10 +225,11 @@ struct gx_context {
         hipEvent_t fb = nullptr, fe = nullptr, tb = nullptr, te = nullptr, fdone = nullptr, tdone = nullptr;
         TbOut out;
         DevBuf held[4];                      // traceback buffers the copy stream still reads (until tb_collect)
-    } slots[2];
+    } slots[4];   // 0, 1: pipelined steps by parity (overlapped batches: group A's fills and the walks); 2, 3: group B's fills
     int last_lay = 0, last_W = 0, last_pbytes = 0;   // the last fill launch (gx_fill_info)
     int last_chunks = 1;                             // chunks of the last staged / batch call
     int last_twin = 0;                               // the last fill was the twin (packed 16-bit) fill
+    int last_groups = 1;                             // fill launches per pass of the last staged / batch call
     // GX_STAGED_PLANE_SUMS: plane checksums of every pass of a staged run
     DevBuf sums_dev;
     unsigned long long* sums_dst = nullptr;          // where the next fill's checksums go (nullptr: off)
@@ -273,6 +276,9 @@ static int pool_get(gx_context* ctx, size_t bytes, DevBuf* out) {
         const DevBuf& b = ctx->free_list[k];
         if (b.cap >= bytes && b.cap < best) { best = b.cap; bi = (int)k; }
     }
+    // a large request does not take a cached buffer more than twice its size
+    // (that buffer may fit a later, larger request of the same launch)
+    if (bi >= 0 && bytes >= ((size_t)1 << 30) && best > 2 * bytes) bi = -1;
     if (bi >= 0) {
         *out = ctx->free_list[bi];
         ctx->free_list.erase(ctx->free_list.begin() + bi);
@@ -283,8 +289,11 @@ static int pool_get(gx_context* ctx, size_t bytes, DevBuf* out) {
         fprintf(stderr, "[gx DEBUG] pool miss: hipMalloc %zu B (%zu cached)\n", bytes, ctx->free_list.size());
     hipError_t e = hipMalloc(&p, bytes);
     if (e != hipSuccess) {
-        // drop cached buffers and retry once
+        // drop cached buffers and retry once (after the device has drained:
+        // an overlapped batch returns a buffer to the pool while the walk
+        // enqueued before it may still read it)
         (void)hipGetLastError();
+        (void)hipDeviceSynchronize();
         for (auto& b : ctx->free_list) (void)hipFree(b.p);
         ctx->free_list.clear();
         e = hipMalloc(&p, bytes);
@@ -379,6 +388,8 @@ extern "C" void gx_context_destroy(gx_context* ctx) {
     if (ctx->ev2) (void)hipEventDestroy(ctx->ev2);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
+    if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
+    if (ctx->tstream) (void)hipStreamDestroy(ctx->tstream);
     delete ctx;
 }
 
@@ -641,6 +652,7 @@ struct FillJob {
     bool w16 = false;                   // twin plane codes, 2 B per cell (w16_ok; batches only)
     bool nocodes = false;               // w16 without code words: the traceback derives them from the planes
     bool noskel = false;                // nocodes without landing columns: the traceback walks the strips in sequence
+    hipStream_t stream = nullptr;       // the stream its fill runs on (nullptr: the context's)
     bool table = false;                 // an alignment table (exportable planes: never the twin codes)
     int g = 0;
     double fill_ms = 0.0;
@@ -671,7 +683,8 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // at offsets off1/off2 (staged path); otherwise c1/c2 are uploaded.
 // track: first max cell + LCS field (alignment_table's max_cell and
 // matches_at_max, algo.rs:258-262, 279); lcs: also keep the LCS plane.
-static hipError_t enqueue_plane_sums(gx_context* ctx, const FillJob& job, const Scores32& sc, unsigned long long* out);
+static hipError_t enqueue_plane_sums(gx_context* ctx, const FillJob& job, const Scores32& sc, unsigned long long* out,
+                                     hipStream_t st = nullptr);
 
 // The twin fill (gx_fill_pk.hip): two pairs per band, one in each 16-bit
 // half.  Its values are kept relative to bases that a band's
@@ -759,6 +772,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                     const std::vector<size_t>* off1 = nullptr, const std::vector<size_t>* off2 = nullptr,
                     const SmallAlpha* alpha = nullptr, int slot = -1, bool collect = true) {
     const int lay = fill_layout(ph, sc, fill_grid_cap(ctx->device));
+    hipStream_t const fs = job.stream ? job.stream : ctx->stream;
     const int SR = strip_rows(lay);
     int total_strips = 0;
     for (const PairHost& h : ph) total_strips += ceil_div((int)h.n, SR);
@@ -959,8 +973,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
             if (ph[p].n) memcpy(&hc[c1o[p]], proc[p].first, ph[p].n);
             if (ph[p].m) memcpy(&hc[c2o[p]], proc[p].second, ph[p].m);
         }
-        HIPCHK(hipMemcpyAsync(job.chars.p, hc.data(), chars_bytes, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));  // hc goes out of scope
+        HIPCHK(hipMemcpyAsync(job.chars.p, hc.data(), chars_bytes, hipMemcpyHostToDevice, fs));
+        HIPCHK(hipStreamSynchronize(fs));  // hc goes out of scope
         cbase = (const uint8_t*)job.chars.p;
     }
     for (size_t p = 0; p < P; ++p) {
@@ -982,7 +996,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     DevBuf trace;
     if (trace_file && *trace_file) {
         if ((rc = pool_get(ctx, (size_t)std::max(strips, 1) * sizeof(StripTrace), &trace))) return rc;
-        HIPCHK(hipMemsetAsync(trace.p, 0, (size_t)std::max(strips, 1) * sizeof(StripTrace), ctx->stream));
+        HIPCHK(hipMemsetAsync(trace.p, 0, (size_t)std::max(strips, 1) * sizeof(StripTrace), fs));
         for (size_t p = 0; p < P; ++p) job.pd[p].trace = (StripTrace*)trace.p + job.pd[p].strip_base;
     }
     // descriptors in (and results out) through pinned staging, laid out [PairDev x P | PairRes x P | status]
@@ -991,10 +1005,10 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     if (!pin) return fail(GX_ENOMEM, "pinned staging buffer");
     memcpy(pin, job.pd.data(), P * sizeof(PairDev));
     if (!order.empty()) memcpy(pin + P * sizeof(PairDev), order.data(), order.size() * sizeof(int));
-    HIPCHK(hipMemcpyAsync(job.pairs.p, pin, P * sizeof(PairDev) + ord_bytes, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemsetAsync(job.progress.p, 0, std::max<size_t>(prog_elems, 1) * sizeof(int), ctx->stream));
-    HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, ctx->stream));
-    HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), ctx->stream));
+    HIPCHK(hipMemcpyAsync(job.pairs.p, pin, P * sizeof(PairDev) + ord_bytes, hipMemcpyHostToDevice, fs));
+    HIPCHK(hipMemsetAsync(job.progress.p, 0, std::max<size_t>(prog_elems, 1) * sizeof(int), fs));
+    HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, fs));
+    HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), fs));
     // twin workgroups: as many per CU as fit 16 waves (the twin kernels hold
     // up to 128 VGPRs: 4 waves per SIMD)
     const int per_cu = (twin && !getenv("GX_FILL_GRID")) ? std::max(1, 16 / (Wf + 1)) : 1;
@@ -1004,42 +1018,42 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                 lay, Wf, twin ? 1 : 0, ctx->last_pbytes, (twin ? twin_tbl : tbl) ? 1 : 0, grid, bands);
     const auto h_launch = std::chrono::steady_clock::now();
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].fb : ctx->ev0, eve = slot >= 0 ? ctx->slots[slot].fe : ctx->ev1;
-    HIPCHK(hipEventRecord(evb, ctx->stream));
+    HIPCHK(hipEventRecord(evb, fs));
     if (bands > 0 && twin)
         HIPCHK(launch_fill_pk(Wf, (planes ? (w16 ? 2 : 1) : 0) + (twin_tbl ? 4 : 0) + (job.nocodes ? 8 : 0) +
                                   (job.noskel ? 16 : 0),
                               (const PairDev*)job.pairs.p, (int)P, (int)tw.size(), bands, (int*)job.counter.p,
-                              (PairRes*)job.pres.p, scl, grid, ctx->stream));
+                              (PairRes*)job.pres.p, scl, grid, fs));
     else if (bands > 0 && cs2)
         HIPCHK(launch_fill_cs2(W, is_local != 0, planes, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
-                               (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, ctx->stream));
+                               (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
     else if (bands > 0)
         HIPCHK(launch_fill(W, lay, is_local != 0, planes ? (d8 ? 2 : 1) : 0, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
-                           (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, ctx->stream));
-    HIPCHK(hipEventRecord(eve, ctx->stream));   // evb..eve brackets the fill kernel alone
+                           (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
+    HIPCHK(hipEventRecord(eve, fs));   // evb..eve brackets the fill kernel alone
     if (ctx->sums_dst && planes && bands > 0) {   // staged checksum run: this pass's plane sums
-        HIPCHK(enqueue_plane_sums(ctx, job, sc, ctx->sums_dst));
+        HIPCHK(enqueue_plane_sums(ctx, job, sc, ctx->sums_dst, fs));
         ctx->sums_dst += 3 * P;
     }
     // strip results exist only for the tracked and local fills (the untracked
     // global fill writes end_SM / end_E itself): no reduction launch otherwise
     if (bands > 0 && (track || is_local))
         HIPCHK(launch_finalize((const PairDev*)job.pairs.p, (int)P, (const StripRes*)job.sres.p,
-                               (PairRes*)job.pres.p, ctx->stream));
+                               (PairRes*)job.pres.p, fs));
     job.res.assign(P, PairRes{});
     int status[2] = {0, 0};
     PairRes* pin_res = (PairRes*)(pin + P * sizeof(PairDev) + ord_bytes);
     int* pin_status = (int*)(pin + P * (sizeof(PairDev) + sizeof(PairRes)) + ord_bytes);
-    HIPCHK(hipMemcpyAsync(pin_res, job.pres.p, P * sizeof(PairRes), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(pin_status, job.counter.p, sizeof status, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(pin_res, job.pres.p, P * sizeof(PairRes), hipMemcpyDeviceToHost, fs));
+    HIPCHK(hipMemcpyAsync(pin_status, job.counter.p, sizeof status, hipMemcpyDeviceToHost, fs));
     job.pin_res = pin_res;
     job.pin_status = pin_status;
     job.slot = slot;
     if (!collect) {   // pipelined: fill_collect() waits for the results later
-        HIPCHK(hipEventRecord(ctx->slots[slot].fdone, ctx->stream));
+        HIPCHK(hipEventRecord(ctx->slots[slot].fdone, fs));
         return GX_OK;
     }
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipStreamSynchronize(fs));
     memcpy(job.res.data(), pin_res, P * sizeof(PairRes));
     unshift_results(job);
     memcpy(status, pin_status, sizeof status);
@@ -1318,17 +1332,28 @@ struct TbStart {
 // dev_end_E: take each start cell's landing column from the fill's device
 // results (global mode, start (n, m)), so the traceback can be queued right
 // behind the fill without waiting for its results on the host.
-static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<TbStart>& starts, TbOut& out,
-                         int slot = -1, bool collect = true, bool dev_end_E = false) {
+// The traceback of the pairs of one or more fills (jv: their pairs in order,
+// `starts` over all of them; the fills share layout and code format), its
+// kernels on stream ts (nullptr: the context's stream).
+static int run_traceback(gx_context* ctx, const std::vector<const FillJob*>& jv, const std::vector<TbStart>& starts,
+                         TbOut& out, int slot, bool collect, bool dev_end_E, hipStream_t ts) {
     const size_t P = starts.size();
+    const FillJob& job = *jv[0];
+    std::vector<const PairDev*> pdv;
+    std::vector<const PairRes*> presv;
+    for (const FillJob* j : jv)
+        for (size_t q = 0; q < j->pd.size(); ++q) { pdv.push_back(&j->pd[q]); presv.push_back((const PairRes*)j->pres.p + q); }
+    // (starts may cover a prefix: a table filled as a twin of itself walks its first pair only)
+    if (pdv.size() < P) return fail(GX_EINVAL, "traceback: more starts than the fills' pairs");
+    if (!ts) ts = ctx->stream;
     std::vector<TbDev> jobs(P);
     std::vector<size_t> so(P);
     size_t stot = 0;   // strips over all pairs
     int max_strips = 1;
     for (size_t p = 0; p < P; ++p) {
         so[p] = stot;
-        stot += (size_t)job.pd[p].strips;
-        max_strips = std::max(max_strips, job.pd[p].strips);
+        stot += (size_t)pdv[p]->strips;
+        max_strips = std::max(max_strips, pdv[p]->strips);
     }
     DevBuf recs, seg, jb, cnt;
     int rc;
@@ -1342,32 +1367,33 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     }
     for (size_t p = 0; p < P; ++p) {
         TbDev& t = jobs[p];
-        const PairDev& d = job.pd[p];
+        const PairDev& d = *pdv[p];
         t.codes = d.codes;
         t.skel = d.skel;
         t.skel_stride = d.skel_stride;
         t.n = d.n; t.m = d.m; t.t16 = d.t16; t.strips = d.strips;
         t.start_i = starts[p].i; t.start_j = starts[p].j; t.start_E = starts[p].E;
-        t.start_E_dev = (dev_end_E && starts[p].i >= 1) ? &((const PairRes*)job.pres.p)[p].end_E : nullptr;
+        t.start_E_dev = (dev_end_E && starts[p].i >= 1) ? &presv[p]->end_E : nullptr;
         t.seg = (int*)seg.p + 4 * so[p];
         t.recs = (uint32_t*)recs.p + so[p] * SR;
         t.srows = SR;
-        t.skel_half = job.twin ? job.pd[p].twin_half : -1;
+        t.skel_half = job.twin ? d.twin_half : -1;
         t.end_ij = (int*)cnt.p + 4 * p;
         t.w16 = job.nocodes ? (const uint8_t*)d.pI : nullptr;   // the twin's code plane (shared by its pairs)
         t.w16_half = d.twin_half;
         t.t4 = d.t4;
     }
+    (void)presv;
     TbDev* pin_jobs = (TbDev*)(slot >= 0 ? pinned_grow(ctx->slots[slot].tjpin, P * sizeof(TbDev))
                                          : io_pinned(ctx, P * sizeof(TbDev)));
     if (!pin_jobs) { cleanup(); return fail(GX_ENOMEM, "pinned staging buffer"); }
     memcpy(pin_jobs, jobs.data(), P * sizeof(TbDev));
-    hipError_t e = hipMemcpyAsync(jb.p, pin_jobs, P * sizeof(TbDev), hipMemcpyHostToDevice, ctx->stream);
-    if (e == hipSuccess) e = hipMemsetAsync(seg.p, 0, std::max<size_t>(stot, 1) * 4 * sizeof(int), ctx->stream);
+    hipError_t e = hipMemcpyAsync(jb.p, pin_jobs, P * sizeof(TbDev), hipMemcpyHostToDevice, ts);
+    if (e == hipSuccess) e = hipMemsetAsync(seg.p, 0, std::max<size_t>(stot, 1) * 4 * sizeof(int), ts);
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].tb : ctx->ev1, eve = slot >= 0 ? ctx->slots[slot].te : ctx->ev2;
-    if (e == hipSuccess) e = hipEventRecord(evb, ctx->stream);
-    if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, max_strips, job.nocodes, job.noskel, ctx->stream);
-    if (e == hipSuccess) e = hipEventRecord(eve, ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(evb, ts);
+    if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, max_strips, job.nocodes, job.noskel, ts);
+    if (e == hipSuccess) e = hipEventRecord(eve, ts);
     // one pinned host block: c | sg | hr
     const size_t nc = 4 * P, nsg = 4 * std::max<size_t>(stot, 1), nhr = std::max<size_t>(stot, 1) * SR;
     const size_t bytes = (nc + nsg) * sizeof(int) + nhr * sizeof(uint32_t);
@@ -1381,7 +1407,7 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     // pipelined: the record copies go on the copy stream after the traceback
     // kernels, so the next fill (queued on the fill stream) starts as soon as
     // the kernels end; the buffers stay held until tb_collect
-    hipStream_t cs = collect ? ctx->stream : ctx->cstream;
+    hipStream_t cs = collect ? ts : ctx->cstream;
     if (!collect && e == hipSuccess) e = hipStreamWaitEvent(cs, eve, 0);
     if (e == hipSuccess) e = hipMemcpyAsync(c, cnt.p, nc * sizeof(int), hipMemcpyDeviceToHost, cs);
     if (e == hipSuccess) e = hipMemcpyAsync(sg, seg.p, nsg * sizeof(int), hipMemcpyDeviceToHost, cs);
@@ -1399,7 +1425,7 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
     }
     if (e == hipSuccess) e = hipEventSynchronize(eve);
     const auto q2 = clk::now();
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ts);
     if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug"))
         fprintf(stderr, "[gx DEBUG] traceback: D2H enqueue %.3f ms, kernels done +%.3f ms, copies done +%.3f ms\n",
                 std::chrono::duration<double, std::milli>(q1 - q0).count(),
@@ -1418,6 +1444,11 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
         if (out.end_i[p] < 0) return fail(GX_EHIP, "traceback: landing column out of range (incomplete fill)");
     }
     return GX_OK;
+}
+
+static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<TbStart>& starts, TbOut& out,
+                         int slot = -1, bool collect = true, bool dev_end_E = false) {
+    return run_traceback(ctx, std::vector<const FillJob*>{&job}, starts, out, slot, collect, dev_end_E, nullptr);
 }
 
 // Records of a traceback enqueued with collect = false (pipelined path).
@@ -1689,12 +1720,12 @@ extern "C" int gx_table_export_rows(const gx_table* t, int which, size_t row0, s
 
 // Plane checksums of job `job`'s pairs into the device buffer out[P][3].
 static hipError_t enqueue_plane_sums(gx_context* ctx, const FillJob& job, const Scores32& sc,
-                                     unsigned long long* out) {
+                                     unsigned long long* out, hipStream_t st) {
     int max_strips = 0;
     for (const PairDev& d : job.pd) max_strips = std::max(max_strips, d.strips);
     return launch_plane_sums((const PairDev*)job.pairs.p, (int)job.pd.size(), max_strips, job.lay,
                              job.w16 ? 3 : job.d8 ? 2 : 1,
-                             sc.h, sc.g, sc.floor_, job.shift ? sc.g : 0, out, ctx->stream);
+                             sc.h, sc.g, sc.floor_, job.shift ? sc.g : 0, out, st ? st : ctx->stream);
 }
 
 extern "C" int gx_table_plane_sums(const gx_table* t, uint64_t* sums) {
@@ -2096,6 +2127,135 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
 // go back to the pool as soon as their last user is queued (everything runs on
 // one stream); pinned staging and events alternate between two slots.  Walks
 // and results are those of the last pass; *fill_ms is the mean fill time.
+// Overlapped pipeline for a global untracked batch on the twin fill without
+// landing columns (the sequential strip walk, tb_seq_kernel, ~5 ms for a 30k
+// pair, uses a few CUs): the pairs are split into a small group A (about a
+// fifth) and the rest, B, each filled by its own launch on its own stream.
+// Step k's walk (stream tstream, after both fills) then runs beside step k+1's
+// group-A fill, whose plane codes go to a second A buffer (two A buffers, one
+// B buffer: the device holds P + |A| pairs' planes); step k+1's group-B fill
+// waits on the device for step k's walk before it reuses B's buffers.  Only
+// buffers no pending work uses go back to the pool (a walk's fills after it
+// was collected; B's before its next fill, which waits for the walk that
+// reads them), so any stream may take them.  Returns GX_EAGAIN (nothing
+// left enqueued) when the two groups' fills do not both take the twin fill
+// without landing columns: the caller then runs the plain pipeline.
+static constexpr int kOverlapNo = -1000;
+static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
+                              const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc, const HostScores& hs,
+                              const Scores32& sc, bool planes, int nsteps, std::vector<Walk>& walks, double* fill_ms,
+                              const uint8_t* chars_dev, const std::vector<size_t>* off1,
+                              const std::vector<size_t>* off2, const SmallAlpha& alpha,
+                              const std::vector<size_t>& idx) {
+    const size_t P = ph.size(), Q = idx.size();
+    const size_t G = std::max<size_t>(2, (Q / 5) & ~(size_t)1);   // group A: about a fifth, even (twins)
+    std::vector<size_t> gi[2];
+    gi[0].assign(idx.begin(), idx.begin() + (long)G);
+    gi[1].assign(idx.begin() + (long)G, idx.end());
+    std::vector<PairHost> dph[2];
+    std::vector<std::pair<const uint8_t*, const uint8_t*>> dproc[2];
+    std::vector<size_t> o1[2], o2[2];
+    for (int g = 0; g < 2; ++g)
+        for (size_t p : gi[g]) {
+            dph[g].push_back(ph[p]);
+            dproc[g].push_back(proc[p]);
+            if (chars_dev) { o1[g].push_back((*off1)[p]); o2[g].push_back((*off2)[p]); }
+        }
+    for (hipStream_t* st : {&ctx->stream2, &ctx->tstream})
+        if (!*st) HIPCHK(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+    hipStream_t const sA = ctx->stream, sB = ctx->stream2, sT = ctx->tstream;
+    FillJob jA[2], jB;
+    bool jb_live = false;
+    std::vector<int> dev_of(P, -1);
+    for (size_t q = 0; q < Q; ++q) dev_of[q < G ? gi[0][q] : gi[1][q - G]] = (int)q;
+    std::vector<TbStart> starts(Q);
+    for (size_t q = 0; q < Q; ++q) {
+        const PairHost& h = q < G ? dph[0][q] : dph[1][q - G];
+        starts[q] = TbStart{(int)h.n, (int)h.m, 0};
+    }
+    std::vector<PairRes> res(P, PairRes{});
+    std::vector<uint64_t> si(P), sj(P);
+    std::vector<int64_t> score(P);
+    double fsum = 0;
+    auto fill = [&](int g, int k) {
+        FillJob& j = g == 0 ? jA[k & 1] : jB;
+        j.stream = g == 0 ? sA : sB;
+        return run_fill(ctx, dproc[g], dph[g], sc, 0, planes, false, false, j, chars_dev,
+                        chars_dev ? &o1[g] : nullptr, chars_dev ? &o2[g] : nullptr, &alpha, 2 * g + (k & 1), false);
+    };
+    auto trace = [&](int k) {
+        HIPCHK(hipStreamWaitEvent(sT, ctx->slots[k & 1].fdone, 0));
+        HIPCHK(hipStreamWaitEvent(sT, ctx->slots[2 + (k & 1)].fdone, 0));
+        return run_traceback(ctx, std::vector<const FillJob*>{&jA[k & 1], &jB}, starts, ctx->slots[k & 1].out, k & 1,
+                             false, false, sT);
+    };
+    auto take = [&](const FillJob& j, const std::vector<size_t>& g) {
+        for (size_t q = 0; q < g.size(); ++q) res[g[q]] = j.res[q];
+    };
+    // the fills' time per step: one step's fills overlap the next step's and
+    // the walks, so the whole fill pipeline (the first fill's start to the
+    // last fill's end, ev0..ev1) over the steps
+    auto drain = [&]() {
+        (void)hipStreamSynchronize(sA); (void)hipStreamSynchronize(sB); (void)hipStreamSynchronize(sT);
+        (void)hipStreamSynchronize(ctx->cstream);
+        for (auto& j : jA) job_release(ctx, j);
+        job_release(ctx, jB);
+        release_held(ctx, 0);
+        release_held(ctx, 1);
+    };
+    unsigned long long* const sums0 = ctx->sums_dst;
+    HIPCHK(hipEventRecord(ctx->ev0, sA));
+    int rc = fill(0, 0);
+    if (!rc) { rc = fill(1, 0); jb_live = !rc; }
+    if (!rc && !(jA[0].noskel && jB.noskel && jA[0].lay == jB.lay && jA[0].twin && jB.twin)) {
+        drain();
+        ctx->sums_dst = sums0;   // (the plain pipeline writes this pass's checksums again)
+        return kOverlapNo;
+    }
+    if (!rc) rc = trace(0);
+    for (int k = 0; k < nsteps && !rc; ++k) {
+        const int a = k & 1;
+        if (k + 1 < nsteps) {
+            if ((rc = fill(0, k + 1))) break;                 // beside step k's walk (its buffers: step k-1's, collected)
+            if ((rc = fill_collect(ctx, jB))) break;          // step k's group B, before jB is refilled
+            take(jB, gi[1]);
+            job_release(ctx, jB);                             // read by step k's walk: the next B fill waits for it
+            HIPCHK(hipStreamWaitEvent(sB, ctx->slots[a].te, 0));
+            if ((rc = fill(1, k + 1))) break;
+            if (k + 2 == nsteps) {                            // behind the last fill (B's comes after A's, below)
+                HIPCHK(hipStreamWaitEvent(sB, ctx->slots[(k + 1) & 1].fdone, 0));
+                HIPCHK(hipEventRecord(ctx->ev1, sB));
+            }
+            if (!(jA[(k + 1) & 1].noskel && jB.noskel)) { rc = fail(GX_EHIP, "overlapped batch: fill formats changed"); break; }
+            if ((rc = trace(k + 1))) break;
+        } else {
+            if ((rc = fill_collect(ctx, jB))) break;
+            take(jB, gi[1]);
+        }
+        if ((rc = fill_collect(ctx, jA[a]))) break;
+        take(jA[a], gi[0]);
+        if (k + 1 == nsteps) {
+            HIPCHK(hipEventSynchronize(ctx->ev1));
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+            fsum = ms;
+        }
+        if ((rc = tb_collect(ctx, a, Q, ctx->slots[a].out))) break;
+        job_release(ctx, jA[a]);                              // its walk is done
+        for (size_t p = 0; p < P; ++p)
+            start_cell_common(hs, 0, ph[p].n, ph[p].m, start_in(res[p]), &si[p], &sj[p], &score[p]);
+        if ((rc = label_batch(ctx, ph, hs, 0, false, dev_of, si, sj, score, res, ctx->slots[a].out,
+                              jA[a].fill_ms + jB.fill_ms, walks)))
+            break;
+    }
+    drain();
+    (void)jb_live;
+    if (rc) return rc;
+    ctx->last_groups = 2;
+    if (fill_ms) *fill_ms = fsum / nsteps;
+    return GX_OK;
+}
+
 static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
                             const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc, const HostScores& hs,
                             const Scores32& sc, int is_local, bool planes, bool track, int nsteps,
@@ -2103,6 +2263,7 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
                             const std::vector<size_t>* off1, const std::vector<size_t>* off2,
                             const SmallAlpha* staged_alpha) {
     const size_t P = ph.size();
+    ctx->last_groups = 1;
     std::vector<size_t> idx;
     for (size_t p = 0; p < P; ++p) if (ph[p].n >= 1 && ph[p].m >= 1) idx.push_back(p);
     if (nsteps <= 1 || idx.empty() || getenv("GX_TRACE_FILE")) {
@@ -2168,6 +2329,16 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
     auto since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     double t_fill = 0, t_tbwait = 0, t_label = 0, t_trace = 0;   // host time per phase (GX_LOG=debug)
     const auto t_all = clk::now();
+    size_t nmax_b = 0;
+    for (const PairHost& h : dph) nmax_b = std::max(nmax_b, h.n);
+    // (long pairs only: a short pair's walk is short; and both groups must
+    // fill the grid on the twin fill, or the attempt falls back)
+    if (!is_local && !track && planes && idx.size() >= 16 && nmax_b >= 4096 && !pool_poison() &&
+        !(getenv("GX_OVERLAP") && !strcmp(getenv("GX_OVERLAP"), "0"))) {
+        const int orc = batch_core_overlap(ctx, ph, proc, hs, sc, planes, nsteps, walks, fill_ms, chars_dev, off1, off2,
+                                           alpha, idx);
+        if (orc != kOverlapNo) return orc;
+    }
     if (!is_local && !track) {
         // global untracked: every start cell is (n, m) and its landing column
         // is read on the device, so each step's traceback is queued right
@@ -2547,6 +2718,7 @@ extern "C" int gx_staged_steps(const gx_context* ctx, size_t pair, gx_step* step
 
 extern "C" int gx_batch_chunks(const gx_context* ctx) { return ctx ? ctx->last_chunks : -1; }
 extern "C" int gx_fill_twin(const gx_context* ctx) { return ctx ? ctx->last_twin : -1; }
+extern "C" int gx_fill_groups(const gx_context* ctx) { return ctx ? ctx->last_groups : -1; }
 
 extern "C" int gx_fill_info(const gx_context* ctx, int* layout, int* band_waves, int* plane_bytes_per_cell) {
     if (!ctx) return fail(GX_EINVAL, "context is NULL");

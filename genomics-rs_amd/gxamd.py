@@ -75,7 +75,7 @@ EXPORTED = ["gx_last_error", "gx_version", "gx_context_create", "gx_context_dest
             "gx_table_plane_sums", "gx_retrace", "gx_table_free", "gx_align", "gx_align_batch", "gx_align_batch_multi",
             "gx_stage_pairs",
             "gx_run_staged", "gx_run_staged_steps", "gx_staged_plane_sums", "gx_staged_steps",
-            "gx_fill_info", "gx_batch_chunks", "gx_fill_twin", "gx_plane_bytes_per_cell", "gx_twin_admission",
+            "gx_fill_info", "gx_batch_chunks", "gx_fill_twin", "gx_fill_groups", "gx_plane_bytes_per_cell", "gx_twin_admission",
             "gx_fasta_load",
             "gx_config_load", "gx_format_alignment", "gx_format_table"]
 
@@ -123,6 +123,7 @@ def lib():
     L.gx_fill_info.argtypes = [vp] + [ctypes.POINTER(ctypes.c_int)] * 3
     L.gx_batch_chunks.argtypes = [vp]
     L.gx_fill_twin.argtypes = [vp]
+    L.gx_fill_groups.argtypes = [vp]
     L.gx_plane_bytes_per_cell.argtypes = [ctypes.POINTER(CScores), ctypes.c_int]
     L.gx_twin_admission.argtypes = [ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int64,
                                     ctypes.POINTER(ctypes.c_int64)]
@@ -325,7 +326,8 @@ class Context:
         v = [ctypes.c_int() for _ in range(3)]
         _check(lib().gx_fill_info(self.ptr, *[ctypes.byref(x) for x in v]))
         return {"layout": v[0].value, "band_waves": v[1].value, "plane_bytes_per_cell": v[2].value,
-                "chunks": lib().gx_batch_chunks(self.ptr), "twin": lib().gx_fill_twin(self.ptr)}
+                "chunks": lib().gx_batch_chunks(self.ptr), "twin": lib().gx_fill_twin(self.ptr),
+                "groups": lib().gx_fill_groups(self.ptr)}
 
     def __del__(self):
         try:

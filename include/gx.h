@@ -223,6 +223,11 @@ int gx_batch_chunks(const gx_context* ctx);
  * Measurement only (GX_TWIN=0 disables it, GX_TWIN=1 forces it where the
  * range bound admits it; by default deep band queues take it). */
 int gx_fill_twin(const gx_context* ctx);
+
+/* Fill launches per pass of the last staged / batch call: 2 when the pairs
+ * ran as two groups whose walks overlap the next pass's fills (a batch of
+ * long pairs on the twin fill), else 1. */
+int gx_fill_groups(const gx_context* ctx);
 /* Score-plane bytes per cell a batch launch (layout 0, no max tracking)
  * writes with these scores: 3 when the compact format's range proof holds
  * (global mode, g, h <= 0, differences within a signed byte), else 12; -1 on

@@ -72,8 +72,11 @@ def main():
     with open(bj if os.path.exists(bj) else os.path.join(src, "kt_bench.json")) as f:
         bench = json.loads(f.read().strip().splitlines()[-1])
     workload = bench["config"]["workload"]
-    wr = pmc["WRITE_SIZE"]["avg_kib"] * 1024
-    rd = pmc["FETCH_SIZE"]["avg_kib"] * 1024 * 2
+    # a pass may be two fill launches (the overlapped batch):
+    # the per-pass figures are the launch average times the launches per pass
+    groups = int(bench.get("fill_launch", {}).get("groups", 1) or 1)
+    wr = pmc["WRITE_SIZE"]["avg_kib"] * 1024 * groups
+    rd = pmc["FETCH_SIZE"]["avg_kib"] * 1024 * 2 * groups
     out = {
         "workload": workload,
         "kernel": pmc["WRITE_SIZE"]["kernel"],
@@ -82,7 +85,9 @@ def main():
         "hbm_bytes_per_launch": int(wr + rd),
         "algorithmic_bytes_per_launch": bench["roofline"].get("hbm", bench["roofline"])["algorithmic_bytes_per_launch"],
         "correction": "WRITE_SIZE KiB x1024 (exact for 16-B/lane stores); FETCH_SIZE KiB x1024 x2 (gfx950 "
-                      "reports half of wide coalesced reads; MI355X_MICROARCH.md 'HBM')",
+                      "reports half of wide coalesced reads; MI355X_MICROARCH.md 'HBM'); per pass = the launch "
+                      "average x fill launches per pass",
+        "fill_launches_per_pass": groups,
         "raw": pmc,
         "source": f"rocprofv3 --pmc WRITE_SIZE / --pmc FETCH_SIZE, separate passes, bench.py --steps 2 --warmup 1",
     }
