@@ -87,7 +87,10 @@ def main():
         k, v = counters(os.path.join(src, case))
         with open(os.path.join(src, f"{case}.json")) as f:
             bench = json.loads(f.read().strip().splitlines()[-1])
-        cells = bench["config"]["cells_per_step"] // bench["n_gpus"]
+        # a pass may be two fill launches: the counters are per
+        # launch (rocprofv3 --pmc serialises dispatches), so per launch cells
+        groups = int(bench.get("fill_launch", {}).get("groups", 1) or 1)
+        cells = bench["config"]["cells_per_step"] // bench["n_gpus"] // groups
         cyc = v["GRBM_GUI_ACTIVE"] / 8
         dur = v["duration_ns"] * 1e-9
         clk = cyc / dur
