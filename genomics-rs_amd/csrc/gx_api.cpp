@@ -653,6 +653,7 @@ struct FillJob {
     bool nocodes = false;               // w16 without code words: the traceback derives them from the planes
     bool noskel = false;                // nocodes without landing columns: the traceback walks the strips in sequence
     hipStream_t stream = nullptr;       // the stream its fill runs on (nullptr: the context's)
+    bool plan_only = false;             // run_fill: decide layout and formats only (no buffers, no launch)
     bool table = false;                 // an alignment table (exportable planes: never the twin codes)
     int g = 0;
     double fill_ms = 0.0;
@@ -862,6 +863,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     ctx->last_lay = cs2 ? 2 : lay; ctx->last_W = Wf;
     ctx->last_pbytes = planes ? (w16 ? 2 : (int)(plane_esz * 3)) : 0;
     const size_t P = ph.size();
+    if (job.plan_only) { job.twin = twin; return GX_OK; }
     job.pd.assign(P, PairDev{});
     // -- sizes
     size_t chars_bytes = 0, plane_elems = 0, code_elems = 0, feed_recs = 0, prog_elems = 0, skel_elems = 0;
@@ -2203,6 +2205,16 @@ static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
         release_held(ctx, 0);
         release_held(ctx, 1);
     };
+    {   // both groups must take the twin fill without landing columns: decided before anything is enqueued
+        FillJob pa, pb;
+        pa.plan_only = pb.plan_only = true;
+        int prc = run_fill(ctx, dproc[0], dph[0], sc, 0, planes, false, false, pa, chars_dev, chars_dev ? &o1[0] : nullptr,
+                           chars_dev ? &o2[0] : nullptr, &alpha, 0, false);
+        if (!prc)
+            prc = run_fill(ctx, dproc[1], dph[1], sc, 0, planes, false, false, pb, chars_dev,
+                           chars_dev ? &o1[1] : nullptr, chars_dev ? &o2[1] : nullptr, &alpha, 2, false);
+        if (prc || !(pa.noskel && pb.noskel && pa.twin && pb.twin && pa.lay == pb.lay)) return kOverlapNo;
+    }
     unsigned long long* const sums0 = ctx->sums_dst;
     HIPCHK(hipEventRecord(ctx->ev0, sA));
     int rc = fill(0, 0);

@@ -75,6 +75,10 @@ def main():
     # a pass may be two fill launches (the overlapped batch):
     # the per-pass figures are the launch average times the launches per pass
     groups = int(bench.get("fill_launch", {}).get("groups", 1) or 1)
+    pwb = os.path.join(src, "pw_bench.json")   # (the PMC pass's own launch shape, if it differs)
+    if os.path.exists(pwb):
+        with open(pwb) as f:
+            groups = int(json.loads(f.read().strip().splitlines()[-1]).get("fill_launch", {}).get("groups", 1) or 1)
     wr = pmc["WRITE_SIZE"]["avg_kib"] * 1024 * groups
     rd = pmc["FETCH_SIZE"]["avg_kib"] * 1024 * 2 * groups
     out = {
