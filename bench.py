@@ -616,6 +616,11 @@ def main():
            "kernel": kname, "fill_ms_avg": round(avg_fill_ms, 3),
            "algorithmic_bytes_per_cell": bytes_per_cell,
            "algorithmic_bytes_per_launch": fill_bytes}
+    if finfo.get("groups", 1) == 2:
+        # the overlapped batch: a pass is two concurrent fill
+        # launches; "launch" figures are per pass, the time is the fill
+        # pipeline's per pass, the PMC profile the same kernel run one launch a pass
+        hbm["fill_launches_per_pass"] = 2
     if valu is not None and keep_planes and bytes_per_cell in (2, 3):
         # compact planes / twin codes: the fill is bound by VALU issue, not HBM -- lane-ops
         # per launch (VALU/cell x cells, SQ_INSTS_VALU profile) over the live
@@ -631,6 +636,8 @@ def main():
                     "peak_basis": f"1024 SIMDs x 64 lanes x {valu['clock_ghz']} GHz / {valu['cpi_fill_mix']} cycles "
                                   f"per wave64 VALU instruction at the fill's mix (tools/valu_probe.hip)",
                     "source": valu["source"], "hbm": hbm}
+        if finfo.get("groups", 1) == 2:
+            roofline["fill_launches_per_pass"] = 2
     else:
         roofline = hbm
 
