@@ -327,6 +327,57 @@ def config_record(gx, ctx, which: str, steps: int):
     return out
 
 
+LOCAL_BATCH_PAIRS = 32   # tests/golden/make_golden.py LOCAL_RELATED
+
+
+def local_batch_record(gx, ctx, steps: int):
+    """A Smith-Waterman batch (BASELINE config 3's mode at config 2's size):
+    the first 32 related 30k pairs (SURVEY 8(d) M1's variant, s2 = s1 with ~10 %
+    substitutions and ~1 % indels, so every pair has a long local alignment)
+    aligned locally (algo.rs:231-248 with the 0 floor, last-max start
+    algo.rs:310-322), resident in HBM, score planes + traceback + labelled
+    alignment per step -- the local twin fill (gx_fill_pk.hip LOCAL) when the
+    host admits it.  `steps` timed passes, then one untimed pass whose every
+    pair is compared with tests/golden/synthetic_related_local_L30000.json
+    (score, statistics, alignment sha256, the three plane checksums)."""
+    pairs = [related_pair(k, 30000) for k in range(LOCAL_BATCH_PAIRS)]
+    scores = gx.Scores(*SCORES)
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    st.run(scores, True, True)
+    t0 = time.perf_counter()
+    _, fms = st.run(scores, True, True, steps=steps)
+    el = time.perf_counter() - t0
+    finfo = ctx.fill_info()
+    cells = sum(len(a) * len(b) for a, b in pairs)
+    bpc = finfo["plane_bytes_per_cell"]
+    ach = bpc * cells / (fms * 1e-3) / 1e9
+    out = {"workload": f"{len(pairs)} related 30k pairs (SURVEY 8(d) M1 variant), local SW, scores {SCORES}, "
+                       f"{plane_desc(bpc)}",
+           "gcups": round(cells * steps / el / 1e9, 3), "ms_per_step": round(el / steps * 1e3, 3),
+           "fill_ms_avg": round(fms, 3), "fill_gcups": round(cells / (fms * 1e-3) / 1e9, 3), "steps": steps,
+           "fill_launch": finfo,
+           "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(ach / PEAK_HBM_GBS, 4), "algorithmic_bytes_per_cell": bpc,
+                        "note": "plane bytes of the fill; the local twin fill is VALU-bound like the global one "
+                                "(DESIGN.md 6.7)"}}
+    path = os.path.join(ROOT, "tests", "golden", "synthetic_related_local_L30000.json")
+    with open(path) as f:
+        gold = {c["k"]: c for c in json.load(f)["cases"]}
+    res, _ = st.run(scores, True, True, plane_sums=True)
+    sums = st.plane_sums()
+    for p in range(len(pairs)):
+        r, c = res[p], gold[p]
+        got = (r.score, [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps], r.n_steps,
+               alignment_sha256(st.steps(p)), [int(x) for x in sums[0, p]])
+        want = (c["score"], c["stats"], c["n_steps"], c["alignment_sha256"], [int(x) for x in c["plane_sums"]])
+        if got != want:
+            raise RuntimeError(f"local_batch: pair {p} differs from the oracle digest: {got[:3]} != {want[:3]}")
+    out["parity"] = {"pairs_checked": len(pairs), "bit_exact": True,
+                     "fields": "score, statistics, alignment sha256, I/D/S plane checksums",
+                     "source": os.path.relpath(path, ROOT)}
+    return out
+
+
 def allvsall_share(gx, rank: int, world: int):
     """BASELINE config 4: rank r's longest-processing-time share of the 45
     pairs i<j of the comparison_data genomes (files in name order, the same
@@ -510,6 +561,8 @@ def main():
                     help="also time the batch with int32 score planes (12 B/cell, HBM roofline), 1 GPU only; 0 = skip")
     ap.add_argument("--no-plane-steps", type=int, default=2,
                     help="also time the batch without plane stores (compute ceiling), 1 GPU only; 0 = skip")
+    ap.add_argument("--local-batch-steps", type=int, default=3,
+                    help="synthetic, 1 GPU: also time a local (SW) batch of 32 related 30k pairs (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -730,6 +783,8 @@ def main():
         # BASELINE configs 2 and 3, the drop-in single-pair align calls, timed here
         out["config2"] = config_record(gx, ctx, "covid", args.config_steps)
         out["config3"] = config_record(gx, ctx, "brca2", args.config_steps)
+    if world == 1 and args.workload == "synthetic" and args.local_batch_steps > 0 and not args.local:
+        out["local_batch"] = local_batch_record(gx, ctx, args.local_batch_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if len(pairs[0][1]) > 40000:
             # the reference layout needs (n+1)(m+1) x 48 B (197 GB at 64k)

@@ -43,7 +43,7 @@ hipError_t launch_fill_cs2(int W, bool local, bool planes, bool tbl, const PairD
                            int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                            hipStream_t st);
 hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int npairs, int ntwins, int total_bands,
-                          int* d_counter, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st);
+                          int* d_counter, PairRes* d_pres, StripRes* d_sres, Scores32 sc, int grid, hipStream_t st);
 hipError_t launch_fill_wide(const WideDev* d_pairs, int npairs, WideScores sc, WideRes* d_res, int local, int track,
                             hipStream_t st);
 hipError_t launch_wide_plane_sums(const int64_t* pI, const int64_t* pD, const int64_t* pS, int n, int m,
@@ -445,6 +445,7 @@ static int check_scores(const gx_scores* s, size_t n, size_t m, HostScores* hs, 
     sc->dbg = dbg ? atoi(dbg) : 0;
     sc->shift = 0;
     for (int k = 0; k < 4; ++k) sc->sym[k] = -1;
+    sc->koff = 0;
     return GX_OK;
 }
 
@@ -746,12 +747,42 @@ static std::vector<std::pair<int, int>> twin_table(const std::vector<PairHost>& 
 // long_ok: the launch will be the twin fill without landing columns (twin
 // plane codes, no code words, no skeleton): no int16 column quantity is
 // left, so the 31,920-column limit of the int16 landing columns is lifted.
+// The local twin fill (gx_fill_pk.hip LOCAL) keeps plain values on base 0: a
+// local value lies in [-(|a| + |s_min|), min(n, m) max(s_max, 0)] (algo.rs:103:
+// I, D and score_max are floored at 0 and only matches raise them), so the
+// biased halves hold every value, score-table add and tracker difference while
+// that bound plus the constants stays below 32,000; the row trackers keep
+// 16-bit columns (m <= 65,535).  No base moves, so twins of any shapes and any
+// band width qualify.  Only as the launch without code words or skeleton
+// (twin plane codes, the sequential walk): long_ok.
+static long long twin_local_bound(const std::vector<PairHost>& ph, const std::vector<std::pair<int, int>>& tw,
+                                  const Scores32& sc) {
+    const long long g = sc.g, a = (long long)sc.h + sc.g;
+    const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
+    long long vmax = 0;
+    for (const auto& t : tw)
+        for (int p : {t.first, t.second})
+            vmax = std::max(vmax, (long long)std::min(ph[p].n, ph[p].m) * std::max(smax, 0LL));
+    return vmax + std::llabs(smax) + std::llabs(smin) + std::max(0LL, -smin) + std::llabs(a) + std::llabs(g) + 64;
+}
 static int twin_width(const std::vector<PairHost>& ph, const std::vector<std::pair<int, int>>& tw, const Scores32& sc,
                       int is_local, bool track, bool lcs, int lay, bool planes, bool d8, int W_want,
                       bool long_ok = false) {
     if (const char* e = getenv("GX_TWIN"); e && !strcmp(e, "0")) return 0;
-    if (lay != 0 || is_local || track || lcs || (planes && !d8) || sc.g > 0 || sc.h > 0) return 0;
+    if (lay != 0 || track || lcs || (planes && !d8) || sc.g > 0 || sc.h > 0) return 0;
     if (ph.empty()) return 0;
+    if (is_local) {
+        if (!planes || !long_ok) return 0;
+        for (const auto& t : tw) {
+            const PairHost& x = ph[t.first];
+            const PairHost& y = ph[t.second];
+            if (!x.n || !x.m || !y.n || !y.m || std::max(x.m, y.m) > 65535) return 0;
+        }
+        if (twin_local_bound(ph, tw, sc) >= 32000) return 0;
+        for (int W : {15, 8, 7, 4, 3})
+            if (W <= W_want || W == 3) return W;
+        return 0;
+    }
     long long dm = 0;
     for (const auto& t : tw) {
         const PairHost& x = ph[t.first];
@@ -810,7 +841,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     int wt_want = 15;
     if (const char* e = getenv("GX_BAND_WAVES")) wt_want = atoi(e);
     else wt_want = fill_band_waves(false, total_strips / 2, fill_grid_cap(ctx->device), lay, min_strips);
-    const std::vector<std::pair<int, int>> tw = twin_table(ph, twin_gap_cap(sc, wt_want >= 15 ? 15 : wt_want >= 8 ? 8 : wt_want >= 7 ? 7 : wt_want >= 4 ? 4 : 3));
+    const std::vector<std::pair<int, int>> tw = twin_table(
+        ph, is_local ? INT_MAX : twin_gap_cap(sc, wt_want >= 15 ? 15 : wt_want >= 8 ? 8 : wt_want >= 7 ? 7 : wt_want >= 4 ? 4 : 3));
     {
         const char* tce0 = getenv("GX_TWIN_CODES");
         const char* tse0 = getenv("GX_TWIN_SKEL");
@@ -838,6 +870,10 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     }
     const bool twin = Wt > 0;
     job.twin = twin;
+    if (twin && is_local) {   // the local twin's scores carry + K so that its score tables hold bytes >= 0
+        const int K = std::max(0, -std::min(sc.sm, sc.smm));
+        scl.koff = K; scl.sm = sc.sm + K; scl.smm = sc.smm + K;
+    }
     const bool w16 = twin && planes && !job.table && w16_ok(sc);
     job.w16 = w16;
     // with twin plane codes the fill stores no code words (0.25 B/cell less):
@@ -1023,9 +1059,9 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     HIPCHK(hipEventRecord(evb, fs));
     if (bands > 0 && twin)
         HIPCHK(launch_fill_pk(Wf, (planes ? (w16 ? 2 : 1) : 0) + (twin_tbl ? 4 : 0) + (job.nocodes ? 8 : 0) +
-                                  (job.noskel ? 16 : 0),
+                                  (job.noskel ? 16 : 0) + (is_local ? 32 : 0),
                               (const PairDev*)job.pairs.p, (int)P, (int)tw.size(), bands, (int*)job.counter.p,
-                              (PairRes*)job.pres.p, scl, grid, fs));
+                              (PairRes*)job.pres.p, (StripRes*)job.sres.p, scl, grid, fs));
     else if (bands > 0 && cs2)
         HIPCHK(launch_fill_cs2(W, is_local != 0, planes, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
                                (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
@@ -1727,7 +1763,7 @@ static hipError_t enqueue_plane_sums(gx_context* ctx, const FillJob& job, const 
     for (const PairDev& d : job.pd) max_strips = std::max(max_strips, d.strips);
     return launch_plane_sums((const PairDev*)job.pairs.p, (int)job.pd.size(), max_strips, job.lay,
                              job.w16 ? 3 : job.d8 ? 2 : 1,
-                             sc.h, sc.g, sc.floor_, job.shift ? sc.g : 0, out, st ? st : ctx->stream);
+                             sc.h, sc.g, sc.floor_, (job.shift || job.w16) ? sc.g : 0, out, st ? st : ctx->stream);
 }
 
 extern "C" int gx_table_plane_sums(const gx_table* t, uint64_t* sums) {

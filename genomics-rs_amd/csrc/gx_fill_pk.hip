@@ -132,6 +132,7 @@ __device__ __forceinline__ void bytes_step(uint32_t (&xI)[2][2], uint32_t (&xS)[
 // Packed scores (both halves equal): h, sm'' = s_match - 2g, dsm = (s_mismatch - 2g) - sm''
 struct PkScores {
     uint32_t nh, smp, dsm;   // -h (>= 0) in both halves, the score_max offset, the mismatch - match delta
+    uint32_t ng, na, Z;      // local (unshifted values): -g, -(h + g) (>= 0), and the biased zero of the floor
 };
 
 // Twin plane code (PLANES == 2, 2 B per cell): the three differences of a
@@ -167,6 +168,7 @@ struct RowPk {
     uint32_t I, SD, Dd, SMp, SMtl;   // insert, max(sub, delete), delete successor, score_max + sm'', SMp(i-1, j-1)
     uint32_t cI, cD;                 // code bit-planes, negated (16 steps, one per half; pcode)
     uint32_t E, Etl;                 // landing columns (int16 per half)
+    uint32_t lb, lc;                 // local: last max of score_max along the row (biased) and its column
 };
 struct LanePk {
     RowPk a, b;
@@ -176,12 +178,24 @@ struct LanePk {
 // algo.rs:222-268 on the shifted values, both pairs at once; MASKED keeps
 // the lanes outside columns 1..m unchanged, per pair (a twin's two pairs may
 // differ in length: the shorter one's state stays at its last column).
-template <bool MASKED, bool TBL, bool CODES, bool NOE = false>
+//
+// LOCAL (Smith-Waterman, algo.rs:231-248 with is_local): plain (unshifted)
+// values on base 0 -- a local value lies in [0, min(n, m) max(s, 0)] and the
+// host admits the launch only while that fits the biased halves
+// (twin_width) -- so the 0 floor of score_max is one v_pk_max_u16 against the
+// biased zero k.Z in each gap recurrence, and the row keeps the last maximum
+// of score_max with its column (algo.rs:310-322, row-major: the later column
+// wins ties; jv = the column, both halves).  Plane codes store x_I - g as the
+// shifted fill does (Iold - |g| is the insert recurrence's own term).
+template <bool MASKED, bool TBL, bool CODES, bool NOE = false, bool LOCAL = false>
 __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const uint32_t sm_in, const uint32_t e_up,
                                         const uint32_t c2, const uint32_t c1, const uint32_t c1h, const uint32_t act,
                                         const PkScores& k,
-                                        uint32_t& oI, uint32_t& oD, uint32_t& oS, uint32_t& oIold) {
-    const uint32_t In = pmaxu(st.I, st.SD - k.nh);                // max(I, max(S,D) + h)   (algo.rs:231-236)
+                                        uint32_t& oI, uint32_t& oD, uint32_t& oS, uint32_t& oIold,
+                                        const uint32_t jv = 0u) {
+    const uint32_t Ig = LOCAL ? st.I - k.ng : st.I;                // (biased halves: no borrow across them)
+    const uint32_t In = LOCAL ? pmaxu(pmaxu(Ig, st.SD - k.na), k.Z)   // max(I + g, max(S,D) + h + g, 0)
+                              : pmaxu(st.I, st.SD - k.nh);          // max(I, max(S,D) + h)   (algo.rs:231-236)
     // SM(i-1,j-1) + s''  (algo.rs:245-248).  TBL: c1/c1h are the row's score
     // tables of the two pairs (byte k: s_match'' if the row's char is symbol
     // k, else s_mismatch''; SM is then kept without the s_match'' offset) and
@@ -193,7 +207,8 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
     const uint32_t IS = pmaxu(In, Sn);
     const uint32_t SMn = pmaxu(IS, Dn);
     const uint32_t SDn = pmaxu(Sn, Dn);
-    const uint32_t Ddn = pmaxu(IS - k.nh, Dn);                     // D(i+1, j)
+    const uint32_t Ddn = LOCAL ? pmaxu(pmaxu(IS - k.na, Dn - k.ng), k.Z)   // D(i+1, j), local
+                               : pmaxu(IS - k.nh, Dn);             // D(i+1, j)
     // retrace priority S > I > D (algo.rs:351-400): m1 = I beats S, m2 = D beats both
     // (NOE: no landing columns -- the twin fill without a skeleton, whose
     // traceback walks the strips in sequence, tb_seq_kernel; with no code
@@ -203,8 +218,19 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
     const uint32_t En = NOE ? 0u : bfi(m2, e_up, E1);
     const uint32_t cIn = CODES ? pcode(st.cI, m1) : 0u;   // (no code words: the traceback derives
     const uint32_t cDn = CODES ? pcode(st.cD, m2) : 0u;   // them from the plane codes, tb_w16_codes_kernel)
-    const uint32_t SMpn = TBL ? SMn : padds(SMn, k.smp);           // TBL: no offset (k.smp = 0, the tables hold s'')
-    oI = In; oD = Dn; oS = Sn; oIold = st.I;
+    const uint32_t SMpn = (TBL && !LOCAL) ? SMn : padds(SMn, k.smp);   // TBL: no offset (the tables hold s''; local: - K)
+    oI = In; oD = Dn; oS = Sn; oIold = Ig;
+    if (LOCAL) {    // last max of the row: SMn >= lb takes the later column (biased halves compare as unsigned)
+        const uint32_t lt = psign(psub(SMn, st.lb));            // halves where SMn < lb
+        if (MASKED) {
+            const uint32_t upd = act & ~lt;
+            st.lb = bfi(upd, SMn, st.lb);
+            st.lc = bfi(upd, jv, st.lc);
+        } else {
+            st.lb = pmaxu(st.lb, SMn);
+            st.lc = bfi(lt, st.lc, jv);
+        }
+    }
     if (MASKED) {   // act: 0xFFFF in each half whose pair has this column
         st.I = bfi(act, In, st.I); st.SD = bfi(act, SDn, st.SD); st.Dd = bfi(act, Ddn, st.Dd);
         st.SMp = bfi(act, SMpn, st.SMp);
@@ -218,7 +244,7 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
     if (!NOE) st.Etl = e_up;
 }
 
-template <bool MASKED, bool TBL, bool CODES, bool NOE = false>
+template <bool MASKED, bool TBL, bool CODES, bool NOE = false, bool LOCAL = false>
 __device__ __forceinline__ void dp_step_pk(LanePk& st, const Rec& r, const int t, const int lane, const int m0,
                                            const int m1, const uint32_t c1a, const uint32_t c1b, const uint32_t c1ah,
                                            const uint32_t c1bh, const PkScores& k,
@@ -231,8 +257,9 @@ __device__ __forceinline__ void dp_step_pk(LanePk& st, const Rec& r, const int t
     const uint32_t act = MASKED ? ((unsigned)(t - lane) < (unsigned)m0 ? 0xFFFFu : 0u) |
                                       ((unsigned)(t - lane) < (unsigned)m1 ? 0xFFFF0000u : 0u)
                                 : ~0u;
-    cell_pk<MASKED, TBL, CODES, NOE>(st.a, dd_in, sm_in, e_in, c2, c1a, c1ah, act, k, oI[0], oD[0], oS[0], oL[0]);
-    cell_pk<MASKED, TBL, CODES, NOE>(st.b, st.a.Dd, st.a.SMp, st.a.E, c2, c1b, c1bh, act, k, oI[1], oD[1], oS[1], oL[1]);
+    const uint32_t jv = LOCAL ? (uint32_t)(t - lane + 1) * 0x10001u : 0u;   // the column, both halves
+    cell_pk<MASKED, TBL, CODES, NOE, LOCAL>(st.a, dd_in, sm_in, e_in, c2, c1a, c1ah, act, k, oI[0], oD[0], oS[0], oL[0], jv);
+    cell_pk<MASKED, TBL, CODES, NOE, LOCAL>(st.b, st.a.Dd, st.a.SMp, st.a.E, c2, c1b, c1bh, act, k, oI[1], oD[1], oS[1], oL[1], jv);
     st.c2c = c2;
 }
 
@@ -314,26 +341,26 @@ __device__ __forceinline__ void group4_pk(LanePk& st, Rec (&nxt)[4], WavePk& w, 
     if (MASKED) {
         auto sko = [&](int c) { return (c >= 0 && c <= w.m) ? w.skel_voff + 4u * (uint32_t)c : kSkelOff; };
         push63_pk<4 * G4 + 0>(out_base, st, lane63_mask(push_on && col0 >= 0 && col0 <= w.m));
-        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[0], bD[0], bS[0], bL[0]);
+        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0, (PLANES & 32) != 0>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[0], bD[0], bS[0], bL[0]);
         if ((PLANES & 3) == 1) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
         if ((PLANES & 3) == 2) { wc[0][0] = w16_code(bI[0][0], bD[0][0], bS[0][0], bL[0][0]);
                            wc[1][0] = w16_code(bI[0][1], bD[0][1], bS[0][1], bL[0][1]); }
         if ((PLANES & 16) == 0) skel_store(w.skel_rsrc, sko(col0 + 1), (int)st.b.E);
         push63_pk<4 * G4 + 1>(out_base, st, lane63_mask(push_on && col0 + 1 >= 0 && col0 + 1 <= w.m));
-        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[1], bD[1], bS[1], bL[1]);
+        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0, (PLANES & 32) != 0>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[1], bD[1], bS[1], bL[1]);
         if ((PLANES & 3) == 1) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
         if ((PLANES & 3) == 2) { wc[0][1] = w16_code(bI[1][0], bD[1][0], bS[1][0], bL[1][0]);
                            wc[1][1] = w16_code(bI[1][1], bD[1][1], bS[1][1], bL[1][1]); }
         if ((PLANES & 16) == 0) skel_store(w.skel_rsrc, sko(col0 + 2), (int)st.b.E);
         push63_pk<4 * G4 + 2>(out_base, st, lane63_mask(push_on && col0 + 2 >= 0 && col0 + 2 <= w.m));
-        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[2], bD[2], bS[2], bL[2]);
+        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0, (PLANES & 32) != 0>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[2], bD[2], bS[2], bL[2]);
         if ((PLANES & 3) == 1) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
         if ((PLANES & 3) == 2) { wc[0][2] = w16_code(bI[2][0], bD[2][0], bS[2][0], bL[2][0]);
                            wc[1][2] = w16_code(bI[2][1], bD[2][1], bS[2][1], bL[2][1]); }
         if ((PLANES & 16) == 0) skel_store(w.skel_rsrc, sko(col0 + 3), (int)st.b.E);
         push63_pk<4 * G4 + 3>(out_base, st, lane63_mask(push_on && col0 + 3 >= 0 && col0 + 3 <= w.m));
         if (push_on && col0 + 3 >= 0 && col0 <= w.m) lds_store_lane0(w.wcnt_out, min(col0 + 3, w.m) + 1);
-        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[3], bD[3], bS[3], bL[3]);
+        dp_step_pk<true, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0, (PLANES & 32) != 0>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[3], bD[3], bS[3], bL[3]);
         if ((PLANES & 3) == 1) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
         if ((PLANES & 3) == 2) { wc[0][3] = w16_code(bI[3][0], bD[3][0], bS[3][0], bL[3][0]);
                            wc[1][3] = w16_code(bI[3][1], bD[3][1], bS[3][1], bL[3][1]); }
@@ -341,26 +368,26 @@ __device__ __forceinline__ void group4_pk(LanePk& st, Rec (&nxt)[4], WavePk& w, 
     } else {
         const uint32_t pa = push_on && w.lane == kWave - 1 ? out_base : w.scratch;
         push_all_pk<4 * G4 + 0>(pa, st);
-        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[0], bD[0], bS[0], bL[0]);
+        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0, (PLANES & 32) != 0>(st, cur[0], t + 0, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[0], bD[0], bS[0], bL[0]);
         if ((PLANES & 3) == 1) bytes_step<0>(xI, xS, xD, bI[0], bD[0], bS[0], bL[0]);
         if ((PLANES & 3) == 2) { wc[0][0] = w16_code(bI[0][0], bD[0][0], bS[0][0], bL[0][0]);
                            wc[1][0] = w16_code(bI[0][1], bD[0][1], bS[0][1], bL[0][1]); }
         const uint32_t e0 = st.b.E;
         push_all_pk<4 * G4 + 1>(pa, st);
-        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[1], bD[1], bS[1], bL[1]);
+        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0, (PLANES & 32) != 0>(st, cur[1], t + 1, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[1], bD[1], bS[1], bL[1]);
         if ((PLANES & 3) == 1) bytes_step<1>(xI, xS, xD, bI[1], bD[1], bS[1], bL[1]);
         if ((PLANES & 3) == 2) { wc[0][1] = w16_code(bI[1][0], bD[1][0], bS[1][0], bL[1][0]);
                            wc[1][1] = w16_code(bI[1][1], bD[1][1], bS[1][1], bL[1][1]); }
         const uint32_t e1 = st.b.E;
         push_all_pk<4 * G4 + 2>(pa, st);
-        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[2], bD[2], bS[2], bL[2]);
+        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0, (PLANES & 32) != 0>(st, cur[2], t + 2, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[2], bD[2], bS[2], bL[2]);
         if ((PLANES & 3) == 1) bytes_step<2>(xI, xS, xD, bI[2], bD[2], bS[2], bL[2]);
         if ((PLANES & 3) == 2) { wc[0][2] = w16_code(bI[2][0], bD[2][0], bS[2][0], bL[2][0]);
                            wc[1][2] = w16_code(bI[2][1], bD[2][1], bS[2][1], bL[2][1]); }
         const uint32_t e2 = st.b.E;
         push_all_pk<4 * G4 + 3>(pa, st);
         publish_all(w.cnt_addr, col0 + 3 + 1);
-        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[3], bD[3], bS[3], bL[3]);
+        dp_step_pk<false, (PLANES & 4) != 0, (PLANES & 8) == 0, (PLANES & 16) != 0, (PLANES & 32) != 0>(st, cur[3], t + 3, w.lane, w.m0, w.m1, w.c1a, w.c1b, w.c1ah, w.c1bh, k, bI[3], bD[3], bS[3], bL[3]);
         if ((PLANES & 3) == 1) bytes_step<3>(xI, xS, xD, bI[3], bD[3], bS[3], bL[3]);
         if ((PLANES & 3) == 2) { wc[0][3] = w16_code(bI[3][0], bD[3][0], bS[3][0], bL[3][0]);
                            wc[1][3] = w16_code(bI[3][1], bD[3][1], bS[3][1], bL[3][1]); }
@@ -423,7 +450,20 @@ __device__ __forceinline__ void sub_block_pk(LanePk& st, Rec (&nxt)[4], WavePk& 
 // Initial state of row i (column 0, algo.rs:204-211) in shifted values:
 // H(i, 0) = h + i g -> h; I = H + h (compact planes' seed) -> 2h;
 // delete successor (row i+1) -> h; relative to the bases (B0, B1).
+// LOCAL (plain values, base 0): H(i, 0) = score_max = 0, I = H + h = h; the
+// max(S, D) seed only needs max(S, D) + h + g <= 0 (the floor decides I(i, 1)).
+template <bool LOCAL = false>
 __device__ __forceinline__ void init_row_pk(RowPk& rs, const Scores32& sc, int B0, int B1, const PkScores& k) {
+    rs.lb = kBias2; rs.lc = 0;
+    if (LOCAL) {
+        rs.I = pk2(sc.h, sc.h) ^ kBias2;
+        rs.SD = pk2(sc.h, sc.h) ^ kBias2;
+        rs.Dd = kBias2;
+        rs.SMp = padds(kBias2, k.smp);
+        rs.SMtl = 0;
+        rs.cI = 0; rs.cD = 0;
+        return;
+    }
     rs.I = pk2(2 * sc.h - B0, 2 * sc.h - B1) ^ kBias2;
     rs.SD = pk2(sc.h - B0, sc.h - B1) ^ kBias2;
     rs.Dd = pk2(sc.h - B0, sc.h - B1) ^ kBias2;
@@ -437,7 +477,8 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
                                 const PkScores& k, const Rec* ring_in, Rec* ring_out, lds_int* wcnt_in,
                                 lds_int* rcnt_in, lds_int* wcnt_out, lds_int* rcnt_out, lds_int* base_in,
                                 lds_int* base_out, const bool has_consumer, PairRes* pres0, PairRes* pres1,
-                                int* status, const uint32_t scratch_base) {
+                                int* status, const uint32_t scratch_base, StripRes* sres) {
+    constexpr bool LOCAL = (PLANES & 32) != 0;
     // a twin's pairs may differ in shape: the sweep covers the longer's rows
     // and columns (the host lays both out for that shape); each pair keeps
     // its own characters, column masks and end cell
@@ -480,8 +521,8 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
     w.B0 = __builtin_amdgcn_readfirstlane(base_in[0]);   // slot 0: column 0
     w.B1 = __builtin_amdgcn_readfirstlane(base_in[1]);
     LanePk st;
-    init_row_pk(st.a, sc, w.B0, w.B1, k);
-    init_row_pk(st.b, sc, w.B0, w.B1, k);
+    init_row_pk<LOCAL>(st.a, sc, w.B0, w.B1, k);
+    init_row_pk<LOCAL>(st.b, sc, w.B0, w.B1, k);
     st.c2c = 0;
     st.b.SMtl = st.a.SMp;                                   // (A, 0) is row B's top-left for column 1
     st.a.E = pk2(-(kRowsPerLane * lane + 1), -(kRowsPerLane * lane + 1));
@@ -538,6 +579,33 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
         }
         lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
     }
+    if constexpr (LOCAL) {
+        // each pair's last max of the strip (row-major: the later row wins
+        // ties, each row's tracker holds its later column) -> StripRes, which
+        // finalize_kernel reduces over the strips (algo.rs:310-322)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const PairDev& P = h ? P1 : P0;
+            const bool oka = ia <= P.n, okb = ia + 1 <= P.n;
+            const int va = oka ? (h ? hi16(st.a.lb ^ kBias2) : lo16(st.a.lb ^ kBias2)) : INT_MIN;
+            const int vb = okb ? (h ? hi16(st.b.lb ^ kBias2) : lo16(st.b.lb ^ kBias2)) : INT_MIN;
+            const bool tb = okb && vb >= va;
+            const int v = tb ? vb : va;
+            const uint32_t lc = tb ? st.b.lc : st.a.lc;
+            const int col = (int)((h ? lc >> 16 : lc) & 0xFFFFu);
+            int mx = v;
+            for (int off = 32; off > 0; off >>= 1) mx = max(mx, __shfl_xor(mx, off));
+            const unsigned long long lm = __ballot(oka && v == mx);
+            const int ll = lm ? 63 - __clzll((long long)lm) : 0;
+            const int lj = __shfl(col, ll), lh = __shfl((int)tb, ll);
+            if (lane == 0 && (h == 0 || &P1 != &P0)) {
+                StripRes r;
+                r.best = INT_MIN; r.bi = 0; r.bj = 0; r.bl = 0;
+                r.lbest = mx; r.li = s * kStripRows + kRowsPerLane * ll + lh + 1; r.lj = lj; r.lE = 0;
+                sres[P.strip_base + s] = r;
+            }
+        }
+    }
     // cell (n, m) of each pair: score_max (shifted, absolute) and landing
     // column (a shorter pair's lanes stopped at its own last column)
     if (ia == P0.n || ia + 1 == P0.n) {
@@ -561,7 +629,7 @@ struct __attribute__((aligned(16))) RecW {
 // I/O wave of a twin band: ring 0 from row 0 (analytic) or the previous
 // band's bottom row (absolute -> relative to the bases it picks per block);
 // ring W to HBM (relative -> absolute with the last strip's bases).
-template <bool TBL>
+template <bool TBL, bool LOCAL>
 __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, const int lane, const Scores32& sc,
                            const PkScores& k, Rec* ring0, const Rec* ringW, lds_int* wcnt0, lds_int* rcnt0,
                            lds_int* wcntW, lds_int* rcntW, lds_int* base0, lds_int* baseW, const bool do_out,
@@ -574,7 +642,9 @@ __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, c
     RecW* feed_out = do_out ? feed + (size_t)lb * P0.feed_stride : nullptr;
     const int* prog_in = lb > 0 ? P0.progress + (size_t)(lb - 1) * kProgStride : nullptr;
     int* prog_out = do_out ? P0.progress + (size_t)lb * kProgStride : nullptr;
-    const int smp = TBL ? 0 : sc.sm;    // sm'' (the launch's scores carry the shift's -2g, Scores32.shift); TBL: no offset
+    // sm'' (the launch's scores carry the shift's -2g, Scores32.shift); TBL: no
+    // offset.  LOCAL: plain values on base 0, the score_max offset of k.smp.
+    const int smp = LOCAL ? lo16(k.smp) : TBL ? 0 : sc.sm;
     unsigned idle = 0;
     int bprev0 = 0, bprev1 = 0;         // bases of the block before the current chunk's first column
     while (in_next <= m || (do_out && out_next <= m)) {
@@ -589,10 +659,10 @@ __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, c
                 int dd0 = 0, dd1 = 0, sm0 = 0, sm1 = 0, c2 = 0;
                 if (lane < chunk) {
                     if (lb == 0) {   // row 0 (algo.rs:195-202, 213-220), shifted: D' = 2h, SM = h
-                        if (j == 0) { dd0 = dd1 = 0; sm0 = sm1 = smp; c2 = 0; }
-                        else {
-                            dd0 = dd1 = 2 * sc.h;
-                            sm0 = sm1 = sc.h + smp;
+                        if (j == 0) { dd0 = dd1 = 0; sm0 = sm1 = smp; c2 = 0; }   // (local: every row-0 SM and
+                        else {                                                    // D(1, j) is the 0 floor)
+                            dd0 = dd1 = LOCAL ? 0 : 2 * sc.h;
+                            sm0 = sm1 = (LOCAL ? 0 : sc.h) + smp;
                             if (TBL)   // the column's v_perm_b32 selector (cell_pk)
                                 c2 = (int)perm_selector(j <= P0.m ? sym_code(P0.c2[j - 1], sc) : 0,
                                                         j <= P1.m ? sym_code(P1.c2[j - 1], sc) : 0);
@@ -611,15 +681,16 @@ __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, c
                 }
                 // bases: column 0 -> slot 0; block c (columns 16c+1 ..) from its first column
                 const int c0 = in_next >> 4;                     // chunk = columns 16c0 .. 16c0+15
-                if (in_next == 0) {
+                if (in_next == 0 && !LOCAL) {   // (local: every base is 0)
                     bprev0 = __builtin_amdgcn_readlane(sm0, 0);
                     bprev1 = __builtin_amdgcn_readlane(sm1, 0);
                     if (lane == 0) { base0[0] = bprev0; base0[1] = bprev1; }
                 }
+                if (in_next == 0 && LOCAL && lane == 0) { base0[0] = 0; base0[1] = 0; }
                 int nb0 = bprev0, nb1 = bprev1;
                 if (chunk > 1) {
-                    nb0 = __builtin_amdgcn_readlane(sm0, 1);
-                    nb1 = __builtin_amdgcn_readlane(sm1, 1);
+                    nb0 = LOCAL ? 0 : __builtin_amdgcn_readlane(sm0, 1);
+                    nb1 = LOCAL ? 0 : __builtin_amdgcn_readlane(sm1, 1);
                     if (lane == 0) {
                         const int kk = 1 + (c0 & (kBaseSlots - 1));
                         base0[2 * kk] = nb0;
@@ -691,7 +762,7 @@ __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, c
 template <int W, int PLANES>
 __global__ __launch_bounds__((W + 1) * kWave, (W + 1 + 3) / 4) void fill_pk_kernel(
     const PairDev* __restrict__ pairs, const int npairs, const int ntwins, const int total_bands, int* band_counter,
-    PairRes* pres, const Scores32 sc) {
+    PairRes* pres, StripRes* sres, const Scores32 sc) {
     __shared__ Rec rings[W + 1][kRing];
     __shared__ uint32_t push_scratch[W][kPushScratch];
     __shared__ int bases[W + 1][2 * (1 + kBaseSlots)];
@@ -701,9 +772,12 @@ __global__ __launch_bounds__((W + 1) * kWave, (W + 1 + 3) / 4) void fill_pk_kern
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int lane = threadIdx.x & (kWave - 1);
     const int smp = sc.sm, smmp = sc.smm;   // s - 2g: the launch's scores carry the shift (Scores32.shift)
-    // score_max is kept as SM + sm'' (TBL: as SM; its tables add the score)
-    const int off = (PLANES & 4) ? 0 : smp;
-    const PkScores k{pk2(-sc.h, -sc.h), pk2(off, off), pk2(smmp - smp, smmp - smp)};
+    // score_max is kept as SM + sm'' (TBL: as SM; its tables add the score).
+    // LOCAL: the scores carry + K (sc.koff, so the tables' bytes are >= 0):
+    // SM + s - K, i.e. SM - K with the tables
+    const int off = (PLANES & 32) ? ((PLANES & 4) ? -sc.koff : smp - sc.koff) : (PLANES & 4) ? 0 : smp;
+    const PkScores k{pk2(-sc.h, -sc.h), pk2(off, off), pk2(smmp - smp, smmp - smp),
+                     pk2(-sc.g, -sc.g), pk2(-sc.hg, -sc.hg), kBias2};
     for (;;) {
         if (threadIdx.x == 0) band_sh = atomicAdd(band_counter, 1);
         if (threadIdx.x < W + 1) { wcnt[threadIdx.x] = 0; rcnt[threadIdx.x] = 0; }
@@ -728,10 +802,10 @@ __global__ __launch_bounds__((W + 1) * kWave, (W + 1 + 3) / 4) void fill_pk_kern
                                         (lds_int*)&rcnt[wave], (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1],
                                         (lds_int*)bases[wave], (lds_int*)bases[wave + 1], has_consumer,
                                         pres + pa, pres + pb, band_counter + 1,
-                                        lds_addr(push_scratch[wave]));
+                                        lds_addr(push_scratch[wave]), sres);
             }
         } else {
-            io_wave_pk<(PLANES & 4) != 0>(P0, P1, lb, lane, sc, k, rings[0], rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0],
+            io_wave_pk<(PLANES & 4) != 0, (PLANES & 32) != 0>(P0, P1, lb, lane, sc, k, rings[0], rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0],
                        (lds_int*)&wcnt[W], (lds_int*)&rcnt[W], (lds_int*)bases[0], (lds_int*)bases[W],
                        lb + 1 < P0.bands, band_counter + 1);
         }
@@ -741,10 +815,11 @@ __global__ __launch_bounds__((W + 1) * kWave, (W + 1 + 3) / 4) void fill_pk_kern
 
 template <int W0, int... Ws>
 static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int npairs, int ntwins, int total_bands,
-                              int* d_counter, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
+                              int* d_counter, PairRes* d_pres, StripRes* d_sres, Scores32 sc, int grid,
+                              hipStream_t st) {
     if (W == W0) {
 #define GX_PK(PL) hipLaunchKernelGGL((fill_pk_kernel<W0, PL>), dim3(grid), dim3((W0 + 1) * kWave), 0, st, d_pairs, \
-                                     npairs, ntwins, total_bands, d_counter, d_pres, sc)
+                                     npairs, ntwins, total_bands, d_counter, d_pres, d_sres, sc)
         switch (planes) {
             case 0: GX_PK(0); break;
             case 1: GX_PK(1); break;
@@ -755,24 +830,28 @@ static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int npa
             case 14: GX_PK(14); break;
             case 26: GX_PK(26); break;   // twin codes, no code words, no skeleton (tb_seq_kernel)
             case 30: GX_PK(30); break;
+            case 58: GX_PK(58); break;   // local (Smith-Waterman): twin codes, no code words, no skeleton
+            case 62: GX_PK(62); break;
             default: return hipErrorInvalidValue;
         }
 #undef GX_PK
         return hipGetLastError();
     }
     if constexpr (sizeof...(Ws) > 0) return launch_pk_w<Ws...>(W, planes, d_pairs, npairs, ntwins, total_bands,
-                                                               d_counter, d_pres, sc, grid, st);
+                                                               d_counter, d_pres, d_sres, sc, grid, st);
     return hipErrorInvalidValue;
 }
 
 // Twin launch: W from {3, 4, 7, 8, 15}; planes: 0 none, 1 compact bytes per
 // pair (3 B/cell), 2 twin codes (2 B/cell); + 4: small-alphabet score tables
 // (with none or twin codes: the batch launches); + 8 (with twin codes): no
-// code words (the traceback derives them from the plane codes).
+// code words (the traceback derives them from the plane codes); + 16: no
+// skeleton; + 32 (with 2 + 8 + 16): local mode, each strip's last max of each
+// pair into d_sres (finalize_kernel reduces them).
 hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int npairs, int ntwins, int total_bands,
-                          int* d_counter, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
-    return launch_pk_w<3, 4, 7, 8, 15>(W, planes, d_pairs, npairs, ntwins, total_bands, d_counter, d_pres, sc, grid,
-                                       st);
+                          int* d_counter, PairRes* d_pres, StripRes* d_sres, Scores32 sc, int grid, hipStream_t st) {
+    return launch_pk_w<3, 4, 7, 8, 15>(W, planes, d_pairs, npairs, ntwins, total_bands, d_counter, d_pres, d_sres, sc,
+                                       grid, st);
 }
 
 }  // namespace gx

@@ -67,6 +67,7 @@ struct Scores32 {
     int dbg;     // GX_DEBUG_FLAGS: bit0 = rolled (ramp) path only
     int shift;   // layout-0 untracked global launches: values kept as V - (i + j) g (sm, smm hold s - 2g)
     int sym[4];  // small-alphabet launches: the job's distinct processed bytes (code k = sym[k])
+    int koff;    // local twin fill (gx_fill_pk.hip): K = max(0, -min(sm, smm)) added to sm / smm (score tables >= 0)
 };
 
 // One inter-strip record: the bottom-row cell (r, j) of a strip, as needed by

@@ -193,7 +193,7 @@ SYNTH_SETS = {30000: 80, 1024: 1024, 4096: 64, 16384: 8, 65536: 1}
 def _synth_job(job):
     length, k = job[:2]
     a, b = (related_pair if len(job) > 2 and job[2] else synth_pair)(k, length)
-    r = o.align_lean(a, b, CONFIG, is_local=False)
+    r = o.align_lean(a, b, CONFIG, is_local=len(job) > 3 and job[3])
     assert r.status == 0
     return length, {"k": k, "n": len(a), "m": len(b), "score": r.score,
                     "stats": [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps],
@@ -201,11 +201,17 @@ def _synth_job(job):
                     "plane_sums": [str(x) for x in r.extra["plane_sums"]]}
 
 
-def synthetic_cases(workers: int, lengths, related: bool = False):
+# The local (Smith-Waterman) batch of bench.py's `local_batch` record: the
+# first LOCAL_RELATED related 30k pairs (a long local alignment each).
+LOCAL_RELATED = 32
+
+
+def synthetic_cases(workers: int, lengths, related: bool = False, local: bool = False):
     """Oracle digests of the synthetic batches (related: the SURVEY 8(d) M1
-    "related" variant, s2 derived from s1, 80 pairs at 30k)."""
+    "related" variant, s2 derived from s1, 80 pairs at 30k; local: its first
+    LOCAL_RELATED pairs aligned locally)."""
     from multiprocessing import Pool
-    jobs = [(L, k, related) for L in lengths for k in range(SYNTH_SETS[L])]
+    jobs = [(L, k, related, local) for L in lengths for k in range(LOCAL_RELATED if local else SYNTH_SETS[L])]
     jobs.sort(key=lambda x: -x[0])
     out = {L: [] for L in lengths}
     with Pool(workers) as pool:
@@ -215,8 +221,9 @@ def synthetic_cases(workers: int, lengths, related: bool = False):
                 print(f"synthetic L={L} k={rec['k']} done ({n_done}/{len(jobs)})", flush=True)
     for L in lengths:
         out[L].sort(key=lambda c: c["k"])
-        name = f"synthetic_related_L{L}.json" if related else f"synthetic_L{L}.json"
-        src = ("tests/golden/make_golden.py --related (oracle_align_lean, global, config.toml scores; pair k = "
+        name = f"synthetic_related{'_local' if local else ''}_L{L}.json" if related else f"synthetic_L{L}.json"
+        src = ("tests/golden/make_golden.py --related-local (oracle_align_lean, LOCAL, config.toml scores; pair k = "
+               "related_pair(k), k < 32)") if local else ("tests/golden/make_golden.py --related (oracle_align_lean, global, config.toml scores; pair k = "
                "related_pair(k): s1 of synthetic pair k, s2 derived with seed 0x5EED0003 + 0x10000 k)") if related else \
               ("tests/golden/make_golden.py --synthetic (oracle_align_lean, global, config.toml "
                "scores; pair k = splitmix64 seeds 0x5EED0001/2 + 0x10000 k, bench.py synth_pair)")
@@ -232,9 +239,14 @@ def main():
     ap.add_argument("--synthetic", type=str, default=None,
                     help="comma-separated lengths of SYNTH_SETS to digest, or 'all'")
     ap.add_argument("--related", action="store_true", help="the related 30k batch (SURVEY 8(d) M1 variant)")
+    ap.add_argument("--related-local", action="store_true",
+                    help="local digests of the first 32 related 30k pairs (bench.py local_batch)")
     ap.add_argument("--workers", type=int, default=7)
     args = ap.parse_args()
     o.build()
+    if args.related_local:
+        synthetic_cases(args.workers, [30000], related=True, local=True)
+        return
     if args.related:
         synthetic_cases(args.workers, [30000], related=True)
         return

@@ -1,0 +1,123 @@
+"""GPU parity of the local (Smith-Waterman) twin fill (gx_fill_pk.hip LOCAL):
+batches of local alignments run two pairs per band on plain 16-bit values
+with the 0 floor of algo.rs:103 in every gap recurrence and a per-row
+last-max tracker (algo.rs:310-322).  Every result -- the start cell through
+the score, the alignment, the statistics and the compact score planes -- must
+equal the oracle's local restatement (oracle/gx_oracle.c), on shapes around
+the strip and band edges, tie-heavy inputs (all-mismatch tables are all
+zeros, so the last maximum is cell (n, m)), scores with and without the
+small-alphabet tables, and values up to the admission bound."""
+import random
+
+import pytest
+
+from conftest import CONFIG_SCORES
+from test_gpu_twin import LAUNCH, SHAPES, _steps_list, _twin_pairs
+from test_twin_bound import _families
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _force_twin(monkeypatch):
+    """Small batches: force the twin fill (run_fill's grid-fill rule)."""
+    monkeypatch.setenv("GX_TWIN", "1")
+
+
+@pytest.fixture(params=sorted(LAUNCH))
+def launch(request, monkeypatch):
+    for k, v in LAUNCH[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
+def _check(gx, ctx, oracle, pairs, scores, steps=1, twin=1):
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, _ = st.run(gx.Scores(*scores), True, keep_planes=True, steps=steps, plane_sums=True)
+    info = ctx.fill_info()
+    assert info["twin"] == twin, info
+    sums = st.plane_sums()
+    for p, (a, b) in enumerate(pairs):
+        o = oracle.align_lean(a, b, scores, is_local=True)
+        for k in range(steps):
+            assert [int(x) for x in sums[k, p]] == o.extra["plane_sums"], (p, len(a), len(b), k)
+        assert (res[p].score, res[p].matches, res[p].mismatches, res[p].gap_extensions, res[p].opening_gaps) == \
+               (o.score, o.matches, o.mismatches, o.gap_extensions, o.opening_gaps), (p, len(a), len(b))
+        assert _steps_list(st.steps(p)) == o.alignment(), (p, len(a), len(b))
+    return info
+
+
+def test_local_twin_shapes(gx, ctx, oracle, launch):
+    """Shapes around the strip / band edges, every band width and small grids
+    (bands queued for workgroups); two pipelined passes."""
+    _check(gx, ctx, oracle, _twin_pairs(23, SHAPES), CONFIG_SCORES, steps=2)
+
+
+def _planted(rng, n, m, core, al=b"ACGT"):
+    """Random rows and columns sharing a planted core with ~8 % substitutions
+    (a long local alignment in the middle of the table)."""
+    c = bytes(rng.choice(al) for _ in range(core))
+    c2 = bytes(x if rng.random() > 0.08 else rng.choice(al) for x in c)
+    a = bytes(rng.choice(al) for _ in range(rng.randint(0, n - core))) + c
+    b = bytes(rng.choice(al) for _ in range(rng.randint(0, m - core))) + c2
+    a += bytes(rng.choice(al) for _ in range(n - len(a)))
+    b += bytes(rng.choice(al) for _ in range(m - len(b)))
+    return a, b
+
+
+@pytest.mark.parametrize("scores", [CONFIG_SCORES, (2, -3, -2, -4), (5, -4, 0, -10), (1, -1, 0, 0), (3, -3, -1, -1)])
+def test_local_twin_planted_cores(gx, ctx, oracle, monkeypatch, scores):
+    """A planted shared core per pair (a long local alignment inside the
+    table, started at the last maximum), unequal twins; several scores."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    rng = random.Random(hash(scores) & 0xffff)
+    pairs = [_planted(rng, n, m, core) for n, m, core in
+             [(900, 700, 300), (700, 900, 250), (1500, 400, 200), (333, 1200, 150), (257, 256, 256), (129, 3000, 100)]]
+    _check(gx, ctx, oracle, pairs, scores)
+
+
+def test_local_twin_large_alphabet(gx, ctx, oracle, monkeypatch):
+    """More than four symbols: the plain match test instead of the score
+    tables (cell_pk without TBL), planted cores over 20 amino-acid letters."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    rng = random.Random(5)
+    al = b"ACDEFGHIKLMNPQRSTVWY"
+    pairs = [_planted(rng, n, m, core, al) for n, m, core in [(800, 600, 200), (600, 800, 300), (400, 400, 100)]]
+    _check(gx, ctx, oracle, pairs, CONFIG_SCORES)
+
+
+@pytest.mark.parametrize("family", ["all_mismatch", "all_match", "gap_rows", "gap_cols", "repeat"])
+def test_local_twin_tie_families(gx, ctx, oracle, monkeypatch, family):
+    """Inputs full of ties (all-zero tables, repeats, all-match diagonals)
+    at W = 15 and 8: the last maximum in row-major order must be the
+    reference's."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    for W in ("15", "8"):
+        monkeypatch.setenv("GX_BAND_WAVES", W)
+        pair = _families(128 * int(W) + 300, 1400)[family]
+        _check(gx, ctx, oracle, [pair, (pair[0][:-37], pair[1][:-11])], CONFIG_SCORES)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_local_twin_random_batches(gx, ctx, oracle, monkeypatch, seed):
+    """Randomised local batches: shapes, alphabets, scores, band widths and
+    grids; every result against the oracle."""
+    rng = random.Random(4000 + seed)
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    monkeypatch.setenv("GX_BAND_WAVES", rng.choice(["3", "4", "7", "8", "15"]))
+    monkeypatch.setenv("GX_FILL_GRID", rng.choice(["1", "2", "5", "64"]))
+    scores = rng.choice([CONFIG_SCORES, (1, -2, -2, -5), (2, -3, -1, -4), (1, -1, 0, -3), (3, -2, -2, -2)])
+    al = rng.choice([b"ACGT", b"AC", b"ACGTN", b"ACDEFGHIKLMNPQRSTVWY"])
+    pairs = [_planted(rng, n, m, rng.randint(1, min(n, m)), al)
+             for n, m in [(rng.randint(2, 700), rng.randint(2, 700)) for _ in range(rng.randint(2, 9))]]
+    _check(gx, ctx, oracle, pairs, scores)
+
+
+def test_local_twin_bound_binds(gx, ctx, oracle, monkeypatch):
+    """Values at the admission bound: 15,000-long all-match twins at s = 2
+    reach 30,000 (bound 30,079 < 32,000, admitted); 16,000 columns at s = 2
+    (bound 32,079) are refused and run the scalar fill.  Both bit-exact."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    scores = (2, -3, -1, -5)
+    _check(gx, ctx, oracle, [(b"A" * 15000, b"A" * 15000), (b"A" * 14990, b"A" * 15000)], scores, twin=1)
+    _check(gx, ctx, oracle, [(b"A" * 16000, b"A" * 16000), (b"A" * 15990, b"A" * 16000)], scores, twin=0)
