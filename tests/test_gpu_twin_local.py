@@ -47,6 +47,15 @@ def _check(gx, ctx, oracle, pairs, scores, steps=1, twin=1):
     return info
 
 
+def _w16_ok(scores):
+    """gx_api.cpp w16_ok: the twin plane codes' field ranges."""
+    sm, smm, g, h = scores
+    a = h + g
+    U = max(0, max(sm, smm) - a)
+    return (U - a - g <= 15 and min(sm, smm) - U >= -16 and max(sm, smm) - 2 * a <= 15 and 2 * a - U >= -64
+            and U - 2 * a <= 63)
+
+
 def test_local_twin_shapes(gx, ctx, oracle, launch):
     """Shapes around the strip / band edges, every band width and small grids
     (bands queued for workgroups); two pipelined passes."""
@@ -65,15 +74,20 @@ def _planted(rng, n, m, core, al=b"ACGT"):
     return a, b
 
 
-@pytest.mark.parametrize("scores", [CONFIG_SCORES, (2, -3, -2, -4), (5, -4, 0, -10), (1, -1, 0, 0), (3, -3, -1, -1)])
-def test_local_twin_planted_cores(gx, ctx, oracle, monkeypatch, scores):
+# (scores, twin fill expected): the local twin needs the twin plane codes'
+# ranges (gx_api.cpp w16_ok: x_I - g in [0, 15] ...); (2, -3, -2, -4) and
+# (5, -4, 0, -10) exceed them and run the scalar local fill
+@pytest.mark.parametrize("scores,twin", [(CONFIG_SCORES, 1), ((2, -3, -1, -4), 1), ((3, -2, -1, -3), 1),
+                                         ((1, -1, 0, 0), 1), ((3, -3, -1, -1), 1), ((2, -3, -2, -4), 0),
+                                         ((5, -4, 0, -10), 0)])
+def test_local_twin_planted_cores(gx, ctx, oracle, monkeypatch, scores, twin):
     """A planted shared core per pair (a long local alignment inside the
     table, started at the last maximum), unequal twins; several scores."""
     monkeypatch.setenv("GX_LAYOUT", "0")
     rng = random.Random(hash(scores) & 0xffff)
     pairs = [_planted(rng, n, m, core) for n, m, core in
              [(900, 700, 300), (700, 900, 250), (1500, 400, 200), (333, 1200, 150), (257, 256, 256), (129, 3000, 100)]]
-    _check(gx, ctx, oracle, pairs, scores)
+    _check(gx, ctx, oracle, pairs, scores, twin=twin)
 
 
 def test_local_twin_large_alphabet(gx, ctx, oracle, monkeypatch):
@@ -106,11 +120,11 @@ def test_local_twin_random_batches(gx, ctx, oracle, monkeypatch, seed):
     monkeypatch.setenv("GX_LAYOUT", "0")
     monkeypatch.setenv("GX_BAND_WAVES", rng.choice(["3", "4", "7", "8", "15"]))
     monkeypatch.setenv("GX_FILL_GRID", rng.choice(["1", "2", "5", "64"]))
-    scores = rng.choice([CONFIG_SCORES, (1, -2, -2, -5), (2, -3, -1, -4), (1, -1, 0, -3), (3, -2, -2, -2)])
+    scores = rng.choice([CONFIG_SCORES, (1, -2, -2, -5), (2, -3, -1, -4), (1, -1, 0, -3), (3, -2, -1, -3)])
     al = rng.choice([b"ACGT", b"AC", b"ACGTN", b"ACDEFGHIKLMNPQRSTVWY"])
     pairs = [_planted(rng, n, m, rng.randint(1, min(n, m)), al)
              for n, m in [(rng.randint(2, 700), rng.randint(2, 700)) for _ in range(rng.randint(2, 9))]]
-    _check(gx, ctx, oracle, pairs, scores)
+    _check(gx, ctx, oracle, pairs, scores, twin=1 if _w16_ok(scores) else 0)
 
 
 def test_local_twin_bound_binds(gx, ctx, oracle, monkeypatch):
