@@ -653,6 +653,7 @@ struct FillJob {
     bool w16 = false;                   // twin plane codes, 2 B per cell (w16_ok; batches only)
     bool nocodes = false;               // w16 without code words: the traceback derives them from the planes
     bool noskel = false;                // nocodes without landing columns: the traceback walks the strips in sequence
+    bool local_on = false;              // local (Smith-Waterman) fill: the start cell is the last max (PairRes.lmax_*)
     hipStream_t stream = nullptr;       // the stream its fill runs on (nullptr: the context's)
     bool plan_only = false;             // run_fill: decide layout and formats only (no buffers, no launch)
     bool table = false;                 // an alignment table (exportable planes: never the twin codes)
@@ -819,6 +820,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     const int W = cs2 ? cs2_band_waves(total_strips, fill_grid_cap(ctx->device))
                       : fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device), lay, min_strips);
     job.lay = lay;
+    job.local_on = is_local != 0;
     // layout-0 untracked global fills and the split column step keep every
     // value as V - (i + j) g (one add less per recurrence, gx_kernels.hip
     // cell; the local floor becomes -(i + j) g); the sub scores carry -2g
@@ -1412,6 +1414,7 @@ static int run_traceback(gx_context* ctx, const std::vector<const FillJob*>& jv,
         t.n = d.n; t.m = d.m; t.t16 = d.t16; t.strips = d.strips;
         t.start_i = starts[p].i; t.start_j = starts[p].j; t.start_E = starts[p].E;
         t.start_E_dev = (dev_end_E && starts[p].i >= 1) ? &presv[p]->end_E : nullptr;
+        t.start_ij_dev = (dev_end_E && job.local_on && starts[p].i >= 1) ? &presv[p]->lmax_i : nullptr;
         t.seg = (int*)seg.p + 4 * so[p];
         t.recs = (uint32_t*)recs.p + so[p] * SR;
         t.srows = SR;
@@ -2181,7 +2184,7 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
 static constexpr int kOverlapNo = -1000;
 static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
                               const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc, const HostScores& hs,
-                              const Scores32& sc, bool planes, int nsteps, std::vector<Walk>& walks, double* fill_ms,
+                              const Scores32& sc, int is_local, bool planes, int nsteps, std::vector<Walk>& walks, double* fill_ms,
                               const uint8_t* chars_dev, const std::vector<size_t>* off1,
                               const std::vector<size_t>* off2, const SmallAlpha& alpha,
                               const std::vector<size_t>& idx) {
@@ -2218,14 +2221,15 @@ static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
     auto fill = [&](int g, int k) {
         FillJob& j = g == 0 ? jA[k & 1] : jB;
         j.stream = g == 0 ? sA : sB;
-        return run_fill(ctx, dproc[g], dph[g], sc, 0, planes, false, false, j, chars_dev,
+        return run_fill(ctx, dproc[g], dph[g], sc, is_local, planes, false, false, j, chars_dev,
                         chars_dev ? &o1[g] : nullptr, chars_dev ? &o2[g] : nullptr, &alpha, 2 * g + (k & 1), false);
     };
     auto trace = [&](int k) {
         HIPCHK(hipStreamWaitEvent(sT, ctx->slots[k & 1].fdone, 0));
         HIPCHK(hipStreamWaitEvent(sT, ctx->slots[2 + (k & 1)].fdone, 0));
+        // (local: the start cells are read on the device, TbDev.start_ij_dev)
         return run_traceback(ctx, std::vector<const FillJob*>{&jA[k & 1], &jB}, starts, ctx->slots[k & 1].out, k & 1,
-                             false, false, sT);
+                             false, is_local != 0, sT);
     };
     auto take = [&](const FillJob& j, const std::vector<size_t>& g) {
         for (size_t q = 0; q < g.size(); ++q) res[g[q]] = j.res[q];
@@ -2244,10 +2248,10 @@ static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
     {   // both groups must take the twin fill without landing columns: decided before anything is enqueued
         FillJob pa, pb;
         pa.plan_only = pb.plan_only = true;
-        int prc = run_fill(ctx, dproc[0], dph[0], sc, 0, planes, false, false, pa, chars_dev, chars_dev ? &o1[0] : nullptr,
+        int prc = run_fill(ctx, dproc[0], dph[0], sc, is_local, planes, false, false, pa, chars_dev, chars_dev ? &o1[0] : nullptr,
                            chars_dev ? &o2[0] : nullptr, &alpha, 0, false);
         if (!prc)
-            prc = run_fill(ctx, dproc[1], dph[1], sc, 0, planes, false, false, pb, chars_dev,
+            prc = run_fill(ctx, dproc[1], dph[1], sc, is_local, planes, false, false, pb, chars_dev,
                            chars_dev ? &o1[1] : nullptr, chars_dev ? &o2[1] : nullptr, &alpha, 2, false);
         if (prc || !(pa.noskel && pb.noskel && pa.twin && pb.twin && pa.lay == pb.lay)) return kOverlapNo;
     }
@@ -2291,8 +2295,8 @@ static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
         if ((rc = tb_collect(ctx, a, Q, ctx->slots[a].out))) break;
         job_release(ctx, jA[a]);                              // its walk is done
         for (size_t p = 0; p < P; ++p)
-            start_cell_common(hs, 0, ph[p].n, ph[p].m, start_in(res[p]), &si[p], &sj[p], &score[p]);
-        if ((rc = label_batch(ctx, ph, hs, 0, false, dev_of, si, sj, score, res, ctx->slots[a].out,
+            start_cell_common(hs, is_local, ph[p].n, ph[p].m, start_in(res[p]), &si[p], &sj[p], &score[p]);
+        if ((rc = label_batch(ctx, ph, hs, is_local, false, dev_of, si, sj, score, res, ctx->slots[a].out,
                               jA[a].fill_ms + jB.fill_ms, walks)))
             break;
     }
@@ -2381,9 +2385,13 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
     for (const PairHost& h : dph) nmax_b = std::max(nmax_b, h.n);
     // (long pairs only: a short pair's walk is short; and both groups must
     // fill the grid on the twin fill, or the attempt falls back)
-    if (!is_local && !track && planes && idx.size() >= 16 && nmax_b >= 4096 && !pool_poison() &&
-        !(getenv("GX_OVERLAP") && !strcmp(getenv("GX_OVERLAP"), "0"))) {
-        const int orc = batch_core_overlap(ctx, ph, proc, hs, sc, planes, nsteps, walks, fill_ms, chars_dev, off1, off2,
+    // (local batches from 64 pairs: at 32 related 30k pairs the split launches
+    // fill worse than the walk they hide, 27.2 vs 21.6 ms a step; GX_OVERLAP=1
+    // forces it from 16 pairs, GX_OVERLAP=0 turns it off)
+    const char* ov = getenv("GX_OVERLAP");
+    if (!track && planes && idx.size() >= 16 && nmax_b >= 4096 && !pool_poison() && !(ov && !strcmp(ov, "0")) &&
+        (!is_local || idx.size() >= 64 || (ov && !strcmp(ov, "1")))) {
+        const int orc = batch_core_overlap(ctx, ph, proc, hs, sc, is_local, planes, nsteps, walks, fill_ms, chars_dev, off1, off2,
                                            alpha, idx);
         if (orc != kOverlapNo) return orc;
     }

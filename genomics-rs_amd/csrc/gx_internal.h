@@ -151,6 +151,8 @@ struct TbDev {           // per-pair traceback job
     const uint8_t* w16;    // the twin's code plane (strip 0), [strip][t/4][row-in-lane][lane][t%4] dwords
     int w16_half;          // this pair's 16-bit half of each dword
     int t4;                // 4-step groups per strip
+    const int* start_ij_dev;// local twin fill in the overlapped pipeline: the start cell {i, j} read on the device
+                           // (PairRes.lmax_i / lmax_j after finalize_kernel: no host round trip); tb_seq_kernel only
 };
 
 // ---- wide (int64) fill (gx_wide.hip): jobs outside the exact-int32 range --

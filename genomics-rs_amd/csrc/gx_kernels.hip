@@ -1475,7 +1475,9 @@ __global__ __launch_bounds__((1 + kSqHelp) * kWave) void tb_seq_kernel(const TbD
     const TbDev J = jobs[blockIdx.x];
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
     const int lane = threadIdx.x & (kWave - 1);
-    const int i = J.start_i, j = J.start_j;
+    // (local fills in the overlapped pipeline: the last max, from the fill's results on the device)
+    const int i = J.start_ij_dev ? ((gcint*)J.start_ij_dev)[0] : J.start_i;
+    const int j = J.start_ij_dev ? ((gcint*)J.start_ij_dev)[1] : J.start_j;
     if (i < 1 || j < 1) {
         if (threadIdx.x == 0) { J.end_ij[0] = i; J.end_ij[1] = j; J.end_ij[2] = -1; }
         return;

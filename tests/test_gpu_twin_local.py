@@ -135,3 +135,17 @@ def test_local_twin_bound_binds(gx, ctx, oracle, monkeypatch):
     scores = (2, -3, -1, -5)
     _check(gx, ctx, oracle, [(b"A" * 15000, b"A" * 15000), (b"A" * 14990, b"A" * 15000)], scores, twin=1)
     _check(gx, ctx, oracle, [(b"A" * 16000, b"A" * 16000), (b"A" * 15990, b"A" * 16000)], scores, twin=0)
+
+
+def test_local_twin_overlapped(gx, ctx, oracle, monkeypatch):
+    """A long-pair local batch (>= 16 pairs, n >= 4,096) takes the overlapped
+    two-group pipeline (gx_api.cpp batch_core_overlap): each pass's walk runs
+    beside the next pass's fill and reads its start cells (the last maxima,
+    finalize_kernel's PairRes) on the device.  Three passes, every result of
+    every pass against the oracle."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    monkeypatch.setenv("GX_OVERLAP", "1")   # (local batches take it by default from 64 pairs)
+    rng = random.Random(321)
+    pairs = [_planted(rng, 4300 + 37 * k, 2500 + 53 * k, 600 + 40 * k) for k in range(18)]
+    info = _check(gx, ctx, oracle, pairs, CONFIG_SCORES, steps=3)
+    assert info["groups"] == 2, info
