@@ -2389,8 +2389,9 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
     // fill worse than the walk they hide, 27.2 vs 21.6 ms a step; GX_OVERLAP=1
     // forces it from 16 pairs, GX_OVERLAP=0 turns it off)
     const char* ov = getenv("GX_OVERLAP");
-    if (!track && planes && idx.size() >= 16 && nmax_b >= 4096 && !pool_poison() && !(ov && !strcmp(ov, "0")) &&
-        (!is_local || idx.size() >= 64 || (ov && !strcmp(ov, "1")))) {
+    const bool ov_force = ov && !strcmp(ov, "1");
+    if (!track && planes && idx.size() >= 16 && (nmax_b >= 4096 || ov_force) && !pool_poison() &&
+        !(ov && !strcmp(ov, "0")) && (!is_local || idx.size() >= 64 || ov_force)) {
         const int orc = batch_core_overlap(ctx, ph, proc, hs, sc, is_local, planes, nsteps, walks, fill_ms, chars_dev, off1, off2,
                                            alpha, idx);
         if (orc != kOverlapNo) return orc;

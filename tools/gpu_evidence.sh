@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 TAG=${1:-r03}
 O=gpurun_out/ev_$TAG
 rm -rf "$O" && mkdir -p "$O"
-A="--no-cpu-baseline --config-steps 0 --int32-steps 0 --no-plane-steps 0 --single-pair-steps 0"
+A="--no-cpu-baseline --config-steps 0 --int32-steps 0 --no-plane-steps 0 --single-pair-steps 0 --local-batch-steps 0"
 timeout -k 10 120 ./tools/valu_probe > "$O/valu_probe.json" 2> "$O/valu_probe.err" || { echo PROBE_FAIL; exit 1; }
 echo probe ok
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/kt" -o kt --output-format csv -- python3 bench.py $A --steps 5 --warmup 1 \
