@@ -39,6 +39,7 @@ hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, 
                             int floor_, int gshift, int row0, int rows, hipStream_t st);
 hipError_t launch_plane_sums(const PairDev* d_pairs, int npairs, int max_strips, int lay, int mode, int h, int g,
                              int floor_, int gshift, unsigned long long* out, hipStream_t st);
+hipError_t launch_local_col(const PairDev* d_pairs, int npairs, PairRes* d_pres, int h, int g, hipStream_t st);
 hipError_t launch_fill_cs2(int W, bool local, bool planes, bool tbl, const PairDev* d_pairs, int npairs,
                            int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                            hipStream_t st);
@@ -1080,6 +1081,10 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     if (bands > 0 && (track || is_local))
         HIPCHK(launch_finalize((const PairDev*)job.pairs.p, (int)P, (const StripRes*)job.sres.p,
                                (PairRes*)job.pres.p, fs));
+    // the local twin fill tracks each row's maximum only: the last column of
+    // the chosen row from its plane codes (gx_kernels.hip local_col_kernel)
+    if (bands > 0 && twin && is_local)
+        HIPCHK(launch_local_col((const PairDev*)job.pairs.p, (int)P, (PairRes*)job.pres.p, sc.h, sc.g, fs));
     job.res.assign(P, PairRes{});
     int status[2] = {0, 0};
     PairRes* pin_res = (PairRes*)(pin + P * sizeof(PairDev) + ord_bytes);

@@ -168,7 +168,7 @@ struct RowPk {
     uint32_t I, SD, Dd, SMp, SMtl;   // insert, max(sub, delete), delete successor, score_max + sm'', SMp(i-1, j-1)
     uint32_t cI, cD;                 // code bit-planes, negated (16 steps, one per half; pcode)
     uint32_t E, Etl;                 // landing columns (int16 per half)
-    uint32_t lb, lc;                 // local: last max of score_max along the row (biased) and its column
+    uint32_t lb;                     // local: the largest score_max along the row (biased)
 };
 struct LanePk {
     RowPk a, b;
@@ -183,16 +183,16 @@ struct LanePk {
 // values on base 0 -- a local value lies in [0, min(n, m) max(s, 0)] and the
 // host admits the launch only while that fits the biased halves
 // (twin_width) -- so the 0 floor of score_max is one v_pk_max_u16 against the
-// biased zero k.Z in each gap recurrence, and the row keeps the last maximum
-// of score_max with its column (algo.rs:310-322, row-major: the later column
-// wins ties; jv = the column, both halves).  Plane codes store x_I - g as the
+// biased zero k.Z in each gap recurrence, and the row keeps its largest
+// score_max (one v_pk_max_u16; the last column holding it, algo.rs:310-322,
+// is recovered from the chosen row's plane codes by local_col_kernel, so the
+// fill tracks no columns).  Plane codes store x_I - g as the
 // shifted fill does (Iold - |g| is the insert recurrence's own term).
 template <bool MASKED, bool TBL, bool CODES, bool NOE = false, bool LOCAL = false>
 __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const uint32_t sm_in, const uint32_t e_up,
                                         const uint32_t c2, const uint32_t c1, const uint32_t c1h, const uint32_t act,
                                         const PkScores& k,
-                                        uint32_t& oI, uint32_t& oD, uint32_t& oS, uint32_t& oIold,
-                                        const uint32_t jv = 0u) {
+                                        uint32_t& oI, uint32_t& oD, uint32_t& oS, uint32_t& oIold) {
     const uint32_t Ig = LOCAL ? st.I - k.ng : st.I;                // (biased halves: no borrow across them)
     const uint32_t In = LOCAL ? pmaxu(pmaxu(Ig, st.SD - k.na), k.Z)   // max(I + g, max(S,D) + h + g, 0)
                               : pmaxu(st.I, st.SD - k.nh);          // max(I, max(S,D) + h)   (algo.rs:231-236)
@@ -220,17 +220,8 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
     const uint32_t cDn = CODES ? pcode(st.cD, m2) : 0u;   // them from the plane codes, tb_w16_codes_kernel)
     const uint32_t SMpn = (TBL && !LOCAL) ? SMn : padds(SMn, k.smp);   // TBL: no offset (the tables hold s''; local: - K)
     oI = In; oD = Dn; oS = Sn; oIold = Ig;
-    if (LOCAL) {    // last max of the row: SMn >= lb takes the later column (biased halves compare as unsigned)
-        const uint32_t lt = psign(psub(SMn, st.lb));            // halves where SMn < lb
-        if (MASKED) {
-            const uint32_t upd = act & ~lt;
-            st.lb = bfi(upd, SMn, st.lb);
-            st.lc = bfi(upd, jv, st.lc);
-        } else {
-            st.lb = pmaxu(st.lb, SMn);
-            st.lc = bfi(lt, st.lc, jv);
-        }
-    }
+    if (LOCAL)      // the row's largest score_max (its last column: local_col_kernel, from the plane codes)
+        st.lb = pmaxu(st.lb, MASKED ? bfi(act, SMn, k.Z) : SMn);
     if (MASKED) {   // act: 0xFFFF in each half whose pair has this column
         st.I = bfi(act, In, st.I); st.SD = bfi(act, SDn, st.SD); st.Dd = bfi(act, Ddn, st.Dd);
         st.SMp = bfi(act, SMpn, st.SMp);
@@ -257,9 +248,8 @@ __device__ __forceinline__ void dp_step_pk(LanePk& st, const Rec& r, const int t
     const uint32_t act = MASKED ? ((unsigned)(t - lane) < (unsigned)m0 ? 0xFFFFu : 0u) |
                                       ((unsigned)(t - lane) < (unsigned)m1 ? 0xFFFF0000u : 0u)
                                 : ~0u;
-    const uint32_t jv = LOCAL ? (uint32_t)(t - lane + 1) * 0x10001u : 0u;   // the column, both halves
-    cell_pk<MASKED, TBL, CODES, NOE, LOCAL>(st.a, dd_in, sm_in, e_in, c2, c1a, c1ah, act, k, oI[0], oD[0], oS[0], oL[0], jv);
-    cell_pk<MASKED, TBL, CODES, NOE, LOCAL>(st.b, st.a.Dd, st.a.SMp, st.a.E, c2, c1b, c1bh, act, k, oI[1], oD[1], oS[1], oL[1], jv);
+    cell_pk<MASKED, TBL, CODES, NOE, LOCAL>(st.a, dd_in, sm_in, e_in, c2, c1a, c1ah, act, k, oI[0], oD[0], oS[0], oL[0]);
+    cell_pk<MASKED, TBL, CODES, NOE, LOCAL>(st.b, st.a.Dd, st.a.SMp, st.a.E, c2, c1b, c1bh, act, k, oI[1], oD[1], oS[1], oL[1]);
     st.c2c = c2;
 }
 
@@ -454,7 +444,7 @@ __device__ __forceinline__ void sub_block_pk(LanePk& st, Rec (&nxt)[4], WavePk& 
 // max(S, D) seed only needs max(S, D) + h + g <= 0 (the floor decides I(i, 1)).
 template <bool LOCAL = false>
 __device__ __forceinline__ void init_row_pk(RowPk& rs, const Scores32& sc, int B0, int B1, const PkScores& k) {
-    rs.lb = kBias2; rs.lc = 0;
+    rs.lb = kBias2;
     if (LOCAL) {
         rs.I = pk2(sc.h, sc.h) ^ kBias2;
         rs.SD = pk2(sc.h, sc.h) ^ kBias2;
@@ -580,9 +570,10 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
         lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
     }
     if constexpr (LOCAL) {
-        // each pair's last max of the strip (row-major: the later row wins
-        // ties, each row's tracker holds its later column) -> StripRes, which
-        // finalize_kernel reduces over the strips (algo.rs:310-322)
+        // each pair's last max row of the strip (row-major: the later row wins
+        // ties) -> StripRes, which finalize_kernel reduces over the strips;
+        // local_col_kernel then finds the row's last column holding it
+        // (algo.rs:310-322)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const PairDev& P = h ? P1 : P0;
@@ -591,17 +582,15 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
             const int vb = okb ? (h ? hi16(st.b.lb ^ kBias2) : lo16(st.b.lb ^ kBias2)) : INT_MIN;
             const bool tb = okb && vb >= va;
             const int v = tb ? vb : va;
-            const uint32_t lc = tb ? st.b.lc : st.a.lc;
-            const int col = (int)((h ? lc >> 16 : lc) & 0xFFFFu);
             int mx = v;
             for (int off = 32; off > 0; off >>= 1) mx = max(mx, __shfl_xor(mx, off));
             const unsigned long long lm = __ballot(oka && v == mx);
             const int ll = lm ? 63 - __clzll((long long)lm) : 0;
-            const int lj = __shfl(col, ll), lh = __shfl((int)tb, ll);
+            const int lh = __shfl((int)tb, ll);
             if (lane == 0 && (h == 0 || &P1 != &P0)) {
                 StripRes r;
                 r.best = INT_MIN; r.bi = 0; r.bj = 0; r.bl = 0;
-                r.lbest = mx; r.li = s * kStripRows + kRowsPerLane * ll + lh + 1; r.lj = lj; r.lE = 0;
+                r.lbest = mx; r.li = s * kStripRows + kRowsPerLane * ll + lh + 1; r.lj = 0; r.lE = 0;
                 sres[P.strip_base + s] = r;
             }
         }

@@ -1811,6 +1811,58 @@ hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t
 
 // Plane checksums of the npairs pairs of a launch (descriptors on the device)
 // into out[npairs][3] (zeroed here); max_strips = the most strips of any pair.
+// The local twin fill (gx_fill_pk.hip LOCAL) keeps each row's largest
+// score_max only; finalize_kernel has picked the last row holding the pair's
+// maximum (PairRes.lmax_i, lmax_val).  This finds that row's LAST column
+// holding it (the reference's row-major max_by, algo.rs:310-322) from the twin
+// plane codes: I(i, j) = I(i, 0) + sum (x_I' + g), I(i, 0) = H(i, 0) + h = h
+// (local), score_max = I + max(0, x_S, x_D).  One wave per
+// pair: each lane decodes a chunk of the row, an exclusive scan of the chunk
+// sums gives every lane its starting I, and the highest matching column wins.
+__global__ __launch_bounds__(64) void local_col_kernel(const PairDev* __restrict__ pairs, PairRes* __restrict__ pres,
+                                                      const int h, const int g) {
+    const PairDev d = pairs[blockIdx.x];
+    PairRes* const r = pres + blockIdx.x;
+    const int lane = threadIdx.x;
+    const int i = __builtin_amdgcn_readfirstlane(r->lmax_i), target = __builtin_amdgcn_readfirstlane(r->lmax_val);
+    if (i < 1 || i > d.n || d.m < 1 || !d.pI) return;
+    const int s = (i - 1) / kStripRows, rr = (i - 1) % kStripRows, l = rr >> 1, hh = rr & 1;
+    const uint8_t* base = (const uint8_t*)d.pI + (size_t)s * d.t4 * kTwinGroupBytes + (size_t)hh * (kTwinGroupBytes / 2) +
+                          (size_t)l * 16;
+    const int sh = 16 * d.twin_half;
+    const int C = (d.m + kWave - 1) / kWave, j0 = lane * C + 1, j1 = min(d.m, j0 + C - 1);
+    auto code_at = [&](int j, int& xI, int& xS, int& xD) {
+        const int t = j + l - 1;   // the step at which this row computes column j (anti-diagonal skew)
+        const uint32_t w = *(const uint32_t*)(base + (size_t)(t >> 2) * kTwinGroupBytes + (size_t)(t & 3) * 4);
+        const uint32_t code = (0u - (w >> sh)) & 0xFFFFu;   // (stored negated, gx_fill_pk.hip w16_code)
+        xI = (int)(code & 15u);
+        const uint32_t q = code >> 4;
+        xS = (int)(q << 27) >> 27;
+        xD = (int)(((q - (uint32_t)xS) >> 5) << 25) >> 25;
+    };
+    int sum = 0;
+    for (int j = j0; j <= j1; ++j) { int a, b, c; code_at(j, a, b, c); sum += a + g; }
+    int pre = sum;   // inclusive scan over the lanes
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int v = __shfl_up(pre, o);
+        if (lane >= o) pre += v;
+    }
+    int I = h + pre - sum, last = 0;
+    for (int j = j0; j <= j1; ++j) {
+        int a, b, c;
+        code_at(j, a, b, c);
+        I += a + g;
+        if (I + max(0, max(b, c)) == target) last = j;
+    }
+    for (int o = 32; o > 0; o >>= 1) last = max(last, __shfl_xor(last, o));
+    if (lane == 0) r->lmax_j = last;
+}
+hipError_t launch_local_col(const PairDev* d_pairs, int npairs, PairRes* d_pres, int h, int g, hipStream_t st) {
+    if (npairs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(local_col_kernel, dim3((unsigned)npairs), dim3(64), 0, st, d_pairs, d_pres, h, g);
+    return hipGetLastError();
+}
+
 hipError_t launch_plane_sums(const PairDev* d_pairs, int npairs, int max_strips, int lay, int mode, int h, int g,
                              int floor_, int gshift, unsigned long long* out, hipStream_t st) {
     if (npairs <= 0 || max_strips <= 0) return hipSuccess;
