@@ -2499,15 +2499,30 @@ extern "C" int gx_align_batch(gx_context* ctx, const uint8_t* const* s1, const s
         ph[p] = PairHost{s1[p], s2[p], n[p], m[p]};
         proc[p] = {s1[p], s2[p]};
     }
-    // traceback codes only (no planes); batches beyond the free HBM run in chunks
-    const auto chunks = plan_chunks(ctx, ph, 0.0);
+    // traceback codes only (no planes); batches beyond the free HBM run in
+    // chunks.  Local batches that a plan of the whole batch puts on the local
+    // twin fill keep its plane codes as scratch for the walk
+    // (2 B/cell; chunks planned at the scalar byte format's 3 B/cell, should a
+    // chunk fall back)
+    bool lplanes = false;
+    if (is_local && !wide && !(flags & GX_ALIGN_MAX_CELL)) {
+        std::vector<PairHost> nz;
+        std::vector<std::pair<const uint8_t*, const uint8_t*>> np;
+        for (size_t p = 0; p < npairs; ++p)
+            if (n[p] && m[p]) { nz.push_back(ph[p]); np.push_back(proc[p]); }
+        FillJob pj;
+        pj.plan_only = true;
+        lplanes = !nz.empty() && !run_fill(ctx, np, nz, sc, is_local, true, false, false, pj) && pj.twin;
+    }
+    const auto chunks = plan_chunks(ctx, ph, lplanes ? 3.0 : 0.0);
     ctx->last_chunks = (int)chunks.size();
     std::vector<Walk> walks;
     for (const auto& c : chunks) {
         std::vector<PairHost> phc(ph.begin() + c.first, ph.begin() + c.second);
         std::vector<std::pair<const uint8_t*, const uint8_t*>> pc(proc.begin() + c.first, proc.begin() + c.second);
         rc = wide ? batch_core_wide(ctx, phc, pc, hs, is_local, false, (flags & GX_ALIGN_MAX_CELL) != 0, walks, nullptr)
-                  : batch_core(ctx, phc, pc, hs, sc, is_local, false, (flags & GX_ALIGN_MAX_CELL) != 0, walks, nullptr);
+                  : batch_core(ctx, phc, pc, hs, sc, is_local, lplanes, (flags & GX_ALIGN_MAX_CELL) != 0, walks,
+                               nullptr);
         if (rc) return rc;
         for (size_t k = 0; k < phc.size(); ++k) {
             const size_t p = c.first + k;

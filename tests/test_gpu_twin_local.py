@@ -149,3 +149,20 @@ def test_local_twin_overlapped(gx, ctx, oracle, monkeypatch):
     pairs = [_planted(rng, 4300 + 37 * k, 2500 + 53 * k, 600 + 40 * k) for k in range(18)]
     info = _check(gx, ctx, oracle, pairs, CONFIG_SCORES, steps=3)
     assert info["groups"] == 2, info
+
+
+def test_local_twin_align_batch(gx, ctx, oracle, monkeypatch):
+    """gx_align_batch (the drop-in batch call, no planes asked for) on local
+    pairs: the local twin fill with its plane codes kept as scratch for the
+    walk; every alignment and statistic against the oracle."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    rng = random.Random(808)
+    pairs = [_planted(rng, n, m, c) for n, m, c in [(900, 700, 300), (700, 900, 250), (1500, 400, 200),
+                                                    (333, 1200, 150), (257, 256, 256), (5, 5, 1), (6, 5, 2)]]
+    out = gx.align_batch(pairs, gx.Scores(*CONFIG_SCORES), True, ctx=ctx, max_cell=False)
+    assert ctx.fill_info()["twin"] == 1, ctx.fill_info()
+    for (a, b), (steps, r) in zip(pairs, out):
+        o = oracle.align(a, b, CONFIG_SCORES, is_local=True)
+        assert _steps_list(steps) == o.alignment(), (len(a), len(b))
+        assert (r.score, r.matches, r.mismatches, r.gap_extensions, r.opening_gaps) == \
+               (o.score, o.matches, o.mismatches, o.gap_extensions, o.opening_gaps), (len(a), len(b))
