@@ -2408,10 +2408,27 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
         // for the labelling (no host round trip between fill and traceback)
         for (size_t q = 0; q < idx.size(); ++q) starts[q] = TbStart{dph[q].n >= 1 && dph[q].m >= 1 ? (int)dph[q].n : 0,
                                                                      (int)dph[q].m, 0};
+        // GX_TB_STREAM=1 (batches whose step buffers fit 32 GB): the walk on
+        // its own stream, beside the next step's fill; each slot keeps its
+        // buffers until its walk was collected.  Measured (one box): 1024 x
+        // 4k 11.93 -> 11.28 ms a step, but 1024 x 1k 1.49 -> 3.66 ms (the
+        // host's enqueue of the next fill stalls ~2.5 ms behind the running
+        // walk), so it is off by default: the fill's buffers return to the
+        // pool right behind the walk on the one stream (stream-ordered reuse).
+        double step_bytes = 0;
+        for (const PairHost& h : dph) step_bytes += pair_device_bytes(h.n, h.m, planes ? 3.0 : 0.0);
+        const char* tsp = getenv("GX_TB_STREAM");
+        const bool split = tsp && !strcmp(tsp, "1") && step_bytes <= 32e9;
+        if (split && !ctx->tstream) HIPCHK(hipStreamCreateWithFlags(&ctx->tstream, hipStreamNonBlocking));
         auto trace_dev = [&](int s) {
-            int r = run_traceback(ctx, jobs[s], starts, ctx->slots[s].out, s, false, true);
-            job_release(ctx, jobs[s]);   // stream order: later users come after the traceback
-            return r;
+            if (!split) {
+                int r = run_traceback(ctx, jobs[s], starts, ctx->slots[s].out, s, false, true);
+                job_release(ctx, jobs[s]);   // stream order: later users come after the traceback
+                return r;
+            }
+            HIPCHK(hipStreamWaitEvent(ctx->tstream, ctx->slots[s].fdone, 0));   // (the fill's results are in)
+            return run_traceback(ctx, std::vector<const FillJob*>{&jobs[s]}, starts, ctx->slots[s].out, s, false, true,
+                                 ctx->tstream);
         };
         auto results = [&](int s) {
             int r = fill_collect(ctx, jobs[s]);
@@ -2424,19 +2441,28 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
         };
         using clk = std::chrono::steady_clock;
         const auto t_all = clk::now();
+        double h_enq = 0, h_tbw = 0, h_res = 0, h_lab = 0;   // host time per phase (GX_LOG=debug)
         if (!(rc = fill(0))) rc = trace_dev(0);
         for (int k = 0; k < nsteps && !rc; ++k) {
             const int s = k & 1;
+            auto t = clk::now();
             if (k + 1 < nsteps && ((rc = fill(s ^ 1)) || (rc = trace_dev(s ^ 1)))) break;
+            h_enq += since(t); t = clk::now();
             if ((rc = tb_collect(ctx, s, idx.size(), ctx->slots[s].out))) break;
+            h_tbw += since(t); t = clk::now();
             if ((rc = results(s))) break;
+            if (split) job_release(ctx, jobs[s]);   // its walk is done (tb_collect)
+            h_res += since(t); t = clk::now();
             if ((rc = label_batch(ctx, ph, hs, is_local, track, dev_of, si, sj, score, res, ctx->slots[s].out,
                                   jobs[s].fill_ms, walks)))
                 break;
+            h_lab += since(t);
         }
         if (const char* e = getenv("GX_LOG"); e && !strcmp(e, "debug"))
-            fprintf(stderr, "[gx DEBUG] pipelined %d steps P=%zu (device traceback starts): %.3f ms/step\n", nsteps, P,
-                    std::chrono::duration<double, std::milli>(clk::now() - t_all).count() / nsteps);
+            fprintf(stderr, "[gx DEBUG] pipelined %d steps P=%zu (device traceback starts): %.3f ms/step; host per step: "
+                    "enqueue fill+traceback %.3f, traceback wait %.3f, fill results %.3f, labelling %.3f ms\n", nsteps, P,
+                    std::chrono::duration<double, std::milli>(clk::now() - t_all).count() / nsteps, h_enq / nsteps,
+                    h_tbw / nsteps, h_res / nsteps, h_lab / nsteps);
         if (rc) {
             (void)hipStreamSynchronize(ctx->stream);
             (void)hipStreamSynchronize(ctx->cstream);
