@@ -302,7 +302,7 @@ def config_record(gx, ctx, which: str, steps: int):
     cells = len(a) * len(b)
     out = {"workload": f"{'Covid_Wuhan x Covid_USA-CA4' if which == 'covid' else 'Human x Mouse BRCA2 cds'} "
                        f"({len(a)}x{len(b)}), {'local SW' if local else 'global NW'}, scores {SCORES}, "
-                       f"{plane_desc(finfo['plane_bytes_per_cell'])} + traceback",
+                       f"{plane_desc(finfo['plane_bytes_per_cell'])}",
            "gcups": round(cells * steps / el / 1e9, 3), "ms_per_step": round(el / steps * 1e3, 3),
            "fill_ms_avg": round(fms, 3), "fill_gcups": round(cells / (fms * 1e-3) / 1e9, 3), "steps": steps,
            "fill_launch": finfo}
@@ -446,32 +446,60 @@ def alignment_sha256(steps) -> str:
     return h.hexdigest()
 
 
-def verify_against_golden(staged, scores, is_local, keep_planes, rank: int, P: int, L: int, related: bool = False):
-    """Parity of the benchmarked launch itself: one more (untimed) pass of
-    the same staged batch with on-device plane checksums; every pair that has
-    an oracle digest (tests/golden/synthetic_L{L}.json: score, statistics,
-    alignment sha256, the three plane checksums) must match it bit for bit.
-    Raises on any difference.  Returns (pairs checked, source)."""
+def golden_digests(rank: int, P: int, L: int, related: bool = False):
+    """{pair index on this rank: oracle digest} from tests/golden/synthetic(_related)_L{L}.json
+    (score, statistics, alignment sha256, plane checksums), and the file's path."""
     path = os.path.join(ROOT, "tests", "golden", f"synthetic_related_L{L}.json" if related else f"synthetic_L{L}.json")
-    if is_local or not os.path.exists(path):
-        return 0, None
+    if not os.path.exists(path):
+        return {}, None
     with open(path) as f:
         golden = {c["k"]: c for c in json.load(f)["cases"]}
-    mine = {p: golden[rank * P + p] for p in range(P) if rank * P + p in golden}
-    if not mine:
-        return 0, os.path.relpath(path, ROOT)
-    res, _ = staged.run(scores, is_local, keep_planes, steps=1, plane_sums=keep_planes)
+    return {p: golden[rank * P + p] for p in range(P) if rank * P + p in golden}, os.path.relpath(path, ROOT)
+
+
+def check_passes(pass_res, mine, rank: int, P: int, what: str):
+    """Every pass's per-pair results (gx_staged_pass_results) against the
+    oracle digests: score, statistics, alignment length.  Raises on any
+    difference; returns the number of passes checked."""
+    for k, row in enumerate(pass_res):
+        for p, c in mine.items():
+            r = row[p]
+            got = (r.score, [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps], r.n_steps)
+            want = (c["score"], c["stats"], c["n_steps"])
+            if got != want:
+                raise RuntimeError(f"parity ({what}): pass {k}, pair {rank * P + p} differs from the oracle digest: "
+                                   f"{got} != {want}")
+    return len(pass_res)
+
+
+def verify_against_golden(staged, ctx, scores, is_local, keep_planes, rank: int, P: int, L: int, related: bool,
+                          timed_info: dict, passes: int = 2):
+    """Parity of the benchmarked launch itself: `passes` more (untimed)
+    pipelined passes of the same staged batch through the same launch as the
+    timed call (fill_info must equal the timed call's: layout, band width,
+    plane format, twin fill, fill groups -- the overlapped two-group pipeline
+    when the timed call took it), with on-device plane checksums of every
+    pass.  Every pair that has an oracle digest (tests/golden/synthetic_L{L}.json)
+    must match it bit for bit: each pass's score, statistics, length and three
+    plane checksums, and the last pass's alignment sha256.  Raises on any
+    difference.  Returns (pairs checked, source, fill_info of the pass)."""
+    mine, src = golden_digests(rank, P, L, related)
+    if is_local or not mine:
+        return 0, src, None
+    staged.run(scores, is_local, keep_planes, steps=passes, plane_sums=keep_planes)
+    info = ctx.fill_info()
+    if info != timed_info:
+        raise RuntimeError(f"parity pass took a different launch than the timed call: {info} != {timed_info}")
+    check_passes(staged.pass_results(), mine, rank, P, "parity pass")
     sums = staged.plane_sums() if keep_planes else None
     for p, c in mine.items():
-        r = res[p]
-        got = (r.score, [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps], r.n_steps,
-               alignment_sha256(staged.steps(p)))
-        want = (c["score"], c["stats"], c["n_steps"], c["alignment_sha256"])
-        if got != want:
-            raise RuntimeError(f"parity: pair {rank * P + p} differs from the oracle digest: {got} != {want}")
-        if keep_planes and [int(x) for x in sums[0, p]] != [int(x) for x in c["plane_sums"]]:
-            raise RuntimeError(f"parity: pair {rank * P + p} score planes differ from the oracle's checksums")
-    return len(mine), os.path.relpath(path, ROOT)
+        if alignment_sha256(staged.steps(p)) != c["alignment_sha256"]:
+            raise RuntimeError(f"parity: pair {rank * P + p} alignment differs from the oracle digest")
+        for k in range(passes if keep_planes else 0):
+            if [int(x) for x in sums[k, p]] != [int(x) for x in c["plane_sums"]]:
+                raise RuntimeError(f"parity: pass {k}, pair {rank * P + p} score planes differ from the oracle's "
+                                   f"checksums")
+    return len(mine), src, info
 
 
 def simulate_world(args, gx, ctx):
@@ -611,12 +639,10 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    ref = None
     for _ in range(args.warmup):
         # (two pipelined passes: the same launches, streams and pooled buffers
         # as the timed call, so it allocates nothing)
-        res, _ = staged.run(scores, args.local, keep_planes, steps=2)
-        ref = [(r.score, r.n_steps, r.matches) for r in res]
+        staged.run(scores, args.local, keep_planes, steps=2)
     barrier()
     fill_ms = []
     tb_us = []
@@ -627,12 +653,22 @@ def main():
     res, fms = staged.run(scores, args.local, keep_planes, steps=args.steps)
     fill_ms.append(fms)
     tb_us.append(res[0].retrace_us)
-    got = [(r.score, r.n_steps, r.matches) for r in res]
-    if ref is not None and got != ref:
-        raise RuntimeError("non-deterministic result between steps")
     barrier()
     elapsed = time.perf_counter() - t0
     finfo = ctx.fill_info()
+    # every timed pass's results against the oracle digests (after the timed region)
+    timed_passes = staged.pass_results()
+    if len(timed_passes) != args.steps:
+        raise RuntimeError(f"{len(timed_passes)} pass records for {args.steps} timed steps")
+    timed_checked = 0
+    if args.workload == "synthetic" and not args.local and not args.no_verify:
+        mine, _ = golden_digests(rank, P, L, args.related)
+        if mine:
+            timed_checked = check_passes(timed_passes, mine, rank, P, "timed passes")
+    else:   # no digests: every pass must at least agree with the last
+        for k, row in enumerate(timed_passes):
+            if [(r.score, r.n_steps, r.matches) for r in row] != [(r.score, r.n_steps, r.matches) for r in res]:
+                raise RuntimeError(f"timed pass {k} differs from the last pass")
     bytes_per_cell = finfo["plane_bytes_per_cell"]
 
     # max over ranks (time) and gather of per-pair results, over RCCL
@@ -717,7 +753,9 @@ def main():
         "traceback_us_pair0": int(np.mean(tb_us)),
     }
     if args.workload == "synthetic" and not args.no_verify:
-        checked, src = verify_against_golden(staged, scores, args.local, keep_planes, rank, P, L, args.related)
+        vpasses = 2 if args.steps >= 2 else 1
+        checked, src, vinfo = verify_against_golden(staged, ctx, scores, args.local, keep_planes, rank, P, L,
+                                                    args.related, finfo, vpasses)
         if dist is not None:
             import torch
             t = torch.tensor([checked], dtype=torch.int64, device="cuda")
@@ -726,7 +764,16 @@ def main():
         out["parity"] = {"pairs_checked": checked, "pairs_total": P * world, "bit_exact": True,
                          "fields": "score, statistics, alignment sha256" + (", I/D/S plane checksums" if keep_planes
                                                                             else ""),
-                         "source": src, "pass": "one extra untimed pass of the same staged launch"}
+                         "source": src,
+                         "timed_passes_checked": timed_checked,
+                         "timed_pass_fields": "score, statistics, alignment length of every pair with a digest, "
+                                              "every timed pass",
+                         "pass": f"{vpasses} extra untimed pipelined passes through the timed call's launch "
+                                 f"(fill_info identical: layout {finfo['layout']}, band width {finfo['band_waves']}, "
+                                 f"{finfo['plane_bytes_per_cell']} B/cell, twin {finfo['twin']}, "
+                                 f"{finfo['groups']} fill group(s) per pass"
+                                 + (", the overlapped two-group pipeline" if finfo.get('groups') == 2 else "")
+                                 + "); plane checksums of every pass, alignment sha256 of the last"}
     if world == 1 and keep_planes and bytes_per_cell == 2 and args.no_plane_steps > 0:
         # the same batch with the per-pair byte planes (3 B/cell, the table format)
         os.environ["GX_PLANES_W16"] = "0"

@@ -235,6 +235,12 @@ struct gx_context {
     DevBuf sums_dev;
     unsigned long long* sums_dst = nullptr;          // where the next fill's checksums go (nullptr: off)
     std::vector<uint64_t> sums_host;                 // [passes][staged pairs][3] of the last run
+    // every pass's results of a staged run (gx_staged_pass_results): label_batch
+    // appends one pass of the current chunk (pairs pass_off ..) when pass_rec
+    bool pass_rec = false;
+    size_t pass_off = 0, pass_P = 0;
+    int pass_k = 0;
+    std::vector<gx_result> pass_res;                 // [passes][staged pairs]
 };
 
 static void* pinned_grow(PinnedBuf& b, size_t bytes) {
@@ -588,8 +594,14 @@ static bool w16_ok(const Scores32& sc) {
 // 30k global pair its two-wave strips in two-strip bands lose to layout 1's
 // one-wave strips in four-strip bands (more band hand-offs through HBM,
 // 5.33 vs 4.53 ms; BRCA2 local 1.76 vs 1.79 ms, profiles/r03a_bench.json).
-// GX_CS2=1 / 0 forces it on / off.
-static bool cs2_enabled(int is_local) {
+// GX_CS2=1 / 0 forces it on / off.  Local fills need g <= 0: the split
+// core applies the shifted 0 floor, -(i + j) g, after the delete chain's
+// prefix max, which is the reference's per-row floor (algo.rs:238-243) only
+// while the floor does not decrease down the rows; with g > 0 a floor reached
+// at an upper row must carry down the chain, which the one-wave column step
+// does (its per-lane chain offsets) and the split core does not.
+static bool cs2_enabled(int is_local, const Scores32& sc) {
+    if (is_local && sc.g > 0) return false;
     const char* e = getenv("GX_CS2");
     if (e && *e) return strcmp(e, "0") != 0;
     return is_local != 0;
@@ -817,7 +829,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     for (const PairHost& h : ph) min_strips = std::min(min_strips, ceil_div((int)h.n, SR));
     // the split column step (gx_cs2.hip): layout 1's formats, each strip on a
     // core and a side wave; untracked fills (global or local)
-    const bool cs2 = lay == 1 && !track && cs2_enabled(is_local);
+    const bool cs2 = lay == 1 && !track && cs2_enabled(is_local, sc);
     const int W = cs2 ? cs2_band_waves(total_strips, fill_grid_cap(ctx->device))
                       : fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device), lay, min_strips);
     job.lay = lay;
@@ -2046,6 +2058,12 @@ static int label_batch(gx_context* ctx, const std::vector<PairHost>& ph, const H
         w.res.fill_us = (int64_t)(fill_ms * 1000.0);
         w.res.retrace_us = (int64_t)(tb.ms * 1000.0);
     }
+    if (ctx->pass_rec) {   // a staged run keeps every pass's results (this chunk's pairs)
+        const size_t base = (size_t)ctx->pass_k * ctx->pass_P + ctx->pass_off;
+        if (base + P <= ctx->pass_res.size())
+            for (size_t p = 0; p < P; ++p) ctx->pass_res[base + p] = walks[p].res;
+        ++ctx->pass_k;
+    }
     return GX_OK;
 }
 
@@ -2684,6 +2702,16 @@ extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int
         proc[p] = {ph[p].s1, ph[p].s2};
     }
     const bool track = (flags & GX_ALIGN_MAX_CELL) != 0;
+    // every pass's results (label_batch records them; chunks set pass_off)
+    struct PassRec {
+        gx_context* c;
+        ~PassRec() { c->pass_rec = false; }
+    } pass_guard{ctx};
+    ctx->pass_res.assign((size_t)std::max(nsteps, 1) * P, gx_result{});
+    ctx->pass_rec = true;
+    ctx->pass_P = P;
+    ctx->pass_off = 0;
+    ctx->pass_k = 0;
     if (wide) {   // int64 fill: one synchronous pass at a time (a rare path, no pipelining or chunking)
         std::vector<Walk>& walks = ctx->walk_cache;
         const int passes = std::max(nsteps, 1);
@@ -2769,6 +2797,8 @@ extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int
             std::vector<std::pair<const uint8_t*, const uint8_t*>> pc(proc.begin() + a, proc.begin() + b);
             std::vector<size_t> o1(ctx->st_off1.begin() + a, ctx->st_off1.begin() + b),
                 o2(ctx->st_off2.begin() + a, ctx->st_off2.begin() + b);
+            ctx->pass_off = a;
+            ctx->pass_k = 0;
             double f = 0;
             rc = batch_core_steps(ctx, phc, pc, hs, sc, is_local, keep_planes != 0, track, passes, wc, &f,
                                   (const uint8_t*)ctx->st_chars.p, &o1, &o2, &ctx->st_alpha);
@@ -2806,6 +2836,15 @@ extern "C" int gx_staged_plane_sums(const gx_context* ctx, uint64_t* out, size_t
     if (!out) return GX_OK;
     if (cap < ctx->sums_host.size()) return fail(GX_ECAP, "out too small");
     std::copy(ctx->sums_host.begin(), ctx->sums_host.end(), out);
+    return GX_OK;
+}
+
+extern "C" int gx_staged_pass_results(const gx_context* ctx, gx_result* out, size_t cap, size_t* n_values) {
+    if (!ctx) return fail(GX_EINVAL, "context is NULL");
+    if (n_values) *n_values = ctx->pass_res.size();
+    if (!out) return GX_OK;
+    if (cap < ctx->pass_res.size()) return fail(GX_ECAP, "out too small");
+    std::copy(ctx->pass_res.begin(), ctx->pass_res.end(), out);
     return GX_OK;
 }
 

@@ -75,7 +75,7 @@ EXPORTED = ["gx_last_error", "gx_version", "gx_context_create", "gx_context_dest
             "gx_table_plane_sums", "gx_retrace", "gx_table_free", "gx_align", "gx_align_batch", "gx_align_batch_multi",
             "gx_stage_pairs",
             "gx_run_staged", "gx_run_staged_steps", "gx_staged_plane_sums", "gx_staged_steps",
-            "gx_fill_info", "gx_batch_chunks", "gx_fill_twin", "gx_fill_groups", "gx_plane_bytes_per_cell", "gx_twin_admission",
+            "gx_staged_pass_results", "gx_fill_info", "gx_batch_chunks", "gx_fill_twin", "gx_fill_groups", "gx_plane_bytes_per_cell", "gx_twin_admission",
             "gx_fasta_load",
             "gx_config_load", "gx_format_alignment", "gx_format_table"]
 
@@ -106,6 +106,7 @@ def lib():
     L.gx_table_plane_sums.argtypes = [vp, vp]
     L.gx_staged_plane_sums.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     L.gx_staged_steps.argtypes = [vp, sz, vp, sz, ctypes.POINTER(sz)]
+    L.gx_staged_pass_results.argtypes = [vp, vp, sz, ctypes.POINTER(sz)]
     L.gx_retrace.argtypes = [vp, ctypes.c_int, vp, sz, ctypes.POINTER(CResult)]
     L.gx_table_free.argtypes = [vp]
     L.gx_table_free.restype = None
@@ -611,6 +612,15 @@ class StagedPairs:
         out = np.zeros(max(n.value, 1), np.uint64)
         _check(lib().gx_staged_plane_sums(self.ctx.ptr, out.ctypes.data, out.size, ctypes.byref(n)))
         return out[: n.value].reshape(-1, self.P, 3)
+
+    def pass_results(self) -> List[List["CResult"]]:
+        """Every pass's per-pair results of the last run, [pass][pair] (gx_staged_pass_results)."""
+        n = ctypes.c_size_t(0)
+        _check(lib().gx_staged_pass_results(self.ctx.ptr, None, 0, ctypes.byref(n)))
+        out = (CResult * max(n.value, 1))()
+        _check(lib().gx_staged_pass_results(self.ctx.ptr, out, n.value, ctypes.byref(n)))
+        rows = list(out)[: n.value]
+        return [rows[k * self.P:(k + 1) * self.P] for k in range(n.value // max(self.P, 1))]
 
     def steps(self, pair: int) -> np.ndarray:
         """The alignment of staged pair `pair` from the last pass of the last run (STEP_DTYPE array)."""

@@ -206,6 +206,10 @@ int gx_staged_plane_sums(const gx_context* ctx, uint64_t* out, size_t cap, size_
  * last pass of the last gx_run_staged(_steps) call; *n_steps = its length
  * (steps may be NULL to query it). */
 int gx_staged_steps(const gx_context* ctx, size_t pair, gx_step* steps, size_t cap, size_t* n_steps);
+/* Every pass's results of the last gx_run_staged(_steps) call, [pass][pair]
+ * (nsteps * npairs records; `out` of that call is the last pass's row), so
+ * that each timed pass can be checked, not only the last.  Verification only. */
+int gx_staged_pass_results(const gx_context* ctx, gx_result* out, size_t cap, size_t* n_values);
 /* The last fill launch on ctx: its layout (0: anti-diagonal 128-row strips,
  * 1: column step over 64-row strips), band width (strips per workgroup) and
  * score-plane bytes written per cell (0: none, 12: int32 planes, 3: compact

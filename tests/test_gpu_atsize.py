@@ -145,10 +145,13 @@ def _staged_check(gx, ctx, pairs, cases, steps=2, **kw):
     assert fill_ms > 0
     sums = st.plane_sums()
     assert sums.shape == (steps, len(pairs), 3)
+    passes = st.pass_results()
+    assert len(passes) == steps
     for p, c in enumerate(cases):
         want = [int(x) for x in c["plane_sums"]]
         for k in range(steps):   # every pass of the pipelined run, not just the last
             assert [int(x) for x in sums[k, p]] == want, (p, c["k"], "pass", k)
+            _check_result(passes[k][p], None, c, (p, c["k"], "pass", k))
         _check_result(res[p], st.steps(p), c, (p, c["k"]))
     return ctx.fill_info()
 
@@ -186,6 +189,23 @@ def test_bench_launch_synthetic_30k(gx, ctx, monkeypatch, launch):
         assert info["layout"] == lay and (pb is None or info["plane_bytes_per_cell"] == pb), info
         if W:
             assert info["band_waves"] == W, info
+
+
+@pytest.mark.parametrize("npairs,env", [(20, {"GX_TWIN": "1"}), (80, {})], ids=["20_twin", "80_default"])
+def test_overlapped_bench_launch_30k(gx, ctx, monkeypatch, npairs, env):
+    """The launch the headline times: synthetic 30k pairs through the
+    overlapped two-group pipeline (gx_api.cpp batch_core_overlap), three
+    passes -- 20 pairs with the twin fill forced (group A's 4 pairs alone
+    would not fill the grid and take the scalar fill, so the pipeline would
+    not run by default) and the bench's whole 80-pair batch under the default
+    environment.  Every pass's plane checksums and results, the last pass's
+    alignments, against the oracle digests; groups == 2."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cases = _synth(30000)[:npairs]
+    pairs = [_synth_pair(c["k"], 30000) for c in cases]
+    info = _staged_check(gx, ctx, pairs, cases, steps=3)
+    assert info["groups"] == 2 and info["twin"] == 1 and info["plane_bytes_per_cell"] == 2, info
 
 
 @pytest.mark.parametrize("L", [1024, 4096, 16384])

@@ -130,7 +130,8 @@ def test_random_pairs_batched(gx, ctx, oracle, is_local):
         assert_same(steps, r, oracle.align(a, b, CONFIG_SCORES, is_local=is_local), (len(a), len(b)))
 
 
-@pytest.mark.parametrize("scores", [(1, -2, -1, -5), (2, -3, -2, -4), (5, -4, 0, -10), (1, -1, -1, 0), (3, 1, -1, -2)])
+@pytest.mark.parametrize("scores", [(1, -2, -1, -5), (2, -3, -2, -4), (5, -4, 0, -10), (1, -1, -1, 0), (3, 1, -1, -2),
+                                    (1, -2, 1, -3)])
 def test_scoring_variants(gx, ctx, oracle, scores):
     rng = random.Random(hash(scores) & 0xffff)
     for _ in range(20):
@@ -172,13 +173,17 @@ def test_exported_planes_and_cells(gx, ctx, oracle, n, m, is_local):
 
 
 @pytest.mark.parametrize("scores", [(1, -2, -1, -5), (1, -2, -2, -5), (2, -3, -2, -4), (5, -4, 0, -10),
-                                    (10, -10, -5, -20), (1, -1, 0, 0), (30, -30, -10, -40), (3, 1, -1, -2)])
+                                    (10, -10, -5, -20), (1, -1, 0, 0), (30, -30, -10, -40), (3, 1, -1, -2),
+                                    (1, -2, 1, -3), (2, -1, 1, -4)])
 @pytest.mark.parametrize("is_local", [False, True], ids=["global", "local"])
 def test_untracked_table_planes(gx, ctx, oracle, scores, is_local):
     """Tables built without the max-cell tracking: on layout 0 their
     score planes are stored as per-cell byte differences when the scores pass
     the range proof (gx_api.cpp d8_planes_ok; (30, -30, -10, -40) does not and
-    (3, 1, -1, -2) has g > 0, both keep int32 planes).  Every exported plane
+    (1, -2, 1, -3), (2, -1, 1, -4) have g > 0, all keep int32 planes).  On
+    layout 1 a local fill with g > 0 must not take the split column step
+    (gx_api.cpp cs2_enabled: its 0 floor is applied after the delete chain's
+    prefix max, exact only for g <= 0), even where GX_CS2=1 asks for it.  Every exported plane
     value equals the oracle's, including dense-tie and long-match inputs that
     push the differences towards the proof's bounds."""
     rng = random.Random(hash(scores) & 0xffff)

@@ -337,3 +337,39 @@ def test_twin_auto_selection(gx, ctx, oracle, monkeypatch, kind):
         o = oracle.align_lean(a, b, CONFIG_SCORES)
         assert r.score == o.score and r.n_steps == len(o.choices)
         assert _steps_list(steps) == o.alignment()
+
+
+@pytest.mark.parametrize("launch_env", ["auto", "w4_grid3"])
+def test_twin_overlapped_global(gx, ctx, oracle, monkeypatch, launch_env):
+    """The headline's launch shape: a long-pair global batch through the
+    overlapped two-group pipeline (gx_api.cpp batch_core_overlap: group A's
+    fill of pass k+1 beside pass k's walk into a second A buffer, group B's
+    fill of pass k+1 waiting on the device for pass k's walk before it reuses
+    B's buffers).  20 mixed shapes, three passes: every pass's plane
+    checksums and results (gx_staged_pass_results), the last pass's
+    alignments, against the oracle; the pipeline must have run (groups == 2)."""
+    monkeypatch.setenv("GX_LAYOUT", "0")
+    monkeypatch.setenv("GX_OVERLAP", "1")   # (by default from n >= 4,096)
+    if launch_env == "w4_grid3":   # bands queued for three workgroups per launch: the two launches interleave
+        monkeypatch.setenv("GX_BAND_WAVES", "4")
+        monkeypatch.setenv("GX_FILL_GRID", "3")
+    rng = random.Random(2024)
+    shapes = [(1300 + 97 * k, 1100 + 61 * ((k * 7) % 20)) for k in range(20)]
+    pairs = [(bytes(rng.choice(b"ACGT") for _ in range(n)), bytes(rng.choice(b"ACGT") for _ in range(m)))
+             for n, m in shapes]
+    steps = 3
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=steps, plane_sums=True)
+    info = ctx.fill_info()
+    assert info["groups"] == 2 and info["twin"] == 1 and info["plane_bytes_per_cell"] == 2, info
+    sums = st.plane_sums()
+    passes = st.pass_results()
+    assert len(passes) == steps
+    for p, (a, b) in enumerate(pairs):
+        o = oracle.align_lean(a, b, CONFIG_SCORES)
+        want = (o.score, o.matches, o.mismatches, o.gap_extensions, o.opening_gaps, len(o.choices))
+        for k in range(steps):
+            assert [int(x) for x in sums[k, p]] == o.extra["plane_sums"], (p, len(a), len(b), k)
+            r = passes[k][p]
+            assert (r.score, r.matches, r.mismatches, r.gap_extensions, r.opening_gaps, r.n_steps) == want, (p, k)
+        assert _steps_list(st.steps(p)) == o.alignment(), (p, len(a), len(b))
