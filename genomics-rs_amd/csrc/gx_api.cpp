@@ -43,6 +43,9 @@ hipError_t launch_local_col(const PairDev* d_pairs, int npairs, PairRes* d_pres,
 hipError_t launch_fill_cs2(int W, bool local, bool planes, bool tbl, const PairDev* d_pairs, int npairs,
                            int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                            hipStream_t st);
+hipError_t launch_fill_skew(int W, bool local, bool planes, bool tbl, const PairDev* d_pairs, int npairs,
+                            int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
+                            hipStream_t st);
 hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int npairs, int ntwins, int total_bands,
                           int* d_counter, PairRes* d_pres, StripRes* d_sres, Scores32 sc, int grid, hipStream_t st);
 hipError_t launch_fill_wide(const WideDev* d_pairs, int npairs, WideScores sc, WideRes* d_res, int local, int track,
@@ -606,6 +609,17 @@ static bool cs2_enabled(int is_local, const Scores32& sc) {
     if (e && *e) return strcmp(e, "0") != 0;
     return is_local != 0;
 }
+// Layout 3 (gx_skew.hip): 4-strip bands, one compute wave per SIMD (a
+// strip's step is one wave's VALU issue); GX_BAND_WAVES picks another
+// instantiated width (must match gx_skew.hip launch_fill_skew).
+static int skew_band_waves() {
+    static constexpr int kSkewWidths[] = {2, 3, 4, 8};
+    if (const char* e = getenv("GX_BAND_WAVES")) {
+        const int w = atoi(e);
+        for (int x : kSkewWidths) if (x == w) return w;
+    }
+    return 4;
+}
 static int cs2_band_waves(int total_strips, int grid_cap) {
     static constexpr int kCs2Widths[] = {1, 2, 3, 4, 7};
     if (const char* e = getenv("GX_BAND_WAVES")) {
@@ -625,17 +639,22 @@ struct PairHost {
 
 // Fill layout (gx_internal.h): 0 = anti-diagonal 128-row strips, 1 = column
 // step over 64-row strips (delete chain as a wave prefix max; a strip follows
-// the one above a few columns behind instead of 64+ steps).  GX_LAYOUT forces
-// one.  Layout 1 offsets the delete chain by up to 64 (|g| + |h|) inside the
-// scan, so it needs that much int32 headroom above the range guard's 2^28.
+// the one above a few columns behind instead of 64+ steps), 3 = anti-diagonal
+// 64-row strips with one row per lane (gx_skew.hip, the latency fill).
+// GX_LAYOUT forces one.  Layout 1 offsets the delete chain by up to 64
+// (|g| + |h|) inside the scan, so it needs that much int32 headroom above the
+// range guard's 2^28.
 //
-// Default: layout 1 while the job is latency-bound -- its 64-row strips fit
-// about two per SIMD (one to three 30k pairs: 1.45x on one, 1.33x on two,
-// 1.06x on three); layout 0 from four 30k pairs on, where the band-major
-// queue keeps every CU busy and layout 0's 2-row lanes issue fewer
-// instructions per cell (four 30k pairs 7.7 vs 8.4 ms, eight 10.6 vs 15.9 ms;
-// profiles/r01o_round_sweep.txt, profiles/r01d_layouts.txt).
-static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int grid_cap) {
+// Default: a latency layout while the job is latency-bound -- its 64-row
+// strips fit about two per SIMD (one to three 30k pairs); layout 0 from four
+// 30k pairs on, where the band-major queue keeps every CU busy and layout 0's
+// 2-row lanes issue fewer instructions per cell (four 30k pairs 7.7 vs 8.4
+// ms, eight 10.6 vs 15.9 ms; profiles/r01o_round_sweep.txt,
+// profiles/r01d_layouts.txt).  The latency layout is 3 for untracked fills
+// with h <= 0 (its recurrences fold the gap opening onto score_max, which is
+// exact only then), else the column step.
+static bool skew_ok(const Scores32& sc, bool track) { return !track && sc.h <= 0; }
+static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int grid_cap, bool track) {
     const long long span = 65LL * (std::llabs((long long)sc.g) + std::llabs((long long)sc.h));
     size_t mmax = 0;
     long long strips64 = 0;
@@ -644,8 +663,13 @@ static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int 
         strips64 += ceil_div((int)h.n, kStripRows1);
     }
     const bool cs_ok = span < (1LL << 29) && mmax + 128 < (1u << 24);   // landing keys hold E + 64 in 24 bits
-    if (const char* e = getenv("GX_LAYOUT"); e && *e) return (atoi(e) == 1 && cs_ok) ? 1 : 0;
-    return (cs_ok && strips64 <= 6LL * grid_cap) ? 1 : 0;
+    const int lat = skew_ok(sc, track) ? 3 : cs_ok ? 1 : 0;
+    if (const char* e = getenv("GX_LAYOUT"); e && *e) {
+        const int want = atoi(e);
+        if (want == 3) return skew_ok(sc, track) ? 3 : cs_ok ? 1 : 0;
+        return (want == 1 && cs_ok) ? 1 : 0;
+    }
+    return strips64 <= 6LL * grid_cap ? lat : 0;
 }
 
 struct FillJob {
@@ -654,7 +678,7 @@ struct FillJob {
     std::vector<PairDev> pd;
     std::vector<PairRes> res;
     int W = 4;
-    int lay = 0;   // 0: anti-diagonal 128-row strips, 1: column-step 64-row strips (gx_internal.h)
+    int lay = 0;   // 0: anti-diagonal 128-row strips, 1: column-step 64-row strips, 3: skewed 64-row strips (gx_internal.h)
     int slot = -1;                      // pipelined path: the context slot whose pinned staging / events it uses
     PairRes* pin_res = nullptr;         // results in pinned staging (collected by fill_collect)
     int* pin_status = nullptr;
@@ -817,7 +841,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                     bool lcs, FillJob& job, const uint8_t* chars_dev = nullptr,
                     const std::vector<size_t>* off1 = nullptr, const std::vector<size_t>* off2 = nullptr,
                     const SmallAlpha* alpha = nullptr, int slot = -1, bool collect = true) {
-    const int lay = fill_layout(ph, sc, fill_grid_cap(ctx->device));
+    const int lay = fill_layout(ph, sc, fill_grid_cap(ctx->device), track || (lcs && planes));
     hipStream_t const fs = job.stream ? job.stream : ctx->stream;
     const int SR = strip_rows(lay);
     int total_strips = 0;
@@ -830,15 +854,16 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     // the split column step (gx_cs2.hip): layout 1's formats, each strip on a
     // core and a side wave; untracked fills (global or local)
     const bool cs2 = lay == 1 && !track && cs2_enabled(is_local, sc);
-    const int W = cs2 ? cs2_band_waves(total_strips, fill_grid_cap(ctx->device))
-                      : fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device), lay, min_strips);
+    const int W = cs2         ? cs2_band_waves(total_strips, fill_grid_cap(ctx->device))
+                  : lay == 3 ? skew_band_waves()
+                             : fill_band_waves(track || is_local, total_strips, fill_grid_cap(ctx->device), lay, min_strips);
     job.lay = lay;
     job.local_on = is_local != 0;
     // layout-0 untracked global fills and the split column step keep every
     // value as V - (i + j) g (one add less per recurrence, gx_kernels.hip
     // cell; the local floor becomes -(i + j) g); the sub scores carry -2g
     Scores32 scl = sc;
-    const bool shift = (lay == 0 && !is_local && !track) || cs2;
+    const bool shift = ((lay == 0 || lay == 3) && !is_local && !track) || cs2;
     scl.shift = shift ? 1 : 0;
     if (shift) { scl.sm = sc.sm - 2 * sc.g; scl.smm = sc.smm - 2 * sc.g; }
     job.shift = shift; job.g = sc.g;
@@ -859,10 +884,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     const std::vector<std::pair<int, int>> tw = twin_table(
         ph, is_local ? INT_MAX : twin_gap_cap(sc, wt_want >= 15 ? 15 : wt_want >= 8 ? 8 : wt_want >= 7 ? 7 : wt_want >= 4 ? 4 : 3));
     {
-        const char* tce0 = getenv("GX_TWIN_CODES");
-        const char* tse0 = getenv("GX_TWIN_SKEL");
-        const bool long_ok = planes && !job.table && w16_ok(sc) && !(tce0 && !strcmp(tce0, "1")) &&
-                             !(tse0 && !strcmp(tse0, "1"));   // (the noskel rule below)
+        const bool long_ok = planes && !job.table && w16_ok(sc);   // (the noskel rule below)
         Wt = twin_width(ph, tw, sc, is_local, track, lcs, lay, planes, d8, wt_want, long_ok);
         // auto: the twin fill once its own bands fill the grid (a twin band
         // is slower per step than a scalar one, so fewer bands than CUs
@@ -893,15 +915,12 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     job.w16 = w16;
     // with twin plane codes the fill stores no code words (0.25 B/cell less):
     // the traceback rebuilds the words of the path's strips from the planes
-    // (tb_w16_codes_kernel); GX_TWIN_CODES=1 keeps them
-    const char* tce = getenv("GX_TWIN_CODES");
-    job.nocodes = w16 && !(tce && !strcmp(tce, "1"));
-    // ... and no landing columns either (a quarter of the twin cell's VALU):
-    // the traceback then walks the strips one after another, each entered
-    // where the one below left it (tb_seq_kernel); GX_TWIN_SKEL=1 keeps the
-    // skeleton and the parallel strip walks
-    const char* tse = getenv("GX_TWIN_SKEL");
-    job.noskel = job.nocodes && !(tse && !strcmp(tse, "1"));
+    // (tb_w16_codes_kernel), and no landing columns either (a quarter of the
+    // twin cell's VALU): the traceback walks the strips one after another,
+    // each entered where the one below left it (tb_seq_kernel).  The byte
+    // planes (tables, GX_PLANES_W16=0) keep both.
+    job.nocodes = w16;
+    job.noskel = job.nocodes;
     // small-alphabet twins: the match test through score tables (cell_pk; the
     // shifted scores must fit an unsigned byte);
     // the byte-plane twin (tables) keeps the plain test
@@ -941,7 +960,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         d.strips = ceil_div(ns, SR);
         d.bands = ceil_div(d.strips, Wf);
         // steps per strip: layout 0, lane 63 pushes column m at step m + 63; layout 1, column m at step m - 1
-        const int T = lay ? ms + 1 : ms + kWave;
+        const int T = lay == 1 ? ms + 1 : ms + kWave;
         d.t16 = ceil_div(T, 16);
         d.t4 = d.t16 * 4;
         d.strip_base = strips;
@@ -992,28 +1011,23 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     // band queue order, stored after the pair descriptors: band-major ("round"
     // order: band 0 of every pair, then band 1, ...; a band's predecessor in its
     // pair is always dequeued before it, so a waiting band is never waiting on
-    // an unstarted one) unless GX_BAND_ORDER=pair (all bands of pair 0 first)
+    // an unstarted one; pair-major order, all bands of pair 0 first, was 10-25 %
+    // slower, profiles/r01o_band_order_ab.txt)
     std::vector<int> order;
     order.reserve(2 * (size_t)bands);
-    {
-        const char* bo = getenv("GX_BAND_ORDER");
-        if (twin) {   // band-major over the twins: entries (twin q, band), then the twin table
-            int maxb = 0;
-            for (const auto& t : tw) maxb = std::max(maxb, job.pd[t.first].bands);
-            for (int lb = 0; lb < maxb; ++lb)
-                for (size_t q = 0; q < tw.size(); ++q)
-                    if (lb < job.pd[tw[q].first].bands) { order.push_back((int)q); order.push_back(lb); }
-            for (const auto& t : tw) { order.push_back(t.first); order.push_back(t.second); }
-        } else if (bo && !strcmp(bo, "pair")) {
+    if (twin) {   // band-major over the twins: entries (twin q, band), then the twin table
+        int maxb = 0;
+        for (const auto& t : tw) maxb = std::max(maxb, job.pd[t.first].bands);
+        for (int lb = 0; lb < maxb; ++lb)
+            for (size_t q = 0; q < tw.size(); ++q)
+                if (lb < job.pd[tw[q].first].bands) { order.push_back((int)q); order.push_back(lb); }
+        for (const auto& t : tw) { order.push_back(t.first); order.push_back(t.second); }
+    } else {
+        int maxb = 0;
+        for (size_t p = 0; p < P; ++p) maxb = std::max(maxb, job.pd[p].bands);
+        for (int lb = 0; lb < maxb; ++lb)
             for (size_t p = 0; p < P; ++p)
-                for (int lb = 0; lb < job.pd[p].bands; ++lb) { order.push_back((int)p); order.push_back(lb); }
-        } else {
-            int maxb = 0;
-            for (size_t p = 0; p < P; ++p) maxb = std::max(maxb, job.pd[p].bands);
-            for (int lb = 0; lb < maxb; ++lb)
-                for (size_t p = 0; p < P; ++p)
-                    if (lb < job.pd[p].bands) { order.push_back((int)p); order.push_back(lb); }
-        }
+                if (lb < job.pd[p].bands) { order.push_back((int)p); order.push_back(lb); }
     }
     const size_t ord_bytes = align_up(order.size() * sizeof(int), 16);   // keeps the PairRes staging 16-B aligned
     if ((rc = pool_get(ctx, P * sizeof(PairDev) + ord_bytes, &job.pairs))) return rc;
@@ -1060,6 +1074,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     if (!order.empty()) memcpy(pin + P * sizeof(PairDev), order.data(), order.size() * sizeof(int));
     HIPCHK(hipMemcpyAsync(job.pairs.p, pin, P * sizeof(PairDev) + ord_bytes, hipMemcpyHostToDevice, fs));
     HIPCHK(hipMemsetAsync(job.progress.p, 0, std::max<size_t>(prog_elems, 1) * sizeof(int), fs));
+    // layout 3 hands band rows over in tagged granules (gx_skew.hip io_wave_tag): valid once written
+    if (lay == 3 && feed_recs > 0) HIPCHK(hipMemsetAsync(job.feed.p, 0, feed_recs * sizeof(Rec), fs));
     HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, fs));
     HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), fs));
     // twin workgroups: as many per CU as fit 16 waves (the twin kernels hold
@@ -1077,6 +1093,9 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                                   (job.noskel ? 16 : 0) + (is_local ? 32 : 0),
                               (const PairDev*)job.pairs.p, (int)P, (int)tw.size(), bands, (int*)job.counter.p,
                               (PairRes*)job.pres.p, (StripRes*)job.sres.p, scl, grid, fs));
+    else if (bands > 0 && lay == 3)
+        HIPCHK(launch_fill_skew(W, is_local != 0, planes, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
+                                (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
     else if (bands > 0 && cs2)
         HIPCHK(launch_fill_cs2(W, is_local != 0, planes, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
                                (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
@@ -1435,6 +1454,7 @@ static int run_traceback(gx_context* ctx, const std::vector<const FillJob*>& jv,
         t.seg = (int*)seg.p + 4 * so[p];
         t.recs = (uint32_t*)recs.p + so[p] * SR;
         t.srows = SR;
+        t.skew = job.lay == 3 ? 1 : 0;
         t.skel_half = job.twin ? d.twin_half : -1;
         t.end_ij = (int*)cnt.p + 4 * p;
         t.w16 = job.nocodes ? (const uint8_t*)d.pI : nullptr;   // the twin's code plane (shared by its pairs)
@@ -2426,27 +2446,15 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
         // for the labelling (no host round trip between fill and traceback)
         for (size_t q = 0; q < idx.size(); ++q) starts[q] = TbStart{dph[q].n >= 1 && dph[q].m >= 1 ? (int)dph[q].n : 0,
                                                                      (int)dph[q].m, 0};
-        // GX_TB_STREAM=1 (batches whose step buffers fit 32 GB): the walk on
-        // its own stream, beside the next step's fill; each slot keeps its
-        // buffers until its walk was collected.  Measured (one box): 1024 x
-        // 4k 11.93 -> 11.28 ms a step, but 1024 x 1k 1.49 -> 3.66 ms (the
-        // host's enqueue of the next fill stalls ~2.5 ms behind the running
-        // walk), so it is off by default: the fill's buffers return to the
-        // pool right behind the walk on the one stream (stream-ordered reuse).
-        double step_bytes = 0;
-        for (const PairHost& h : dph) step_bytes += pair_device_bytes(h.n, h.m, planes ? 3.0 : 0.0);
-        const char* tsp = getenv("GX_TB_STREAM");
-        const bool split = tsp && !strcmp(tsp, "1") && step_bytes <= 32e9;
-        if (split && !ctx->tstream) HIPCHK(hipStreamCreateWithFlags(&ctx->tstream, hipStreamNonBlocking));
+        // the walk stays on the fill's stream: the fill's buffers return to
+        // the pool right behind it (stream-ordered reuse).  (A walk on its own
+        // stream beside the next step's fill measured 1024 x 4k +6 % but made
+        // 1024 x 1k 2.5x slower: the host's enqueue of the next fill stalled
+        // behind the running walk.)
         auto trace_dev = [&](int s) {
-            if (!split) {
-                int r = run_traceback(ctx, jobs[s], starts, ctx->slots[s].out, s, false, true);
-                job_release(ctx, jobs[s]);   // stream order: later users come after the traceback
-                return r;
-            }
-            HIPCHK(hipStreamWaitEvent(ctx->tstream, ctx->slots[s].fdone, 0));   // (the fill's results are in)
-            return run_traceback(ctx, std::vector<const FillJob*>{&jobs[s]}, starts, ctx->slots[s].out, s, false, true,
-                                 ctx->tstream);
+            int r = run_traceback(ctx, jobs[s], starts, ctx->slots[s].out, s, false, true);
+            job_release(ctx, jobs[s]);   // stream order: later users come after the traceback
+            return r;
         };
         auto results = [&](int s) {
             int r = fill_collect(ctx, jobs[s]);
@@ -2469,7 +2477,6 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
             if ((rc = tb_collect(ctx, s, idx.size(), ctx->slots[s].out))) break;
             h_tbw += since(t); t = clk::now();
             if ((rc = results(s))) break;
-            if (split) job_release(ctx, jobs[s]);   // its walk is done (tb_collect)
             h_res += since(t); t = clk::now();
             if ((rc = label_batch(ctx, ph, hs, is_local, track, dev_of, si, sj, score, res, ctx->slots[s].out,
                                   jobs[s].fill_ms, walks)))

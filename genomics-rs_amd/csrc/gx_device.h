@@ -137,19 +137,6 @@ __device__ __forceinline__ void bstore1(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 #endif
 }
 
-// Per-strip descriptor store: VGPR offset + SGPR soffset + immediate (a
-// group's offset inside the strip's plane), no descriptor SALU per group.
-__device__ __forceinline__ void bstore1_so(__amdgpu_buffer_rsrc_t r, uint32_t voff, int soff, uint32_t imm,
-                                           uint32_t v) {
-#ifndef GX_DIAG_NO_PLANES
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)(voff + imm), soff, GX_PLANE_AUX);
-#endif
-}
-#ifndef GX_D8_STRIPDESC
-#define GX_D8_STRIPDESC 0   // 1: compact planes through one descriptor per strip plane (measured
-                            // 0.8 % slower than one per sub-block, profiles/r01n_d8_desc_ab.txt)
-#endif
-
 // Occupancy floor (waves per SIMD), which sets the fill kernel's VGPR cap
 // (512 / floor, at most 256): one workgroup per CU, so the floor is the
 // workgroup's waves per SIMD.  The variants that also track the maxima
@@ -251,5 +238,57 @@ __device__ __forceinline__ int score_table(int c1, const Scores32& sc) {
     for (int k = 0; k < 4; ++k) t |= ((c1 == sc.sym[k] ? sc.sm : sc.smm) & 0xFF) << (8 * k);
     return t;
 }
+
+// The ring pointers are deliberately NOT __restrict__: another wave writes the
+// ring, and with noalias the compiler may fold the re-read after a wait into
+// the earlier speculative read of the same slots (stale records).
+__device__ __forceinline__ void read4(Rec (&r)[4], const Rec* rin) {
+    r[0] = rin[0]; r[1] = rin[1]; r[2] = rin[2]; r[3] = rin[3];
+}
+
+// record pushes with explicit values (all lanes write: lane 63 to the ring,
+// the others to scratch; or exec-masked to lane 63 in the tail)
+template <int U, bool TRACK>
+__device__ __forceinline__ void cs_push_all(uint32_t vaddr, int dd, int sm, int c2, int l) {
+    if (TRACK)
+        asm volatile(
+            "ds_write2_b32 %0, %1, %2 offset0:%5 offset1:%6\n\t"
+            "ds_write2_b32 %0, %3, %4 offset0:%7 offset1:%8"
+            :
+            : "v"(vaddr), "v"(dd), "v"(sm), "v"(c2), "v"(l), "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2),
+              "i"(4 * U + 3)
+            : "memory");
+    else
+        asm volatile(
+            "ds_write2_b32 %0, %1, %2 offset0:%4 offset1:%5\n\t"
+            "ds_write_b32 %0, %3 offset:%6"
+            :
+            : "v"(vaddr), "v"(dd), "v"(sm), "v"(c2), "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8)
+            : "memory");
+}
+template <int U, bool TRACK>
+__device__ __forceinline__ void cs_push63(uint32_t base, unsigned long long m63, int dd, int sm, int c2, int l) {
+    if (TRACK)
+        asm volatile(
+            "s_mov_b64 exec, %0\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%6 offset1:%7\n\t"
+            "ds_write2_b32 %1, %4, %5 offset0:%8 offset1:%9\n\t"
+            "s_mov_b64 exec, -1"
+            :
+            : "s"(m63), "v"(base), "v"(dd), "v"(sm), "v"(c2), "v"(l), "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2),
+              "i"(4 * U + 3)
+            : "memory");
+    else
+        asm volatile(
+            "s_mov_b64 exec, %0\n\t"
+            "ds_write2_b32 %1, %2, %3 offset0:%5 offset1:%6\n\t"
+            "ds_write_b32 %1, %4 offset:%7\n\t"
+            "s_mov_b64 exec, -1"
+            :
+            : "s"(m63), "v"(base), "v"(dd), "v"(sm), "v"(c2), "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8)
+            : "memory");
+}
+
+constexpr uint32_t kNoStore = 0xFFFFFFF0u;   // past every strip plane's range: the store is dropped
 
 }  // namespace gx

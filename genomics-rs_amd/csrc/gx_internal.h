@@ -45,6 +45,10 @@ constexpr int kTwinGroupBytes = kRowsPerLane * kWave * 4 * 4;
 // the wave (gx_kernels.hip, compute_wave_cs).
 constexpr int kGroupInts1 = kWave * 4;
 constexpr int kStripRows1 = kWave;
+// Layout 3 (gx_skew.hip, the latency fill): 64-row strips like layout 1, lane
+// l owns row 64s + l + 1, but on the anti-diagonal skew like layout 0 (step t
+// = column t - l + 1); planes plane[strip][t/4][lane][t%4], codes
+// codes[strip][t/16][lane], both indexed by step; skeleton E + 64 per column.
 inline int strip_rows(int lay) { return lay ? kStripRows1 : kStripRows; }
 // Compute waves per band (workgroup = W compute waves + 1 I/O wave).  The
 // host picks the narrowest width whose bands fit one workgroup per CU (a
@@ -140,7 +144,8 @@ struct TbDev {           // per-pair traceback job
     int start_i, start_j;  // interior start cell (1-based), or 0 = nothing to walk
     int start_E;           // landing column of the start cell (PairRes.end_E / lmax_E)
     const int* start_E_dev;// or, when non-null, read on the device (the fill's PairRes.end_E: no host round trip)
-    int srows;             // rows per strip: 128 (layout 0, anti-diagonal) or 64 (layout 1, column-step)
+    int srows;             // rows per strip: 128 (layout 0, anti-diagonal) or 64 (layouts 1 and 3)
+    int skew;              // layout 3 (gx_skew.hip): 64-row strips on the anti-diagonal skew, one row per lane
     int skel_half;         // -1: int32 skeleton; 0 / 1: the low / high int16 of a twin fill's packed skeleton
     int* seg;              // out: [strips][4] {entry_i, entry_j, records, active} per strip on the path
     uint32_t* recs;        // out: [strips][kStripRows] one record per row, (insert run << 2) | kind

@@ -30,10 +30,6 @@
 
 namespace gx {
 
-#ifndef GX_D8_PIPE
-#define GX_D8_PIPE 0   // 1: compact plane stores issued during the next group (9..12-wave
-                       // workgroups); measured 2 % slower than storing at the group end
-#endif
 #ifndef GX_FILL_MIN_WAVES_TRACK
 #define GX_FILL_MIN_WAVES_TRACK 2
 #endif
@@ -240,13 +236,6 @@ __device__ __forceinline__ void dp_step(LaneState& st, const Rec& r, const int t
     st.c2c = c2;
 }
 
-// The ring pointers are deliberately NOT __restrict__: another wave writes the
-// ring, and with noalias the compiler may fold the re-read after a wait into
-// the earlier speculative read of the same slots (stale records).
-__device__ __forceinline__ void read4(Rec (&r)[4], const Rec* rin) {
-    r[0] = rin[0]; r[1] = rin[1]; r[2] = rin[2]; r[3] = rin[3];
-}
-
 // Uniform per-strip values of a compute wave, hoisted out of the pair
 // descriptor (which lives in global memory the plane stores could alias).
 struct WaveCtx {
@@ -274,7 +263,6 @@ struct WaveCtx {
 // bytes = 0 (nothing pending) empties the descriptor's range.
 struct PendStore {
     int4 I0, I1, D0, D1, S0, S1, L0, L1;   // rows A/B of each plane
-    uint32_t xI0, xI1, xS0, xS1, xD0, xD1; // compact planes (mode 4): rows A/B, one dword each
     size_t sb_off;                         // the group's sub-block (ints)
     int bytes;
 };
@@ -288,16 +276,6 @@ __device__ __forceinline__ void pend_store(const PendStore& pd, const WaveCtx& w
     const auto r = rsrc_of(base + pd.sb_off, pd.bytes);
     bstore4(r, v0, PLANE == 0 ? pd.I0 : PLANE == 1 ? pd.D0 : PLANE == 2 ? pd.S0 : pd.L0);
     bstore4(r, v1, PLANE == 0 ? pd.I1 : PLANE == 1 ? pd.D1 : PLANE == 2 ? pd.S1 : pd.L1);
-}
-
-// Compact planes, pipelined (mode 4): the previous group's dwords of one plane.
-template <int PLANE, int G4P>
-__device__ __forceinline__ void pend_store_d8(const PendStore& pd, const WaveCtx& w) {
-    const uint32_t v0 = (uint32_t)w.lane * 4u + G4P * kGroupInts, v1 = v0 + kWave * 4;
-    const int32_t* base = PLANE == 0 ? w.pI : PLANE == 1 ? w.pS : w.pD;
-    const auto r = rsrc_of((const uint8_t*)base + pd.sb_off, pd.bytes);
-    bstore1(r, v0, PLANE == 0 ? pd.xI0 : PLANE == 1 ? pd.xS0 : pd.xD0);
-    bstore1(r, v1, PLANE == 0 ? pd.xI1 : PLANE == 1 ? pd.xS1 : pd.xD1);
 }
 
 // One 4-step group of a sub-block.  `nxt` holds validated ring records for
@@ -331,17 +309,14 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
         dp_step<LOCAL, true, CODES, TRACK, TBL>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
         skel_store(w.skel_rsrc, sko(col0 + 1), st.b.E);   // lane 63's column after the step
         if (PLANES == 2) pend_store<LCSP, 0, G4P>(pend, w);
-        if (PLANES == 4) pend_store_d8<0, G4P>(pend, w);
         push63<4 * G4 + 1, TRACK>(out_base, st, lane63_mask(push_on && col0 + 1 >= 0 && col0 + 1 <= w.m));
         dp_step<LOCAL, true, CODES, TRACK, TBL>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
         skel_store(w.skel_rsrc, sko(col0 + 2), st.b.E);   // lane 63's column after the step
         if (PLANES == 2) pend_store<LCSP, 1, G4P>(pend, w);
-        if (PLANES == 4) pend_store_d8<1, G4P>(pend, w);
         push63<4 * G4 + 2, TRACK>(out_base, st, lane63_mask(push_on && col0 + 2 >= 0 && col0 + 2 <= w.m));
         dp_step<LOCAL, true, CODES, TRACK, TBL>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
         skel_store(w.skel_rsrc, sko(col0 + 3), st.b.E);   // lane 63's column after the step
         if (PLANES == 2) pend_store<LCSP, 2, G4P>(pend, w);
-        if (PLANES == 4) pend_store_d8<2, G4P>(pend, w);
         if (PLANES == 2 && LCSP) pend_store<LCSP, 3, G4P>(pend, w);
         push63<4 * G4 + 3, TRACK>(out_base, st, lane63_mask(push_on && col0 + 3 >= 0 && col0 + 3 <= w.m));
         // publish the pushes (same wave, DS operations in order)
@@ -354,17 +329,14 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
         push_all<4 * G4 + 0, TRACK>(pa, st);
         dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[0], t + 0, w.lane, w.m, w.c1a, w.c1b, sc, bI[0], bD[0], bS[0], bL[0]);
         if (PLANES == 2) pend_store<LCSP, 0, G4P>(pend, w);
-        if (PLANES == 4) pend_store_d8<0, G4P>(pend, w);
         const int e0 = st.b.E;              // lane 63: column col0 + 1
         push_all<4 * G4 + 1, TRACK>(pa, st);
         dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[1], t + 1, w.lane, w.m, w.c1a, w.c1b, sc, bI[1], bD[1], bS[1], bL[1]);
         if (PLANES == 2) pend_store<LCSP, 1, G4P>(pend, w);
-        if (PLANES == 4) pend_store_d8<1, G4P>(pend, w);
         const int e1 = st.b.E;
         push_all<4 * G4 + 2, TRACK>(pa, st);
         dp_step<LOCAL, false, CODES, TRACK, TBL>(st, cur[2], t + 2, w.lane, w.m, w.c1a, w.c1b, sc, bI[2], bD[2], bS[2], bL[2]);
         if (PLANES == 2) pend_store<LCSP, 2, G4P>(pend, w);
-        if (PLANES == 4) pend_store_d8<2, G4P>(pend, w);
         if (PLANES == 2 && LCSP) pend_store<LCSP, 3, G4P>(pend, w);
         const int e2 = st.b.E;
         push_all<4 * G4 + 3, TRACK>(pa, st);
@@ -393,10 +365,11 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
             bstore4(rL, v1, make_int4(bL[0][1], bL[1][1], bL[2][1], bL[3][1]));
         }
     }
-    if (PLANES == 3 || PLANES == 4) {
+    if (PLANES == 3) {
         // compact planes: this group's 4 steps of a row are one dword per lane
-        // and plane (x_I, x_S, x_D above put_byte), 256 B per wave; mode 3
-        // stores them now, mode 4 during the next group
+        // and plane (x_I, x_S, x_D above put_byte), 256 B per wave, stored
+        // at the group's end (storing them during the next group measured 2 %
+        // slower, profiles/r01k_d8_pipe_ab.txt)
         uint32_t xI[2], xS[2], xD[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -408,26 +381,11 @@ __device__ __forceinline__ void group4(LaneState& st, Rec (&nxt)[4], WaveCtx& w,
         constexpr int kSubBytes = kSub / 4 * kGroupInts;              // one sub-block of one byte plane
         constexpr uint32_t kG = G4 * kGroupInts;
         const uint32_t v0 = (uint32_t)w.lane * 4u + kG, v1 = v0 + kWave * 4;
-        if (PLANES == 3 && GX_D8_STRIPDESC) {
-            const int so = __builtin_amdgcn_readfirstlane((int)sb_off);
-            bstore1_so(w.rI, (uint32_t)w.lane * 4u, so, kG, xI[0]);
-            bstore1_so(w.rS, (uint32_t)w.lane * 4u, so, kG, xS[0]);
-            bstore1_so(w.rD, (uint32_t)w.lane * 4u, so, kG, xD[0]);
-            bstore1_so(w.rI, (uint32_t)w.lane * 4u, so, kG + kWave * 4, xI[1]);
-            bstore1_so(w.rS, (uint32_t)w.lane * 4u, so, kG + kWave * 4, xS[1]);
-            bstore1_so(w.rD, (uint32_t)w.lane * 4u, so, kG + kWave * 4, xD[1]);
-        } else if (PLANES == 3) {
-            const auto rI = rsrc_of((const uint8_t*)w.pI + sb_off, kSubBytes),
-                       rD = rsrc_of((const uint8_t*)w.pD + sb_off, kSubBytes),
-                       rS = rsrc_of((const uint8_t*)w.pS + sb_off, kSubBytes);
-            bstore1(rI, v0, xI[0]); bstore1(rS, v0, xS[0]); bstore1(rD, v0, xD[0]);
-            bstore1(rI, v1, xI[1]); bstore1(rS, v1, xS[1]); bstore1(rD, v1, xD[1]);
-        } else {
-            (void)v0; (void)v1;
-            pend.xI0 = xI[0]; pend.xI1 = xI[1]; pend.xS0 = xS[0]; pend.xS1 = xS[1]; pend.xD0 = xD[0]; pend.xD1 = xD[1];
-            pend.sb_off = sb_off;
-            pend.bytes = kSubBytes;
-        }
+        const auto rI = rsrc_of((const uint8_t*)w.pI + sb_off, kSubBytes),
+                   rD = rsrc_of((const uint8_t*)w.pD + sb_off, kSubBytes),
+                   rS = rsrc_of((const uint8_t*)w.pS + sb_off, kSubBytes);
+        bstore1(rI, v0, xI[0]); bstore1(rS, v0, xS[0]); bstore1(rD, v0, xD[0]);
+        bstore1(rI, v1, xI[1]); bstore1(rS, v1, xS[1]); bstore1(rD, v1, xD[1]);
     }
     if (PLANES == 2) {
         // this group's cells: 16 B per lane per row and plane, stored during the next group
@@ -506,14 +464,6 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         w.pS = PLANES ? at(P.pS) : nullptr;
         w.pL = LCSP ? P.pL + strip_planes : nullptr;
         w.codes = CODES ? P.codes + (size_t)s * P.t16 * kWave * kRowsPerLane : nullptr;
-        if (PLANES == 3 && GX_D8_STRIPDESC) {
-            // compact planes: one descriptor per plane over the strip's whole
-            // plane, built once; a group's offset rides in soffset + imm
-            const int pbytes = P.t4 * kGroupInts;
-            w.rI = rsrc_of(uniform_ptr(w.pI), pbytes);
-            w.rD = rsrc_of(uniform_ptr(w.pD), pbytes);
-            w.rS = rsrc_of(uniform_ptr(w.pS), pbytes);
-        }
     }
     w.ring_in = ring_in; w.ring_out = ring_out; w.wcnt_in = wcnt_in; w.wcnt_out = wcnt_out; w.status = status;
     // skeleton row (only stored when there is a strip below: otherwise an empty range)
@@ -597,11 +547,6 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         lds_store_lane0(rcnt_in, min(t0 + kSub + 5, m + 1));
     }
 
-    if (PLANES == 4) {   // the last group's compact planes
-        pend_store_d8<0, 3>(pend, w);
-        pend_store_d8<1, 3>(pend, w);
-        pend_store_d8<2, 3>(pend, w);
-    }
     if (PLANES == 2) {   // the last group's planes (group 3 of the last sub-block)
         pend_store<LCSP, 0, 3>(pend, w);
         pend_store<LCSP, 1, 3>(pend, w);
@@ -774,54 +719,10 @@ __device__ __forceinline__ void cs_step(CsState& st, const CsConst& k, const Rec
     oI = In; oD = Dn; oS = Sn;
 }
 
-// record pushes with explicit values (all lanes write: lane 63 to the ring,
-// the others to scratch; or exec-masked to lane 63 in the tail)
-template <int U, bool TRACK>
-__device__ __forceinline__ void cs_push_all(uint32_t vaddr, int dd, int sm, int c2, int l) {
-    if (TRACK)
-        asm volatile(
-            "ds_write2_b32 %0, %1, %2 offset0:%5 offset1:%6\n\t"
-            "ds_write2_b32 %0, %3, %4 offset0:%7 offset1:%8"
-            :
-            : "v"(vaddr), "v"(dd), "v"(sm), "v"(c2), "v"(l), "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2),
-              "i"(4 * U + 3)
-            : "memory");
-    else
-        asm volatile(
-            "ds_write2_b32 %0, %1, %2 offset0:%4 offset1:%5\n\t"
-            "ds_write_b32 %0, %3 offset:%6"
-            :
-            : "v"(vaddr), "v"(dd), "v"(sm), "v"(c2), "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8)
-            : "memory");
-}
-template <int U, bool TRACK>
-__device__ __forceinline__ void cs_push63(uint32_t base, unsigned long long m63, int dd, int sm, int c2, int l) {
-    if (TRACK)
-        asm volatile(
-            "s_mov_b64 exec, %0\n\t"
-            "ds_write2_b32 %1, %2, %3 offset0:%6 offset1:%7\n\t"
-            "ds_write2_b32 %1, %4, %5 offset0:%8 offset1:%9\n\t"
-            "s_mov_b64 exec, -1"
-            :
-            : "s"(m63), "v"(base), "v"(dd), "v"(sm), "v"(c2), "v"(l), "i"(4 * U), "i"(4 * U + 1), "i"(4 * U + 2),
-              "i"(4 * U + 3)
-            : "memory");
-    else
-        asm volatile(
-            "s_mov_b64 exec, %0\n\t"
-            "ds_write2_b32 %1, %2, %3 offset0:%5 offset1:%6\n\t"
-            "ds_write_b32 %1, %4 offset:%7\n\t"
-            "s_mov_b64 exec, -1"
-            :
-            : "s"(m63), "v"(base), "v"(dd), "v"(sm), "v"(c2), "i"(4 * U), "i"(4 * U + 1), "i"(16 * U + 8)
-            : "memory");
-}
-
 struct CsPend {
     int4 I, D, S, L;   // the previous group's cells (one row per lane)
     uint32_t voff;     // this lane's byte offset in the strip plane; kNoStore: nothing pending
 };
-constexpr uint32_t kNoStore = 0xFFFFFFF0u;   // past every strip plane's range: the store is dropped
 
 template <bool LCSP>
 __device__ __forceinline__ void cs_pend_store(const CsPend& pd, const WaveCtx& w, int plane) {
@@ -1081,7 +982,7 @@ __global__ __launch_bounds__((W + 1) * kWave, (LOCAL || TRACK) ? GX_FILL_MIN_WAV
                 // plane stores pipelined one group late, except in 16-wave
                 // workgroups (128 VGPRs: no room for a group of pending cells)
                 if constexpr (LAY == 0)
-                    compute_wave<LOCAL, PLANES == 2 ? (GX_D8_PIPE && (W + 1) <= 12 ? 4 : 3) : PLANES ? ((W + 1) <= 12 ? 2 : 1) : 0, CODES, TRACK, LCSP, TBL>(
+                    compute_wave<LOCAL, PLANES == 2 ? 3 : PLANES ? ((W + 1) <= 12 ? 2 : 1) : 0, CODES, TRACK, LCSP, TBL>(
                         P, s, lane, sc, rings[wave], rings[wave + 1], (lds_int*)&wcnt[wave], (lds_int*)&rcnt[wave],
                         (lds_int*)&wcnt[wave + 1], (lds_int*)&rcnt[wave + 1], has_consumer, sres, pres + p,
                         band_counter + 1, lds_addr(push_scratch[wave]));
@@ -1196,7 +1097,9 @@ __device__ __forceinline__ size_t tb_word(const TbDev& J, int s, int q, int rho)
 __device__ __forceinline__ int tb_rho(const TbDev& J, int vb, int lane) {
     return J.srows == kStripRows ? ((vb & 1) << 6) + lane : lane;
 }
-__device__ __forceinline__ int tb_lot(const TbDev& J, int rho) { return J.srows == kStripRows ? rho >> 1 : 0; }
+__device__ __forceinline__ int tb_lot(const TbDev& J, int rho) {
+    return J.srows == kStripRows ? rho >> 1 : J.skew ? rho : 0;   // layout 3: one row per lane, skewed
+}
 __device__ __forceinline__ int tb_strip_of(const TbDev& J, int vb) { return J.srows == kStripRows ? vb >> 1 : vb; }
 
 // async: words q0 .. q0+kTbWin-1 of block vb (rows 64*vb .. +63), lane = row -> buf[k][lane]
@@ -1229,8 +1132,8 @@ __global__ void tb_chase_kernel(const TbDev* __restrict__ jobs) {
             J.seg[4 * s + 0] = (s + 1) * SR; J.seg[4 * s + 1] = E; J.seg[4 * s + 3] = 1;
             E = ((gcint*)J.skel)[(size_t)s * J.skel_stride + E];
             if (J.skel_half >= 0) E = (int)(short)((unsigned)E >> (16 * J.skel_half));   // twin fill (gx_fill_pk.hip)
-            if (SR == kStripRows1) E = (E & 0xFFFFFF) - 64;        // layout 1 stores E + 64 (the split column step
-                                                                   // keeps the key's lane field above it)
+            if (SR == kStripRows1) E = (E & 0xFFFFFF) - 64;        // layouts 1 and 3 store E + 64 (the split column
+                                                                   // step keeps the key's lane field above it)
         }
     }
     J.end_ij[0] = i; J.end_ij[1] = j; J.end_ij[2] = first;
@@ -1567,7 +1470,7 @@ __global__ __launch_bounds__(64) void plane_sums_kernel(const PairDev* __restric
     const int hh = lay ? 0 : (int)(blockIdx.x & 1);     // layout 0: row-in-lane of this block
     if (s >= d.strips || !d.pI) return;
     const int i = lay ? s * SR + lane + 1 : s * SR + 2 * lane + hh + 1;
-    const int l = lay ? 0 : lane;                       // step of column 1 on this row
+    const int l = lay == 1 ? 0 : lane;                  // step of column 1 on this row (layouts 0 and 3: the skew)
     const bool row_ok = i <= d.n;
     unsigned long long sI = 0, sD = 0, sS = 0;
     const unsigned long long wi = 1ull + (unsigned long long)i * 0x9E3779B1ull;
@@ -1670,7 +1573,8 @@ __global__ void export_kernel(const int32_t* __restrict__ plane, int32_t* __rest
         const int l = rho >> 1, h = rho & 1, t = j - 1 + l;
         o = ((size_t)s * t4 + (t >> 2)) * kGroupInts + h * kWave * 4 + l * 4 + (t & 3);
     } else {
-        const int s = (i - 1) / kStripRows1, l = (i - 1) % kStripRows1, t = j - 1;
+        // layout 1: step t = j - 1; layout 3: the skew, t = j - 1 + l
+        const int s = (i - 1) / kStripRows1, l = (i - 1) % kStripRows1, t = j - 1 + (lay == 3 ? l : 0);
         o = ((size_t)s * t4 + (t >> 2)) * kGroupInts1 + l * 4 + (t & 3);
     }
     out[(size_t)(i - row0) * (m + 1) + j] = plane[o] + (i + j) * gshift;   // shifted fills: V - (i + j) g

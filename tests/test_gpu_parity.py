@@ -7,10 +7,10 @@ reverse_sequences, batched pairs, and the large pairs of BASELINE configs 2
 and 3 through digests.  Every test runs under each fill launch shape: the
 automatic band width, forced 7-strip (tracked variants) and 8-strip bands,
 and 15-strip bands on a 2-workgroup grid (bands wait in the queue for a
-workgroup, hand-offs cross launch order), the pair-major band queue on a
-3-workgroup grid, for both fill layouts (0: the
+workgroup, hand-offs cross launch order), for the three fill layouts (0: the
 anti-diagonal sweep of 128-row strips; 1: the column step over 64-row
-strips) and the automatic layout choice.
+strips; 3: the anti-diagonal sweep of 64-row strips, one row per lane) and
+the automatic layout choice.
 """
 import hashlib
 import json
@@ -29,8 +29,10 @@ LAUNCH_SHAPES = {"auto": {},
                  "lay0": {"GX_LAYOUT": "0"}, "w7": {"GX_LAYOUT": "0", "GX_BAND_WAVES": "7"},
                  "w8": {"GX_LAYOUT": "0", "GX_BAND_WAVES": "8"},
                  "w15_grid2": {"GX_LAYOUT": "0", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "2"},
-                 # the pair-major band queue of earlier versions (the default is band-major)
-                 "pair_order": {"GX_LAYOUT": "0", "GX_BAND_ORDER": "pair", "GX_FILL_GRID": "3"},
+                 # layout 3: the skewed 64-row strips (gx_skew.hip, the default for untracked
+                 # single pairs), two-strip bands queued for one workgroup (every hand-off through HBM)
+                 "skew": {"GX_LAYOUT": "3"},
+                 "skew_w2_grid1": {"GX_LAYOUT": "3", "GX_BAND_WAVES": "2", "GX_FILL_GRID": "1"},
                  # layout 1: column-step fill over 64-row strips (gx_internal.h), as
                  # the split core + side waves (gx_cs2.hip, GX_CS2=1; the default for
                  # local fills); one-band bands queued on a 2-workgroup grid (every

@@ -200,14 +200,15 @@ def test_twin_random_batches(gx, ctx, oracle, monkeypatch, seed):
 @pytest.mark.parametrize("skel", ["noskel", "skel"])
 @pytest.mark.parametrize("m", [31920, 31921, 65536])
 def test_twin_column_limit(gx, ctx, oracle, monkeypatch, m, skel):
-    """With a skeleton the twin fill's landing columns are int16 halves: twins
-    up to 31,920 columns, the scalar fill beyond.  Without one (the default
-    with twin plane codes: no landing columns, the traceback walks the strips
-    in sequence) the twin fill has no column limit: 65,536 columns.  Every
-    pair checked against the oracle (plane checksums, score, alignment)."""
+    """With a skeleton (the per-pair byte planes, GX_PLANES_W16=0, keep code
+    words and landing columns) the twin fill's landing columns are int16
+    halves: twins up to 31,920 columns, the scalar fill beyond.  Without one
+    (twin plane codes: no landing columns, the traceback walks the strips in
+    sequence) the twin fill has no column limit: 65,536 columns.  Every pair
+    checked against the oracle (plane checksums, score, alignment)."""
     monkeypatch.setenv("GX_LAYOUT", "0")
     if skel == "skel":
-        monkeypatch.setenv("GX_TWIN_SKEL", "1")
+        monkeypatch.setenv("GX_PLANES_W16", "0")
     rng = random.Random(m)
     shapes = [(200, m), (150, m - 7), (260, m - 1)]
     pairs = [(bytes(rng.choice(b"ACGT") for _ in range(n)), bytes(rng.choice(b"ACGT") for _ in range(mm)))
