@@ -609,16 +609,15 @@ static bool cs2_enabled(int is_local, const Scores32& sc) {
     if (e && *e) return strcmp(e, "0") != 0;
     return is_local != 0;
 }
-// Layout 3 (gx_skew.hip): 4-strip bands, one compute wave per SIMD (a
-// strip's step is one wave's VALU issue); GX_BAND_WAVES picks another
-// instantiated width (must match gx_skew.hip launch_fill_skew).
+// Layout 3 (gx_skew.hip): 2-strip bands, each strip's core and side wave on
+// SIMDs of their own; GX_BAND_WAVES picks another instantiated width (1-4;
+// must match gx_skew.hip launch_fill_skew).
 static int skew_band_waves() {
-    static constexpr int kSkewWidths[] = {2, 3, 4, 8};
     if (const char* e = getenv("GX_BAND_WAVES")) {
         const int w = atoi(e);
-        for (int x : kSkewWidths) if (x == w) return w;
+        if (w >= 1 && w <= 4) return w;
     }
-    return 4;
+    return 2;
 }
 static int cs2_band_waves(int total_strips, int grid_cap) {
     static constexpr int kCs2Widths[] = {1, 2, 3, 4, 7};

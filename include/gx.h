@@ -211,7 +211,9 @@ int gx_staged_steps(const gx_context* ctx, size_t pair, gx_step* steps, size_t c
  * that each timed pass can be checked, not only the last.  Verification only. */
 int gx_staged_pass_results(const gx_context* ctx, gx_result* out, size_t cap, size_t* n_values);
 /* The last fill launch on ctx: its layout (0: anti-diagonal 128-row strips,
- * 1: column step over 64-row strips), band width (strips per workgroup) and
+ * 1: column step over 64-row strips, 2: the same as core + side waves,
+ * 3: anti-diagonal 64-row strips with one row per lane, the latency fill of
+ * untracked single pairs), band width (strips per workgroup) and
  * score-plane bytes written per cell (0: none, 12: int32 planes, 3: compact
  * planes -- per-cell byte differences, decoded exactly by the exports, 2:
  * the twin fill's plane codes -- the three differences in one 16-bit word,
@@ -240,12 +242,15 @@ int gx_fill_groups(const gx_context* ctx);
  * launch's own figure). */
 int gx_plane_bytes_per_cell(const gx_scores* scores, int is_local);
 
-/* The twin fill's int16 admission rule: *bound receives the
- * largest |value - base| a band of `band_waves` strips can reach with these
- * scores when a twin's two pairs differ by up to col_gap columns; returns 1
- * when the twin fill admits the band (bound < 30,000 < 2^15), 0 when it does
- * not, -1 on invalid scores.  Diagnostic (tests/test_twin_bound.py checks the
- * rule against brute-force spreads).  No reference counterpart. */
+/* The twin fill's int16 admission rule for global batches:
+ * *bound receives the largest |value - base| a band of `band_waves` strips can
+ * reach with these scores when a twin's two pairs differ by up to col_gap
+ * columns; returns 1 when the global twin fill admits the band (bound <
+ * 30,000 < 2^15), 0 when it does not, -1 on invalid scores.  (Local batches
+ * have their own rule, DESIGN.md 6.7: plain values on base 0, admitted while
+ * min(n, m) max(s_match, 0) plus constants stays below 32,000.)  Diagnostic
+ * (tests/test_twin_bound.py checks the rule against brute-force spreads).
+ * No reference counterpart. */
 int gx_twin_admission(const gx_scores* scores, int band_waves, int64_t col_gap, int64_t* bound);
 
 /* ---- sequence.rs / config.rs mirrors ----------------------------------- */

@@ -32,7 +32,7 @@ LAUNCH_SHAPES = {"auto": {},
                  # layout 3: the skewed 64-row strips (gx_skew.hip, the default for untracked
                  # single pairs), two-strip bands queued for one workgroup (every hand-off through HBM)
                  "skew": {"GX_LAYOUT": "3"},
-                 "skew_w2_grid1": {"GX_LAYOUT": "3", "GX_BAND_WAVES": "2", "GX_FILL_GRID": "1"},
+                 "skew_w1_grid1": {"GX_LAYOUT": "3", "GX_BAND_WAVES": "1", "GX_FILL_GRID": "1"},
                  # layout 1: column-step fill over 64-row strips (gx_internal.h), as
                  # the split core + side waves (gx_cs2.hip, GX_CS2=1; the default for
                  # local fills); one-band bands queued on a 2-workgroup grid (every

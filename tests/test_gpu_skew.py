@@ -18,10 +18,10 @@ from conftest import CONFIG_SCORES, TEST_SCORES
 pytestmark = pytest.mark.gpu
 
 NAMES = ["Match", "Mismatch", "Insert", "Delete", "OpenInsert", "OpenDelete"]
-LAUNCH = {"w4": {"GX_LAYOUT": "3"},
+LAUNCH = {"w2": {"GX_LAYOUT": "3"}, "w4": {"GX_LAYOUT": "3", "GX_BAND_WAVES": "4"},
           "w2_grid1": {"GX_LAYOUT": "3", "GX_BAND_WAVES": "2", "GX_FILL_GRID": "1"},
           "w3_grid2": {"GX_LAYOUT": "3", "GX_BAND_WAVES": "3", "GX_FILL_GRID": "2"},
-          "w8": {"GX_LAYOUT": "3", "GX_BAND_WAVES": "8"}}
+          "w1_grid1": {"GX_LAYOUT": "3", "GX_BAND_WAVES": "1", "GX_FILL_GRID": "1"}}
 SIZES = [(1, 1), (1, 7), (7, 1), (2, 70), (63, 64), (64, 63), (64, 64), (65, 65), (127, 3), (3, 127), (128, 128),
          (129, 200), (255, 40), (256, 257), (257, 256), (300, 17), (17, 300), (513, 70), (640, 641), (1000, 1300)]
 

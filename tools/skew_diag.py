@@ -33,8 +33,10 @@ def summarize(path, m, W):
           f"(min {min(dur) * 1e3 / steps:.1f}, max {max(dur) * 1e3 / steps:.1f}); "
           f"lag intra {statistics.mean(intra):.2f} us = {statistics.mean(intra) * 1e3 / (statistics.mean(dur) * 1e3 / steps):.0f} steps, "
           f"inter {statistics.mean(inter):.2f} us; clock {statistics.mean(clk):.0f} MHz; "
-          f"wait_in {statistics.mean(int(r['wait_in']) for r in rows):.0f} wait_out "
-          f"{statistics.mean(int(r['wait_out']) for r in rows):.0f}; last strip first input at {first[-1]:.0f} us, "
+          f"core waits: input {statistics.mean(int(r['wait_in']) for r in rows):.0f} hand-off space "
+          f"{statistics.mean(int(r['q6']) for r in rows):.0f}; side waits {statistics.mean(int(r['wait_out']) for r in rows):.0f}, "
+          f"side ends {statistics.mean(us(r['q7']) - us(r['t_end']) for r in rows):.1f} us after the core; "
+          f"last strip first input at {first[-1]:.0f} us, "
           f"end {max(us(r['t_end']) for r in rows):.0f} us")
 
 

@@ -15,7 +15,7 @@ oracle.build()
 oracle.load()
 ctx = gx.Context(0)
 sc = (1, -2, -1, -5)
-for W in sys.argv[1:] or ["8"]:
+for W in sys.argv[1:] or ["2"]:
     os.environ["GX_LAYOUT"] = "3"
     os.environ["GX_BAND_WAVES"] = W
     for is_local in (False, True):
