@@ -46,6 +46,7 @@ hipError_t launch_fill_cs2(int W, bool local, bool planes, bool tbl, const PairD
 hipError_t launch_fill_skew(int W, bool local, bool planes, bool tbl, const PairDev* d_pairs, int npairs,
                             int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                             hipStream_t st);
+hipError_t launch_skew_codes(const PairDev* d_pairs, int npairs, int mmax, Scores32 sc, bool tbl, hipStream_t st);
 hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int npairs, int ntwins, int total_bands,
                           int* d_counter, PairRes* d_pres, StripRes* d_sres, Scores32 sc, int grid, hipStream_t st);
 hipError_t launch_fill_wide(const WideDev* d_pairs, int npairs, WideScores sc, WideRes* d_res, int local, int track,
@@ -673,7 +674,7 @@ static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int 
 
 struct FillJob {
     // device buffers (owned by the job until released)
-    DevBuf chars, planes, codes, skel, feed, progress, sres, pres, pairs, counter;
+    DevBuf chars, planes, codes, skel, feed, progress, sres, pres, pairs, counter, ccodes;
     std::vector<PairDev> pd;
     std::vector<PairRes> res;
     int W = 4;
@@ -712,7 +713,7 @@ static void unshift_results(FillJob& j) {
 static void job_release(gx_context* ctx, FillJob& j) {
     pool_put(ctx, j.chars); pool_put(ctx, j.planes); pool_put(ctx, j.codes); pool_put(ctx, j.feed);
     pool_put(ctx, j.progress); pool_put(ctx, j.sres); pool_put(ctx, j.pres); pool_put(ctx, j.pairs);
-    pool_put(ctx, j.counter); pool_put(ctx, j.skel);
+    pool_put(ctx, j.counter); pool_put(ctx, j.skel); pool_put(ctx, j.ccodes);
     pool_put(ctx, j.wrows); pool_put(ctx, j.wdesc); pool_put(ctx, j.wres_d);
 }
 
@@ -1058,6 +1059,14 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         d.feed = (Rec*)job.feed.p + fo[p];
         d.progress = (int*)job.progress.p + gofs[p];
     }
+    // layout 3 reads each lane's column symbols from an int32 copy (gx_skew.hip)
+    if (lay == 3) {
+        size_t cc = 0;
+        for (size_t p = 0; p < P; ++p) cc += (size_t)job.pd[p].m + 192;
+        if ((rc = pool_get(ctx, cc * sizeof(int), &job.ccodes))) return rc;
+        cc = 0;
+        for (size_t p = 0; p < P; ++p) { job.pd[p].ccodes = (const int*)job.ccodes.p + cc; cc += (size_t)job.pd[p].m + 192; }
+    }
     const char* trace_file = slot < 0 ? getenv("GX_TRACE_FILE") : nullptr;
     DevBuf trace;
     if (trace_file && *trace_file) {
@@ -1086,6 +1095,11 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                 lay, Wf, twin ? 1 : 0, ctx->last_pbytes, (twin ? twin_tbl : tbl) ? 1 : 0, grid, bands);
     const auto h_launch = std::chrono::steady_clock::now();
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].fb : ctx->ev0, eve = slot >= 0 ? ctx->slots[slot].fe : ctx->ev1;
+    if (bands > 0 && lay == 3) {   // the column symbols as int32 for layout 3's lanes (before the timed fill)
+        int mmax = 0;
+        for (size_t p = 0; p < P; ++p) mmax = std::max(mmax, job.pd[p].m);
+        HIPCHK(launch_skew_codes((const PairDev*)job.pairs.p, (int)P, mmax, scl, tbl, fs));
+    }
     HIPCHK(hipEventRecord(evb, fs));
     if (bands > 0 && twin)
         HIPCHK(launch_fill_pk(Wf, (planes ? (w16 ? 2 : 1) : 0) + (twin_tbl ? 4 : 0) + (job.nocodes ? 8 : 0) +

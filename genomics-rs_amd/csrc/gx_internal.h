@@ -133,6 +133,8 @@ struct __attribute__((aligned(16))) PairDev {   // 16-B multiple: the pinned sta
     int feed_stride;
     int skel_stride;
     int twin_half;       // twin fill: this pair's 16-bit half (0 low, 1 high) in its twin's shared buffers
+    const int* ccodes;   // layout 3: the column symbols as int32 (code * 8 with score tables), 64 zeros
+                         // before and after (index j - 1 + 64 for column j; gx_skew.hip)
 };
 static_assert(sizeof(PairDev) % 16 == 0, "PairDev staging keeps the PairRes that follow it 16-B aligned");
 

@@ -38,10 +38,12 @@
 // "insert beats sub"), and each strip's bottom-row landing columns + 64 as the
 // skeleton, so the traceback chases it and walks all strips at once
 // (gx_kernels.hip tb_chase_kernel / tb_strip_kernel, TbDev.skew).
-// Strip-to-strip rings hold 4-column groups in SoA form (dd[4], sm[4], c2[4]
-// of columns 4G-3 .. 4G, column c in group (c + 3) / 4): the core wave of the
-// strip above pushes a group as three ds_write_b128 from lane 63 and the core
-// below reads it as three ds_read_b128.
+// Strip-to-strip rings hold 4-column groups in SoA form (dd[4], sm[4] of
+// columns 4G-3 .. 4G, column c in group (c + 3) / 4): the core wave of the
+// strip above pushes a group as two ds_write_b128 from lane 63 and the core
+// below reads it as two ds_read_b128.  Each lane reads its own column symbols
+// (one dwordx4 per group, prefetched four groups ahead) from an int32 copy of
+// s2 (skew_codes_kernel), so no symbol moves between lanes.
 // No MFMA: an integer max-plus recurrence.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -58,7 +60,6 @@ constexpr int kSkHo = 8;         // core -> side hand-off ring depth (4-step gro
 struct SkRing {                  // one strip boundary (see the file header)
     int dd[kSkRingG][4];
     int sm[kSkRingG][4];
-    int c2[kSkRingG][4];
 };
 struct SkHo {                    // one strip's core -> side ring: [group][plane I, S, D][lane] int4
     int4 v[kSkHo][3][kWave];
@@ -74,19 +75,17 @@ struct CoreState {               // cell (i, j-1) of the lane's row
     int Hx;                      // H + h (global) / H + h + g (local): the next insert's and delete's gap term
     int H;                       // score_max
     int Dd;                      // delete successor D(i+1, j-1)
-    int c2;                      // column symbol (moved to the row below with the cell)
     int Hd;                      // score_max(i-1, j-1)
 };
 
-// One anti-diagonal step: cell (i, j), j = t - lane + 1.  (rdd, rsm, rc2) =
-// lane 0's cell above from the ring.  MASKED (ramp-down): act = false keeps
-// the row at its last column.
+// One anti-diagonal step: cell (i, j), j = t - lane + 1.  (rdd, rsm) = lane
+// 0's cell above from the ring; c2 = s2[j-1] (its symbol code * 8 with score
+// tables).  MASKED (ramp-down): act = false keeps the row at its last column.
 template <bool LOCAL, bool TBL, bool MASKED>
-__device__ __forceinline__ void core_step(CoreState& st, const int rdd, const int rsm, const int rc2, const bool act,
+__device__ __forceinline__ void core_step(CoreState& st, const int rdd, const int rsm, const int c2, const bool act,
                                           const int c1v, const Scores32& sc, int& oI, int& oS, int& oD) {
     const int Dn = shr1(rdd, st.Dd);         // D(i, j): the delete successor of the cell above
     const int hu = shr1(rsm, st.H);          // score_max(i-1, j)
-    const int c2 = shr1(rc2, st.c2);         // s2[j-1] (or its symbol code * 8, TBL)
     const bool mt = c2 == c1v;               // sequence.rs:113-114
     const int Sn = st.Hd + (TBL ? __builtin_amdgcn_sbfe(c1v, c2, 8) : (mt ? sc.sm : sc.smm));
     const int In = LOCAL ? max3i(st.I + sc.g, st.Hx, 0) : max(st.I, st.Hx);
@@ -96,15 +95,17 @@ __device__ __forceinline__ void core_step(CoreState& st, const int rdd, const in
     const int Ddn = LOCAL ? max3i(Dn + sc.g, Hxn, 0) : max(Dn, Hxn);
     if (MASKED) {
         st.I = act ? In : st.I; st.Hx = act ? Hxn : st.Hx; st.H = act ? Hn : st.H; st.Dd = act ? Ddn : st.Dd;
-        st.c2 = act ? c2 : st.c2;
     } else {
-        st.I = In; st.Hx = Hxn; st.H = Hn; st.Dd = Ddn; st.c2 = c2;
+        st.I = In; st.Hx = Hxn; st.H = Hn; st.Dd = Ddn;
     }
     st.Hd = hu;
     oI = In; oS = Sn; oD = Dn;
 }
 
 struct CoreCtx {
+    __amdgpu_buffer_rsrc_t crs;  // the pair's int32 column symbols (PairDev.ccodes)
+    uint32_t cvoff;              // 4 (64 - lane): this lane's column of step 0, less one
+    uint32_t cnt_addr;           // wcnt_out (LDS address) for the push
     const SkRing* rin;
     SkRing* rout;
     lds_int* wcnt_in;            // columns the strip above published
@@ -120,36 +121,42 @@ struct CoreCtx {
     unsigned tr_win, tr_ho;      // (diagnostics: spins waiting for the strip above / for hand-off space)
 };
 
-__device__ __forceinline__ void read_grp(int4 (&r)[3], const SkRing* ring, int G) {
+__device__ __forceinline__ void read_grp(int4 (&r)[2], const SkRing* ring, int G) {
     r[0] = *(const int4*)ring->dd[G];
     r[1] = *(const int4*)ring->sm[G];
-    r[2] = *(const int4*)ring->c2[G];
 }
+// This lane's column symbols of steps t .. t+3 (columns t-lane+1 ..).
+__device__ __forceinline__ int4 load_codes(const CoreCtx& w, int t) {
+    const v4i x = __builtin_amdgcn_raw_buffer_load_b128(w.crs, (int)w.cvoff, __builtin_amdgcn_readfirstlane(4 * t), 0);
+    return make_int4(x[0], x[1], x[2], x[3]);
+}
+typedef int v4ia __attribute__((ext_vector_type(4)));
 
 // One 4-step group of the core wave.  MODE 0: full; 1: ramp-up (lanes past
 // the step not started yet: each step under `lane <= t`, so their column-0
 // state stays); 2: ramp-down (lanes past column m keep their state).
 template <bool LOCAL, bool TBL, int MODE>
-__device__ __forceinline__ void core_group(CoreState& st, const int4 (&cur)[3], int4 (&nxt)[3], CoreCtx& w,
+__device__ __forceinline__ void core_group(CoreState& st, const int4 (&cur)[2], int4 (&nxt)[2], int4& cc, CoreCtx& w,
                                            const Scores32& sc, const int t) {
     const int need = min(t + 8, w.m) + 1;                      // columns of the next group: t+5 .. t+8
     const int seen_v = *w.wcnt_in;
     asm volatile("" ::: "memory");
     read_grp(nxt, w.rin, sk_grp(t + 5));
-    const int pdd = st.Dd, psm = st.H, pc2 = st.c2;            // lane 63: column t - 63 (the push below)
-    int oI[4] = {}, oS[4] = {}, oD[4] = {}, qdd[3], qsm[3], qc2[3];
+    const int pdd = st.Dd, psm = st.H;                         // lane 63: column t - 63 (the push below)
+    int oI[4] = {}, oS[4] = {}, oD[4] = {}, qdd[3], qsm[3];
     const int cd[4] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w};
     const int cs[4] = {cur[1].x, cur[1].y, cur[1].z, cur[1].w};
-    const int cc[4] = {cur[2].x, cur[2].y, cur[2].z, cur[2].w};
+    const int c2[4] = {cc.x, cc.y, cc.z, cc.w};
+    cc = load_codes(w, t + 16);                                // four groups ahead
 #pragma unroll
     for (int U = 0; U < 4; ++U) {
         if (MODE == 1) {
-            if (w.lane <= t + U) core_step<LOCAL, TBL, false>(st, cd[U], cs[U], cc[U], true, w.c1, sc, oI[U], oS[U], oD[U]);
+            if (w.lane <= t + U) core_step<LOCAL, TBL, false>(st, cd[U], cs[U], c2[U], true, w.c1, sc, oI[U], oS[U], oD[U]);
         } else {
             const bool act = MODE == 2 ? (unsigned)(t + U - w.lane) < (unsigned)w.m : true;
-            core_step<LOCAL, TBL, MODE == 2>(st, cd[U], cs[U], cc[U], act, w.c1, sc, oI[U], oS[U], oD[U]);
+            core_step<LOCAL, TBL, MODE == 2>(st, cd[U], cs[U], c2[U], act, w.c1, sc, oI[U], oS[U], oD[U]);
         }
-        if (U < 3) { qdd[U] = st.Dd; qsm[U] = st.H; qc2[U] = st.c2; }
+        if (U < 3) { qdd[U] = st.Dd; qsm[U] = st.H; }
     }
     // hand the group's cells to the side wave (slot t/4 mod kSkHo; the side
     // wave has read the slot's previous group: checked per sub-block)
@@ -161,15 +168,21 @@ __device__ __forceinline__ void core_group(CoreState& st, const int4 (&cur)[3], 
         *w.hcnt = (t >> 2) + 1;                                // (every lane, one value; LDS keeps the order)
     }
     // lane 63 pushes ring group (t - 60) / 4: its columns t-63 .. t-60 (before
-    // this group's step 0, after steps 0, 1, 2)
-    if (w.push_on && t >= 64 && t - 63 <= w.m) {
-        if (w.lane == kWave - 1) {
-            const int G = sk_grp(t - 63);
-            *(int4*)w.rout->dd[G] = make_int4(pdd, qdd[0], qdd[1], qdd[2]);
-            *(int4*)w.rout->sm[G] = make_int4(psm, qsm[0], qsm[1], qsm[2]);
-            *(int4*)w.rout->c2[G] = make_int4(pc2, qc2[0], qc2[1], qc2[2]);
-            *w.wcnt_out = min(t - 60, w.m) + 1;                 // after the records (LDS in order)
-        }
+    // this group's step 0, after steps 0, 1, 2), then the count (same wave,
+    // LDS in order); exec = lane 63 in one asm block, so no branch
+    if (w.push_on && (MODE == 0 || (t >= 64 && t - 63 <= w.m))) {   // (full groups: always inside)
+        const uint32_t a = lds_addr(w.rout->dd[sk_grp(t - 63)]);
+        const v4ia vd = {pdd, qdd[0], qdd[1], qdd[2]}, vs = {psm, qsm[0], qsm[1], qsm[2]};
+        asm volatile(
+            "s_mov_b64 exec, %[m]\n\t"
+            "ds_write_b128 %[a], %[vd]\n\t"
+            "ds_write_b128 %[a], %[vs] offset:%[so]\n\t"
+            "ds_write_b32 %[ca], %[cv]\n\t"
+            "s_mov_b64 exec, -1"
+            :
+            : [m] "s"(lane63_mask(true)), [a] "v"(a), [vd] "v"(vd), [vs] "v"(vs), [so] "i"(kSkRingG * 16),
+              [ca] "v"(w.cnt_addr), [cv] "v"(min(t - 60, w.m) + 1)
+            : "memory");
     }
     if (__builtin_amdgcn_readfirstlane(seen_v) < need) {       // the strip above was behind: wait, re-read
         w.tr_win += wait_ge(w.wcnt_in, need, w.status);
@@ -198,13 +211,14 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
         st.H = H0;
         st.Hx = H0 + (LOCAL ? sc.hg : sc.h);
         st.Dd = H0;                               // (column 0's successor is never read: column 0 is analytic)
-        st.c2 = 0;
     }
+    w.crs = rsrc_of(uniform_ptr(P.ccodes), 4 * (m + 192));
+    w.cvoff = 4u * (uint32_t)(64 - lane);
+    w.cnt_addr = lds_addr((const void*)w.wcnt_out);
     if (w.push_on) {                              // column 0 of the bottom row: the next strip's first top-left
         if (lane == kWave - 1) {
             w.rout->dd[0][3] = st.Dd;
             w.rout->sm[0][3] = st.H;
-            w.rout->c2[0][3] = 0;
             *w.wcnt_out = 1;
         }
     }
@@ -212,7 +226,10 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
     long long tr_q[kTraceQ] = {};
     if (trace) tr_start = __builtin_amdgcn_s_memrealtime();
     w.tr_win += wait_ge(w.wcnt_in, min(4, m) + 1, w.status);
-    int4 ra[3], rb[3];
+    int4 ra[2], rb[2];
+    int4 cc[4];                                   // column symbols of the next four groups
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cc[q] = load_codes(w, 4 * q);
     st.Hd = shr1(w.rin->sm[0][3], st.H);          // column 1's top-left: (64 s, 0) for lane 0, lane-1's column 0
     read_grp(ra, w.rin, sk_grp(1));
     if (trace) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
@@ -231,20 +248,20 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
         // ramp-up (lane l starts at step l) while no lane passes column m;
         // every lane inside columns 1..m; otherwise masked per lane
         if (t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1) {
-            core_group<LOCAL, TBL, 1>(st, ra, rb, w, sc, t0);
-            core_group<LOCAL, TBL, 1>(st, rb, ra, w, sc, t0 + 4);
-            core_group<LOCAL, TBL, 1>(st, ra, rb, w, sc, t0 + 8);
-            core_group<LOCAL, TBL, 1>(st, rb, ra, w, sc, t0 + 12);
+            core_group<LOCAL, TBL, 1>(st, ra, rb, cc[0], w, sc, t0);
+            core_group<LOCAL, TBL, 1>(st, rb, ra, cc[1], w, sc, t0 + 4);
+            core_group<LOCAL, TBL, 1>(st, ra, rb, cc[2], w, sc, t0 + 8);
+            core_group<LOCAL, TBL, 1>(st, rb, ra, cc[3], w, sc, t0 + 12);
         } else if (t0 >= kWave && t0 + kSub - 1 <= m - 1) {
-            core_group<LOCAL, TBL, 0>(st, ra, rb, w, sc, t0);
-            core_group<LOCAL, TBL, 0>(st, rb, ra, w, sc, t0 + 4);
-            core_group<LOCAL, TBL, 0>(st, ra, rb, w, sc, t0 + 8);
-            core_group<LOCAL, TBL, 0>(st, rb, ra, w, sc, t0 + 12);
+            core_group<LOCAL, TBL, 0>(st, ra, rb, cc[0], w, sc, t0);
+            core_group<LOCAL, TBL, 0>(st, rb, ra, cc[1], w, sc, t0 + 4);
+            core_group<LOCAL, TBL, 0>(st, ra, rb, cc[2], w, sc, t0 + 8);
+            core_group<LOCAL, TBL, 0>(st, rb, ra, cc[3], w, sc, t0 + 12);
         } else {
-            core_group<LOCAL, TBL, 2>(st, ra, rb, w, sc, t0);
-            core_group<LOCAL, TBL, 2>(st, rb, ra, w, sc, t0 + 4);
-            core_group<LOCAL, TBL, 2>(st, ra, rb, w, sc, t0 + 8);
-            core_group<LOCAL, TBL, 2>(st, rb, ra, w, sc, t0 + 12);
+            core_group<LOCAL, TBL, 2>(st, ra, rb, cc[0], w, sc, t0);
+            core_group<LOCAL, TBL, 2>(st, rb, ra, cc[1], w, sc, t0 + 4);
+            core_group<LOCAL, TBL, 2>(st, ra, rb, cc[2], w, sc, t0 + 8);
+            core_group<LOCAL, TBL, 2>(st, rb, ra, cc[3], w, sc, t0 + 12);
         }
         // every ring read up to column t0+20 (incl. the next group's) was issued before this store
         *w.rcnt_in = min(t0 + kSub + 5, m + 1);
@@ -420,7 +437,7 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, SideCtx
 // (MI355X_MICROARCH.md "handoff-1to1": a data-tagged granule is the cheapest
 // cross-CU hand-off, no progress counter and no store drain before a flag).
 // The next band needs each bottom-row cell's delete successor dd and
-// score_max sm (the column symbol it reads from the pair's chars itself);
+// score_max sm (every lane reads its column symbols from PairDev.ccodes);
 // dd - sm lies in [h + g, max(g, 0)] (Ddn = max(Dn, H + h) with Dn <= H; local:
 // the floor and + g), so one granule holds sm (low word) and (dd - sm) in 31
 // bits under a valid bit (bit 63).  The feed rows are zeroed before the launch
@@ -467,7 +484,6 @@ __device__ void io_wave_tag(const PairDev& P, const int lb, const int lane, cons
                     const int G = sk_grp(j), u = sk_pos(j);
                     ring0->dd[G][u] = dd;
                     ring0->sm[G][u] = sm;
-                    ring0->c2[G][u] = j == 0 ? 0 : TBL ? sym_code(P.c2[j - 1], sc) * 8 : (int)P.c2[j - 1];
                 }
                 lds_wait();
                 if (lane == 0) *wcnt0 = in_next + cnt;
@@ -561,6 +577,25 @@ __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const
         }
         __syncthreads();
     }
+}
+
+// The column symbols of every pair as int32, 64 zeros on each side (the
+// steps where a lane is outside columns 1..m read them): index j - 1 + 64
+// holds s2[j-1], or its symbol code * 8 with score tables (Scores32.sym).
+__global__ void skew_codes_kernel(const PairDev* __restrict__ pairs, const Scores32 sc, const int tbl) {
+    const PairDev& P = pairs[blockIdx.y];
+    const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (k >= P.m + 192) return;
+    const int j = k - 64;
+    int v = 0;
+    if (j >= 0 && j < P.m) v = tbl ? sym_code(P.c2[j], sc) * 8 : (int)P.c2[j];
+    ((int*)P.ccodes)[k] = v;
+}
+hipError_t launch_skew_codes(const PairDev* d_pairs, int npairs, int mmax, Scores32 sc, bool tbl, hipStream_t st) {
+    if (npairs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(skew_codes_kernel, dim3((unsigned)((mmax + 192 + 255) / 256), (unsigned)npairs), dim3(256), 0, st,
+                       d_pairs, sc, (int)tbl);
+    return hipGetLastError();
 }
 
 template <int W, bool LOCAL, bool PLANES, bool TBL>
