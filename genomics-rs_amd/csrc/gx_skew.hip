@@ -332,6 +332,7 @@ struct SideCtx {
     uint32_t skel_voff;                  // lane 63: 0; other lanes: out of range
     int m, lane;
     unsigned tr_wait;                    // (diagnostics: spins waiting for the core wave)
+    bool diag_idle;                      // (GX_DEBUG_FLAGS & 2: the side only consumes; timing only)
 };
 
 template <bool LOCAL, bool PLANES, int MODE>
@@ -341,6 +342,7 @@ __device__ __forceinline__ void side_group(SideState& st, SideCtx& w, const int 
     const int4* hv = &w.ho->v[g & (kSkHo - 1)][0][w.lane];
     const int4 vI = hv[0], vS = hv[kWave], vD = hv[2 * kWave];
     *w.bcnt = g + 1;                                           // (reads issued first: LDS keeps the order)
+    if (w.diag_idle) return;                                   // (GX_DEBUG_FLAGS & 2: timing only, wrong results)
     if (PLANES) {   // the group's cells as they came, one dwordx4 per lane and plane
         const uint32_t vo = (uint32_t)w.lane * 16u + (uint32_t)g * (kGroupInts1 * 4);
         bstore4(w.rI, vo, vI);
@@ -516,18 +518,19 @@ __device__ void io_wave_tag(const PairDev& P, const int lb, const int lane, cons
             __hip_atomic_store((gint*)status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
         } else {
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(4);   // (a poll costs its SIMD's issue slots: keep it rare)
         }
     }
 }
 
 // ---------------------------------------------------------------------------
 
-// One workgroup = one band of W strips: waves 0..W-1 the strips' core waves,
-// W..2W-1 their side waves, 2W the I/O wave (waves go to SIMDs round-robin:
-// at W = 2 every compute wave has a SIMD of its own, at W = 4 strip k's core
-// and side share SIMD k).  Persistent workgroups take bands from the host's
-// band-major queue (gx_api.cpp run_fill), as fill_kernel does.
+// One workgroup = one band of W strips: wave 0 the I/O wave, waves 1..W the
+// strips' core waves, W+1..2W their side waves.  Waves go to the CU's SIMDs
+// round-robin, so at W = 2 the two core waves have SIMDs of their own (the
+// I/O wave, which polls, shares one with a side wave); at W = 4 strip k's
+// core and side share a SIMD.  Persistent workgroups take bands from the
+// host's band-major queue (gx_api.cpp run_fill), as fill_kernel does.
 template <int W, bool LOCAL, bool PLANES, bool TBL>
 __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const PairDev* __restrict__ pairs,
                                                                            const int npairs, const int total_bands,
@@ -550,10 +553,13 @@ __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const
         const int p = __builtin_amdgcn_readfirstlane(ob.x);
         const PairDev& P = pairs[p];
         const int lb = __builtin_amdgcn_readfirstlane(ob.y);
-        const int k = wave < W ? wave : wave - W;   // the strip (in the band) of a compute wave
+        const int k = wave <= W ? wave - 1 : wave - 1 - W;   // the strip (in the band) of a compute wave
         const int s = lb * W + k;
         const bool has_consumer = k == W - 1 ? (lb + 1 < P.bands) : (s + 1 < P.strips);
-        if (wave < W) {
+        if (wave == 0) {
+            io_wave_tag<TBL>(P, lb, lane, sc, &rings[0], &rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0],
+                             (lds_int*)&wcnt[W], (lds_int*)&rcnt[W], lb + 1 < P.bands, band_counter + 1);
+        } else if (wave <= W) {
             if (s < P.strips) {
                 CoreCtx w;
                 w.rin = &rings[k]; w.rout = &rings[k + 1];
@@ -564,16 +570,14 @@ __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const
                 w.push_on = has_consumer;
                 core_wave<LOCAL, TBL>(P, s, lane, sc, w, pres + p);
             }
-        } else if (wave < 2 * W) {
+        } else {
             if (s < P.strips) {
                 SideCtx w;
                 w.ho = &ho[k]; w.hcnt = (lds_int*)&hcnt[k]; w.bcnt = (lds_int*)&bcnt[k];
                 w.status = band_counter + 1;
+                w.diag_idle = (sc.dbg & 2) != 0;
                 side_wave<LOCAL, PLANES>(P, s, lane, w, has_consumer, sres, pres + p);
             }
-        } else {
-            io_wave_tag<TBL>(P, lb, lane, sc, &rings[0], &rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0],
-                             (lds_int*)&wcnt[W], (lds_int*)&rcnt[W], lb + 1 < P.bands, band_counter + 1);
         }
         __syncthreads();
     }
