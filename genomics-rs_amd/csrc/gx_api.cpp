@@ -611,12 +611,12 @@ static bool cs2_enabled(int is_local, const Scores32& sc) {
     return is_local != 0;
 }
 // Layout 3 (gx_skew.hip): 2-strip bands, each strip's core and side wave on
-// SIMDs of their own; GX_BAND_WAVES picks another instantiated width (1-4;
+// SIMDs of their own; GX_BAND_WAVES picks another instantiated width (1-3;
 // must match gx_skew.hip launch_fill_skew).
 static int skew_band_waves() {
     if (const char* e = getenv("GX_BAND_WAVES")) {
         const int w = atoi(e);
-        if (w >= 1 && w <= 4) return w;
+        if (w >= 1 && w <= 3) return w;
     }
     return 2;
 }

@@ -23,6 +23,10 @@ __device__ __forceinline__ int shr1(int old, int src) {
     // lane l <- src[l-1]; lane 0 keeps `old` (bound_ctrl off)
     return __builtin_amdgcn_update_dpp(old, src, DPP_WAVE_SHR1, 0xF, 0xF, false);
 }
+__device__ __forceinline__ int shz(int src) {
+    // lane l <- src[l-1]; lane 0 reads 0 (bound_ctrl): shz(x) + y folds into one v_add_u32_dpp
+    return __builtin_amdgcn_update_dpp(0, src, DPP_WAVE_SHR1, 0xF, 0xF, true);
+}
 __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
 
 __device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }

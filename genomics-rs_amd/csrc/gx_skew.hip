@@ -54,6 +54,9 @@
 
 namespace gx {
 
+#ifndef GX_SKEW_EXP
+#define GX_SKEW_EXP 0            // (timing experiments only: tools/skew_exp.sh)
+#endif
 constexpr int kSkRingG = 64;     // ring groups per strip boundary (256 columns)
 constexpr int kSkHo = 8;         // core -> side hand-off ring depth (4-step groups)
 
@@ -79,13 +82,13 @@ struct CoreState {               // cell (i, j-1) of the lane's row
 };
 
 // One anti-diagonal step: cell (i, j), j = t - lane + 1.  (rdd, rsm) = lane
-// 0's cell above from the ring; c2 = s2[j-1] (its symbol code * 8 with score
+// 0's cell above from the ring (0 in the other lanes); c2 = s2[j-1] (its symbol code * 8 with score
 // tables).  MASKED (ramp-down): act = false keeps the row at its last column.
 template <bool LOCAL, bool TBL, bool MASKED>
 __device__ __forceinline__ void core_step(CoreState& st, const int rdd, const int rsm, const int c2, const bool act,
                                           const int c1v, const Scores32& sc, int& oI, int& oS, int& oD) {
-    const int Dn = shr1(rdd, st.Dd);         // D(i, j): the delete successor of the cell above
-    const int hu = shr1(rsm, st.H);          // score_max(i-1, j)
+    const int Dn = shz(st.Dd) + rdd;         // D(i, j): the delete successor of the cell above
+    const int hu = shz(st.H) + rsm;          // score_max(i-1, j)  (rdd, rsm: 0 but in lane 0)
     const bool mt = c2 == c1v;               // sequence.rs:113-114
     const int Sn = st.Hd + (TBL ? __builtin_amdgcn_sbfe(c1v, c2, 8) : (mt ? sc.sm : sc.smm));
     const int In = LOCAL ? max3i(st.I + sc.g, st.Hx, 0) : max(st.I, st.Hx);
@@ -105,7 +108,11 @@ __device__ __forceinline__ void core_step(CoreState& st, const int rdd, const in
 struct CoreCtx {
     __amdgpu_buffer_rsrc_t crs;  // the pair's int32 column symbols (PairDev.ccodes)
     uint32_t cvoff;              // 4 (64 - lane): this lane's column of step 0, less one
-    uint32_t cnt_addr;           // wcnt_out (LDS address) for the push
+    int4* push_base;             // lane 63: the ring below's dd[0]; other lanes (or no consumer): their sink slot
+    int push_m16;                // lane 63: 16 (a ring group's bytes); other lanes: 0
+    lds_int* pcnt;               // wcnt_out (no consumer: a sink)
+    const int4* rd_base;         // lane 0: the ring above's dd[0]; other lanes: a zero block
+    int rd_m16;                  // lane 0: 16; other lanes: 0
     const SkRing* rin;
     SkRing* rout;
     lds_int* wcnt_in;            // columns the strip above published
@@ -121,33 +128,47 @@ struct CoreCtx {
     unsigned tr_win, tr_ho;      // (diagnostics: spins waiting for the strip above / for hand-off space)
 };
 
-__device__ __forceinline__ void read_grp(int4 (&r)[2], const SkRing* ring, int G) {
-    r[0] = *(const int4*)ring->dd[G];
-    r[1] = *(const int4*)ring->sm[G];
+// Lane 0 reads ring group G (dd, then sm 1 KB on), the other lanes a zero block.
+__device__ __forceinline__ void read_grp(v4i (&r)[2], const CoreCtx& w, int G) {
+    const v4i* p = (const v4i*)((const char*)w.rd_base + G * w.rd_m16);
+    r[0] = p[0];
+    r[1] = p[kSkRingG];
 }
 // This lane's column symbols of steps t .. t+3 (columns t-lane+1 ..).
 __device__ __forceinline__ int4 load_codes(const CoreCtx& w, int t) {
     const v4i x = __builtin_amdgcn_raw_buffer_load_b128(w.crs, (int)w.cvoff, __builtin_amdgcn_readfirstlane(4 * t), 0);
     return make_int4(x[0], x[1], x[2], x[3]);
 }
-typedef int v4ia __attribute__((ext_vector_type(4)));
 
 // One 4-step group of the core wave.  MODE 0: full; 1: ramp-up (lanes past
 // the step not started yet: each step under `lane <= t`, so their column-0
 // state stays); 2: ramp-down (lanes past column m keep their state).
+// A group's LDS store data (hand-off I, S, D; push dd, sm) stays allocated
+// through the next group (pinned there), so the next group's results never
+// reuse registers an LDS store may still be reading (which would cost a wait
+// for that store: LDS reads store data after issue).
+struct CorePend {
+    v4i v[5];
+};
+__device__ __forceinline__ void pin(const CorePend& p) {
+    asm volatile("" ::"v"(p.v[0]), "v"(p.v[1]), "v"(p.v[2]), "v"(p.v[3]), "v"(p.v[4]));
+}
+
 template <bool LOCAL, bool TBL, int MODE>
-__device__ __forceinline__ void core_group(CoreState& st, const int4 (&cur)[2], int4 (&nxt)[2], int4& cc, CoreCtx& w,
-                                           const Scores32& sc, const int t) {
+__device__ __forceinline__ void core_group(CoreState& st, const v4i (&cur)[2], v4i (&nxt)[2], int4& cc, CoreCtx& w,
+                                           const Scores32& sc, const int t, CorePend& mine, const CorePend& prev) {
     const int need = min(t + 8, w.m) + 1;                      // columns of the next group: t+5 .. t+8
-    const int seen_v = *w.wcnt_in;
+    const int seen_v = (GX_SKEW_EXP & 4) ? 1 << 30 : *w.wcnt_in;
     asm volatile("" ::: "memory");
-    read_grp(nxt, w.rin, sk_grp(t + 5));
+    if (GX_SKEW_EXP & 4) { nxt[0] = v4i{t, t, t, t}; nxt[1] = nxt[0]; }
+    else read_grp(nxt, w, sk_grp(t + 5));
     const int pdd = st.Dd, psm = st.H;                         // lane 63: column t - 63 (the push below)
     int oI[4] = {}, oS[4] = {}, oD[4] = {}, qdd[3], qsm[3];
-    const int cd[4] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w};
-    const int cs[4] = {cur[1].x, cur[1].y, cur[1].z, cur[1].w};
+    const int cd[4] = {cur[0][0], cur[0][1], cur[0][2], cur[0][3]};
+    const int cs[4] = {cur[1][0], cur[1][1], cur[1][2], cur[1][3]};
     const int c2[4] = {cc.x, cc.y, cc.z, cc.w};
-    cc = load_codes(w, t + 16);                                // four groups ahead
+    if (GX_SKEW_EXP & 1) cc = make_int4(t & 3, t & 1, t & 2, 1);
+    else cc = load_codes(w, t + 16);                           // four groups ahead
 #pragma unroll
     for (int U = 0; U < 4; ++U) {
         if (MODE == 1) {
@@ -160,34 +181,39 @@ __device__ __forceinline__ void core_group(CoreState& st, const int4 (&cur)[2], 
     }
     // hand the group's cells to the side wave (slot t/4 mod kSkHo; the side
     // wave has read the slot's previous group: checked per sub-block)
-    {
-        int4* hv = &w.ho->v[(t >> 2) & (kSkHo - 1)][0][w.lane];
-        hv[0] = make_int4(oI[0], oI[1], oI[2], oI[3]);
-        hv[kWave] = make_int4(oS[0], oS[1], oS[2], oS[3]);
-        hv[2 * kWave] = make_int4(oD[0], oD[1], oD[2], oD[3]);
+    if (!(GX_SKEW_EXP & 2)) {
+        v4i* hv = (v4i*)&w.ho->v[(t >> 2) & (kSkHo - 1)][0][w.lane];
+        mine.v[0] = v4i{oI[0], oI[1], oI[2], oI[3]};
+        mine.v[1] = v4i{oS[0], oS[1], oS[2], oS[3]};
+        mine.v[2] = v4i{oD[0], oD[1], oD[2], oD[3]};
+        hv[0] = mine.v[0];
+        hv[kWave] = mine.v[1];
+        hv[2 * kWave] = mine.v[2];
         *w.hcnt = (t >> 2) + 1;                                // (every lane, one value; LDS keeps the order)
     }
     // lane 63 pushes ring group (t - 60) / 4: its columns t-63 .. t-60 (before
     // this group's step 0, after steps 0, 1, 2), then the count (same wave,
-    // LDS in order); exec = lane 63 in one asm block, so no branch
-    if (w.push_on && (MODE == 0 || (t >= 64 && t - 63 <= w.m))) {   // (full groups: always inside)
-        const uint32_t a = lds_addr(w.rout->dd[sk_grp(t - 63)]);
-        const v4ia vd = {pdd, qdd[0], qdd[1], qdd[2]}, vs = {psm, qsm[0], qsm[1], qsm[2]};
-        asm volatile(
-            "s_mov_b64 exec, %[m]\n\t"
-            "ds_write_b128 %[a], %[vd]\n\t"
-            "ds_write_b128 %[a], %[vs] offset:%[so]\n\t"
-            "ds_write_b32 %[ca], %[cv]\n\t"
-            "s_mov_b64 exec, -1"
-            :
-            : [m] "s"(lane63_mask(true)), [a] "v"(a), [vd] "v"(vd), [vs] "v"(vs), [so] "i"(kSkRingG * 16),
-              [ca] "v"(w.cnt_addr), [cv] "v"(min(t - 60, w.m) + 1)
-            : "memory");
+    // LDS in order).  Every lane writes (lanes 0..62 into a sink), so the
+    // compiler sees and counts the stores: no exec change, no branch.
+    mine.v[3] = v4i{pdd, qdd[0], qdd[1], qdd[2]};
+    mine.v[4] = v4i{psm, qsm[0], qsm[1], qsm[2]};
+    if (MODE == 0 || (t >= 64 && t - 63 <= w.m)) {   // (full groups: always inside; no consumer: all into the sink)
+        v4i* a = (v4i*)((char*)w.push_base + sk_grp(t - 63) * w.push_m16);
+        a[0] = mine.v[3];
+        a[kSkRingG] = mine.v[4];
+        *w.pcnt = min(t - 60, w.m) + 1;
     }
     if (__builtin_amdgcn_readfirstlane(seen_v) < need) {       // the strip above was behind: wait, re-read
         w.tr_win += wait_ge(w.wcnt_in, need, w.status);
-        read_grp(nxt, w.rin, sk_grp(t + 5));
+        // re-read into the same registers and wait for it here (one asm: no
+        // copies on the fast path, nothing pending after the join)
+        const uint32_t a = lds_addr(w.rd_base) + (uint32_t)(sk_grp(t + 5) * w.rd_m16);
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:%3\n\ts_waitcnt lgkmcnt(0)"
+                     : "+v"(nxt[0]), "+v"(nxt[1])
+                     : "v"(a), "i"(kSkRingG * 16)
+                     : "memory");
     }
+    pin(prev);
     __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -214,7 +240,6 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
     }
     w.crs = rsrc_of(uniform_ptr(P.ccodes), 4 * (m + 192));
     w.cvoff = 4u * (uint32_t)(64 - lane);
-    w.cnt_addr = lds_addr((const void*)w.wcnt_out);
     if (w.push_on) {                              // column 0 of the bottom row: the next strip's first top-left
         if (lane == kWave - 1) {
             w.rout->dd[0][3] = st.Dd;
@@ -226,12 +251,13 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
     long long tr_q[kTraceQ] = {};
     if (trace) tr_start = __builtin_amdgcn_s_memrealtime();
     w.tr_win += wait_ge(w.wcnt_in, min(4, m) + 1, w.status);
-    int4 ra[2], rb[2];
+    v4i ra[2], rb[2];
     int4 cc[4];                                   // column symbols of the next four groups
+    CorePend pa = {}, pb = {};
 #pragma unroll
     for (int q = 0; q < 4; ++q) cc[q] = load_codes(w, 4 * q);
     st.Hd = shr1(w.rin->sm[0][3], st.H);          // column 1's top-left: (64 s, 0) for lane 0, lane-1's column 0
-    read_grp(ra, w.rin, sk_grp(1));
+    read_grp(ra, w, sk_grp(1));
     if (trace) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
     const int T = m + kWave;                      // lane 63 computes column m at step m + 62; pushes run to t = m + 63
     for (int t0 = 0; t0 < T; t0 += kSub) {
@@ -240,28 +266,31 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
         const int last_col = min(t0 - 48, m);
         if (w.push_on && last_col >= kSkRingG * 4 - 4) wait_ge(w.rcnt_out, last_col - (kSkRingG * 4 - 4) + 1, w.status);
         // hand-off space: the side wave has read this sub-block's slots' previous groups
-        if (t0 >= 4 * kSkHo) w.tr_ho += wait_ge(w.bcnt, (t0 >> 2) + 4 - kSkHo, w.status);
+        if (t0 >= 4 * kSkHo && !(GX_SKEW_EXP & 2)) w.tr_ho += wait_ge(w.bcnt, (t0 >> 2) + 4 - kSkHo, w.status);
         if (trace) {
             const int q = (int)((long long)t0 * (kTraceQ + 1) / T) - 1;
-            if (q >= 0 && q < kTraceQ && tr_q[q] == 0) tr_q[q] = __builtin_amdgcn_s_memrealtime();
+            const long long now = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+            for (int k = 0; k < kTraceQ; ++k)   // (constant indices: the stamps stay in registers)
+                if (k == q && tr_q[k] == 0) tr_q[k] = now;
         }
         // ramp-up (lane l starts at step l) while no lane passes column m;
         // every lane inside columns 1..m; otherwise masked per lane
         if (t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1) {
-            core_group<LOCAL, TBL, 1>(st, ra, rb, cc[0], w, sc, t0);
-            core_group<LOCAL, TBL, 1>(st, rb, ra, cc[1], w, sc, t0 + 4);
-            core_group<LOCAL, TBL, 1>(st, ra, rb, cc[2], w, sc, t0 + 8);
-            core_group<LOCAL, TBL, 1>(st, rb, ra, cc[3], w, sc, t0 + 12);
+            core_group<LOCAL, TBL, 1>(st, ra, rb, cc[0], w, sc, t0, pa, pb);
+            core_group<LOCAL, TBL, 1>(st, rb, ra, cc[1], w, sc, t0 + 4, pb, pa);
+            core_group<LOCAL, TBL, 1>(st, ra, rb, cc[2], w, sc, t0 + 8, pa, pb);
+            core_group<LOCAL, TBL, 1>(st, rb, ra, cc[3], w, sc, t0 + 12, pb, pa);
         } else if (t0 >= kWave && t0 + kSub - 1 <= m - 1) {
-            core_group<LOCAL, TBL, 0>(st, ra, rb, cc[0], w, sc, t0);
-            core_group<LOCAL, TBL, 0>(st, rb, ra, cc[1], w, sc, t0 + 4);
-            core_group<LOCAL, TBL, 0>(st, ra, rb, cc[2], w, sc, t0 + 8);
-            core_group<LOCAL, TBL, 0>(st, rb, ra, cc[3], w, sc, t0 + 12);
+            core_group<LOCAL, TBL, 0>(st, ra, rb, cc[0], w, sc, t0, pa, pb);
+            core_group<LOCAL, TBL, 0>(st, rb, ra, cc[1], w, sc, t0 + 4, pb, pa);
+            core_group<LOCAL, TBL, 0>(st, ra, rb, cc[2], w, sc, t0 + 8, pa, pb);
+            core_group<LOCAL, TBL, 0>(st, rb, ra, cc[3], w, sc, t0 + 12, pb, pa);
         } else {
-            core_group<LOCAL, TBL, 2>(st, ra, rb, cc[0], w, sc, t0);
-            core_group<LOCAL, TBL, 2>(st, rb, ra, cc[1], w, sc, t0 + 4);
-            core_group<LOCAL, TBL, 2>(st, ra, rb, cc[2], w, sc, t0 + 8);
-            core_group<LOCAL, TBL, 2>(st, rb, ra, cc[3], w, sc, t0 + 12);
+            core_group<LOCAL, TBL, 2>(st, ra, rb, cc[0], w, sc, t0, pa, pb);
+            core_group<LOCAL, TBL, 2>(st, rb, ra, cc[1], w, sc, t0 + 4, pb, pa);
+            core_group<LOCAL, TBL, 2>(st, ra, rb, cc[2], w, sc, t0 + 8, pa, pb);
+            core_group<LOCAL, TBL, 2>(st, rb, ra, cc[3], w, sc, t0 + 12, pb, pa);
         }
         // every ring read up to column t0+20 (incl. the next group's) was issued before this store
         *w.rcnt_in = min(t0 + kSub + 5, m + 1);
@@ -381,6 +410,7 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, SideCtx
     const int i = s * kWave + lane + 1;
     const bool ok = i <= n;
     w.m = m; w.lane = lane; w.tr_wait = 0;
+    if (GX_SKEW_EXP & 2) return;
     if (PLANES) {
         const size_t strip_planes = (size_t)s * P.t4 * kGroupInts1;
         const int pbytes = P.t4 * kGroupInts1 * 4;   // one strip's plane
@@ -528,8 +558,8 @@ __device__ void io_wave_tag(const PairDev& P, const int lb, const int lane, cons
 // One workgroup = one band of W strips: wave 0 the I/O wave, waves 1..W the
 // strips' core waves, W+1..2W their side waves.  Waves go to the CU's SIMDs
 // round-robin, so at W = 2 the two core waves have SIMDs of their own (the
-// I/O wave, which polls, shares one with a side wave); at W = 4 strip k's
-// core and side share a SIMD.  Persistent workgroups take bands from the
+// I/O wave, which polls, shares one with a side wave); at W = 3 two core
+// waves share a SIMD with other waves.  Persistent workgroups take bands from the
 // host's band-major queue (gx_api.cpp run_fill), as fill_kernel does.
 template <int W, bool LOCAL, bool PLANES, bool TBL>
 __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const PairDev* __restrict__ pairs,
@@ -540,6 +570,10 @@ __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const
     __shared__ SkHo ho[W];
     __shared__ int wcnt[W + 1], rcnt[W + 1], hcnt[W], bcnt[W];
     __shared__ int band_sh;
+    __shared__ int4 push_sink[2 * kWave];          // the core waves' lanes 0..62 push here (core_group)
+    __shared__ int push_sink_cnt;
+    __shared__ int4 zero_blk[kSkRingG + 1];        // ... and their lanes 1..63 read [0] and [64] (read_grp)
+    if (threadIdx.x <= kSkRingG) zero_blk[threadIdx.x] = make_int4(0, 0, 0, 0);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int lane = threadIdx.x & (kWave - 1);
     for (;;) {
@@ -568,6 +602,12 @@ __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const
                 w.ho = &ho[k]; w.hcnt = (lds_int*)&hcnt[k]; w.bcnt = (lds_int*)&bcnt[k];
                 w.status = band_counter + 1;
                 w.push_on = has_consumer;
+                const bool pl = has_consumer && lane == kWave - 1;
+                w.push_base = pl ? (int4*)rings[k + 1].dd[0] : &push_sink[lane];
+                w.push_m16 = pl ? 16 : 0;
+                w.pcnt = has_consumer ? w.wcnt_out : (lds_int*)&push_sink_cnt;
+                w.rd_base = lane == 0 ? (const int4*)rings[k].dd[0] : zero_blk;
+                w.rd_m16 = lane == 0 ? 16 : 0;
                 core_wave<LOCAL, TBL>(P, s, lane, sc, w, pres + p);
             }
         } else {
@@ -619,13 +659,14 @@ static hipError_t launch_skew_w(int W, const PairDev* d_pairs, int npairs, int t
     return hipErrorInvalidValue;
 }
 
-// Band widths of layout 3 (must match gx_api.cpp skew_band_waves).
+// Band widths of layout 3 (must match gx_api.cpp skew_band_waves; at 4, nine
+// waves leave too few registers per wave for the pinned store data).
 hipError_t launch_fill_skew(int W, bool local, bool planes, bool tbl, const PairDev* d_pairs, int npairs,
                             int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                             hipStream_t st) {
 #define GX_SKEW_CASE(LO, PL, TB)                                                                                    \
     if (local == LO && planes == PL && tbl == TB)                                                                   \
-        return launch_skew_w<LO, PL, TB, 1, 2, 3, 4>(W, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc, \
+        return launch_skew_w<LO, PL, TB, 1, 2, 3>(W, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc, \
                                                      grid, st);
     GX_SKEW_CASE(false, false, false)
     GX_SKEW_CASE(false, false, true)

@@ -18,7 +18,7 @@ from conftest import CONFIG_SCORES, TEST_SCORES
 pytestmark = pytest.mark.gpu
 
 NAMES = ["Match", "Mismatch", "Insert", "Delete", "OpenInsert", "OpenDelete"]
-LAUNCH = {"w2": {"GX_LAYOUT": "3"}, "w4": {"GX_LAYOUT": "3", "GX_BAND_WAVES": "4"},
+LAUNCH = {"w2": {"GX_LAYOUT": "3"}, "w3": {"GX_LAYOUT": "3", "GX_BAND_WAVES": "3"},
           "w2_grid1": {"GX_LAYOUT": "3", "GX_BAND_WAVES": "2", "GX_FILL_GRID": "1"},
           "w3_grid2": {"GX_LAYOUT": "3", "GX_BAND_WAVES": "3", "GX_FILL_GRID": "2"},
           "w1_grid1": {"GX_LAYOUT": "3", "GX_BAND_WAVES": "1", "GX_FILL_GRID": "1"}}
