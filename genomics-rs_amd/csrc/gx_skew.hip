@@ -120,8 +120,9 @@ struct CoreCtx {
     lds_int* wcnt_out;
     lds_int* rcnt_out;
     SkHo* ho;
-    lds_int* hcnt;               // hand-off groups written (core) / read (side)
+    lds_int* hcnt;               // hand-off groups written (core) / read (side), per sub-block
     lds_int* bcnt;
+    v4i* hv_sub;                 // this lane's slot of the sub-block's first group (ho->v[(t0/4) % kSkHo][0][lane])
     int* status;
     int m, lane, c1;
     bool push_on;
@@ -154,7 +155,7 @@ __device__ __forceinline__ void pin(const CorePend& p) {
     asm volatile("" ::"v"(p.v[0]), "v"(p.v[1]), "v"(p.v[2]), "v"(p.v[3]), "v"(p.v[4]));
 }
 
-template <bool LOCAL, bool TBL, int MODE>
+template <bool LOCAL, bool TBL, int MODE, int Q>
 __device__ __forceinline__ void core_group(CoreState& st, const v4i (&cur)[2], v4i (&nxt)[2], int4& cc, CoreCtx& w,
                                            const Scores32& sc, const int t, CorePend& mine, const CorePend& prev) {
     const int need = min(t + 8, w.m) + 1;                      // columns of the next group: t+5 .. t+8
@@ -182,14 +183,14 @@ __device__ __forceinline__ void core_group(CoreState& st, const v4i (&cur)[2], v
     // hand the group's cells to the side wave (slot t/4 mod kSkHo; the side
     // wave has read the slot's previous group: checked per sub-block)
     if (!(GX_SKEW_EXP & 2)) {
-        v4i* hv = (v4i*)&w.ho->v[(t >> 2) & (kSkHo - 1)][0][w.lane];
+        v4i* hv = w.hv_sub + Q * 3 * kWave;
         mine.v[0] = v4i{oI[0], oI[1], oI[2], oI[3]};
         mine.v[1] = v4i{oS[0], oS[1], oS[2], oS[3]};
         mine.v[2] = v4i{oD[0], oD[1], oD[2], oD[3]};
         hv[0] = mine.v[0];
         hv[kWave] = mine.v[1];
         hv[2 * kWave] = mine.v[2];
-        *w.hcnt = (t >> 2) + 1;                                // (every lane, one value; LDS keeps the order)
+        if (Q == 3) *w.hcnt = (t >> 2) + 1;                    // (per sub-block; every lane, one value; LDS keeps the order)
     }
     // lane 63 pushes ring group (t - 60) / 4: its columns t-63 .. t-60 (before
     // this group's step 0, after steps 0, 1, 2), then the count (same wave,
@@ -267,6 +268,7 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
         if (w.push_on && last_col >= kSkRingG * 4 - 4) wait_ge(w.rcnt_out, last_col - (kSkRingG * 4 - 4) + 1, w.status);
         // hand-off space: the side wave has read this sub-block's slots' previous groups
         if (t0 >= 4 * kSkHo && !(GX_SKEW_EXP & 2)) w.tr_ho += wait_ge(w.bcnt, (t0 >> 2) + 4 - kSkHo, w.status);
+        w.hv_sub = (v4i*)&w.ho->v[(t0 >> 2) & (kSkHo - 1)][0][lane];
         if (trace) {
             const int q = (int)((long long)t0 * (kTraceQ + 1) / T) - 1;
             const long long now = __builtin_amdgcn_s_memrealtime();
@@ -277,20 +279,20 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
         // ramp-up (lane l starts at step l) while no lane passes column m;
         // every lane inside columns 1..m; otherwise masked per lane
         if (t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1) {
-            core_group<LOCAL, TBL, 1>(st, ra, rb, cc[0], w, sc, t0, pa, pb);
-            core_group<LOCAL, TBL, 1>(st, rb, ra, cc[1], w, sc, t0 + 4, pb, pa);
-            core_group<LOCAL, TBL, 1>(st, ra, rb, cc[2], w, sc, t0 + 8, pa, pb);
-            core_group<LOCAL, TBL, 1>(st, rb, ra, cc[3], w, sc, t0 + 12, pb, pa);
+            core_group<LOCAL, TBL, 1, 0>(st, ra, rb, cc[0], w, sc, t0, pa, pb);
+            core_group<LOCAL, TBL, 1, 1>(st, rb, ra, cc[1], w, sc, t0 + 4, pb, pa);
+            core_group<LOCAL, TBL, 1, 2>(st, ra, rb, cc[2], w, sc, t0 + 8, pa, pb);
+            core_group<LOCAL, TBL, 1, 3>(st, rb, ra, cc[3], w, sc, t0 + 12, pb, pa);
         } else if (t0 >= kWave && t0 + kSub - 1 <= m - 1) {
-            core_group<LOCAL, TBL, 0>(st, ra, rb, cc[0], w, sc, t0, pa, pb);
-            core_group<LOCAL, TBL, 0>(st, rb, ra, cc[1], w, sc, t0 + 4, pb, pa);
-            core_group<LOCAL, TBL, 0>(st, ra, rb, cc[2], w, sc, t0 + 8, pa, pb);
-            core_group<LOCAL, TBL, 0>(st, rb, ra, cc[3], w, sc, t0 + 12, pb, pa);
+            core_group<LOCAL, TBL, 0, 0>(st, ra, rb, cc[0], w, sc, t0, pa, pb);
+            core_group<LOCAL, TBL, 0, 1>(st, rb, ra, cc[1], w, sc, t0 + 4, pb, pa);
+            core_group<LOCAL, TBL, 0, 2>(st, ra, rb, cc[2], w, sc, t0 + 8, pa, pb);
+            core_group<LOCAL, TBL, 0, 3>(st, rb, ra, cc[3], w, sc, t0 + 12, pb, pa);
         } else {
-            core_group<LOCAL, TBL, 2>(st, ra, rb, cc[0], w, sc, t0, pa, pb);
-            core_group<LOCAL, TBL, 2>(st, rb, ra, cc[1], w, sc, t0 + 4, pb, pa);
-            core_group<LOCAL, TBL, 2>(st, ra, rb, cc[2], w, sc, t0 + 8, pa, pb);
-            core_group<LOCAL, TBL, 2>(st, rb, ra, cc[3], w, sc, t0 + 12, pb, pa);
+            core_group<LOCAL, TBL, 2, 0>(st, ra, rb, cc[0], w, sc, t0, pa, pb);
+            core_group<LOCAL, TBL, 2, 1>(st, rb, ra, cc[1], w, sc, t0 + 4, pb, pa);
+            core_group<LOCAL, TBL, 2, 2>(st, ra, rb, cc[2], w, sc, t0 + 8, pa, pb);
+            core_group<LOCAL, TBL, 2, 3>(st, rb, ra, cc[3], w, sc, t0 + 12, pb, pa);
         }
         // every ring read up to column t0+20 (incl. the next group's) was issued before this store
         *w.rcnt_in = min(t0 + kSub + 5, m + 1);
@@ -365,13 +367,9 @@ struct SideCtx {
 };
 
 template <bool LOCAL, bool PLANES, int MODE>
-__device__ __forceinline__ void side_group(SideState& st, SideCtx& w, const int t) {
+__device__ __forceinline__ void side_group(SideState& st, SideCtx& w, const int t, const int4 (&hv)[3]) {
     const int g = t >> 2;
-    w.tr_wait += wait_ge(w.hcnt, g + 1, w.status);
-    const int4* hv = &w.ho->v[g & (kSkHo - 1)][0][w.lane];
-    const int4 vI = hv[0], vS = hv[kWave], vD = hv[2 * kWave];
-    *w.bcnt = g + 1;                                           // (reads issued first: LDS keeps the order)
-    if (w.diag_idle) return;                                   // (GX_DEBUG_FLAGS & 2: timing only, wrong results)
+    const int4 vI = hv[0], vS = hv[1], vD = hv[2];
     if (PLANES) {   // the group's cells as they came, one dwordx4 per lane and plane
         const uint32_t vo = (uint32_t)w.lane * 16u + (uint32_t)g * (kGroupInts1 * 4);
         bstore4(w.rI, vo, vI);
@@ -428,15 +426,27 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, SideCtx
     st.lbest = ok ? INT_MIN : INT_MAX; st.lstep = 0; st.lE = 0;
     const int T = m + kWave;
     for (int t0 = 0; t0 < T; t0 += kSub) {
+        // the core publishes whole sub-blocks: read all four groups at once
+        w.tr_wait += wait_ge(w.hcnt, (t0 >> 2) + 4, w.status);
+        int4 sub[4][3];
+        {
+            const int4* hv = &w.ho->v[(t0 >> 2) & (kSkHo - 1)][0][lane];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) sub[q][k] = hv[(3 * q + k) * kWave];
+        }
+        *w.bcnt = (t0 >> 2) + 4;                  // (reads issued first: LDS keeps the order)
+        if (w.diag_idle) continue;                // (GX_DEBUG_FLAGS & 2: timing only, wrong results)
         if (t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1) {
-            side_group<LOCAL, PLANES, 1>(st, w, t0); side_group<LOCAL, PLANES, 1>(st, w, t0 + 4);
-            side_group<LOCAL, PLANES, 1>(st, w, t0 + 8); side_group<LOCAL, PLANES, 1>(st, w, t0 + 12);
+            side_group<LOCAL, PLANES, 1>(st, w, t0, sub[0]); side_group<LOCAL, PLANES, 1>(st, w, t0 + 4, sub[1]);
+            side_group<LOCAL, PLANES, 1>(st, w, t0 + 8, sub[2]); side_group<LOCAL, PLANES, 1>(st, w, t0 + 12, sub[3]);
         } else if (t0 >= kWave && t0 + kSub - 1 <= m - 1) {
-            side_group<LOCAL, PLANES, 0>(st, w, t0); side_group<LOCAL, PLANES, 0>(st, w, t0 + 4);
-            side_group<LOCAL, PLANES, 0>(st, w, t0 + 8); side_group<LOCAL, PLANES, 0>(st, w, t0 + 12);
+            side_group<LOCAL, PLANES, 0>(st, w, t0, sub[0]); side_group<LOCAL, PLANES, 0>(st, w, t0 + 4, sub[1]);
+            side_group<LOCAL, PLANES, 0>(st, w, t0 + 8, sub[2]); side_group<LOCAL, PLANES, 0>(st, w, t0 + 12, sub[3]);
         } else {
-            side_group<LOCAL, PLANES, 2>(st, w, t0); side_group<LOCAL, PLANES, 2>(st, w, t0 + 4);
-            side_group<LOCAL, PLANES, 2>(st, w, t0 + 8); side_group<LOCAL, PLANES, 2>(st, w, t0 + 12);
+            side_group<LOCAL, PLANES, 2>(st, w, t0, sub[0]); side_group<LOCAL, PLANES, 2>(st, w, t0 + 4, sub[1]);
+            side_group<LOCAL, PLANES, 2>(st, w, t0 + 8, sub[2]); side_group<LOCAL, PLANES, 2>(st, w, t0 + 12, sub[3]);
         }
         // codes[strip][t/16][lane]
         gstore1(w.codes + (size_t)(t0 >> 4) * kWave + lane, (st.cD << 16) | (st.cI & 0xFFFFu));
