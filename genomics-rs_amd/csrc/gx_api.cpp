@@ -653,7 +653,13 @@ struct PairHost {
 // profiles/r01d_layouts.txt).  The latency layout is 3 for untracked fills
 // with h <= 0 (its recurrences fold the gap opening onto score_max, which is
 // exact only then), else the column step.
-static bool skew_ok(const Scores32& sc, bool track) { return !track && sc.h <= 0; }
+// Layout 3 needs h <= 0 (the folded gap opening) and, for the virtual
+// columns of its global ramp-up (values drift from -2^30 by up to 64 steps of
+// |g| + |h| + |s|), small penalties.
+static bool skew_ok(const Scores32& sc, bool track) {
+    const long long drift = 64LL * (std::llabs((long long)sc.g) + std::llabs((long long)sc.h) + 256);
+    return !track && sc.h <= 0 && drift < (1LL << 28);
+}
 static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int grid_cap, bool track) {
     const long long span = 65LL * (std::llabs((long long)sc.g) + std::llabs((long long)sc.h));
     size_t mmax = 0;

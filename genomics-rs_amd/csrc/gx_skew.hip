@@ -168,18 +168,23 @@ __device__ __forceinline__ void core_group(CoreState& st, const v4i (&cur)[2], v
     const int cd[4] = {cur[0][0], cur[0][1], cur[0][2], cur[0][3]};
     const int cs[4] = {cur[1][0], cur[1][1], cur[1][2], cur[1][3]};
     const int c2[4] = {cc.x, cc.y, cc.z, cc.w};
-    if (GX_SKEW_EXP & 1) cc = make_int4(t & 3, t & 1, t & 2, 1);
-    else cc = load_codes(w, t + 16);                           // four groups ahead
 #pragma unroll
     for (int U = 0; U < 4; ++U) {
         if (MODE == 1) {
             if (w.lane <= t + U) core_step<LOCAL, TBL, false>(st, cd[U], cs[U], c2[U], true, w.c1, sc, oI[U], oS[U], oD[U]);
         } else {
-            const bool act = MODE == 2 ? (unsigned)(t + U - w.lane) < (unsigned)w.m : true;
+            // (global fills run the virtual columns <= 0 too: only columns > m stop)
+            const int c = t + U - w.lane;   // column - 1
+            const bool act = MODE == 2 ? (LOCAL ? (unsigned)c < (unsigned)w.m : c < w.m) : true;
             core_step<LOCAL, TBL, MODE == 2>(st, cd[U], cs[U], c2[U], act, w.c1, sc, oI[U], oS[U], oD[U]);
         }
         if (U < 3) { qdd[U] = st.Dd; qsm[U] = st.H; }
     }
+    // the symbols of this group's steps four groups on, into the registers
+    // just consumed (loaded after the steps, so that the loop carries them
+    // in place)
+    if (GX_SKEW_EXP & 1) cc = make_int4(t & 3, t & 1, t & 2, 1);
+    else cc = load_codes(w, t + 16);
     // hand the group's cells to the side wave (slot t/4 mod kSkHo; the side
     // wave has read the slot's previous group: checked per sub-block)
     if (!(GX_SKEW_EXP & 2)) {
@@ -190,6 +195,7 @@ __device__ __forceinline__ void core_group(CoreState& st, const v4i (&cur)[2], v
         hv[0] = mine.v[0];
         hv[kWave] = mine.v[1];
         hv[2 * kWave] = mine.v[2];
+        asm volatile("" ::: "memory");                         // (the data stores stay before the count)
         if (Q == 3) *w.hcnt = (t >> 2) + 1;                    // (per sub-block; every lane, one value; LDS keeps the order)
     }
     // lane 63 pushes ring group (t - 60) / 4: its columns t-63 .. t-60 (before
@@ -202,7 +208,8 @@ __device__ __forceinline__ void core_group(CoreState& st, const v4i (&cur)[2], v
         v4i* a = (v4i*)((char*)w.push_base + sk_grp(t - 63) * w.push_m16);
         a[0] = mine.v[3];
         a[kSkRingG] = mine.v[4];
-        *w.pcnt = min(t - 60, w.m) + 1;
+        asm volatile("" ::: "memory");
+        *w.pcnt = (MODE == 0 ? t - 60 : min(t - 60, w.m)) + 1;   // (MODE 0: t - 60 < m)
     }
     if (__builtin_amdgcn_readfirstlane(seen_v) < need) {       // the strip above was behind: wait, re-read
         w.tr_win += wait_ge(w.wcnt_in, need, w.status);
@@ -218,6 +225,41 @@ __device__ __forceinline__ void core_group(CoreState& st, const v4i (&cur)[2], v
     __builtin_amdgcn_sched_barrier(0);
 }
 
+struct CoreLoop {                 // the core wave's loop-carried state besides CoreState
+    v4i ra[2], rb[2];            // ring groups (current / next), alternating
+    int4 cc[4];                  // column symbols of the next four groups
+    CorePend pa, pb;             // pinned store data, alternating
+    long long tr_q[kTraceQ];     // (diagnostics: timeline stamps)
+};
+
+// One 16-step sub-block: flow control, then four groups.
+template <bool LOCAL, bool TBL, int MODE>
+__device__ __forceinline__ void core_sub(CoreState& st, CoreLoop& L, CoreCtx& w, const Scores32& sc, const int t0,
+                                         const int T, const bool trace) {
+    // ring space below: the strip below has read what these pushes
+    // overwrite (the last group pushes columns up to t0 + 12 - 60)
+    const int last_col = min(t0 - 48, w.m);
+    if (w.push_on && last_col >= kSkRingG * 4 - 4) wait_ge(w.rcnt_out, last_col - (kSkRingG * 4 - 4) + 1, w.status);
+    // hand-off space: the side wave has read this sub-block's slots' previous groups
+    if (t0 >= 4 * kSkHo && !(GX_SKEW_EXP & 2)) w.tr_ho += wait_ge(w.bcnt, (t0 >> 2) + 4 - kSkHo, w.status);
+    w.hv_sub = (v4i*)&w.ho->v[(t0 >> 2) & (kSkHo - 1)][0][w.lane];
+    if (trace) {
+        const int q = (int)((long long)t0 * (kTraceQ + 1) / T) - 1;
+        const long long now = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+        for (int k = 0; k < kTraceQ; ++k)   // (constant indices: the stamps stay in registers)
+            if (k >= 1 && k == q && L.tr_q[k] == 0) L.tr_q[k] = now;
+        if (t0 == kWave) L.tr_q[0] = now;                  // (the end of the ramp-up)
+    }
+    core_group<LOCAL, TBL, MODE, 0>(st, L.ra, L.rb, L.cc[0], w, sc, t0, L.pa, L.pb);
+    core_group<LOCAL, TBL, MODE, 1>(st, L.rb, L.ra, L.cc[1], w, sc, t0 + 4, L.pb, L.pa);
+    core_group<LOCAL, TBL, MODE, 2>(st, L.ra, L.rb, L.cc[2], w, sc, t0 + 8, L.pa, L.pb);
+    core_group<LOCAL, TBL, MODE, 3>(st, L.rb, L.ra, L.cc[3], w, sc, t0 + 12, L.pb, L.pa);
+    // every ring read up to column t0+20 (incl. the next group's) was issued before this store
+    asm volatile("" ::: "memory");
+    *w.rcnt_in = min(t0 + kSub + 5, w.m + 1);
+}
+
 template <bool LOCAL, bool TBL>
 __device__ void core_wave(const PairDev& P, const int s, const int lane, const Scores32& sc, CoreCtx& w,
                           PairRes* pres) {
@@ -230,80 +272,67 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
     if (TBL) w.c1 = score_table(w.c1, sc);
     // column 0 (algo.rs:204-211): I = S = neg_inf, D = h + i g, score_max
     // max(D, floor); global fills hold V - (i + 0) g
+    // Global fills: lane l >= 1 starts at step 0 on virtual columns 1 - l .. 0
+    // (no per-lane masks in the ramp-up).  Its state starts at "minus
+    // infinity", so virtual columns < 0 stay there and column 0 comes out of
+    // the recurrence exactly: I = S = -inf, D''(i, 0) = max(D''(i-1, 0),
+    // H''(i-1, 0) + h) = h from lane l-1, score_max = D (algo.rs:204-211).
+    // Local fills keep the masked ramp-up (their 0 floor lifts virtual cells).
     CoreState st;
+    int H0;                                       // score_max(i, 0) (shifted for global fills)
     {
         const int D0 = sc.h + i * sc.g;
-        const int H0 = LOCAL ? max(D0, 0) : D0 - i * sc.g;
+        H0 = LOCAL ? max(D0, 0) : D0 - i * sc.g;
+        const bool virt = !LOCAL && lane > 0;
         st.I = LOCAL ? kNeg : kNeg - i * sc.g;
-        st.H = H0;
-        st.Hx = H0 + (LOCAL ? sc.hg : sc.h);
-        st.Dd = H0;                               // (column 0's successor is never read: column 0 is analytic)
+        st.H = virt ? kNeg : H0;
+        st.Hx = virt ? kNeg : H0 + (LOCAL ? sc.hg : sc.h);
+        st.Dd = virt ? kNeg : H0;                 // (lane 0: the successor D''(i+1, 0) = max(h, 2h) = h)
     }
     w.crs = rsrc_of(uniform_ptr(P.ccodes), 4 * (m + 192));
     w.cvoff = 4u * (uint32_t)(64 - lane);
     if (w.push_on) {                              // column 0 of the bottom row: the next strip's first top-left
         if (lane == kWave - 1) {
-            w.rout->dd[0][3] = st.Dd;
-            w.rout->sm[0][3] = st.H;
+            w.rout->dd[0][3] = H0;                // (the delete successor of column 0: H0, see above)
+            w.rout->sm[0][3] = H0;
+            asm volatile("" ::: "memory");
             *w.wcnt_out = 1;
         }
     }
     long long tr_start = 0, tr_first = 0, clk_first = 0;
-    long long tr_q[kTraceQ] = {};
     if (trace) tr_start = __builtin_amdgcn_s_memrealtime();
     w.tr_win += wait_ge(w.wcnt_in, min(4, m) + 1, w.status);
-    v4i ra[2], rb[2];
-    int4 cc[4];                                   // column symbols of the next four groups
-    CorePend pa = {}, pb = {};
+    CoreLoop L = {};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) cc[q] = load_codes(w, 4 * q);
+    for (int q = 0; q < 4; ++q) L.cc[q] = load_codes(w, 4 * q);
     st.Hd = shr1(w.rin->sm[0][3], st.H);          // column 1's top-left: (64 s, 0) for lane 0, lane-1's column 0
-    read_grp(ra, w, sk_grp(1));
+    if (!LOCAL && lane > 0) st.Hd = kNeg;         // (virtual columns)
+    read_grp(L.ra, w, sk_grp(1));
     if (trace) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
     const int T = m + kWave;                      // lane 63 computes column m at step m + 62; pushes run to t = m + 63
-    for (int t0 = 0; t0 < T; t0 += kSub) {
-        // ring space below: the strip below has read what these pushes
-        // overwrite (the last group pushes columns up to t0 + 12 - 60)
-        const int last_col = min(t0 - 48, m);
-        if (w.push_on && last_col >= kSkRingG * 4 - 4) wait_ge(w.rcnt_out, last_col - (kSkRingG * 4 - 4) + 1, w.status);
-        // hand-off space: the side wave has read this sub-block's slots' previous groups
-        if (t0 >= 4 * kSkHo && !(GX_SKEW_EXP & 2)) w.tr_ho += wait_ge(w.bcnt, (t0 >> 2) + 4 - kSkHo, w.status);
-        w.hv_sub = (v4i*)&w.ho->v[(t0 >> 2) & (kSkHo - 1)][0][lane];
-        if (trace) {
-            const int q = (int)((long long)t0 * (kTraceQ + 1) / T) - 1;
-            const long long now = __builtin_amdgcn_s_memrealtime();
-#pragma unroll
-            for (int k = 0; k < kTraceQ; ++k)   // (constant indices: the stamps stay in registers)
-                if (k == q && tr_q[k] == 0) tr_q[k] = now;
-        }
-        // ramp-up (lane l starts at step l) while no lane passes column m;
-        // every lane inside columns 1..m; otherwise masked per lane
-        if (t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1) {
-            core_group<LOCAL, TBL, 1, 0>(st, ra, rb, cc[0], w, sc, t0, pa, pb);
-            core_group<LOCAL, TBL, 1, 1>(st, rb, ra, cc[1], w, sc, t0 + 4, pb, pa);
-            core_group<LOCAL, TBL, 1, 2>(st, ra, rb, cc[2], w, sc, t0 + 8, pa, pb);
-            core_group<LOCAL, TBL, 1, 3>(st, rb, ra, cc[3], w, sc, t0 + 12, pb, pa);
-        } else if (t0 >= kWave && t0 + kSub - 1 <= m - 1) {
-            core_group<LOCAL, TBL, 0, 0>(st, ra, rb, cc[0], w, sc, t0, pa, pb);
-            core_group<LOCAL, TBL, 0, 1>(st, rb, ra, cc[1], w, sc, t0 + 4, pb, pa);
-            core_group<LOCAL, TBL, 0, 2>(st, ra, rb, cc[2], w, sc, t0 + 8, pa, pb);
-            core_group<LOCAL, TBL, 0, 3>(st, rb, ra, cc[3], w, sc, t0 + 12, pb, pa);
-        } else {
-            core_group<LOCAL, TBL, 2, 0>(st, ra, rb, cc[0], w, sc, t0, pa, pb);
-            core_group<LOCAL, TBL, 2, 1>(st, rb, ra, cc[1], w, sc, t0 + 4, pb, pa);
-            core_group<LOCAL, TBL, 2, 2>(st, ra, rb, cc[2], w, sc, t0 + 8, pa, pb);
-            core_group<LOCAL, TBL, 2, 3>(st, rb, ra, cc[3], w, sc, t0 + 12, pb, pa);
-        }
-        // every ring read up to column t0+20 (incl. the next group's) was issued before this store
-        *w.rcnt_in = min(t0 + kSub + 5, m + 1);
-    }
+    // ramp-up (lane l starts at step l) while no lane passes column m; then
+    // every lane inside columns 1..m; then masked per lane.  One loop per
+    // phase, so that the loop-carried registers (ring groups, prefetched
+    // symbols, pinned store data) keep their places across the back-edge
+    // (a merge of differently allocated phases costs copies that wait for
+    // the symbol loads in flight).
+    int t0 = 0;
+    if (!LOCAL)   // (virtual columns: every lane runs from step 0, see the column-0 state above)
+        for (; t0 < T && t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1; t0 += kSub)
+            core_sub<LOCAL, TBL, 0>(st, L, w, sc, t0, T, trace != nullptr);
+    for (; t0 < T && t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1; t0 += kSub)
+        core_sub<LOCAL, TBL, 1>(st, L, w, sc, t0, T, trace != nullptr);
+    for (; t0 < T && t0 >= kWave && t0 + kSub - 1 <= m - 1; t0 += kSub)
+        core_sub<LOCAL, TBL, 0>(st, L, w, sc, t0, T, trace != nullptr);
+    for (; t0 < T; t0 += kSub)
+        core_sub<LOCAL, TBL, 2>(st, L, w, sc, t0, T, trace != nullptr);
     if (ok && i == n) pres->end_SM = st.H;        // score_max(n, m) (algo.rs:308, 331)
     if (trace && lane == 0) {
         StripTrace tr;
         tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
         tr.wait_in = (int)w.tr_win;
         tr.clk = __builtin_amdgcn_s_memtime() - clk_first;
-        for (int q = 0; q < kTraceQ; ++q) tr.t_q[q] = tr_q[q];
+        for (int q = 0; q < kTraceQ; ++q) tr.t_q[q] = L.tr_q[q];
         tr.t_q[kTraceQ - 2] = w.tr_ho;            // (layout 3: hand-off space waits; the side wave writes wait_out
         trace[s].t_start = tr.t_start;            // and the last stamp, its own waits and end)
         trace[s].t_first = tr.t_first;
@@ -436,6 +465,7 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, SideCtx
 #pragma unroll
                 for (int k = 0; k < 3; ++k) sub[q][k] = hv[(3 * q + k) * kWave];
         }
+        asm volatile("" ::: "memory");
         *w.bcnt = (t0 >> 2) + 4;                  // (reads issued first: LDS keeps the order)
         if (w.diag_idle) continue;                // (GX_DEBUG_FLAGS & 2: timing only, wrong results)
         if (t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1) {

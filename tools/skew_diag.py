@@ -28,9 +28,11 @@ def summarize(path, m, W):
     intra = [lags[k] for k in range(len(lags)) if (k + 1) % W] or [0.0]
     inter = [lags[k] for k in range(len(lags)) if (k + 1) % W == 0] or [0.0]
     clk = [int(r["clk"]) / max(d, 1e-9) for r, d in zip(rows, dur)]
+    ramp = [(us(r["q1"]) - us(r["t_first"])) * 1e3 / 64 for r in rows if int(r["q1"]) > 0]
     steps = m + 64
     print(f"    strips {len(rows)}: pace {statistics.mean(dur) * 1e3 / steps:.1f} ns/step "
           f"(min {min(dur) * 1e3 / steps:.1f}, max {max(dur) * 1e3 / steps:.1f}); "
+          f"ramp-up {statistics.mean(ramp) if ramp else 0:.1f} ns/step; "
           f"lag intra {statistics.mean(intra):.2f} us = {statistics.mean(intra) * 1e3 / (statistics.mean(dur) * 1e3 / steps):.0f} steps, "
           f"inter {statistics.mean(inter):.2f} us; clock {statistics.mean(clk):.0f} MHz; "
           f"core waits: input {statistics.mean(int(r['wait_in']) for r in rows):.0f} hand-off space "
