@@ -55,8 +55,9 @@
 namespace gx {
 
 #ifndef GX_SKEW_EXP
-#define GX_SKEW_EXP 0            // (timing experiments only: tools/skew_exp.sh)
+#define GX_SKEW_EXP 0            // (timing experiments only, wrong results: tools/skew_exp.sh)
 #endif
+typedef __attribute__((address_space(3))) v4i lds_v4i;
 constexpr int kSkRingG = 64;     // ring groups per strip boundary (256 columns)
 constexpr int kSkHo = 8;         // core -> side hand-off ring depth (4-step groups)
 
@@ -108,11 +109,11 @@ __device__ __forceinline__ void core_step(CoreState& st, const int rdd, const in
 struct CoreCtx {
     __amdgpu_buffer_rsrc_t crs;  // the pair's int32 column symbols (PairDev.ccodes)
     uint32_t cvoff;              // 4 (64 - lane): this lane's column of step 0, less one
-    int4* push_base;             // lane 63: the ring below's dd[0]; other lanes (or no consumer): their sink slot
-    int push_m16;                // lane 63: 16 (a ring group's bytes); other lanes: 0
+    uint32_t push_base;          // LDS address; lane 63: the ring below's dd[0]; other lanes (or no consumer): their sink slot
+    uint32_t push_m16;           // lane 63: 16 (a ring group's bytes); other lanes: 0
     lds_int* pcnt;               // wcnt_out (no consumer: a sink)
-    const int4* rd_base;         // lane 0: the ring above's dd[0]; other lanes: a zero block
-    int rd_m16;                  // lane 0: 16; other lanes: 0
+    uint32_t rd_base;            // LDS address; lane 0: the ring above's dd[0]; other lanes: a zero block
+    uint32_t rd_m16;             // lane 0: 16; other lanes: 0
     const SkRing* rin;
     SkRing* rout;
     lds_int* wcnt_in;            // columns the strip above published
@@ -131,7 +132,7 @@ struct CoreCtx {
 
 // Lane 0 reads ring group G (dd, then sm 1 KB on), the other lanes a zero block.
 __device__ __forceinline__ void read_grp(v4i (&r)[2], const CoreCtx& w, int G) {
-    const v4i* p = (const v4i*)((const char*)w.rd_base + G * w.rd_m16);
+    const lds_v4i* p = (const lds_v4i*)(uintptr_t)(w.rd_base + __umul24((uint32_t)G, w.rd_m16));
     r[0] = p[0];
     r[1] = p[kSkRingG];
 }
@@ -141,9 +142,10 @@ __device__ __forceinline__ int4 load_codes(const CoreCtx& w, int t) {
     return make_int4(x[0], x[1], x[2], x[3]);
 }
 
-// One 4-step group of the core wave.  MODE 0: full; 1: ramp-up (lanes past
-// the step not started yet: each step under `lane <= t`, so their column-0
-// state stays); 2: ramp-down (lanes past column m keep their state).
+// One 4-step group of the core wave.  MODE 0: every lane steps; 2: per-lane
+// selects (ramp-down: lanes past column m keep their state; local ramp-up:
+// lanes not started keep their column-0 state.  Selects measured 72 ns a
+// step against 100 for a branch per step).
 // A group's LDS store data (hand-off I, S, D; push dd, sm) stays allocated
 // through the next group (pinned there), so the next group's results never
 // reuse registers an LDS store may still be reading (which would cost a wait
@@ -170,14 +172,11 @@ __device__ __forceinline__ void core_group(CoreState& st, const v4i (&cur)[2], v
     const int c2[4] = {cc.x, cc.y, cc.z, cc.w};
 #pragma unroll
     for (int U = 0; U < 4; ++U) {
-        if (MODE == 1) {
-            if (w.lane <= t + U) core_step<LOCAL, TBL, false>(st, cd[U], cs[U], c2[U], true, w.c1, sc, oI[U], oS[U], oD[U]);
-        } else {
-            // (global fills run the virtual columns <= 0 too: only columns > m stop)
-            const int c = t + U - w.lane;   // column - 1
-            const bool act = MODE == 2 ? (LOCAL ? (unsigned)c < (unsigned)w.m : c < w.m) : true;
-            core_step<LOCAL, TBL, MODE == 2>(st, cd[U], cs[U], c2[U], act, w.c1, sc, oI[U], oS[U], oD[U]);
-        }
+        // MODE 2: selects per lane (global fills run the virtual columns <= 0
+        // too: only columns > m stop; local fills also hold lanes not started)
+        const int c = t + U - w.lane;   // column - 1
+        const bool act = MODE == 2 ? (LOCAL ? (unsigned)c < (unsigned)w.m : c < w.m) : true;
+        core_step<LOCAL, TBL, MODE == 2>(st, cd[U], cs[U], c2[U], act, w.c1, sc, oI[U], oS[U], oD[U]);
         if (U < 3) { qdd[U] = st.Dd; qsm[U] = st.H; }
     }
     // the symbols of this group's steps four groups on, into the registers
@@ -204,18 +203,19 @@ __device__ __forceinline__ void core_group(CoreState& st, const v4i (&cur)[2], v
     // compiler sees and counts the stores: no exec change, no branch.
     mine.v[3] = v4i{pdd, qdd[0], qdd[1], qdd[2]};
     mine.v[4] = v4i{psm, qsm[0], qsm[1], qsm[2]};
-    if (MODE == 0 || (t >= 64 && t - 63 <= w.m)) {   // (full groups: always inside; no consumer: all into the sink)
-        v4i* a = (v4i*)((char*)w.push_base + sk_grp(t - 63) * w.push_m16);
+    if (!(GX_SKEW_EXP & 8) && (MODE == 0 || (t >= 64 && t - 63 <= w.m))) {   // (full groups: always inside; no consumer: all into the sink)
+        lds_v4i* a = (lds_v4i*)(uintptr_t)(w.push_base + __umul24((uint32_t)sk_grp(t - 63), w.push_m16));
+        const int cnt = (MODE == 0 ? t - 60 : min(t - 60, w.m)) + 1;   // (MODE 0: t - 60 < m)
         a[0] = mine.v[3];
         a[kSkRingG] = mine.v[4];
         asm volatile("" ::: "memory");
-        *w.pcnt = (MODE == 0 ? t - 60 : min(t - 60, w.m)) + 1;   // (MODE 0: t - 60 < m)
+        *w.pcnt = cnt;
     }
     if (__builtin_amdgcn_readfirstlane(seen_v) < need) {       // the strip above was behind: wait, re-read
         w.tr_win += wait_ge(w.wcnt_in, need, w.status);
         // re-read into the same registers and wait for it here (one asm: no
         // copies on the fast path, nothing pending after the join)
-        const uint32_t a = lds_addr(w.rd_base) + (uint32_t)(sk_grp(t + 5) * w.rd_m16);
+        const uint32_t a = w.rd_base + __umul24((uint32_t)sk_grp(t + 5), w.rd_m16);
         asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:%3\n\ts_waitcnt lgkmcnt(0)"
                      : "+v"(nxt[0]), "+v"(nxt[1])
                      : "v"(a), "i"(kSkRingG * 16)
@@ -310,8 +310,9 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
     read_grp(L.ra, w, sk_grp(1));
     if (trace) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
     const int T = m + kWave;                      // lane 63 computes column m at step m + 62; pushes run to t = m + 63
-    // ramp-up (lane l starts at step l) while no lane passes column m; then
-    // every lane inside columns 1..m; then masked per lane.  One loop per
+    // ramp-up (global: every lane steps, on virtual columns until its column
+    // 1 at step l; local: per-lane selects) while no lane passes column m;
+    // then every lane inside columns 1..m; then masked per lane.  One loop per
     // phase, so that the loop-carried registers (ring groups, prefetched
     // symbols, pinned store data) keep their places across the back-edge
     // (a merge of differently allocated phases costs copies that wait for
@@ -321,7 +322,7 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
         for (; t0 < T && t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1; t0 += kSub)
             core_sub<LOCAL, TBL, 0>(st, L, w, sc, t0, T, trace != nullptr);
     for (; t0 < T && t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1; t0 += kSub)
-        core_sub<LOCAL, TBL, 1>(st, L, w, sc, t0, T, trace != nullptr);
+        core_sub<LOCAL, TBL, 2>(st, L, w, sc, t0, T, trace != nullptr);
     for (; t0 < T && t0 >= kWave && t0 + kSub - 1 <= m - 1; t0 += kSub)
         core_sub<LOCAL, TBL, 0>(st, L, w, sc, t0, T, trace != nullptr);
     for (; t0 < T; t0 += kSub)
@@ -643,10 +644,10 @@ __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const
                 w.status = band_counter + 1;
                 w.push_on = has_consumer;
                 const bool pl = has_consumer && lane == kWave - 1;
-                w.push_base = pl ? (int4*)rings[k + 1].dd[0] : &push_sink[lane];
+                w.push_base = lds_addr(pl ? (const void*)rings[k + 1].dd[0] : (const void*)&push_sink[lane]);
                 w.push_m16 = pl ? 16 : 0;
                 w.pcnt = has_consumer ? w.wcnt_out : (lds_int*)&push_sink_cnt;
-                w.rd_base = lane == 0 ? (const int4*)rings[k].dd[0] : zero_blk;
+                w.rd_base = lds_addr(lane == 0 ? (const void*)rings[k].dd[0] : (const void*)zero_blk);
                 w.rd_m16 = lane == 0 ? 16 : 0;
                 core_wave<LOCAL, TBL>(P, s, lane, sc, w, pres + p);
             }

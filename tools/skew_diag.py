@@ -51,6 +51,8 @@ def main():
              ("30000x30000", a30, b30)]
     if os.environ.get("SKEW_DIAG_QUICK"):
         cases = cases[:2]
+    if os.environ.get("SKEW_DIAG_LONE"):   # (a lone strip: for experiment builds without pushes)
+        cases = cases[:1]
     os.environ["GX_LAYOUT"] = "3"
     for W in widths:
         os.environ["GX_BAND_WAVES"] = str(W)
