@@ -652,7 +652,12 @@ struct PairHost {
 // ms, eight 10.6 vs 15.9 ms; profiles/r01o_round_sweep.txt,
 // profiles/r01d_layouts.txt).  The latency layout is 3 for untracked fills
 // with h <= 0 (its recurrences fold the gap opening onto score_max, which is
-// exact only then), else the column step.
+// exact only then) when it is predicted faster than the column step, else
+// the column step.  A single pair of S 64-row strips and m columns takes
+// about (m + 80 S) x 62 ns on layout 3 (a strip starts ~80 steps after the
+// one above) and (m + 7 S) x 113 ns on the column step:
+// layout 3 for n below about 0.78 m (Covid 29,903 x 29,882: 4.72 vs 4.63 ms;
+// 64 x 30,000: 1.6 vs 3.4).
 // Layout 3 needs h <= 0 (the folded gap opening) and, for the virtual
 // columns of its global ramp-up (values drift from -2^30 by up to 64 steps of
 // |g| + |h| + |s|), small penalties.
@@ -669,7 +674,13 @@ static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int 
         strips64 += ceil_div((int)h.n, kStripRows1);
     }
     const bool cs_ok = span < (1LL << 29) && mmax + 128 < (1u << 24);   // landing keys hold E + 64 in 24 bits
-    const int lat = skew_ok(sc, track) ? 3 : cs_ok ? 1 : 0;
+    double est1 = 0, est3 = 0;   // the launch's slowest pair on each layout (ns)
+    for (const PairHost& h : ph) {
+        const double S = (double)ceil_div((int)h.n, kStripRows1), m = (double)h.m;
+        est1 = std::max(est1, (m + 7 * S) * 113.0);
+        est3 = std::max(est3, (m + 80 * S) * 62.0);
+    }
+    const int lat = skew_ok(sc, track) && (!cs_ok || est3 < est1) ? 3 : cs_ok ? 1 : 0;
     if (const char* e = getenv("GX_LAYOUT"); e && *e) {
         const int want = atoi(e);
         if (want == 3) return skew_ok(sc, track) ? 3 : cs_ok ? 1 : 0;

@@ -66,7 +66,7 @@ def _check_result(r, steps, c, tag):
         assert len(steps) == c["n_steps"] and _digest(steps) == c["alignment_sha256"], tag
 
 
-@pytest.mark.parametrize("layout", ["auto", "lay0", "cs1", "cs2"])
+@pytest.mark.parametrize("layout", ["auto", "lay0", "cs1", "cs2", "skew"])
 @pytest.mark.parametrize("tracked", [True, False], ids=["tracked", "untracked"])
 @pytest.mark.parametrize("case", range(4), ids=[c["name"] for c in _large_cases()])
 def test_large_table_plane_sums(gx, ctx, monkeypatch, case, tracked, layout):
@@ -76,12 +76,15 @@ def test_large_table_plane_sums(gx, ctx, monkeypatch, case, tracked, layout):
     the single-pair layout (column step, int32 planes); lay0 = the
     anti-diagonal layout, whose untracked tables keep compact byte planes;
     cs1 / cs2 = the column step as one wave per strip / as the split core +
-    side waves (gx_cs2.hip, untracked fills only)."""
+    side waves (gx_cs2.hip, untracked fills only); skew = layout 3
+    (gx_skew.hip, untracked fills; tracked ones fall back to the column step)."""
     if layout == "lay0":
         monkeypatch.setenv("GX_LAYOUT", "0")
     if layout in ("cs1", "cs2"):
         monkeypatch.setenv("GX_LAYOUT", "1")
         monkeypatch.setenv("GX_CS2", "1" if layout == "cs2" else "0")
+    if layout == "skew":
+        monkeypatch.setenv("GX_LAYOUT", "3")
     c = _large_cases()[case]
     a, b = _large_inputs()[c["name"].split("/")[0]]
     cont = gx.SequenceContainer([gx.Sequence("a", a.decode()), gx.Sequence("b", b.decode())])
@@ -91,6 +94,8 @@ def test_large_table_plane_sums(gx, ctx, monkeypatch, case, tracked, layout):
         assert info["layout"] == 0 and info["plane_bytes_per_cell"] == (12 if tracked else 3), info
     if layout in ("cs1", "cs2"):
         assert info["layout"] == (2 if layout == "cs2" and not tracked else 1), info
+    if layout == "skew":
+        assert info["layout"] == (1 if tracked else 3), info
     assert table.plane_sums() == [int(x) for x in c["plane_sums"]], (c["name"], info)
     if tracked:
         assert mam == c["matches_at_max"] and table.info()["max_cell"] == tuple(c["max_cell"])
