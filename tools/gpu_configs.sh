@@ -14,6 +14,9 @@ run config2_covid --workload covid
 run config3_brca2 --workload brca2
 run config4_allvsall --workload allvsall
 run config4_allvsall_planes --workload allvsall --planes
+# config 4 on 8 GPUs, predicted from this GPU: each simulated rank's LPT share
+# timed alone (bench.py --simulate-world)
+run config4_sim8 --workload allvsall --simulate-world 8
 # config 5 as stated: 1024 pairs per length (batches beyond the free HBM run
 # in chunks through the same buffers; 16k: 825 GB, 64k: 13 TB of compact planes)
 run config5_L1024 --length 1024 --pairs-per-gpu 1024 --single-pair-steps 0

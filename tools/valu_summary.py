@@ -32,17 +32,28 @@ SIMDS = 256 * 4
 FILL_WAVES_PER_SIMD = 4
 
 
-def counters(d):
+def counters(d, skip=1):
+    """Per-launch averages of the batch fill's counters, the process's first
+    pass excluded (`skip` dispatches: its first launch is cold, code object
+    load and page faults, 903 ms against 24 in the r04 trace; a pass of the
+    overlapped pipeline is two launches of unequal size, so whole passes are
+    averaged)."""
     db = glob.glob(os.path.join(d, "**", "*.db"), recursive=True)[0]
     c = sqlite3.connect(db)
-    out = {}
-    for kname, ctr, avg, dur in c.execute(
-            "select kernel_name, counter_name, avg(value), avg(duration) from counters_collection "
-            "group by kernel_name, counter_name"):
+    rows = {}
+    for kname, disp, ctr, val, dur in c.execute(
+            "select kernel_name, dispatch_id, counter_name, value, duration from counters_collection"):
         if "fill_kernel" in kname or "fill_pk_kernel" in kname:
-            out.setdefault(kname, {"duration_ns": dur})[ctr] = avg
-    k = max(out, key=lambda n: out[n]["duration_ns"])   # the batch fill: the longest fill launch
-    return k, out[k]
+            rows.setdefault(kname, {}).setdefault(disp, {"duration_ns": dur})[ctr] = val
+    k = max(rows, key=lambda n: sum(v["duration_ns"] for v in rows[n].values()))   # the batch fill
+    disps = sorted(rows[k])
+    if len(disps) > skip:
+        disps = disps[skip:]
+    out = {}
+    for ctr in rows[k][disps[0]]:
+        out[ctr] = sum(rows[k][x][ctr] for x in disps) / len(disps)
+    out["launches_averaged"] = len(disps)
+    return k, out
 
 
 def probe_cpi(probe, waves=FILL_WAVES_PER_SIMD):
@@ -84,9 +95,9 @@ def main():
                        "probe": "valu_probe (chip wall time x clock x SIMDs / instructions)"}}
     cases = [c for c in ("planes", "noplanes") if os.path.isdir(os.path.join(src, c))]
     for case in cases:
-        k, v = counters(os.path.join(src, case))
         with open(os.path.join(src, f"{case}.json")) as f:
             bench = json.loads(f.read().strip().splitlines()[-1])
+        k, v = counters(os.path.join(src, case), int(bench.get("fill_launch", {}).get("groups", 1) or 1))
         # a pass may be two fill launches: the counters are per
         # launch (rocprofv3 --pmc serialises dispatches), so per launch cells
         groups = int(bench.get("fill_launch", {}).get("groups", 1) or 1)
