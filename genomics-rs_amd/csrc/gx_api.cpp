@@ -2457,13 +2457,15 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
     size_t nmax_b = 0;
     for (const PairHost& h : dph) nmax_b = std::max(nmax_b, h.n);
     // (long pairs only: a short pair's walk is short; and both groups must
-    // fill the grid on the twin fill, or the attempt falls back)
+    // fill the grid on the twin fill, or the attempt falls back.  1024 x 4k:
+    // 14.9 ms a step overlapped against 10.8 plain; 1024 x 16k 116.8 against
+    // 145: profiles/r04_config5_*.json, r02k_config5_*.json)
     // (local batches from 64 pairs: at 32 related 30k pairs the split launches
     // fill worse than the walk they hide, 27.2 vs 21.6 ms a step; GX_OVERLAP=1
     // forces it from 16 pairs, GX_OVERLAP=0 turns it off)
     const char* ov = getenv("GX_OVERLAP");
     const bool ov_force = ov && !strcmp(ov, "1");
-    if (!track && planes && idx.size() >= 16 && (nmax_b >= 4096 || ov_force) && !pool_poison() &&
+    if (!track && planes && idx.size() >= 16 && (nmax_b >= 16384 || ov_force) && !pool_poison() &&
         !(ov && !strcmp(ov, "0")) && (!is_local || idx.size() >= 64 || ov_force)) {
         const int orc = batch_core_overlap(ctx, ph, proc, hs, sc, is_local, planes, nsteps, walks, fill_ms, chars_dev, off1, off2,
                                            alpha, idx);

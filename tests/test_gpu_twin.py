@@ -350,7 +350,7 @@ def test_twin_overlapped_global(gx, ctx, oracle, monkeypatch, launch_env):
     checksums and results (gx_staged_pass_results), the last pass's
     alignments, against the oracle; the pipeline must have run (groups == 2)."""
     monkeypatch.setenv("GX_LAYOUT", "0")
-    monkeypatch.setenv("GX_OVERLAP", "1")   # (by default from n >= 4,096)
+    monkeypatch.setenv("GX_OVERLAP", "1")   # (by default from n >= 16,384)
     if launch_env == "w4_grid3":   # bands queued for three workgroups per launch: the two launches interleave
         monkeypatch.setenv("GX_BAND_WAVES", "4")
         monkeypatch.setenv("GX_FILL_GRID", "3")

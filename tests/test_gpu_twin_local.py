@@ -138,7 +138,7 @@ def test_local_twin_bound_binds(gx, ctx, oracle, monkeypatch):
 
 
 def test_local_twin_overlapped(gx, ctx, oracle, monkeypatch):
-    """A long-pair local batch (>= 16 pairs, n >= 4,096) takes the overlapped
+    """A long-pair local batch (>= 16 pairs, n >= 16,384) takes the overlapped
     two-group pipeline (gx_api.cpp batch_core_overlap): each pass's walk runs
     beside the next pass's fill and reads its start cells (the last maxima,
     finalize_kernel's PairRes) on the device.  Three passes, every result of
