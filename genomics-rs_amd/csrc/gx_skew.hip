@@ -22,10 +22,15 @@
 //     cell (algo.rs:351-400 priority S > I > D), stores the three int32 score
 //     planes straight from the registers it read, the code words and the
 //     skeleton, and tracks the local last maximum.
-// The cell above (i-1, j) is lane l-1's previous step (DPP wave_shr:1; lane 0
-// takes it from the ring the strip above's core wave fills, or the band's I/O
-// wave at a band boundary), the top-left (i-1, j-1) the one before (kept from
-// the previous step's move).  Global fills keep V'' = V - (i + j) g (DESIGN.md
+// The cell above (i-1, j) is lane l-1's previous step (DPP wave_shr:1 with
+// bound_ctrl, folded into one v_add_u32_dpp with a register that holds lane
+// 0's ring value and 0 elsewhere: lane 0 takes the cell from the ring the
+// strip above's core wave fills, or the band's I/O wave at a band boundary),
+// the top-left (i-1, j-1) the one before (kept from the previous step's move).
+// Global fills start every lane at step 0 on virtual columns <= 0 whose
+// "minus infinity" state yields column 0 exactly (no per-lane masks in the
+// ramp-up); local fills mask the ramp-up with selects.  Measured costs and
+// the floor of this design: DESIGN.md 4.5.  Global fills keep V'' = V - (i + j) g (DESIGN.md
 // 4.3) and, with h <= 0, fold both gap recurrences onto score_max:
 //         I''(i,j)   = max(I''(i,j-1), H''(i,j-1) + h)        (algo.rs:231-236)
 //         D''(i+1,j) = max(D''(i,j),   H''(i,j)   + h)        (algo.rs:238-243)
