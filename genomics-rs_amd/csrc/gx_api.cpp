@@ -230,6 +230,15 @@ struct gx_context {
         hipEvent_t fb = nullptr, fe = nullptr, tb = nullptr, te = nullptr, fdone = nullptr, tdone = nullptr;
         TbOut out;
         DevBuf held[4];                      // traceback buffers the copy stream still reads (until tb_collect)
+        // the walk's job table of this slot's last pass, kept on the device:
+        // a staged run's passes repeat it, so later passes skip its upload
+        // (a 120 KB copy cost ~130 us on the fill stream, 1024 x 1k)
+        void* tjob = nullptr;
+        size_t tjob_cap = 0;
+        std::vector<TbDev> tjob_last;
+        void* fdesc = nullptr;               // ... and the fill's descriptor block (run_fill)
+        size_t fdesc_cap = 0;
+        std::vector<char> fdesc_last;
     } slots[4];   // 0, 1: pipelined steps by parity (overlapped batches: group A's fills and the walks); 2, 3: group B's fills
     int last_lay = 0, last_W = 0, last_pbytes = 0;   // the last fill launch (gx_fill_info)
     int last_chunks = 1;                             // chunks of the last staged / batch call
@@ -393,6 +402,8 @@ extern "C" void gx_context_destroy(gx_context* ctx) {
             if (b->p) (void)hipHostFree(b->p);
         for (hipEvent_t e : {s.fb, s.fe, s.tb, s.te, s.fdone, s.tdone})
             if (e) (void)hipEventDestroy(e);
+        if (s.tjob) (void)hipFree(s.tjob);
+        if (s.fdesc) (void)hipFree(s.fdesc);
     }
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -692,6 +703,7 @@ static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int 
 struct FillJob {
     // device buffers (owned by the job until released)
     DevBuf chars, planes, codes, skel, feed, progress, sres, pres, pairs, counter, ccodes;
+    bool pairs_borrowed = false;   // pairs is a pipeline slot's cached descriptor block (not pooled)
     std::vector<PairDev> pd;
     std::vector<PairRes> res;
     int W = 4;
@@ -728,6 +740,7 @@ static void unshift_results(FillJob& j) {
 }
 
 static void job_release(gx_context* ctx, FillJob& j) {
+    if (j.pairs_borrowed) { j.pairs = DevBuf{}; j.pairs_borrowed = false; }
     pool_put(ctx, j.chars); pool_put(ctx, j.planes); pool_put(ctx, j.codes); pool_put(ctx, j.feed);
     pool_put(ctx, j.progress); pool_put(ctx, j.sres); pool_put(ctx, j.pres); pool_put(ctx, j.pairs);
     pool_put(ctx, j.counter); pool_put(ctx, j.skel); pool_put(ctx, j.ccodes);
@@ -1022,9 +1035,15 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     if (codes && (rc = pool_get(ctx, code_elems * sizeof(uint32_t), &job.codes))) return rc;
     if ((rc = pool_get(ctx, std::max<size_t>(skel_elems, 1) * sizeof(int), &job.skel))) return rc;
     if ((rc = pool_get(ctx, std::max<size_t>(feed_recs, 1) * sizeof(Rec), &job.feed))) return rc;
-    if ((rc = pool_get(ctx, std::max<size_t>(prog_elems, 1) * sizeof(int), &job.progress))) return rc;
     if ((rc = pool_get(ctx, std::max(strips, 1) * sizeof(StripRes), &job.sres))) return rc;
-    if ((rc = pool_get(ctx, P * sizeof(PairRes), &job.pres))) return rc;
+    // one buffer [PairRes x P | band counter + status (64 B) | band progress]:
+    // one memset before the launch, one copy of the results and status after
+    // it (each small copy or memset on the stream costs a runtime round trip
+    // of ~100 us between a batch's fill and its walk, profiles: r04 1024 x 1k)
+    const size_t res_bytes = P * sizeof(PairRes), prog_bytes = std::max<size_t>(prog_elems, 1) * sizeof(int);
+    if ((rc = pool_get(ctx, res_bytes + 64 + prog_bytes, &job.pres))) return rc;
+    int* const counter = (int*)((char*)job.pres.p + res_bytes);
+    int* const progress = counter + 16;
     // band queue order, stored after the pair descriptors: band-major ("round"
     // order: band 0 of every pair, then band 1, ...; a band's predecessor in its
     // pair is always dequeued before it, so a waiting band is never waiting on
@@ -1047,8 +1066,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                 if (lb < job.pd[p].bands) { order.push_back((int)p); order.push_back(lb); }
     }
     const size_t ord_bytes = align_up(order.size() * sizeof(int), 16);   // keeps the PairRes staging 16-B aligned
-    if ((rc = pool_get(ctx, P * sizeof(PairDev) + ord_bytes, &job.pairs))) return rc;
-    if ((rc = pool_get(ctx, 64, &job.counter))) return rc;
+    if (slot < 0 && (rc = pool_get(ctx, P * sizeof(PairDev) + ord_bytes, &job.pairs))) return rc;
     // -- chars upload
     const uint8_t* cbase = chars_dev;
     if (!chars_dev) {
@@ -1074,7 +1092,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         d.codes = codes ? (uint32_t*)job.codes.p + co[p] : nullptr;
         d.skel = (int*)job.skel.p + so[p];
         d.feed = (Rec*)job.feed.p + fo[p];
-        d.progress = (int*)job.progress.p + gofs[p];
+        d.progress = progress + gofs[p];
     }
     // layout 3 reads each lane's column symbols from an int32 copy (gx_skew.hip)
     if (lay == 3) {
@@ -1097,12 +1115,38 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     if (!pin) return fail(GX_ENOMEM, "pinned staging buffer");
     memcpy(pin, job.pd.data(), P * sizeof(PairDev));
     if (!order.empty()) memcpy(pin + P * sizeof(PairDev), order.data(), order.size() * sizeof(int));
-    HIPCHK(hipMemcpyAsync(job.pairs.p, pin, P * sizeof(PairDev) + ord_bytes, hipMemcpyHostToDevice, fs));
-    HIPCHK(hipMemsetAsync(job.progress.p, 0, std::max<size_t>(prog_elems, 1) * sizeof(int), fs));
+    const size_t dbytes = P * sizeof(PairDev) + ord_bytes;
+    if (slot < 0) {
+        HIPCHK(hipMemcpyAsync(job.pairs.p, pin, dbytes, hipMemcpyHostToDevice, fs));
+    } else {
+        // pipelined passes repeat their descriptors: the slot pair's cached
+        // device copies are looked up first and uploaded only on a change
+        // (the copy engine serialises an upload behind the previous pass's
+        // record copy, ~0.2 ms on a 1024 x 1k step).  A cache is rewritten
+        // on this stream only, after every fill that read it.
+        int hit = -1;
+        for (int x : {slot, slot ^ 1}) {
+            const auto& sl = ctx->slots[x];
+            if (sl.fdesc && sl.fdesc_last.size() == dbytes && !memcmp(sl.fdesc_last.data(), pin, dbytes)) { hit = x; break; }
+        }
+        if (hit < 0) {
+            auto& sl = ctx->slots[slot];
+            if (sl.fdesc_cap < dbytes) {
+                if (sl.fdesc) (void)hipFree(sl.fdesc);
+                sl.fdesc = nullptr; sl.fdesc_cap = 0; sl.fdesc_last.clear();
+                if (hipMalloc(&sl.fdesc, dbytes) != hipSuccess) { sl.fdesc = nullptr; return fail(GX_ENOMEM, "fill descriptors"); }
+                sl.fdesc_cap = dbytes;
+            }
+            sl.fdesc_last.assign(pin, pin + dbytes);
+            HIPCHK(hipMemcpyAsync(sl.fdesc, pin, dbytes, hipMemcpyHostToDevice, fs));
+            hit = slot;
+        }
+        job.pairs = DevBuf{ctx->slots[hit].fdesc, ctx->slots[hit].fdesc_cap};
+        job.pairs_borrowed = true;
+    }
     // layout 3 hands band rows over in tagged granules (gx_skew.hip io_wave_tag): valid once written
     if (lay == 3 && feed_recs > 0) HIPCHK(hipMemsetAsync(job.feed.p, 0, feed_recs * sizeof(Rec), fs));
-    HIPCHK(hipMemsetAsync(job.counter.p, 0, 64, fs));
-    HIPCHK(hipMemsetAsync(job.pres.p, 0, P * sizeof(PairRes), fs));
+    HIPCHK(hipMemsetAsync(job.pres.p, 0, res_bytes + 64 + prog_bytes, fs));
     // twin workgroups: as many per CU as fit 16 waves (the twin kernels hold
     // up to 128 VGPRs: 4 waves per SIMD)
     const int per_cu = (twin && !getenv("GX_FILL_GRID")) ? std::max(1, 16 / (Wf + 1)) : 1;
@@ -1121,17 +1165,17 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     if (bands > 0 && twin)
         HIPCHK(launch_fill_pk(Wf, (planes ? (w16 ? 2 : 1) : 0) + (twin_tbl ? 4 : 0) + (job.nocodes ? 8 : 0) +
                                   (job.noskel ? 16 : 0) + (is_local ? 32 : 0),
-                              (const PairDev*)job.pairs.p, (int)P, (int)tw.size(), bands, (int*)job.counter.p,
+                              (const PairDev*)job.pairs.p, (int)P, (int)tw.size(), bands, counter,
                               (PairRes*)job.pres.p, (StripRes*)job.sres.p, scl, grid, fs));
     else if (bands > 0 && lay == 3)
         HIPCHK(launch_fill_skew(W, is_local != 0, planes, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
-                                (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
+                                counter, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
     else if (bands > 0 && cs2)
         HIPCHK(launch_fill_cs2(W, is_local != 0, planes, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
-                               (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
+                               counter, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
     else if (bands > 0)
         HIPCHK(launch_fill(W, lay, is_local != 0, planes ? (d8 ? 2 : 1) : 0, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
-                           (int*)job.counter.p, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
+                           counter, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
     HIPCHK(hipEventRecord(eve, fs));   // evb..eve brackets the fill kernel alone
     if (ctx->sums_dst && planes && bands > 0) {   // staged checksum run: this pass's plane sums
         HIPCHK(enqueue_plane_sums(ctx, job, sc, ctx->sums_dst, fs));
@@ -1150,8 +1194,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     int status[2] = {0, 0};
     PairRes* pin_res = (PairRes*)(pin + P * sizeof(PairDev) + ord_bytes);
     int* pin_status = (int*)(pin + P * (sizeof(PairDev) + sizeof(PairRes)) + ord_bytes);
-    HIPCHK(hipMemcpyAsync(pin_res, job.pres.p, P * sizeof(PairRes), hipMemcpyDeviceToHost, fs));
-    HIPCHK(hipMemcpyAsync(pin_status, job.counter.p, sizeof status, hipMemcpyDeviceToHost, fs));
+    HIPCHK(hipMemcpyAsync(pin_res, job.pres.p, res_bytes + sizeof status, hipMemcpyDeviceToHost, fs));   // (+ status)
     job.pin_res = pin_res;
     job.pin_status = pin_status;
     job.slot = slot;
@@ -1461,16 +1504,22 @@ static int run_traceback(gx_context* ctx, const std::vector<const FillJob*>& jv,
         stot += (size_t)pdv[p]->strips;
         max_strips = std::max(max_strips, pdv[p]->strips);
     }
-    DevBuf recs, seg, jb, cnt;
+    // one device block cnt | seg | recs, as the pinned host block it is
+    // copied into (one copy: each small copy on a stream costs a runtime
+    // round trip, ~100 us between a short batch's walk and its records)
+    DevBuf tbb, jb;
     int rc;
-    auto cleanup = [&]() { pool_put(ctx, recs); pool_put(ctx, seg); pool_put(ctx, jb); pool_put(ctx, cnt); };
+    auto cleanup = [&]() { pool_put(ctx, tbb); pool_put(ctx, jb); };
     const int SR = strip_rows(job.lay);
-    if ((rc = pool_get(ctx, std::max<size_t>(stot, 1) * SR * sizeof(uint32_t), &recs)) ||
-        (rc = pool_get(ctx, std::max<size_t>(stot, 1) * 4 * sizeof(int), &seg)) ||
-        (rc = pool_get(ctx, P * sizeof(TbDev), &jb)) || (rc = pool_get(ctx, P * 4 * sizeof(int), &cnt))) {
+    const size_t nc = 4 * P, nsg = 4 * std::max<size_t>(stot, 1), nhr = std::max<size_t>(stot, 1) * SR;
+    if ((rc = pool_get(ctx, (nc + nsg) * sizeof(int) + nhr * sizeof(uint32_t), &tbb)) ||
+        (slot < 0 && (rc = pool_get(ctx, P * sizeof(TbDev), &jb)))) {
         cleanup();
         return rc;
     }
+    int* const cnt_d = (int*)tbb.p;
+    int* const seg_d = cnt_d + nc;
+    uint32_t* const recs_d = (uint32_t*)(seg_d + nsg);
     for (size_t p = 0; p < P; ++p) {
         TbDev& t = jobs[p];
         const PairDev& d = *pdv[p];
@@ -1481,29 +1530,45 @@ static int run_traceback(gx_context* ctx, const std::vector<const FillJob*>& jv,
         t.start_i = starts[p].i; t.start_j = starts[p].j; t.start_E = starts[p].E;
         t.start_E_dev = (dev_end_E && starts[p].i >= 1) ? &presv[p]->end_E : nullptr;
         t.start_ij_dev = (dev_end_E && job.local_on && starts[p].i >= 1) ? &presv[p]->lmax_i : nullptr;
-        t.seg = (int*)seg.p + 4 * so[p];
-        t.recs = (uint32_t*)recs.p + so[p] * SR;
+        t.seg = seg_d + 4 * so[p];
+        t.recs = recs_d + so[p] * SR;
         t.srows = SR;
         t.skew = job.lay == 3 ? 1 : 0;
         t.skel_half = job.twin ? d.twin_half : -1;
-        t.end_ij = (int*)cnt.p + 4 * p;
+        t.end_ij = cnt_d + 4 * p;
         t.w16 = job.nocodes ? (const uint8_t*)d.pI : nullptr;   // the twin's code plane (shared by its pairs)
         t.w16_half = d.twin_half;
         t.t4 = d.t4;
     }
     (void)presv;
-    TbDev* pin_jobs = (TbDev*)(slot >= 0 ? pinned_grow(ctx->slots[slot].tjpin, P * sizeof(TbDev))
-                                         : io_pinned(ctx, P * sizeof(TbDev)));
-    if (!pin_jobs) { cleanup(); return fail(GX_ENOMEM, "pinned staging buffer"); }
-    memcpy(pin_jobs, jobs.data(), P * sizeof(TbDev));
-    hipError_t e = hipMemcpyAsync(jb.p, pin_jobs, P * sizeof(TbDev), hipMemcpyHostToDevice, ts);
-    if (e == hipSuccess) e = hipMemsetAsync(seg.p, 0, std::max<size_t>(stot, 1) * 4 * sizeof(int), ts);
+    const size_t jbytes = P * sizeof(TbDev);
+    void* jdev = jb.p;
+    bool upload = true;
+    if (slot >= 0) {   // the slot's table: uploaded again only when it changed (the slot's last walk has ended)
+        auto& sl = ctx->slots[slot];
+        if (sl.tjob_cap < jbytes) {
+            if (sl.tjob) (void)hipFree(sl.tjob);
+            sl.tjob = nullptr; sl.tjob_cap = 0; sl.tjob_last.clear();
+            if (hipMalloc(&sl.tjob, jbytes) != hipSuccess) { sl.tjob = nullptr; cleanup(); return fail(GX_ENOMEM, "traceback jobs"); }
+            sl.tjob_cap = jbytes;
+        }
+        upload = !(sl.tjob_last.size() == P && !memcmp(sl.tjob_last.data(), jobs.data(), jbytes));
+        if (upload) sl.tjob_last = jobs;
+        jdev = sl.tjob;
+    }
+    hipError_t e = hipSuccess;
+    if (upload) {
+        TbDev* pin_jobs = (TbDev*)(slot >= 0 ? pinned_grow(ctx->slots[slot].tjpin, jbytes) : io_pinned(ctx, jbytes));
+        if (!pin_jobs) { cleanup(); return fail(GX_ENOMEM, "pinned staging buffer"); }
+        memcpy(pin_jobs, jobs.data(), jbytes);
+        e = hipMemcpyAsync(jdev, pin_jobs, jbytes, hipMemcpyHostToDevice, ts);
+    }
+    if (e == hipSuccess) e = hipMemsetAsync(seg_d, 0, nsg * sizeof(int), ts);
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].tb : ctx->ev1, eve = slot >= 0 ? ctx->slots[slot].te : ctx->ev2;
     if (e == hipSuccess) e = hipEventRecord(evb, ts);
-    if (e == hipSuccess) e = launch_traceback((const TbDev*)jb.p, (int)P, max_strips, job.nocodes, job.noskel, ts);
+    if (e == hipSuccess) e = launch_traceback((const TbDev*)jdev, (int)P, max_strips, job.nocodes, job.noskel, ts);
     if (e == hipSuccess) e = hipEventRecord(eve, ts);
     // one pinned host block: c | sg | hr
-    const size_t nc = 4 * P, nsg = 4 * std::max<size_t>(stot, 1), nhr = std::max<size_t>(stot, 1) * SR;
     const size_t bytes = (nc + nsg) * sizeof(int) + nhr * sizeof(uint32_t);
     PinnedBuf& recpin = slot >= 0 ? ctx->slots[slot].tbpin : ctx->tb_pin;
     if (e == hipSuccess && !pinned_grow(recpin, bytes)) e = hipErrorOutOfMemory;
@@ -1517,9 +1582,7 @@ static int run_traceback(gx_context* ctx, const std::vector<const FillJob*>& jv,
     // the kernels end; the buffers stay held until tb_collect
     hipStream_t cs = collect ? ts : ctx->cstream;
     if (!collect && e == hipSuccess) e = hipStreamWaitEvent(cs, eve, 0);
-    if (e == hipSuccess) e = hipMemcpyAsync(c, cnt.p, nc * sizeof(int), hipMemcpyDeviceToHost, cs);
-    if (e == hipSuccess) e = hipMemcpyAsync(sg, seg.p, nsg * sizeof(int), hipMemcpyDeviceToHost, cs);
-    if (e == hipSuccess) e = hipMemcpyAsync(hr, recs.p, nhr * sizeof(uint32_t), hipMemcpyDeviceToHost, cs);
+    if (e == hipSuccess) e = hipMemcpyAsync(c, tbb.p, bytes, hipMemcpyDeviceToHost, cs);
     const auto q1 = clk::now();
     out.c = c; out.sg = sg; out.hr = hr;
     out.so = so;
@@ -1527,7 +1590,7 @@ static int run_traceback(gx_context* ctx, const std::vector<const FillJob*>& jv,
     if (!collect) {   // pipelined: tb_collect() waits for the records later
         if (e == hipSuccess) e = hipEventRecord(ctx->slots[slot].tdone, cs);
         DevBuf* h = ctx->slots[slot].held;
-        h[0] = recs; h[1] = seg; h[2] = jb; h[3] = cnt;
+        h[0] = tbb; h[1] = DevBuf{}; h[2] = jb; h[3] = DevBuf{};
         if (e != hipSuccess) return fail(GX_EHIP, std::string("traceback: ") + hipGetErrorString(e));
         return GX_OK;
     }
