@@ -2149,9 +2149,11 @@ static int label_batch(gx_context* ctx, const std::vector<PairHost>& ph, const H
                                 MovesSrc{nullptr, 0}, walks[p]);
         if (prc[p]) perr[p] = g_err;   // g_err is thread-local
     };
-    // the calling thread plus up to 11 pool workers (the box gives a process
-    // 16 CPUs; the HIP runtime's threads and the caller's keep the rest)
-    size_t cap = 12;
+    // the calling thread plus up to 15 pool workers: the 16 CPUs a process
+    // gets on the box (1024 x 1k, GCUPS a step by threads: 4 502, 8 707,
+    // 12 817, 14 872, 16 906; the labelling writes 24-B gx_steps, ~48 MB a
+    // pass, and is on the step's critical path)
+    size_t cap = 16;
     if (const char* e = getenv("GX_LABEL_THREADS"); e && atoi(e) > 0) cap = (size_t)atoi(e);
     const size_t nthreads = std::min<size_t>({P, (size_t)std::max(1u, std::thread::hardware_concurrency()), cap});
     if (nthreads <= 1) {
