@@ -228,6 +228,8 @@ struct gx_context {
     struct Slot {
         PinnedBuf fpin, tjpin, tbpin;        // fill descriptors/results, traceback jobs, traceback records
         hipEvent_t fb = nullptr, fe = nullptr, tb = nullptr, te = nullptr, fdone = nullptr, tdone = nullptr;
+        hipEvent_t fres = nullptr;           // the fill's results copied (copy stream)
+        DevBuf held_pres;                    // the fill's results block, read by that copy (until fill_collect)
         TbOut out;
         DevBuf held[4];                      // traceback buffers the copy stream still reads (until tb_collect)
         // the walk's job table of this slot's last pass, kept on the device:
@@ -269,7 +271,7 @@ static void* pinned_grow(PinnedBuf& b, size_t bytes) {
 
 static int slots_ready(gx_context* ctx) {
     for (auto& s : ctx->slots) {
-        hipEvent_t* evs[] = {&s.fb, &s.fe, &s.tb, &s.te, &s.fdone, &s.tdone};
+        hipEvent_t* evs[] = {&s.fb, &s.fe, &s.tb, &s.te, &s.fdone, &s.tdone, &s.fres};
         for (hipEvent_t* e : evs)
             if (!*e && hipEventCreate(e) != hipSuccess) return GX_EHIP;
     }
@@ -400,7 +402,7 @@ extern "C" void gx_context_destroy(gx_context* ctx) {
     for (auto& s : ctx->slots) {
         for (PinnedBuf* b : {&s.fpin, &s.tjpin, &s.tbpin})
             if (b->p) (void)hipHostFree(b->p);
-        for (hipEvent_t e : {s.fb, s.fe, s.tb, s.te, s.fdone, s.tdone})
+        for (hipEvent_t e : {s.fb, s.fe, s.tb, s.te, s.fdone, s.tdone, s.fres})
             if (e) (void)hipEventDestroy(e);
         if (s.tjob) (void)hipFree(s.tjob);
         if (s.fdesc) (void)hipFree(s.fdesc);
@@ -704,6 +706,7 @@ struct FillJob {
     // device buffers (owned by the job until released)
     DevBuf chars, planes, codes, skel, feed, progress, sres, pres, pairs, counter, ccodes;
     bool pairs_borrowed = false;   // pairs is a pipeline slot's cached descriptor block (not pooled)
+    bool pres_held = false;        // pres is held by its pipeline slot until fill_collect
     std::vector<PairDev> pd;
     std::vector<PairRes> res;
     int W = 4;
@@ -741,6 +744,7 @@ static void unshift_results(FillJob& j) {
 
 static void job_release(gx_context* ctx, FillJob& j) {
     if (j.pairs_borrowed) { j.pairs = DevBuf{}; j.pairs_borrowed = false; }
+    if (j.pres_held) { j.pres = DevBuf{}; j.pres_held = false; }
     pool_put(ctx, j.chars); pool_put(ctx, j.planes); pool_put(ctx, j.codes); pool_put(ctx, j.feed);
     pool_put(ctx, j.progress); pool_put(ctx, j.sres); pool_put(ctx, j.pres); pool_put(ctx, j.pairs);
     pool_put(ctx, j.counter); pool_put(ctx, j.skel); pool_put(ctx, j.ccodes);
@@ -1194,14 +1198,25 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     int status[2] = {0, 0};
     PairRes* pin_res = (PairRes*)(pin + P * sizeof(PairDev) + ord_bytes);
     int* pin_status = (int*)(pin + P * (sizeof(PairDev) + sizeof(PairRes)) + ord_bytes);
-    HIPCHK(hipMemcpyAsync(pin_res, job.pres.p, res_bytes + sizeof status, hipMemcpyDeviceToHost, fs));   // (+ status)
     job.pin_res = pin_res;
     job.pin_status = pin_status;
     job.slot = slot;
     if (!collect) {   // pipelined: fill_collect() waits for the results later
-        HIPCHK(hipEventRecord(ctx->slots[slot].fdone, fs));
+        // the results (+ status) go on the copy stream, so the walk queued
+        // behind this fill does not wait for a device-to-host copy (~0.12 ms
+        // on the copy engine after a long transfer, 1024 x 1k); the block
+        // stays held by the slot until that copy is collected
+        auto& sl = ctx->slots[slot];
+        HIPCHK(hipEventRecord(sl.fdone, fs));
+        HIPCHK(hipStreamWaitEvent(ctx->cstream, sl.fdone, 0));
+        HIPCHK(hipMemcpyAsync(pin_res, job.pres.p, res_bytes + sizeof status, hipMemcpyDeviceToHost, ctx->cstream));
+        HIPCHK(hipEventRecord(sl.fres, ctx->cstream));
+        pool_put(ctx, sl.held_pres);   // (collected already: fill_collect released it)
+        sl.held_pres = job.pres;
+        job.pres_held = true;
         return GX_OK;
     }
+    HIPCHK(hipMemcpyAsync(pin_res, job.pres.p, res_bytes + sizeof status, hipMemcpyDeviceToHost, fs));   // (+ status)
     HIPCHK(hipStreamSynchronize(fs));
     memcpy(job.res.data(), pin_res, P * sizeof(PairRes));
     unshift_results(job);
@@ -1239,7 +1254,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
 // Results of a fill enqueued with collect = false (pipelined path).
 static int fill_collect(gx_context* ctx, FillJob& job) {
     auto& s = ctx->slots[job.slot];
-    HIPCHK(hipEventSynchronize(s.fdone));
+    HIPCHK(hipEventSynchronize(s.fres));
+    pool_put(ctx, s.held_pres);   // its copy is done (the walk that reads it is ordered before any reuse: see callers)
     const size_t P = job.pd.size();
     job.res.assign(P, PairRes{});
     memcpy(job.res.data(), job.pin_res, P * sizeof(PairRes));
