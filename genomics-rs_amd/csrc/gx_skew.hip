@@ -16,10 +16,10 @@
 // doing everything took ~30 instructions (~200 cycles) a step; the strip is
 // therefore split over two waves on different SIMDs:
 //   * the CORE wave runs the recurrence only (10 VALU a step) and hands each
-//     4-step group's cells (I, S, D per lane) to the side wave through an LDS
-//     ring, 3 ds_write_b128 a group;
-//   * the SIDE wave derives the retrace bits and the landing column of every
-//     cell (algo.rs:351-400 priority S > I > D), stores the three int32 score
+//     4-step group's cells (S, D per lane) to the side wave through an LDS
+//     ring, 2 ds_write_b128 a group;
+//   * the SIDE wave re-derives I from the row's previous cell, then the
+//     retrace bits and the landing column of every cell (algo.rs:351-400 priority S > I > D), stores the three int32 score
 //     planes straight from the registers it read, the code words and the
 //     skeleton, and tracks the local last maximum.
 // The cell above (i-1, j) is lane l-1's previous step (DPP wave_shr:1 with
@@ -70,8 +70,8 @@ struct SkRing {                  // one strip boundary (see the file header)
     int dd[kSkRingG][4];
     int sm[kSkRingG][4];
 };
-struct SkHo {                    // one strip's core -> side ring: [group][plane I, S, D][lane] int4
-    int4 v[kSkHo][3][kWave];
+struct SkHo {                    // one strip's core -> side ring: [group][S, D][lane] int4 (the side
+    int4 v[kSkHo][2][kWave];     // wave derives I from them: side_group)
 };
 __device__ __forceinline__ int sk_grp(int c) { return ((c + 3) >> 2) & (kSkRingG - 1); }
 __device__ __forceinline__ int sk_pos(int c) { return (c + 3) & 3; }
@@ -156,10 +156,10 @@ __device__ __forceinline__ int4 load_codes(const CoreCtx& w, int t) {
 // reuse registers an LDS store may still be reading (which would cost a wait
 // for that store: LDS reads store data after issue).
 struct CorePend {
-    v4i v[5];
+    v4i v[4];                    // hand-off S, D; push dd, sm
 };
 __device__ __forceinline__ void pin(const CorePend& p) {
-    asm volatile("" ::"v"(p.v[0]), "v"(p.v[1]), "v"(p.v[2]), "v"(p.v[3]), "v"(p.v[4]));
+    asm volatile("" ::"v"(p.v[0]), "v"(p.v[1]), "v"(p.v[2]), "v"(p.v[3]));
 }
 
 template <bool LOCAL, bool TBL, int MODE, int Q>
@@ -192,13 +192,11 @@ __device__ __forceinline__ void core_group(CoreState& st, const v4i (&cur)[2], v
     // hand the group's cells to the side wave (slot t/4 mod kSkHo; the side
     // wave has read the slot's previous group: checked per sub-block)
     if (!(GX_SKEW_EXP & 2)) {
-        v4i* hv = w.hv_sub + Q * 3 * kWave;
-        mine.v[0] = v4i{oI[0], oI[1], oI[2], oI[3]};
-        mine.v[1] = v4i{oS[0], oS[1], oS[2], oS[3]};
-        mine.v[2] = v4i{oD[0], oD[1], oD[2], oD[3]};
+        v4i* hv = w.hv_sub + Q * 2 * kWave;
+        mine.v[0] = v4i{oS[0], oS[1], oS[2], oS[3]};
+        mine.v[1] = v4i{oD[0], oD[1], oD[2], oD[3]};
         hv[0] = mine.v[0];
         hv[kWave] = mine.v[1];
-        hv[2 * kWave] = mine.v[2];
         asm volatile("" ::: "memory");                         // (the data stores stay before the count)
         if (Q == 3) *w.hcnt = (t >> 2) + 1;                    // (per sub-block; every lane, one value; LDS keeps the order)
     }
@@ -206,13 +204,13 @@ __device__ __forceinline__ void core_group(CoreState& st, const v4i (&cur)[2], v
     // this group's step 0, after steps 0, 1, 2), then the count (same wave,
     // LDS in order).  Every lane writes (lanes 0..62 into a sink), so the
     // compiler sees and counts the stores: no exec change, no branch.
-    mine.v[3] = v4i{pdd, qdd[0], qdd[1], qdd[2]};
-    mine.v[4] = v4i{psm, qsm[0], qsm[1], qsm[2]};
+    mine.v[2] = v4i{pdd, qdd[0], qdd[1], qdd[2]};
+    mine.v[3] = v4i{psm, qsm[0], qsm[1], qsm[2]};
     if (!(GX_SKEW_EXP & 8) && (MODE == 0 || (t >= 64 && t - 63 <= w.m))) {   // (full groups: always inside; no consumer: all into the sink)
         lds_v4i* a = (lds_v4i*)(uintptr_t)(w.push_base + __umul24((uint32_t)sk_grp(t - 63), w.push_m16));
         const int cnt = (MODE == 0 ? t - 60 : min(t - 60, w.m)) + 1;   // (MODE 0: t - 60 < m)
-        a[0] = mine.v[3];
-        a[kSkRingG] = mine.v[4];
+        a[0] = mine.v[2];
+        a[kSkRingG] = mine.v[3];
         asm volatile("" ::: "memory");
         *w.pcnt = cnt;
     }
@@ -353,6 +351,7 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
 // side wave
 
 struct SideState {
+    int I, H;                    // insert score and score_max of (i, j-1) (I of (i, j) follows from them)
     int E, Ed;                   // landing column + 64 of (i, j-1) and of (i-1, j-1)
     uint32_t cI, cD;
     int lbest, lstep, lE;        // LOCAL: the row's last max of score_max (algo.rs:310-322)
@@ -397,31 +396,49 @@ struct SideCtx {
     __amdgpu_buffer_rsrc_t skel_rsrc;    // skeleton row of this strip (bottom-row E + 64)
     uint32_t skel_voff;                  // lane 63: 0; other lanes: out of range
     int m, lane;
+    int h, g, hg;                        // gap open / extend (global fills: shifted, g folded: g = 0)
     unsigned tr_wait;                    // (diagnostics: spins waiting for the core wave)
     bool diag_idle;                      // (GX_DEBUG_FLAGS & 2: the side only consumes; timing only)
 };
 
+// I(i, j) from the row's previous cell, as the core computes it (the core
+// hands over only S and D, one ds_write_b128 fewer per group on its path):
+// global (shifted, h <= 0) max(I, H + h); local max(I + g, H + h + g, 0).
+template <bool LOCAL, bool MASKED>
+__device__ __forceinline__ int side_insert(SideState& st, const SideCtx& w, const int S, const int D, const bool act) {
+    const int In = LOCAL ? max3i(st.I + w.g, st.H + w.hg, 0) : max(st.I, st.H + w.h);
+    const int Hn = max3i(In, S, D);
+    st.I = MASKED ? (act ? In : st.I) : In;
+    st.H = MASKED ? (act ? Hn : st.H) : Hn;
+    return In;
+}
+
 template <bool LOCAL, bool PLANES, int MODE>
-__device__ __forceinline__ void side_group(SideState& st, SideCtx& w, const int t, const int4 (&hv)[3]) {
+__device__ __forceinline__ void side_group(SideState& st, SideCtx& w, const int t, const int4 (&hv)[2]) {
     const int g = t >> 2;
-    const int4 vI = hv[0], vS = hv[1], vD = hv[2];
-    if (PLANES) {   // the group's cells as they came, one dwordx4 per lane and plane
-        const uint32_t vo = (uint32_t)w.lane * 16u + (uint32_t)g * (kGroupInts1 * 4);
-        bstore4(w.rI, vo, vI);
-        bstore4(w.rS, vo, vS);
-        bstore4(w.rD, vo, vD);
-    }
-    const int aI[4] = {vI.x, vI.y, vI.z, vI.w}, aS[4] = {vS.x, vS.y, vS.z, vS.w}, aD[4] = {vD.x, vD.y, vD.z, vD.w};
+    const int4 vS = hv[0], vD = hv[1];
+    const int aS[4] = {vS.x, vS.y, vS.z, vS.w}, aD[4] = {vD.x, vD.y, vD.z, vD.w};
+    int aI[4] = {0, 0, 0, 0};
     int e[4];
 #pragma unroll
     for (int U = 0; U < 4; ++U) {
         if (MODE == 1) {
-            if (w.lane <= t + U) side_step<LOCAL, false>(st, aI[U], aS[U], aD[U], t + U, true);
+            if (w.lane <= t + U) {
+                aI[U] = side_insert<LOCAL, false>(st, w, aS[U], aD[U], true);
+                side_step<LOCAL, false>(st, aI[U], aS[U], aD[U], t + U, true);
+            }
         } else {
             const bool act = MODE == 2 ? (unsigned)(t + U - w.lane) < (unsigned)w.m : true;
+            aI[U] = side_insert<LOCAL, MODE == 2>(st, w, aS[U], aD[U], act);
             side_step<LOCAL, MODE == 2>(st, aI[U], aS[U], aD[U], t + U, act);
         }
         e[U] = st.E;   // lane 63: E + 64 of its column t+U-62
+    }
+    if (PLANES) {   // the group's cells, one dwordx4 per lane and plane
+        const uint32_t vo = (uint32_t)w.lane * 16u + (uint32_t)g * (kGroupInts1 * 4);
+        bstore4(w.rI, vo, make_int4(aI[0], aI[1], aI[2], aI[3]));
+        bstore4(w.rS, vo, vS);
+        bstore4(w.rD, vo, vD);
     }
     // lane 63's landing columns (+64) of its columns t-62 .. t-59: the skeleton
     const int c0 = t - (kWave - 2);
@@ -455,6 +472,11 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, SideCtx
     w.skel_rsrc = rsrc_of(uniform_ptr(P.skel + (size_t)s * P.skel_stride), has_consumer ? 4 * (m + 1) : 0);
     w.skel_voff = lane == kWave - 1 ? 0u : kSkelOff;
     SideState st;
+    {   // column 0 (algo.rs:204-211), as the core starts it (core_wave)
+        const int D0 = w.h + i * w.g;
+        st.H = LOCAL ? max(D0, 0) : w.h;          // (global: shifted, D0 - i g = h)
+        st.I = LOCAL ? kNeg : kNeg - i * w.g;
+    }
     st.E = 64 - (lane + 1);                       // column 0: the path reaches it at local row lane + 1
     st.Ed = shr1(64, st.E);                       // column 1's top-left: (64 s, 0) for lane 0
     st.cI = 0; st.cD = 0;
@@ -463,13 +485,13 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, SideCtx
     for (int t0 = 0; t0 < T; t0 += kSub) {
         // the core publishes whole sub-blocks: read all four groups at once
         w.tr_wait += wait_ge(w.hcnt, (t0 >> 2) + 4, w.status);
-        int4 sub[4][3];
+        int4 sub[4][2];
         {
             const int4* hv = &w.ho->v[(t0 >> 2) & (kSkHo - 1)][0][lane];
 #pragma unroll
             for (int q = 0; q < 4; ++q)
 #pragma unroll
-                for (int k = 0; k < 3; ++k) sub[q][k] = hv[(3 * q + k) * kWave];
+                for (int k = 0; k < 2; ++k) sub[q][k] = hv[(2 * q + k) * kWave];
         }
         asm volatile("" ::: "memory");
         *w.bcnt = (t0 >> 2) + 4;                  // (reads issued first: LDS keeps the order)
@@ -662,6 +684,7 @@ __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const
                 w.ho = &ho[k]; w.hcnt = (lds_int*)&hcnt[k]; w.bcnt = (lds_int*)&bcnt[k];
                 w.status = band_counter + 1;
                 w.diag_idle = (sc.dbg & 2) != 0;
+                w.h = sc.h; w.g = sc.g; w.hg = sc.hg;
                 side_wave<LOCAL, PLANES>(P, s, lane, w, has_consumer, sres, pres + p);
             }
         }
