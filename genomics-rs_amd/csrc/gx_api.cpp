@@ -666,11 +666,10 @@ struct PairHost {
 // profiles/r01d_layouts.txt).  The latency layout is 3 for untracked fills
 // with h <= 0 (its recurrences fold the gap opening onto score_max, which is
 // exact only then) when it is predicted faster than the column step, else
-// the column step.  A single pair of S 64-row strips and m columns takes
-// about (m + 80 S) x 62 ns on layout 3 (a strip starts ~80 steps after the
-// one above) and (m + 7 S) x 113 ns on the column step:
-// layout 3 for n below about 0.78 m (Covid 29,903 x 29,882: 4.72 vs 4.63 ms;
-// 64 x 30,000: 1.6 vs 3.4).
+// the column step (below: a fitted cost model per layout).
+// Covid 29,903 x 29,882 global: layout 3 (4.52 vs 4.62 ms); BRCA2 11,382 x
+// 10,346 local: the split column step (1.74 vs 1.79); 64 x 30,000: layout 3
+// (1.5 vs 3.4).
 // Layout 3 needs h <= 0 (the folded gap opening) and, for the virtual
 // columns of its global ramp-up (values drift from -2^30 by up to 64 steps of
 // |g| + |h| + |s|), small penalties.
@@ -687,11 +686,17 @@ static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int 
         strips64 += ceil_div((int)h.n, kStripRows1);
     }
     const bool cs_ok = span < (1LL << 29) && mmax + 128 < (1u << 24);   // landing keys hold E + 64 in 24 bits
+    // a pair's fill time ~ m x (a strip's pace per column) + S x (a strip's
+    // start lag), fitted per layout on a lone 64-row strip and on the
+    // BASELINE pairs (round 4, profiles/r04_layout_fit.json): layout 3 50 ns
+    // + 6.46 us global, 57.5 ns + 6.66 us local; the column step 113 ns +
+    // 2.66 us (global), split for local fills 110 ns + 3.37 us
+    const bool local = sc.floor_ == 0;
     double est1 = 0, est3 = 0;   // the launch's slowest pair on each layout (ns)
     for (const PairHost& h : ph) {
         const double S = (double)ceil_div((int)h.n, kStripRows1), m = (double)h.m;
-        est1 = std::max(est1, (m + 7 * S) * 113.0);
-        est3 = std::max(est3, (m + 80 * S) * 62.0);
+        est1 = std::max(est1, local ? m * 110.0 + S * 3370.0 : m * 113.0 + S * 2660.0);
+        est3 = std::max(est3, local ? m * 57.5 + S * 6660.0 : m * 50.0 + S * 6460.0);
     }
     const int lat = skew_ok(sc, track) && (!cs_ok || est3 < est1) ? 3 : cs_ok ? 1 : 0;
     if (const char* e = getenv("GX_LAYOUT"); e && *e) {
