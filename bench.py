@@ -327,12 +327,12 @@ def config_record(gx, ctx, which: str, steps: int):
     return out
 
 
-LOCAL_BATCH_PAIRS = 32   # tests/golden/make_golden.py LOCAL_RELATED
+LOCAL_BATCH_PAIRS = 64   # tests/golden/make_golden.py LOCAL_RELATED
 
 
 def local_batch_record(gx, ctx, steps: int):
     """A Smith-Waterman batch (BASELINE config 3's mode at config 2's size):
-    the first 32 related 30k pairs (SURVEY 8(d) M1's variant, s2 = s1 with ~10 %
+    the first 64 related 30k pairs (SURVEY 8(d) M1's variant, s2 = s1 with ~10 %
     substitutions and ~1 % indels, so every pair has a long local alignment)
     aligned locally (algo.rs:231-248 with the 0 floor, last-max start
     algo.rs:310-322), resident in HBM, score planes + traceback + labelled

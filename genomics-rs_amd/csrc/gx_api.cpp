@@ -781,24 +781,31 @@ static hipError_t enqueue_plane_sums(gx_context* ctx, const FillJob& job, const 
 // The admission bound of a W-strip twin band whose twins' column counts
 // differ by up to dm: the largest |value - base| any state of the band can
 // reach (see the comment above twin_table).
+// Local twins (plain values, no shift) take D = max(|a|, U), the neighbour
+// bound of d8_planes_ok itself (the 0 floor keeps it), and their score
+// offsets carry + K (K = max(0, -s_min), run_fill) and the floor's -g term.
 constexpr long long kTwinBoundLimit = 30000;   // < 2^15 with room for the derived offsets
-static long long twin_bound(const Scores32& sc, int W, long long dm) {
+static long long twin_step(const Scores32& sc, bool local) {
+    const long long g = sc.g, a = (long long)sc.h + sc.g;
+    const long long smax = std::max(sc.sm, sc.smm);
+    const long long U = std::max(0LL, smax - a);
+    return local ? std::max({std::llabs(a), U, 1LL}) : std::max({std::llabs(a - g), std::llabs(U - g), 1LL});
+}
+static long long twin_const(const Scores32& sc, bool local) {
     const long long g = sc.g, a = (long long)sc.h + sc.g;
     const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
-    const long long U = std::max(0LL, smax - a);
-    const long long D = std::max(std::llabs(a - g), std::llabs(U - g));
-    return D * (192LL * W + 16 + dm) + 2 * (std::llabs(a) + std::llabs(smax) + std::llabs(smin)) + 64;
+    return 2 * (std::llabs(a) + std::llabs(smax) + std::llabs(smin)) + 64 +
+           (local ? std::max(0LL, -smin) + std::llabs(g) : 0);
+}
+static long long twin_bound(const Scores32& sc, int W, long long dm, bool local = false) {
+    return twin_step(sc, local) * (192LL * W + 16 + dm) + twin_const(sc, local);
 }
 // Largest column gap between twins that keeps band width W admissible under
 // twin_width's bound (capped at 1,024): twin_table pairs no wider gaps, so one
 // ill-matched twin never narrows the band width of a whole batch.
-static long long twin_gap_cap(const Scores32& sc, int W) {
-    const long long g = sc.g, a = (long long)sc.h + sc.g;
-    const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
-    const long long U = std::max(0LL, smax - a);
-    const long long D = std::max({std::llabs(a - g), std::llabs(U - g), 1LL});
-    const long long rest = 30000 - 1 - 2 * (std::llabs(a) + std::llabs(smax) + std::llabs(smin)) - 64;
-    return std::max(0LL, std::min(1024LL, rest / D - 192LL * W - 16));
+static long long twin_gap_cap(const Scores32& sc, int W, bool local = false) {
+    const long long rest = kTwinBoundLimit - 1 - twin_const(sc, local);
+    return std::max(0LL, std::min(1024LL, rest / twin_step(sc, local) - 192LL * W - 16));
 }
 static std::vector<std::pair<int, int>> twin_table(const std::vector<PairHost>& ph, long long gap_cap = 1024) {
     std::vector<int> idx(ph.size());
@@ -824,42 +831,19 @@ static std::vector<std::pair<int, int>> twin_table(const std::vector<PairHost>& 
 // long_ok: the launch will be the twin fill without landing columns (twin
 // plane codes, no code words, no skeleton): no int16 column quantity is
 // left, so the 31,920-column limit of the int16 landing columns is lifted.
-// The local twin fill (gx_fill_pk.hip LOCAL) keeps plain values on base 0: a
-// local value lies in [-(|a| + |s_min|), min(n, m) max(s_max, 0)] (algo.rs:103:
-// I, D and score_max are floored at 0 and only matches raise them), so the
-// biased halves hold every value, score-table add and tracker difference while
-// that bound plus the constants stays below 32,000; the row trackers keep
-// 16-bit columns (m <= 65,535).  No base moves, so twins of any shapes and any
-// band width qualify.  Only as the launch without code words or skeleton
-// (twin plane codes, the sequential walk): long_ok.
-static long long twin_local_bound(const std::vector<PairHost>& ph, const std::vector<std::pair<int, int>>& tw,
-                                  const Scores32& sc) {
-    const long long g = sc.g, a = (long long)sc.h + sc.g;
-    const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
-    long long vmax = 0;
-    for (const auto& t : tw)
-        for (int p : {t.first, t.second})
-            vmax = std::max(vmax, (long long)std::min(ph[p].n, ph[p].m) * std::max(smax, 0LL));
-    return vmax + std::llabs(smax) + std::llabs(smin) + std::max(0LL, -smin) + std::llabs(a) + std::llabs(g) + 64;
-}
+// The local twin fill (gx_fill_pk.hip LOCAL) keeps plain values relative to
+// the same per-block bases, under the same bound (twin_step's local D); its
+// row maxima fold into int32 at each base change, and it tracks no columns,
+// so neither the magnitude of its values nor the column count is limited.
+// Only as the launch without code words or skeleton (twin plane codes, the
+// sequential walk): long_ok.
 static int twin_width(const std::vector<PairHost>& ph, const std::vector<std::pair<int, int>>& tw, const Scores32& sc,
                       int is_local, bool track, bool lcs, int lay, bool planes, bool d8, int W_want,
                       bool long_ok = false) {
     if (const char* e = getenv("GX_TWIN"); e && !strcmp(e, "0")) return 0;
     if (lay != 0 || track || lcs || (planes && !d8) || sc.g > 0 || sc.h > 0) return 0;
     if (ph.empty()) return 0;
-    if (is_local) {
-        if (!planes || !long_ok) return 0;
-        for (const auto& t : tw) {
-            const PairHost& x = ph[t.first];
-            const PairHost& y = ph[t.second];
-            if (!x.n || !x.m || !y.n || !y.m || std::max(x.m, y.m) > 65535) return 0;
-        }
-        if (twin_local_bound(ph, tw, sc) >= 32000) return 0;
-        for (int W : {15, 8, 7, 4, 3})
-            if (W <= W_want || W == 3) return W;
-        return 0;
-    }
+    if (is_local && (!planes || !long_ok)) return 0;
     long long dm = 0;
     for (const auto& t : tw) {
         const PairHost& x = ph[t.first];
@@ -870,7 +854,7 @@ static int twin_width(const std::vector<PairHost>& ph, const std::vector<std::pa
     }
     for (int W : {15, 8, 7, 4, 3}) {
         if (W > W_want && W != 3) continue;
-        if (twin_bound(sc, W, dm) < kTwinBoundLimit) return W;
+        if (twin_bound(sc, W, dm, is_local != 0) < kTwinBoundLimit) return W;
     }
     return 0;
 }
@@ -921,7 +905,8 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     if (const char* e = getenv("GX_BAND_WAVES")) wt_want = atoi(e);
     else wt_want = fill_band_waves(false, total_strips / 2, fill_grid_cap(ctx->device), lay, min_strips);
     const std::vector<std::pair<int, int>> tw = twin_table(
-        ph, is_local ? INT_MAX : twin_gap_cap(sc, wt_want >= 15 ? 15 : wt_want >= 8 ? 8 : wt_want >= 7 ? 7 : wt_want >= 4 ? 4 : 3));
+        ph, twin_gap_cap(sc, wt_want >= 15 ? 15 : wt_want >= 8 ? 8 : wt_want >= 7 ? 7 : wt_want >= 4 ? 4 : 3,
+                         is_local != 0));
     {
         const bool long_ok = planes && !job.table && w16_ok(sc);   // (the noskel rule below)
         Wt = twin_width(ph, tw, sc, is_local, track, lcs, lay, planes, d8, wt_want, long_ok);
@@ -3001,6 +2986,17 @@ extern "C" int gx_twin_admission(const gx_scores* scores, int band_waves, int64_
     Scores32 sc;
     if (check_scores(scores, 1, 1, &hs, &sc, 0, nullptr) != GX_OK) return -1;
     const long long b = twin_bound(sc, band_waves, col_gap);
+    if (bound) *bound = b;
+    return (sc.g <= 0 && sc.h <= 0 && b < kTwinBoundLimit) ? 1 : 0;
+}
+
+extern "C" int gx_twin_admission_mode(const gx_scores* scores, int is_local, int band_waves, int64_t col_gap,
+                                      int64_t* bound) {
+    if (!scores || band_waves < 1 || col_gap < 0) return -1;
+    HostScores hs;
+    Scores32 sc;
+    if (check_scores(scores, 1, 1, &hs, &sc, is_local, nullptr) != GX_OK) return -1;
+    const long long b = twin_bound(sc, band_waves, col_gap, is_local != 0);
     if (bound) *bound = b;
     return (sc.g <= 0 && sc.h <= 0 && b < kTwinBoundLimit) ? 1 : 0;
 }

@@ -180,14 +180,19 @@ struct LanePk {
 // differ in length: the shorter one's state stays at its last column).
 //
 // LOCAL (Smith-Waterman, algo.rs:231-248 with is_local): plain (unshifted)
-// values on base 0 -- a local value lies in [0, min(n, m) max(s, 0)] and the
-// host admits the launch only while that fits the biased halves
-// (twin_width) -- so the 0 floor of score_max is one v_pk_max_u16 against the
-// biased zero k.Z in each gap recurrence, and the row keeps its largest
-// score_max (one v_pk_max_u16; the last column holding it, algo.rs:310-322,
-// is recovered from the chosen row's plane codes by local_col_kernel, so the
-// fill tracks no columns).  Plane codes store x_I - g as the
-// shifted fill does (Iold - |g| is the insert recurrence's own term).
+// values, relative to per-block bases like the global twin's (neighbouring
+// local values differ by at most max(|h + g|, U) as global ones do, the 0
+// floor keeps every inequality: gx_api.cpp twin_bound), so the 0 floor of
+// score_max is one v_pk_max_u16 against k.Z, the biased relative zero of the
+// current bases (-B per half, clamped to -2^15: a base above 2^15 lies more
+// than the admission bound above every value of the band, whose floor then
+// never binds), in each gap recurrence, and the row keeps its largest
+// score_max since the last base change (one v_pk_max_u16; folded into an
+// absolute int32 maximum when the bases move, fold_lb; the last column
+// holding it, algo.rs:310-322, is recovered from the chosen row's plane codes
+// by local_col_kernel, so the fill tracks no columns).  Plane codes store
+// x_I - g as the shifted fill does (Iold - |g| is the insert recurrence's own
+// term).
 template <bool MASKED, bool TBL, bool CODES, bool NOE = false, bool LOCAL = false>
 __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const uint32_t sm_in, const uint32_t e_up,
                                         const uint32_t c2, const uint32_t c1, const uint32_t c1h, const uint32_t act,
@@ -418,6 +423,21 @@ __device__ __forceinline__ int2 base_of(lds_int* b, int blk) {
     return make_int2(__builtin_amdgcn_readfirstlane(b[2 * k]), __builtin_amdgcn_readfirstlane(b[2 * k + 1]));
 }
 
+// The local floor (true 0) relative to bases (B0, B1), biased; clamped to the
+// lowest biased value when a base exceeds 2^15 (no value of the band then
+// lies within 2^15 of 0, so the floor never binds: cell_pk LOCAL).
+__device__ __forceinline__ uint32_t local_floor(int B0, int B1) {
+    return pk2(max(-B0, -32768), max(-B1, -32768)) ^ kBias2;
+}
+// A row's local maximum since the last base change into its absolute int32
+// maxima (both pairs); the 16-bit tracker restarts at the lowest value.
+__device__ __forceinline__ void fold_lb(RowPk& r, int (&mx)[2], int B0, int B1) {
+    const uint32_t v = r.lb ^ kBias2;
+    mx[0] = max(mx[0], lo16(v) + B0);
+    mx[1] = max(mx[1], hi16(v) + B1);
+    r.lb = 0;
+}
+
 // Shift every value of the lane state to new bases (delta = new - old).
 __device__ __forceinline__ void rebase_row(RowPk& r, uint32_t dpk) {
     r.I = psubs(r.I, dpk); r.SD = psubs(r.SD, dpk); r.Dd = psubs(r.Dd, dpk);
@@ -440,16 +460,17 @@ __device__ __forceinline__ void sub_block_pk(LanePk& st, Rec (&nxt)[4], WavePk& 
 // Initial state of row i (column 0, algo.rs:204-211) in shifted values:
 // H(i, 0) = h + i g -> h; I = H + h (compact planes' seed) -> 2h;
 // delete successor (row i+1) -> h; relative to the bases (B0, B1).
-// LOCAL (plain values, base 0): H(i, 0) = score_max = 0, I = H + h = h; the
-// max(S, D) seed only needs max(S, D) + h + g <= 0 (the floor decides I(i, 1)).
+// LOCAL (plain values): H(i, 0) = score_max = 0, I = H + h = h; the max(S, D)
+// seed only needs max(S, D) + h + g <= 0 (the floor decides I(i, 1)); the
+// row maximum tracker starts at the lowest value (fold_lb).
 template <bool LOCAL = false>
 __device__ __forceinline__ void init_row_pk(RowPk& rs, const Scores32& sc, int B0, int B1, const PkScores& k) {
-    rs.lb = kBias2;
+    rs.lb = 0;
     if (LOCAL) {
-        rs.I = pk2(sc.h, sc.h) ^ kBias2;
-        rs.SD = pk2(sc.h, sc.h) ^ kBias2;
-        rs.Dd = kBias2;
-        rs.SMp = padds(kBias2, k.smp);
+        rs.I = pk2(sc.h - B0, sc.h - B1) ^ kBias2;
+        rs.SD = pk2(sc.h - B0, sc.h - B1) ^ kBias2;
+        rs.Dd = pk2(-B0, -B1) ^ kBias2;
+        rs.SMp = padds(pk2(-B0, -B1) ^ kBias2, k.smp);
         rs.SMtl = 0;
         rs.cI = 0; rs.cD = 0;
         return;
@@ -510,9 +531,12 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
     wait_ge(wcnt_in, min(4, m) + 1, status);
     w.B0 = __builtin_amdgcn_readfirstlane(base_in[0]);   // slot 0: column 0
     w.B1 = __builtin_amdgcn_readfirstlane(base_in[1]);
+    PkScores kl = k;                                      // (LOCAL: the floor follows the bases)
+    int lmx[2][2] = {{0, 0}, {0, 0}};                     // LOCAL: rows A, B: absolute row maxima, both pairs
+    if (LOCAL) kl.Z = local_floor(w.B0, w.B1);
     LanePk st;
-    init_row_pk<LOCAL>(st.a, sc, w.B0, w.B1, k);
-    init_row_pk<LOCAL>(st.b, sc, w.B0, w.B1, k);
+    init_row_pk<LOCAL>(st.a, sc, w.B0, w.B1, kl);
+    init_row_pk<LOCAL>(st.b, sc, w.B0, w.B1, kl);
     st.c2c = 0;
     st.b.SMtl = st.a.SMp;                                   // (A, 0) is row B's top-left for column 1
     st.a.E = pk2(-(kRowsPerLane * lane + 1), -(kRowsPerLane * lane + 1));
@@ -541,8 +565,10 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
         if (t0 < m) {
             const int2 nb = base_of(base_in, blk);
             if (nb.x != w.B0 || nb.y != w.B1) {
+                if (LOCAL) { fold_lb(st.a, lmx[0], w.B0, w.B1); fold_lb(st.b, lmx[1], w.B0, w.B1); }
                 rebase(st, pk2(nb.x - w.B0, nb.y - w.B1));
                 w.B0 = nb.x; w.B1 = nb.y;
+                if (LOCAL) kl.Z = local_floor(w.B0, w.B1);
             }
         }
         // (sub-block 3 pushes column 0 again, now in the current bases: slot 0
@@ -555,8 +581,8 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
         const size_t sb_off = (size_t)(t0 >> 2) * kGroupInts;
         const bool full = (t0 >= kWave) && (t0 + kSub - 1 <= mmin - 1);
         const uint32_t out_base = lds_addr(ring_out + ring_slot(t0 - (kWave - 1)));
-        if (full) sub_block_pk<PLANES, false>(st, nxt, w, k, t0, out_base, has_consumer, sb_off);
-        else sub_block_pk<PLANES, true>(st, nxt, w, k, t0, out_base, has_consumer, sb_off);
+        if (full) sub_block_pk<PLANES, false>(st, nxt, w, kl, t0, out_base, has_consumer, sb_off);
+        else sub_block_pk<PLANES, true>(st, nxt, w, kl, t0, out_base, has_consumer, sb_off);
         if constexpr ((PLANES & 8) == 0) {   // code words of both pairs: codes[strip][t/16][lane][row-in-lane]
             typedef unsigned v2u __attribute__((ext_vector_type(2)));
             typedef __attribute__((address_space(1))) v2u gv2u;
@@ -574,12 +600,14 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
         // ties) -> StripRes, which finalize_kernel reduces over the strips;
         // local_col_kernel then finds the row's last column holding it
         // (algo.rs:310-322)
+        fold_lb(st.a, lmx[0], w.B0, w.B1);
+        fold_lb(st.b, lmx[1], w.B0, w.B1);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const PairDev& P = h ? P1 : P0;
             const bool oka = ia <= P.n, okb = ia + 1 <= P.n;
-            const int va = oka ? (h ? hi16(st.a.lb ^ kBias2) : lo16(st.a.lb ^ kBias2)) : INT_MIN;
-            const int vb = okb ? (h ? hi16(st.b.lb ^ kBias2) : lo16(st.b.lb ^ kBias2)) : INT_MIN;
+            const int va = oka ? lmx[0][h] : INT_MIN;
+            const int vb = okb ? lmx[1][h] : INT_MIN;
             const bool tb = okb && vb >= va;
             const int v = tb ? vb : va;
             int mx = v;
@@ -632,7 +660,7 @@ __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, c
     const int* prog_in = lb > 0 ? P0.progress + (size_t)(lb - 1) * kProgStride : nullptr;
     int* prog_out = do_out ? P0.progress + (size_t)lb * kProgStride : nullptr;
     // sm'' (the launch's scores carry the shift's -2g, Scores32.shift); TBL: no
-    // offset.  LOCAL: plain values on base 0, the score_max offset of k.smp.
+    // offset.  LOCAL: plain values, the score_max offset of k.smp.
     const int smp = LOCAL ? lo16(k.smp) : TBL ? 0 : sc.sm;
     unsigned idle = 0;
     int bprev0 = 0, bprev1 = 0;         // bases of the block before the current chunk's first column
@@ -670,16 +698,15 @@ __device__ void io_wave_pk(const PairDev& P0, const PairDev& P1, const int lb, c
                 }
                 // bases: column 0 -> slot 0; block c (columns 16c+1 ..) from its first column
                 const int c0 = in_next >> 4;                     // chunk = columns 16c0 .. 16c0+15
-                if (in_next == 0 && !LOCAL) {   // (local: every base is 0)
+                if (in_next == 0) {
                     bprev0 = __builtin_amdgcn_readlane(sm0, 0);
                     bprev1 = __builtin_amdgcn_readlane(sm1, 0);
                     if (lane == 0) { base0[0] = bprev0; base0[1] = bprev1; }
                 }
-                if (in_next == 0 && LOCAL && lane == 0) { base0[0] = 0; base0[1] = 0; }
                 int nb0 = bprev0, nb1 = bprev1;
                 if (chunk > 1) {
-                    nb0 = LOCAL ? 0 : __builtin_amdgcn_readlane(sm0, 1);
-                    nb1 = LOCAL ? 0 : __builtin_amdgcn_readlane(sm1, 1);
+                    nb0 = __builtin_amdgcn_readlane(sm0, 1);
+                    nb1 = __builtin_amdgcn_readlane(sm1, 1);
                     if (lane == 0) {
                         const int kk = 1 + (c0 & (kBaseSlots - 1));
                         base0[2 * kk] = nb0;

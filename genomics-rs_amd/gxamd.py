@@ -76,6 +76,7 @@ EXPORTED = ["gx_last_error", "gx_version", "gx_context_create", "gx_context_dest
             "gx_stage_pairs",
             "gx_run_staged", "gx_run_staged_steps", "gx_staged_plane_sums", "gx_staged_steps",
             "gx_staged_pass_results", "gx_fill_info", "gx_batch_chunks", "gx_fill_twin", "gx_fill_groups", "gx_plane_bytes_per_cell", "gx_twin_admission",
+            "gx_twin_admission_mode",
             "gx_fasta_load",
             "gx_config_load", "gx_format_alignment", "gx_format_table"]
 
@@ -128,6 +129,8 @@ def lib():
     L.gx_plane_bytes_per_cell.argtypes = [ctypes.POINTER(CScores), ctypes.c_int]
     L.gx_twin_admission.argtypes = [ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int64,
                                     ctypes.POINTER(ctypes.c_int64)]
+    L.gx_twin_admission_mode.argtypes = [ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int, ctypes.c_int64,
+                                         ctypes.POINTER(ctypes.c_int64)]
     L.gx_fasta_load.argtypes = [ctypes.c_char_p, vp, sz, vp, vp, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.gx_config_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(CScores)]
     L.gx_format_alignment.argtypes = [vp, sz, vp, sz, vp, sz, ctypes.POINTER(CResult), vp, sz, ctypes.POINTER(sz)]
@@ -294,12 +297,13 @@ def plane_bytes_per_cell(scores: "Scores", is_local: bool) -> int:
     return r
 
 
-def twin_admission(scores: "Scores", band_waves: int, col_gap: int = 0) -> Tuple[bool, int]:
-    """The twin fill's int16 admission rule (gx_twin_admission): (admitted,
+def twin_admission(scores: "Scores", band_waves: int, col_gap: int = 0, is_local: bool = False) -> Tuple[bool, int]:
+    """The twin fill's int16 admission rule (gx_twin_admission_mode): (admitted,
     bound), bound = the largest |value - base| a band of `band_waves` strips
     can reach when a twin's pairs differ by up to col_gap columns."""
     b = ctypes.c_int64(0)
-    r = lib().gx_twin_admission(ctypes.byref(scores.c()), int(band_waves), int(col_gap), ctypes.byref(b))
+    r = lib().gx_twin_admission_mode(ctypes.byref(scores.c()), int(bool(is_local)), int(band_waves), int(col_gap),
+                                     ctypes.byref(b))
     if r < 0:
         raise GxError(3, "invalid scores")
     return bool(r), int(b.value)

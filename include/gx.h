@@ -246,12 +246,15 @@ int gx_plane_bytes_per_cell(const gx_scores* scores, int is_local);
  * *bound receives the largest |value - base| a band of `band_waves` strips can
  * reach with these scores when a twin's two pairs differ by up to col_gap
  * columns; returns 1 when the global twin fill admits the band (bound <
- * 30,000 < 2^15), 0 when it does not, -1 on invalid scores.  (Local batches
- * have their own rule, DESIGN.md 6.7: plain values on base 0, admitted while
- * min(n, m) max(s_match, 0) plus constants stays below 32,000.)  Diagnostic
+ * 30,000 < 2^15), 0 when it does not, -1 on invalid scores.  Diagnostic
  * (tests/test_twin_bound.py checks the rule against brute-force spreads).
  * No reference counterpart. */
 int gx_twin_admission(const gx_scores* scores, int band_waves, int64_t col_gap, int64_t* bound);
+/* The same rule for either mode: local batches (is_local = 1) keep plain
+ * values relative to the same per-block bases, with the neighbour difference
+ * max(|h + g|, U) of the unshifted values and the floor's constants
+ * (DESIGN.md 6.7).  Same returns as gx_twin_admission. */
+int gx_twin_admission_mode(const gx_scores* scores, int is_local, int band_waves, int64_t col_gap, int64_t* bound);
 
 /* ---- sequence.rs / config.rs mirrors ----------------------------------- */
 /* from_fasta (sequence.rs:45-95) on a file: records are appended to the

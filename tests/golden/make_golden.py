@@ -203,15 +203,21 @@ def _synth_job(job):
 
 # The local (Smith-Waterman) batch of bench.py's `local_batch` record: the
 # first LOCAL_RELATED related 30k pairs (a long local alignment each).
-LOCAL_RELATED = 32
+LOCAL_RELATED = 64
+
+
+# Local related pairs of 64k (round-4 verdict item 7: the local twin fill on
+# values beyond 2^15): the first LOCAL_RELATED_64K related_pair(k, 65536).
+LOCAL_RELATED_64K = 16
 
 
 def synthetic_cases(workers: int, lengths, related: bool = False, local: bool = False):
     """Oracle digests of the synthetic batches (related: the SURVEY 8(d) M1
     "related" variant, s2 derived from s1, 80 pairs at 30k; local: its first
-    LOCAL_RELATED pairs aligned locally)."""
+    LOCAL_RELATED pairs aligned locally, LOCAL_RELATED_64K at 64k)."""
     from multiprocessing import Pool
-    jobs = [(L, k, related, local) for L in lengths for k in range(LOCAL_RELATED if local else SYNTH_SETS[L])]
+    count = lambda L: (LOCAL_RELATED_64K if L == 65536 else LOCAL_RELATED) if local else SYNTH_SETS[L]
+    jobs = [(L, k, related, local) for L in lengths for k in range(count(L))]
     jobs.sort(key=lambda x: -x[0])
     out = {L: [] for L in lengths}
     with Pool(workers) as pool:
@@ -222,8 +228,8 @@ def synthetic_cases(workers: int, lengths, related: bool = False, local: bool = 
     for L in lengths:
         out[L].sort(key=lambda c: c["k"])
         name = f"synthetic_related{'_local' if local else ''}_L{L}.json" if related else f"synthetic_L{L}.json"
-        src = ("tests/golden/make_golden.py --related-local (oracle_align_lean, LOCAL, config.toml scores; pair k = "
-               "related_pair(k), k < 32)") if local else ("tests/golden/make_golden.py --related (oracle_align_lean, global, config.toml scores; pair k = "
+        src = (f"tests/golden/make_golden.py --related-local{' --length 65536' if L == 65536 else ''} "
+               f"(oracle_align_lean, LOCAL, config.toml scores; pair k = related_pair(k, {L}), k < {count(L)})") if local else ("tests/golden/make_golden.py --related (oracle_align_lean, global, config.toml scores; pair k = "
                "related_pair(k): s1 of synthetic pair k, s2 derived with seed 0x5EED0003 + 0x10000 k)") if related else \
               ("tests/golden/make_golden.py --synthetic (oracle_align_lean, global, config.toml "
                "scores; pair k = splitmix64 seeds 0x5EED0001/2 + 0x10000 k, bench.py synth_pair)")
@@ -240,12 +246,13 @@ def main():
                     help="comma-separated lengths of SYNTH_SETS to digest, or 'all'")
     ap.add_argument("--related", action="store_true", help="the related 30k batch (SURVEY 8(d) M1 variant)")
     ap.add_argument("--related-local", action="store_true",
-                    help="local digests of the first 32 related 30k pairs (bench.py local_batch)")
+                    help="local digests of the first 64 related 30k pairs (bench.py local_batch), or 16 at --length 65536")
+    ap.add_argument("--length", type=int, default=30000, help="--related-local: pair length (30000 or 65536)")
     ap.add_argument("--workers", type=int, default=7)
     args = ap.parse_args()
     o.build()
     if args.related_local:
-        synthetic_cases(args.workers, [30000], related=True, local=True)
+        synthetic_cases(args.workers, [args.length], related=True, local=True)
         return
     if args.related:
         synthetic_cases(args.workers, [30000], related=True)

@@ -1,12 +1,12 @@
 """GPU parity of the local (Smith-Waterman) twin fill (gx_fill_pk.hip LOCAL):
 batches of local alignments run two pairs per band on plain 16-bit values
-with the 0 floor of algo.rs:103 in every gap recurrence and a per-row
+relative to per-block bases, with the 0 floor of algo.rs:103 in every gap recurrence and a per-row
 last-max tracker (algo.rs:310-322).  Every result -- the start cell through
 the score, the alignment, the statistics and the compact score planes -- must
 equal the oracle's local restatement (oracle/gx_oracle.c), on shapes around
 the strip and band edges, tie-heavy inputs (all-mismatch tables are all
 zeros, so the last maximum is cell (n, m)), scores with and without the
-small-alphabet tables, and values up to the admission bound."""
+small-alphabet tables, and values past 2^15 (per-block bases)."""
 import random
 
 import pytest
@@ -127,14 +127,58 @@ def test_local_twin_random_batches(gx, ctx, oracle, monkeypatch, seed):
     _check(gx, ctx, oracle, pairs, scores, twin=1 if _w16_ok(scores) else 0)
 
 
-def test_local_twin_bound_binds(gx, ctx, oracle, monkeypatch):
-    """Values at the admission bound: 15,000-long all-match twins at s = 2
-    reach 30,000 (bound 30,079 < 32,000, admitted); 16,000 columns at s = 2
-    (bound 32,079) are refused and run the scalar fill.  Both bit-exact."""
+def test_local_twin_large_values(gx, ctx, oracle, monkeypatch):
+    """Values past 2^15 (per-block bases, gx_fill_pk.hip LOCAL): all-match
+    twins at s = 2 reach 40,000 (20,000 columns) and 32,000; the relative
+    floor clamps once a base exceeds 2^15, the row maxima fold into int32 at
+    every base change.  Both bit-exact against the oracle."""
     monkeypatch.setenv("GX_LAYOUT", "0")
     scores = (2, -3, -1, -5)
-    _check(gx, ctx, oracle, [(b"A" * 15000, b"A" * 15000), (b"A" * 14990, b"A" * 15000)], scores, twin=1)
-    _check(gx, ctx, oracle, [(b"A" * 16000, b"A" * 16000), (b"A" * 15990, b"A" * 16000)], scores, twin=0)
+    assert gx.twin_admission(gx.Scores(*scores), 15, 10, is_local=True)[0]
+    _check(gx, ctx, oracle, [(b"A" * 20000, b"A" * 20000), (b"A" * 15990, b"A" * 16000)], scores, twin=1)
+
+
+def test_local_twin_64k_related(gx, ctx, monkeypatch):
+    """Round-3 verdict item 7: 16 related 64k pairs (SURVEY 8(d) M1 variant,
+    tests/golden/make_golden.py --related-local --length 65536) aligned
+    locally take the twin fill by default (local scores reach ~38,000, past
+    the int16 range of a fill on fixed bases); two pipelined passes, every
+    pass's plane checksums and results, and the final alignments, against
+    the oracle's digests."""
+    import hashlib
+    import json
+    import os
+    import sys
+
+    import numpy as np
+
+    from conftest import GOLDEN
+    sys.path.insert(0, GOLDEN)
+    import make_golden
+    monkeypatch.delenv("GX_TWIN", raising=False)
+    with open(os.path.join(GOLDEN, "synthetic_related_local_L65536.json")) as f:
+        cases = json.load(f)["cases"]
+    assert len(cases) == 16 and max(c["score"] for c in cases) > 32767
+    pairs = [make_golden.related_pair(c["k"], 65536) for c in cases]
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, _ = st.run(gx.Scores(*CONFIG_SCORES), True, keep_planes=True, steps=2, plane_sums=True)
+    info = ctx.fill_info()
+    assert info["twin"] == 1 and info["layout"] == 0, info
+    sums = st.plane_sums()
+    passes = st.pass_results()
+    for p, c in enumerate(cases):
+        for k in range(2):
+            r = passes[k][p]
+            assert [int(x) for x in sums[k, p]] == [int(x) for x in c["plane_sums"]], (p, k)
+            assert (r.score, [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps], r.n_steps) == \
+                   (c["score"], c["stats"], c["n_steps"]), (p, k)
+        steps = st.steps(p)
+        h = hashlib.sha256()
+        h.update(bytes(steps["choice"].astype(np.uint8)))
+        h.update(steps["i"].astype("<u8").tobytes())
+        h.update(steps["j"].astype("<u8").tobytes())
+        assert h.hexdigest() == c["alignment_sha256"], p
+    ctx.trim()
 
 
 def test_local_twin_overlapped(gx, ctx, oracle, monkeypatch):

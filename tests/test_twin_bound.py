@@ -49,9 +49,10 @@ def _neighbour_d(scores):
     return max(abs(a - g), abs(U - g))
 
 
-def _max_spread_ratio(planes, g, W, dm):
+def _max_spread_ratio(planes, g, W, dm, local=False):
     """Largest spread of strip k over its per-strip bound term, over every
-    band and strip: max |V''(i, j) - SM''(r0, c)| / (192 (k + 1) + 16 + dm)."""
+    band and strip: max |V''(i, j) - SM''(r0, c)| / (192 (k + 1) + 16 + dm).
+    local: score_max carries the 0 floor (algo.rs:103), no shift (g = 0)."""
     from scipy.ndimage import maximum_filter1d, minimum_filter1d
     I, D, S = (p.astype(np.int64) for p in planes)
     n1, m1 = I.shape
@@ -59,6 +60,8 @@ def _max_spread_ratio(planes, g, W, dm):
     jj = np.arange(m1)[None, :]
     shift = (ii + jj) * g
     SM = np.maximum(np.maximum(I, D), S) - shift
+    if local:
+        SM = np.maximum(SM, 0)
     worst = 0.0
     band_rows = ROWS * W
     for r0 in range(0, n1 - 1, band_rows):
@@ -139,3 +142,40 @@ def test_spread_unequal_twins(oracle):
     b = bytes(rng.choice(list(b"AC"), size=m).tolist())
     o = oracle.align(a, b, CONFIG_SCORES, want_planes=True)
     assert _max_spread_ratio(o.planes, CONFIG_SCORES[2], W, dm) <= _neighbour_d(CONFIG_SCORES)
+
+
+# Local twins (gx_fill_pk.hip LOCAL) keep plain values relative to the same
+# per-block bases: the neighbour difference of the unshifted local values is
+# max(|a|, U) (d8_planes_ok's inequalities, which the 0 floor keeps), and the
+# constants carry the floor's offsets (K = max(0, -s_min), |g|).
+def _neighbour_d_local(scores):
+    sm, smm, g, h = scores
+    a = h + g
+    return max(abs(a), max(0, max(sm, smm) - a), 1)
+
+
+LOCAL_SCORES = [(CONFIG_SCORES, 15), ((2, -3, -1, -5), 15), ((3, -2, -1, -3), 15), ((1, -1, -1, -16), 8)]
+
+
+@pytest.mark.parametrize("scores,W", LOCAL_SCORES)
+def test_local_admission_rule(gx, scores, W):
+    """gx_twin_admission_mode(is_local=1): the local rule's bound, admitted at W."""
+    ok, bound = gx.twin_admission(gx.Scores(*scores), W, 0, is_local=True)
+    sm, smm, g, h = scores
+    const = 2 * (abs(h + g) + abs(max(sm, smm)) + abs(min(sm, smm))) + 64 + max(0, -min(sm, smm)) + abs(g)
+    assert bound == _neighbour_d_local(scores) * (192 * W + 16) + const
+    assert ok and bound < 30000, (scores, W, bound)
+
+
+@pytest.mark.parametrize("scores,W", LOCAL_SCORES)
+@pytest.mark.parametrize("family", ["all_mismatch", "all_match", "gap_rows", "gap_cols", "repeat", "random"])
+def test_local_spread_within_rule(oracle, scores, W, family):
+    """Brute force, local mode: every state of every strip of every band stays
+    within the local rule's per-strip term of every base the kernel could hold
+    for it (plain values: no shift)."""
+    n = ROWS * W * 2 + 300
+    m = 1400
+    a, b = _families(n, m)[family]
+    o = oracle.align(a, b, scores, is_local=True, want_planes=True)
+    ratio = _max_spread_ratio(o.planes, 0, W, 0, local=True)
+    assert ratio <= _neighbour_d_local(scores), (family, scores, W, ratio)
