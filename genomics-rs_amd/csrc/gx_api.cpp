@@ -9,6 +9,7 @@
 // start search over boundary cells, and the labelling of the walk into
 // AlignmentChoice values (algo.rs:351-400).
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -113,9 +114,50 @@ struct SmallAlpha {
     }
 };
 
+// A walk's labelled steps: a growable array that, unlike std::vector, does
+// not zero what it reserves (the labelling writes every step, ~48 MB a pass
+// of a 1024 x 1k batch, and is on the short-batch step's critical path).
+class StepBuf {
+public:
+    StepBuf() = default;
+    StepBuf(const StepBuf& o) { *this = o; }
+    StepBuf(StepBuf&& o) noexcept : p_(o.p_), n_(o.n_), cap_(o.cap_) { o.p_ = nullptr; o.n_ = o.cap_ = 0; }
+    StepBuf& operator=(const StepBuf& o) {
+        if (this != &o) { clear(); reserve(o.n_); if (o.n_) memcpy(p_, o.p_, o.n_ * sizeof(gx_step)); n_ = o.n_; }
+        return *this;
+    }
+    StepBuf& operator=(StepBuf&& o) noexcept {
+        std::swap(p_, o.p_); std::swap(n_, o.n_); std::swap(cap_, o.cap_);
+        return *this;
+    }
+    ~StepBuf() { free(p_); }
+    void clear() { n_ = 0; }
+    bool reserve(size_t c) {   // keeps the contents
+        if (c <= cap_) return true;
+        gx_step* q = (gx_step*)malloc(c * sizeof(gx_step));
+        if (!q) return false;
+        if (n_) memcpy(q, p_, n_ * sizeof(gx_step));
+        free(p_);
+        p_ = q; cap_ = c;
+        return true;
+    }
+    void push_back(const gx_step& st) {
+        if (n_ == cap_) reserve(std::max<size_t>(16, 2 * cap_));
+        p_[n_++] = st;
+    }
+    size_t size() const { return n_; }
+    size_t capacity() const { return cap_; }
+    gx_step* data() { return p_; }
+    const gx_step* data() const { return p_; }
+    void set_size(size_t n) { n_ = n; }   // (<= capacity; the steps written through data())
+private:
+    gx_step* p_ = nullptr;
+    size_t n_ = 0, cap_ = 0;
+};
+
 // Interior walk + labelling + boundary continuation (algo.rs:306-422).
 struct Walk {
-    std::vector<gx_step> steps;
+    StepBuf steps;
     gx_result res{};
 };
 
@@ -1392,6 +1434,54 @@ static bool tb_match(const uint8_t* s1, size_t n, const uint8_t* s2, size_t m, u
     return a == b;
 }
 
+// The boundary part of a walk from (i, j) on: the reference loop on analytic
+// cells (algo.rs:339-422), appending to w.steps and counting into w.res.
+static int label_boundary(const HostScores& hs, int is_local, const uint8_t* s1, size_t n, const uint8_t* s2,
+                          size_t m, uint64_t i, uint64_t j, int last, Walk& w) {
+    gx_result& r = w.res;
+    for (;;) {
+        int64_t I, D, S;
+        boundary_cell(hs, i, j, &I, &D, &S);
+        const int64_t mx = smax(I, S, D, is_local);
+        gx_step st{};
+        st.i = i; st.j = j;
+        bool di, dj;
+        if (mx == S) {
+            const bool mt = tb_match(s1, n, s2, m, i, j);
+            st.choice = mt ? GX_MATCH : GX_MISMATCH;
+            if (mt) r.matches++; else r.mismatches++;
+            last = st.choice;
+            di = dj = true;
+        } else if (mx == I) {
+            if (last == GX_INSERT) { st.choice = GX_INSERT; r.gap_extensions++; }
+            else { st.choice = GX_OPEN_INSERT; r.opening_gaps++; }
+            last = GX_INSERT;
+            di = false; dj = true;
+        } else if (mx == D) {
+            if (last == GX_DELETE) { st.choice = GX_DELETE; r.gap_extensions++; }
+            else { st.choice = GX_OPEN_DELETE; r.opening_gaps++; }
+            last = GX_DELETE;
+            di = true; dj = false;
+        } else {
+            if (is_local && mx == 0) {
+                if (log_info())   // algo.rs:403
+                    fprintf(stderr, "[gx INFO] Ending local alignment at (%llu, %llu)\n", (unsigned long long)i,
+                            (unsigned long long)j);
+                break;
+            }
+            return fail(GX_EPANIC, "Unexpected score during retrace: " + std::to_string(mx) + " at (" +
+                                       std::to_string(i) + ", " + std::to_string(j) + ")");
+        }
+        w.steps.push_back(st);
+        const bool inone = di && i == 0, jnone = dj && j == 0;
+        if (inone && jnone) break;
+        i = inone ? 0 : i - (di ? 1 : 0);
+        j = jnone ? 0 : j - (dj ? 1 : 0);
+        if (i == 0 && j == 0) break;
+    }
+    return GX_OK;
+}
+
 // Labels the walk (algo.rs:339-422).  The interior moves come from `src`,
 // which calls emit(code) per move (0 sub, 1 insert, 2 delete) while emit
 // returns true; the boundary part follows the reference loop.
@@ -1433,51 +1523,82 @@ static int label_walk(const HostScores& hs, int is_local, const uint8_t* s1, siz
         return true;
     });
     r.matches = nmat; r.mismatches = nmis; r.gap_extensions = next; r.opening_gaps = nopen;
-    // boundary part: the reference loop on analytic cells
-    while (!done) {
-        int64_t I, D, S;
-        boundary_cell(hs, i, j, &I, &D, &S);
-        const int64_t mx = smax(I, S, D, is_local);
-        gx_step st{};
-        st.i = i; st.j = j;
-        bool di, dj;
-        if (mx == S) {
-            const bool mt = tb_match(s1, n, s2, m, i, j);
-            st.choice = mt ? GX_MATCH : GX_MISMATCH;
-            if (mt) r.matches++; else r.mismatches++;
-            last = st.choice;
-            di = dj = true;
-        } else if (mx == I) {
-            if (last == GX_INSERT) { st.choice = GX_INSERT; r.gap_extensions++; }
-            else { st.choice = GX_OPEN_INSERT; r.opening_gaps++; }
-            last = GX_INSERT;
-            di = false; dj = true;
-        } else if (mx == D) {
-            if (last == GX_DELETE) { st.choice = GX_DELETE; r.gap_extensions++; }
-            else { st.choice = GX_OPEN_DELETE; r.opening_gaps++; }
-            last = GX_DELETE;
-            di = true; dj = false;
-        } else {
-            if (is_local && mx == 0) {
-                if (log_info())   // algo.rs:403
-                    fprintf(stderr, "[gx INFO] Ending local alignment at (%llu, %llu)\n", (unsigned long long)i,
-                            (unsigned long long)j);
-                break;
-            }
-            return fail(GX_EPANIC, "Unexpected score during retrace: " + std::to_string(mx) + " at (" +
-                                       std::to_string(i) + ", " + std::to_string(j) + ")");
-        }
-        w.steps.push_back(st);
-        const bool inone = di && i == 0, jnone = dj && j == 0;
-        if (inone && jnone) break;
-        i = inone ? 0 : i - (di ? 1 : 0);
-        j = jnone ? 0 : j - (dj ? 1 : 0);
-        if (i == 0 && j == 0) break;
+    if (!done) {
+        const int rc = label_boundary(hs, is_local, s1, n, s2, m, i, j, last, w);
+        if (rc) return rc;
     }
     r.n_steps = w.steps.size();
     return GX_OK;
 }
 
+
+// One labelled step as three 8-B non-temporal stores: a batch's step buffers
+// are far larger than the caches, so this skips each line's read for
+// ownership (label_walk_records ends with an sfence).
+static inline void put_step(gx_step* o, int choice, uint64_t i, uint64_t j) {
+    _mm_stream_si64((long long*)o, (long long)(unsigned)choice);
+    _mm_stream_si64((long long*)o + 1, (long long)i);
+    _mm_stream_si64((long long*)o + 2, (long long)j);
+}
+
+// label_walk on the device walk's per-row records (tb_strip_kernel /
+// tb_seq_kernel: each row's insert run, then its diagonal or delete move, or
+// the run's end at column 0), written straight into the step buffer: a run of
+// L inserts is one open-or-extend step and L - 1 extensions.  The same steps
+// and statistics as label_walk over RecordsSrc.
+static int label_walk_records(const HostScores& hs, int is_local, const uint8_t* s1, size_t n, const uint8_t* s2,
+                              size_t m, uint64_t si, uint64_t sj, const TbOut& tb, size_t p, Walk& w) {
+    uint64_t i = si, j = sj;
+    int last = GX_MATCH;
+    uint64_t nmat = 0, nmis = 0, next = 0, nopen = 0;
+    const size_t cap = (size_t)si + (size_t)sj + 2;   // every move lowers i + j
+    w.steps.clear();
+    if (!w.steps.reserve(cap)) return fail(GX_ENOMEM, "step buffer");
+    gx_step* const o = w.steps.data();
+    size_t k = 0;
+    bool done = false;
+    for (int s = tb.c[4 * p + 2]; s >= 0 && !done; --s) {
+        const int* g = &tb.sg[4 * (tb.so[p] + s)];
+        if (!g[3]) break;
+        const uint32_t* rr = &tb.hr[(tb.so[p] + s) * tb.srows];
+        for (int q = 0; q < g[2]; ++q) {
+            const uint32_t rec = rr[q], L = rec >> 2, c = rec & 3u;
+            if (k + L + 1 > cap || L > j) { _mm_sfence(); return fail(GX_EPANIC, "device walk record out of range"); }
+            if (L) {
+                const bool ext = last == GX_INSERT;
+                put_step(o + k, ext ? GX_INSERT : GX_OPEN_INSERT, i, j);
+                next += ext + (L - 1); nopen += !ext;
+                ++k; --j;
+                for (uint32_t t = 1; t < L; ++t) { put_step(o + k, GX_INSERT, i, j); ++k; --j; }
+                last = GX_INSERT;
+            }
+            if (c == 0u) {
+                const bool mt = tb_match(s1, n, s2, m, i, j);
+                put_step(o + k, mt ? GX_MATCH : GX_MISMATCH, i, j);
+                nmat += mt; nmis += !mt;
+                last = mt ? GX_MATCH : GX_MISMATCH;
+                ++k; --i; --j;
+            } else if (c != 1u) {
+                const bool ext = last == GX_DELETE;
+                put_step(o + k, ext ? GX_DELETE : GX_OPEN_DELETE, i, j);
+                next += ext; nopen += !ext;
+                last = GX_DELETE;
+                ++k; --i;
+            }
+            if (i == 0 && j == 0) { done = true; break; }   // (only a diagonal move from (1, 1) gets here)
+        }
+    }
+    _mm_sfence();
+    w.steps.set_size(k);
+    gx_result& r = w.res;
+    r.matches = nmat; r.mismatches = nmis; r.gap_extensions = next; r.opening_gaps = nopen;
+    if (!done) {
+        const int rc = label_boundary(hs, is_local, s1, n, s2, m, i, j, last, w);
+        if (rc) return rc;
+    }
+    r.n_steps = w.steps.size();
+    return GX_OK;
+}
 
 struct TbStart {
     int i, j;   // interior start cell, or 0 = nothing to walk
@@ -2148,8 +2269,8 @@ static int label_batch(gx_context* ctx, const std::vector<PairHost>& ph, const H
     std::vector<std::string> perr(P);
     const std::function<void(size_t)> label_one = [&](size_t p) {
         if (dev_of[p] >= 0)
-            prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], ph[p].n + ph[p].m,
-                                RecordsSrc{&tb, (size_t)dev_of[p]}, walks[p]);
+            prc[p] = label_walk_records(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], tb,
+                                        (size_t)dev_of[p], walks[p]);
         else
             prc[p] = label_walk(hs, is_local, ph[p].s1, ph[p].n, ph[p].s2, ph[p].m, si[p], sj[p], 0,
                                 MovesSrc{nullptr, 0}, walks[p]);
