@@ -6,7 +6,6 @@ counters per cell, averaged over the fill dispatches after the first (cold).
 
     python tools/local_fill_summary.py gpurun_out/local_<tag> <tag>
 """
-import csv
 import glob
 import json
 import os
@@ -20,10 +19,15 @@ def main():
     src, tag = sys.argv[1], sys.argv[2]
     with open(os.path.join(src, "kt.json")) as f:
         bench = json.loads(f.read().strip().splitlines()[-1])
-    with open(glob.glob(os.path.join(src, "kt", "**", "*kernel_stats.csv"), recursive=True)[0]) as f:
-        rows = [r for r in csv.DictReader(f) if "fill_pk_kernel" in r["Name"]]
-    kt = [{"kernel": r["Name"][:60], "calls": int(r["Calls"]), "avg_ms": round(float(r["AverageNs"]) / 1e6, 4),
-           "min_ms": round(float(r["MinNs"]) / 1e6, 4), "max_ms": round(float(r["MaxNs"]) / 1e6, 4)} for r in rows]
+    # kernel trace (rocpd database): the local fill's launches, the first (cold) one apart
+    kdb = sqlite3.connect(glob.glob(os.path.join(src, "kt", "**", "*.db"), recursive=True)[0])
+    ks = [(n, d, g, vg, sg) for n, d, g, vg, sg in kdb.execute(
+        "select name, duration, grid_x, vgpr_count, sgpr_count from kernels order by start") if "fill_pk_kernel" in n]
+    durs = [d for _, d, _, _, _ in ks]
+    kt = {"kernel": ks[0][0][:60], "launches": len(ks), "first_ms": round(durs[0] / 1e6, 4),
+          "avg_ms_after_first": round(sum(durs[1:]) / max(len(durs) - 1, 1) / 1e6, 4),
+          "min_ms": round(min(durs) / 1e6, 4), "max_ms": round(max(durs) / 1e6, 4),
+          "grid_x": sorted({g for _, _, g, _, _ in ks}), "vgpr": ks[0][3], "sgpr": ks[0][4]}
     db = glob.glob(os.path.join(src, "pmc", "**", "*.db"), recursive=True)[0]
     c = sqlite3.connect(db)
     per = {}
