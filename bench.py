@@ -364,17 +364,29 @@ def local_batch_record(gx, ctx, steps: int):
     path = os.path.join(ROOT, "tests", "golden", "synthetic_related_local_L30000.json")
     with open(path) as f:
         gold = {c["k"]: c for c in json.load(f)["cases"]}
-    res, _ = st.run(scores, True, True, plane_sums=True)
+    mine = {p: gold[p] for p in range(len(pairs))}
+    # every timed pass (the launch that was measured), then two more passes
+    # through the same pipeline with device plane checksums of each pass
+    timed_checked = check_passes(st.pass_results(), mine, 0, 0, "local_batch timed")
+    passes = 2
+    st.run(scores, True, True, steps=passes, plane_sums=True)
+    if ctx.fill_info() != finfo:
+        raise RuntimeError(f"local_batch: the parity passes took a different launch than the timed call: "
+                           f"{ctx.fill_info()} != {finfo}")
+    check_passes(st.pass_results(), mine, 0, 0, "local_batch parity")
     sums = st.plane_sums()
     for p in range(len(pairs)):
-        r, c = res[p], gold[p]
-        got = (r.score, [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps], r.n_steps,
-               alignment_sha256(st.steps(p)), [int(x) for x in sums[0, p]])
-        want = (c["score"], c["stats"], c["n_steps"], c["alignment_sha256"], [int(x) for x in c["plane_sums"]])
-        if got != want:
-            raise RuntimeError(f"local_batch: pair {p} differs from the oracle digest: {got[:3]} != {want[:3]}")
-    out["parity"] = {"pairs_checked": len(pairs), "bit_exact": True,
-                     "fields": "score, statistics, alignment sha256, I/D/S plane checksums",
+        c = gold[p]
+        if alignment_sha256(st.steps(p)) != c["alignment_sha256"]:
+            raise RuntimeError(f"local_batch: pair {p} alignment differs from the oracle digest")
+        for k in range(passes):
+            if [int(x) for x in sums[k, p]] != [int(x) for x in c["plane_sums"]]:
+                raise RuntimeError(f"local_batch: pass {k}, pair {p} score planes differ from the oracle's checksums")
+    out["parity"] = {"pairs_checked": len(pairs), "bit_exact": True, "timed_passes_checked": timed_checked,
+                     "parity_passes": passes, "fill_groups": finfo.get("groups"),
+                     "fields": "every timed pass: score, statistics, length; two more passes through the same "
+                               "launch: score, statistics, length, I/D/S plane checksums of each pass, "
+                               "alignment sha256",
                      "source": os.path.relpath(path, ROOT)}
     return out
 

@@ -44,7 +44,7 @@ hipError_t launch_local_col(const PairDev* d_pairs, int npairs, PairRes* d_pres,
 hipError_t launch_fill_cs2(int W, bool local, bool planes, bool tbl, const PairDev* d_pairs, int npairs,
                            int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                            hipStream_t st);
-hipError_t launch_fill_skew(int W, bool local, bool planes, bool tbl, const PairDev* d_pairs, int npairs,
+hipError_t launch_fill_skew(int W, bool local, bool planes, bool tbl, bool trace, const PairDev* d_pairs, int npairs,
                             int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                             hipStream_t st);
 hipError_t launch_skew_codes(const PairDev* d_pairs, int npairs, int mmax, Scores32 sc, bool tbl, hipStream_t st);
@@ -332,7 +332,16 @@ static void* io_pinned(gx_context* ctx, size_t bytes) {
     return ctx->io_pin.p;
 }
 
-static int pool_get(gx_context* ctx, size_t bytes, DevBuf* out) {
+static bool pool_poison();
+static int pool_take(gx_context* ctx, size_t bytes, DevBuf* out);
+// `st`: the stream its new user runs on (GX_POOL_POISON fills the buffer there,
+// ahead of that user's work).
+static int pool_get(gx_context* ctx, size_t bytes, DevBuf* out, hipStream_t st = nullptr) {
+    const int rc = pool_take(ctx, bytes, out);
+    if (rc == GX_OK && pool_poison()) (void)hipMemsetAsync(out->p, 0xA5, out->cap, st ? st : ctx->stream);
+    return rc;
+}
+static int pool_take(gx_context* ctx, size_t bytes, DevBuf* out) {
     bytes = std::max<size_t>(bytes, 256);
     size_t best = (size_t)-1;
     int bi = -1;
@@ -370,10 +379,14 @@ static int pool_get(gx_context* ctx, size_t bytes, DevBuf* out) {
     out->cap = bytes;
     return GX_OK;
 }
-// GX_POOL_POISON=1 (debug): every buffer returned to the pool is filled with
-// 0xA5 bytes in stream order, so a later user that reads a buffer it did not
-// write (pool reuse or stream-order bugs) sees garbage instead of the previous
-// pass's identical data.
+// GX_POOL_POISON=1 (debug): every buffer the pool hands out is filled with
+// 0xA5 bytes on the stream of its new user, before that user's work.  A user
+// that reads what it did not write (pool reuse bugs) sees garbage instead of
+// the previous pass's identical data, and a buffer handed to a stream that is
+// not ordered behind the buffer's previous readers (stream-order bugs, e.g. an
+// overlapped pipeline's next fill and the walk still reading its planes) has
+// those readers read garbage.  Poisoning at release instead would have to run
+// on the last reader's stream and order every later user behind it.
 static bool pool_poison() {
     static int v = -1;
     if (v < 0) {
@@ -383,10 +396,7 @@ static bool pool_poison() {
     return v == 1;
 }
 static void pool_put(gx_context* ctx, DevBuf& b) {
-    if (b.p) {
-        if (pool_poison()) (void)hipMemsetAsync(b.p, 0xA5, b.cap, ctx->stream);
-        ctx->free_list.push_back(b);
-    }
+    if (b.p) ctx->free_list.push_back(b);
     b = DevBuf{};
 }
 
@@ -712,12 +722,17 @@ struct PairHost {
 // Covid 29,903 x 29,882 global: layout 3 (4.52 vs 4.62 ms); BRCA2 11,382 x
 // 10,346 local: the split column step (1.74 vs 1.79); 64 x 30,000: layout 3
 // (1.5 vs 3.4).
-// Layout 3 needs h <= 0 (the folded gap opening) and, for the virtual
-// columns of its global ramp-up (values drift from -2^30 by up to 64 steps of
-// |g| + |h| + |s|), small penalties.
-static bool skew_ok(const Scores32& sc, bool track) {
-    const long long drift = 64LL * (std::llabs((long long)sc.g) + std::llabs((long long)sc.h) + 256);
-    return !track && sc.h <= 0 && drift < (1LL << 28);
+// Layout 3 needs h <= 0 (the folded gap opening), small penalties for the
+// virtual columns of its global ramp-up (values drift from -2^30 by up to 64
+// steps of |g| + |h| + |s''|, s'' = s - 2g the shifted substitution score),
+// and fewer than 2^24 - 128 columns: its skeleton holds E + 64 in the 24 bits
+// tb_chase_kernel decodes, and a strip's int32 plane (256 (m + 64) bytes)
+// must stay inside one buffer descriptor's 32-bit range.
+static bool skew_ok(const Scores32& sc, bool track, size_t mmax) {
+    const long long g = sc.g;
+    const long long s2 = std::max(std::llabs((long long)sc.sm - 2 * g), std::llabs((long long)sc.smm - 2 * g));
+    const long long drift = 64LL * (std::llabs(g) + std::llabs((long long)sc.h) + s2);
+    return !track && sc.h <= 0 && drift < (1LL << 28) && mmax + 128 < (1u << 24);
 }
 static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int grid_cap, bool track) {
     const long long span = 65LL * (std::llabs((long long)sc.g) + std::llabs((long long)sc.h));
@@ -740,10 +755,11 @@ static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int 
         est1 = std::max(est1, local ? m * 110.0 + S * 3370.0 : m * 113.0 + S * 2660.0);
         est3 = std::max(est3, local ? m * 57.5 + S * 6660.0 : m * 50.0 + S * 6460.0);
     }
-    const int lat = skew_ok(sc, track) && (!cs_ok || est3 < est1) ? 3 : cs_ok ? 1 : 0;
+    const bool sk_ok = skew_ok(sc, track, mmax);
+    const int lat = sk_ok && (!cs_ok || est3 < est1) ? 3 : cs_ok ? 1 : 0;
     if (const char* e = getenv("GX_LAYOUT"); e && *e) {
         const int want = atoi(e);
-        if (want == 3) return skew_ok(sc, track) ? 3 : cs_ok ? 1 : 0;
+        if (want == 3) return sk_ok ? 3 : cs_ok ? 1 : 0;
         return (want == 1 && cs_ok) ? 1 : 0;
     }
     return strips64 <= 6LL * grid_cap ? lat : 0;
@@ -1065,19 +1081,19 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     int rc;
     const int nplanes = w16 ? 1 : lcs ? 4 : 3;
     if (!chars_dev) {
-        if ((rc = pool_get(ctx, chars_bytes, &job.chars))) return rc;
+        if ((rc = pool_get(ctx, chars_bytes, &job.chars, fs))) return rc;
     }
-    if (planes && (rc = pool_get(ctx, plane_elems * plane_esz * nplanes, &job.planes))) return rc;
-    if (codes && (rc = pool_get(ctx, code_elems * sizeof(uint32_t), &job.codes))) return rc;
-    if ((rc = pool_get(ctx, std::max<size_t>(skel_elems, 1) * sizeof(int), &job.skel))) return rc;
-    if ((rc = pool_get(ctx, std::max<size_t>(feed_recs, 1) * sizeof(Rec), &job.feed))) return rc;
-    if ((rc = pool_get(ctx, std::max(strips, 1) * sizeof(StripRes), &job.sres))) return rc;
+    if (planes && (rc = pool_get(ctx, plane_elems * plane_esz * nplanes, &job.planes, fs))) return rc;
+    if (codes && (rc = pool_get(ctx, code_elems * sizeof(uint32_t), &job.codes, fs))) return rc;
+    if ((rc = pool_get(ctx, std::max<size_t>(skel_elems, 1) * sizeof(int), &job.skel, fs))) return rc;
+    if ((rc = pool_get(ctx, std::max<size_t>(feed_recs, 1) * sizeof(Rec), &job.feed, fs))) return rc;
+    if ((rc = pool_get(ctx, std::max(strips, 1) * sizeof(StripRes), &job.sres, fs))) return rc;
     // one buffer [PairRes x P | band counter + status (64 B) | band progress]:
     // one memset before the launch, one copy of the results and status after
     // it (each small copy or memset on the stream costs a runtime round trip
     // of ~100 us between a batch's fill and its walk, profiles: r04 1024 x 1k)
     const size_t res_bytes = P * sizeof(PairRes), prog_bytes = std::max<size_t>(prog_elems, 1) * sizeof(int);
-    if ((rc = pool_get(ctx, res_bytes + 64 + prog_bytes, &job.pres))) return rc;
+    if ((rc = pool_get(ctx, res_bytes + 64 + prog_bytes, &job.pres, fs))) return rc;
     int* const counter = (int*)((char*)job.pres.p + res_bytes);
     int* const progress = counter + 16;
     // band queue order, stored after the pair descriptors: band-major ("round"
@@ -1102,7 +1118,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                 if (lb < job.pd[p].bands) { order.push_back((int)p); order.push_back(lb); }
     }
     const size_t ord_bytes = align_up(order.size() * sizeof(int), 16);   // keeps the PairRes staging 16-B aligned
-    if (slot < 0 && (rc = pool_get(ctx, P * sizeof(PairDev) + ord_bytes, &job.pairs))) return rc;
+    if (slot < 0 && (rc = pool_get(ctx, P * sizeof(PairDev) + ord_bytes, &job.pairs, fs))) return rc;
     // -- chars upload
     const uint8_t* cbase = chars_dev;
     if (!chars_dev) {
@@ -1134,14 +1150,14 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     if (lay == 3) {
         size_t cc = 0;
         for (size_t p = 0; p < P; ++p) cc += (size_t)job.pd[p].m + 192;
-        if ((rc = pool_get(ctx, cc * sizeof(int), &job.ccodes))) return rc;
+        if ((rc = pool_get(ctx, cc * sizeof(int), &job.ccodes, fs))) return rc;
         cc = 0;
         for (size_t p = 0; p < P; ++p) { job.pd[p].ccodes = (const int*)job.ccodes.p + cc; cc += (size_t)job.pd[p].m + 192; }
     }
     const char* trace_file = slot < 0 ? getenv("GX_TRACE_FILE") : nullptr;
     DevBuf trace;
     if (trace_file && *trace_file) {
-        if ((rc = pool_get(ctx, (size_t)std::max(strips, 1) * sizeof(StripTrace), &trace))) return rc;
+        if ((rc = pool_get(ctx, (size_t)std::max(strips, 1) * sizeof(StripTrace), &trace, fs))) return rc;
         HIPCHK(hipMemsetAsync(trace.p, 0, (size_t)std::max(strips, 1) * sizeof(StripTrace), fs));
         for (size_t p = 0; p < P; ++p) job.pd[p].trace = (StripTrace*)trace.p + job.pd[p].strip_base;
     }
@@ -1204,7 +1220,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                               (const PairDev*)job.pairs.p, (int)P, (int)tw.size(), bands, counter,
                               (PairRes*)job.pres.p, (StripRes*)job.sres.p, scl, grid, fs));
     else if (bands > 0 && lay == 3)
-        HIPCHK(launch_fill_skew(W, is_local != 0, planes, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
+        HIPCHK(launch_fill_skew(W, is_local != 0, planes, tbl, trace.p != nullptr, (const PairDev*)job.pairs.p, (int)P, bands,
                                 counter, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
     else if (bands > 0 && cs2)
         HIPCHK(launch_fill_cs2(W, is_local != 0, planes, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
@@ -1268,6 +1284,9 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         if (FILE* f = fopen(trace_file, "w")) {
             fprintf(f, "pair,strip,band,t_start,t_first,t_end,clk,wait_in,wait_out,W,fill_ms");
             for (int q = 0; q < kTraceQ; ++q) fprintf(f, ",q%d", q + 1);
+            for (int q = 0; q < kTraceTL; ++q) fprintf(f, ",tl%d", q);
+            for (int q = 0; q < kTraceTL; ++q) fprintf(f, ",tc%d", q);
+            for (int q = 0; q < kTraceTL; ++q) fprintf(f, ",ts%d", q);
             fprintf(f, "\n");
             for (size_t p = 0; p < P; ++p)
                 for (int s = 0; s < job.pd[p].strips; ++s) {
@@ -1275,6 +1294,9 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                     fprintf(f, "%zu,%d,%d,%lld,%lld,%lld,%lld,%d,%d,%d,%.4f", p, s, job.pd[p].band_base + s / W,
                             t.t_start, t.t_first, t.t_end, t.clk, t.wait_in, t.wait_out, W, ms);
                     for (int q = 0; q < kTraceQ; ++q) fprintf(f, ",%lld", t.t_q[q]);
+                    for (int q = 0; q < kTraceTL; ++q) fprintf(f, ",%lld", t.tl[q]);
+                    for (int q = 0; q < kTraceTL; ++q) fprintf(f, ",%lld", t.tc[q]);
+                    for (int q = 0; q < kTraceTL; ++q) fprintf(f, ",%lld", t.ts[q]);
                     fprintf(f, "\n");
                 }
             fclose(f);
@@ -1639,8 +1661,8 @@ static int run_traceback(gx_context* ctx, const std::vector<const FillJob*>& jv,
     auto cleanup = [&]() { pool_put(ctx, tbb); pool_put(ctx, jb); };
     const int SR = strip_rows(job.lay);
     const size_t nc = 4 * P, nsg = 4 * std::max<size_t>(stot, 1), nhr = std::max<size_t>(stot, 1) * SR;
-    if ((rc = pool_get(ctx, (nc + nsg) * sizeof(int) + nhr * sizeof(uint32_t), &tbb)) ||
-        (slot < 0 && (rc = pool_get(ctx, P * sizeof(TbDev), &jb)))) {
+    if ((rc = pool_get(ctx, (nc + nsg) * sizeof(int) + nhr * sizeof(uint32_t), &tbb, ts)) ||
+        (slot < 0 && (rc = pool_get(ctx, P * sizeof(TbDev), &jb, ts)))) {
         cleanup();
         return rc;
     }
@@ -1680,7 +1702,6 @@ static int run_traceback(gx_context* ctx, const std::vector<const FillJob*>& jv,
             sl.tjob_cap = jbytes;
         }
         upload = !(sl.tjob_last.size() == P && !memcmp(sl.tjob_last.data(), jobs.data(), jbytes));
-        if (upload) sl.tjob_last = jobs;
         jdev = sl.tjob;
     }
     hipError_t e = hipSuccess;
@@ -1689,6 +1710,10 @@ static int run_traceback(gx_context* ctx, const std::vector<const FillJob*>& jv,
         if (!pin_jobs) { cleanup(); return fail(GX_ENOMEM, "pinned staging buffer"); }
         memcpy(pin_jobs, jobs.data(), jbytes);
         e = hipMemcpyAsync(jdev, pin_jobs, jbytes, hipMemcpyHostToDevice, ts);
+        if (slot >= 0) {   // (what the slot's table holds: only an upload that was issued counts)
+            if (e == hipSuccess) ctx->slots[slot].tjob_last = jobs;
+            else ctx->slots[slot].tjob_last.clear();
+        }
     }
     if (e == hipSuccess) e = hipMemsetAsync(seg_d, 0, nsg * sizeof(int), ts);
     hipEvent_t evb = slot >= 0 ? ctx->slots[slot].tb : ctx->ev1, eve = slot >= 0 ? ctx->slots[slot].te : ctx->ev2;
@@ -2427,6 +2452,20 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
 }
 
 
+// A staged run over two alternating pair sets (GX_STAGED_ALTERNATE): pass k
+// processes set k % 2.  The sets hold pairs of the same shapes (so every
+// buffer, plan and launch is the same for both); `alt` describes set 1, the
+// regular arguments set 0.  Each set's walks and per-pass results (pass_off
+// into ctx->pass_res) are its own.
+struct PassSet {
+    const std::vector<PairHost>* ph;
+    const std::vector<std::pair<const uint8_t*, const uint8_t*>>* proc;
+    const std::vector<size_t>* off1;
+    const std::vector<size_t>* off2;
+    std::vector<Walk>* walks;
+    size_t pass_off;
+};
+
 // `nsteps` passes over the same batch (the staged benchmark path), pipelined
 // one batch deep: batch k+1's fill is queued behind batch k's traceback, so
 // the host labels batch k while the device fills batch k+1.  Device buffers
@@ -2452,21 +2491,29 @@ static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
                               const Scores32& sc, int is_local, bool planes, int nsteps, std::vector<Walk>& walks, double* fill_ms,
                               const uint8_t* chars_dev, const std::vector<size_t>* off1,
                               const std::vector<size_t>* off2, const SmallAlpha& alpha,
-                              const std::vector<size_t>& idx) {
+                              const std::vector<size_t>& idx, const PassSet* alt) {
     const size_t P = ph.size(), Q = idx.size();
     const size_t G = std::max<size_t>(2, (Q / 5) & ~(size_t)1);   // group A: about a fifth, even (twins)
     std::vector<size_t> gi[2];
     gi[0].assign(idx.begin(), idx.begin() + (long)G);
     gi[1].assign(idx.begin() + (long)G, idx.end());
-    std::vector<PairHost> dph[2];
-    std::vector<std::pair<const uint8_t*, const uint8_t*>> dproc[2];
-    std::vector<size_t> o1[2], o2[2];
-    for (int g = 0; g < 2; ++g)
-        for (size_t p : gi[g]) {
-            dph[g].push_back(ph[p]);
-            dproc[g].push_back(proc[p]);
-            if (chars_dev) { o1[g].push_back((*off1)[p]); o2[g].push_back((*off2)[p]); }
-        }
+    // [pair set][group] (one set unless alt: pass k runs set k & 1)
+    const std::vector<PairHost>* const PH[2] = {&ph, alt ? alt->ph : &ph};
+    const std::vector<std::pair<const uint8_t*, const uint8_t*>>* const PR[2] = {&proc, alt ? alt->proc : &proc};
+    const std::vector<size_t>* const O1[2] = {off1, alt ? alt->off1 : off1};
+    const std::vector<size_t>* const O2[2] = {off2, alt ? alt->off2 : off2};
+    std::vector<Walk>* const WK[2] = {&walks, alt ? alt->walks : &walks};
+    const size_t poff[2] = {ctx->pass_off, alt ? alt->pass_off : ctx->pass_off};
+    std::vector<PairHost> dph[2][2];
+    std::vector<std::pair<const uint8_t*, const uint8_t*>> dproc[2][2];
+    std::vector<size_t> o1[2][2], o2[2][2];
+    for (int v = 0; v < 2; ++v)
+        for (int g = 0; g < 2; ++g)
+            for (size_t p : gi[g]) {
+                dph[v][g].push_back((*PH[v])[p]);
+                dproc[v][g].push_back((*PR[v])[p]);
+                if (chars_dev) { o1[v][g].push_back((*O1[v])[p]); o2[v][g].push_back((*O2[v])[p]); }
+            }
     for (hipStream_t* st : {&ctx->stream2, &ctx->tstream})
         if (!*st) HIPCHK(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
     hipStream_t const sA = ctx->stream, sB = ctx->stream2, sT = ctx->tstream;
@@ -2476,7 +2523,7 @@ static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
     for (size_t q = 0; q < Q; ++q) dev_of[q < G ? gi[0][q] : gi[1][q - G]] = (int)q;
     std::vector<TbStart> starts(Q);
     for (size_t q = 0; q < Q; ++q) {
-        const PairHost& h = q < G ? dph[0][q] : dph[1][q - G];
+        const PairHost& h = q < G ? dph[0][0][q] : dph[0][1][q - G];
         starts[q] = TbStart{(int)h.n, (int)h.m, 0};
     }
     std::vector<PairRes> res(P, PairRes{});
@@ -2486,8 +2533,9 @@ static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
     auto fill = [&](int g, int k) {
         FillJob& j = g == 0 ? jA[k & 1] : jB;
         j.stream = g == 0 ? sA : sB;
-        return run_fill(ctx, dproc[g], dph[g], sc, is_local, planes, false, false, j, chars_dev,
-                        chars_dev ? &o1[g] : nullptr, chars_dev ? &o2[g] : nullptr, &alpha, 2 * g + (k & 1), false);
+        const int v = k & 1;
+        return run_fill(ctx, dproc[v][g], dph[v][g], sc, is_local, planes, false, false, j, chars_dev,
+                        chars_dev ? &o1[v][g] : nullptr, chars_dev ? &o2[v][g] : nullptr, &alpha, 2 * g + (k & 1), false);
     };
     auto trace = [&](int k) {
         HIPCHK(hipStreamWaitEvent(sT, ctx->slots[k & 1].fdone, 0));
@@ -2513,11 +2561,11 @@ static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
     {   // both groups must take the twin fill without landing columns: decided before anything is enqueued
         FillJob pa, pb;
         pa.plan_only = pb.plan_only = true;
-        int prc = run_fill(ctx, dproc[0], dph[0], sc, is_local, planes, false, false, pa, chars_dev, chars_dev ? &o1[0] : nullptr,
-                           chars_dev ? &o2[0] : nullptr, &alpha, 0, false);
+        int prc = run_fill(ctx, dproc[0][0], dph[0][0], sc, is_local, planes, false, false, pa, chars_dev,
+                           chars_dev ? &o1[0][0] : nullptr, chars_dev ? &o2[0][0] : nullptr, &alpha, 0, false);
         if (!prc)
-            prc = run_fill(ctx, dproc[1], dph[1], sc, is_local, planes, false, false, pb, chars_dev,
-                           chars_dev ? &o1[1] : nullptr, chars_dev ? &o2[1] : nullptr, &alpha, 2, false);
+            prc = run_fill(ctx, dproc[0][1], dph[0][1], sc, is_local, planes, false, false, pb, chars_dev,
+                           chars_dev ? &o1[0][1] : nullptr, chars_dev ? &o2[0][1] : nullptr, &alpha, 2, false);
         if (prc || !(pa.noskel && pb.noskel && pa.twin && pb.twin && pa.lay == pb.lay)) return kOverlapNo;
     }
     unsigned long long* const sums0 = ctx->sums_dst;
@@ -2561,12 +2609,14 @@ static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
         job_release(ctx, jA[a]);                              // its walk is done
         for (size_t p = 0; p < P; ++p)
             start_cell_common(hs, is_local, ph[p].n, ph[p].m, start_in(res[p]), &si[p], &sj[p], &score[p]);
-        if ((rc = label_batch(ctx, ph, hs, is_local, false, dev_of, si, sj, score, res, ctx->slots[a].out,
-                              jA[a].fill_ms + jB.fill_ms, walks)))
+        ctx->pass_off = poff[a];
+        if ((rc = label_batch(ctx, *PH[a], hs, is_local, false, dev_of, si, sj, score, res, ctx->slots[a].out,
+                              jA[a].fill_ms + jB.fill_ms, *WK[a])))
             break;
     }
     drain();
     (void)jb_live;
+    ctx->pass_off = poff[0];
     if (rc) return rc;
     ctx->last_groups = 2;
     if (fill_ms) *fill_ms = fsum / nsteps;
@@ -2578,16 +2628,30 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
                             const Scores32& sc, int is_local, bool planes, bool track, int nsteps,
                             std::vector<Walk>& walks, double* fill_ms, const uint8_t* chars_dev,
                             const std::vector<size_t>* off1, const std::vector<size_t>* off2,
-                            const SmallAlpha* staged_alpha) {
+                            const SmallAlpha* staged_alpha, const PassSet* alt = nullptr) {
     const size_t P = ph.size();
     ctx->last_groups = 1;
     std::vector<size_t> idx;
     for (size_t p = 0; p < P; ++p) if (ph[p].n >= 1 && ph[p].m >= 1) idx.push_back(p);
+    // the pair sets by pass parity (one set unless alt)
+    const std::vector<PairHost>* const PH[2] = {&ph, alt ? alt->ph : &ph};
+    const std::vector<std::pair<const uint8_t*, const uint8_t*>>* const PR[2] = {&proc, alt ? alt->proc : &proc};
+    const std::vector<size_t>* const O1[2] = {off1, alt ? alt->off1 : off1};
+    const std::vector<size_t>* const O2[2] = {off2, alt ? alt->off2 : off2};
+    std::vector<Walk>* const WK[2] = {&walks, alt ? alt->walks : &walks};
+    const size_t poff[2] = {ctx->pass_off, alt ? alt->pass_off : ctx->pass_off};
+    struct OffBack {   // (the caller's pass offset back on every return)
+        gx_context* c;
+        size_t v;
+        ~OffBack() { c->pass_off = v; }
+    } off_back{ctx, poff[0]};
     if (nsteps <= 1 || idx.empty() || getenv("GX_TRACE_FILE")) {
         double f = 0, fsum = 0;
         for (int s = 0; s < std::max(nsteps, 1); ++s) {
-            const int rc = batch_core(ctx, ph, proc, hs, sc, is_local, planes, track, walks, &f, chars_dev, off1, off2,
-                                      staged_alpha);
+            const int v = s & 1;
+            ctx->pass_off = poff[v];
+            const int rc = batch_core(ctx, *PH[v], *PR[v], hs, sc, is_local, planes, track, *WK[v], &f, chars_dev,
+                                      O1[v], O2[v], staged_alpha);
             if (rc) return rc;
             fsum += f;
         }
@@ -2596,14 +2660,17 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
     }
     int rc = slots_ready(ctx);
     if (rc) return fail(rc, "pipeline events");
-    std::vector<PairHost> dph;
-    std::vector<std::pair<const uint8_t*, const uint8_t*>> dproc;
-    std::vector<size_t> o1, o2;
-    for (size_t p : idx) {
-        dph.push_back(ph[p]);
-        dproc.push_back(proc[p]);
-        if (chars_dev) { o1.push_back((*off1)[p]); o2.push_back((*off2)[p]); }
-    }
+    std::vector<PairHost> dph_s[2];
+    std::vector<std::pair<const uint8_t*, const uint8_t*>> dproc_s[2];
+    std::vector<size_t> o1_s[2], o2_s[2];
+    for (int v = 0; v < 2; ++v)
+        for (size_t p : idx) {
+            dph_s[v].push_back((*PH[v])[p]);
+            dproc_s[v].push_back((*PR[v])[p]);
+            if (chars_dev) { o1_s[v].push_back((*O1[v])[p]); o2_s[v].push_back((*O2[v])[p]); }
+        }
+    const std::vector<PairHost>& dph = dph_s[0];
+    const std::vector<std::pair<const uint8_t*, const uint8_t*>>& dproc = dproc_s[0];
     SmallAlpha alpha;
     if (staged_alpha) alpha = *staged_alpha;
     else
@@ -2619,9 +2686,9 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
     std::vector<int> dev_of(P, -1);
     for (size_t q = 0; q < idx.size(); ++q) dev_of[idx[q]] = (int)q;
     double fsum = 0;
-    auto fill = [&](int s) {
-        return run_fill(ctx, dproc, dph, sc, is_local, planes, track, false, jobs[s], chars_dev,
-                        chars_dev ? &o1 : nullptr, chars_dev ? &o2 : nullptr, &alpha, s, false);
+    auto fill = [&](int s) {   // slot s = the pass's parity = its pair set
+        return run_fill(ctx, dproc_s[s], dph_s[s], sc, is_local, planes, track, false, jobs[s], chars_dev,
+                        chars_dev ? &o1_s[s] : nullptr, chars_dev ? &o2_s[s] : nullptr, &alpha, s, false);
     };
     // results of slot s's fill -> start cells -> its traceback queued; the fill
     // buffers return to the pool (their last user, the traceback, is queued)
@@ -2657,10 +2724,10 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
     // forces it from 16 pairs, GX_OVERLAP=0 turns it off)
     const char* ov = getenv("GX_OVERLAP");
     const bool ov_force = ov && !strcmp(ov, "1");
-    if (!track && planes && idx.size() >= 16 && (nmax_b >= 16384 || ov_force) && !pool_poison() &&
+    if (!track && planes && idx.size() >= 16 && (nmax_b >= 16384 || ov_force) &&
         !(ov && !strcmp(ov, "0")) && (!is_local || idx.size() >= 64 || ov_force)) {
         const int orc = batch_core_overlap(ctx, ph, proc, hs, sc, is_local, planes, nsteps, walks, fill_ms, chars_dev, off1, off2,
-                                           alpha, idx);
+                                           alpha, idx, alt);
         if (orc != kOverlapNo) return orc;
     }
     if (!is_local && !track) {
@@ -2702,8 +2769,9 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
             h_tbw += since(t); t = clk::now();
             if ((rc = results(s))) break;
             h_res += since(t); t = clk::now();
-            if ((rc = label_batch(ctx, ph, hs, is_local, track, dev_of, si, sj, score, res, ctx->slots[s].out,
-                                  jobs[s].fill_ms, walks)))
+            ctx->pass_off = poff[s];
+            if ((rc = label_batch(ctx, *PH[s], hs, is_local, track, dev_of, si, sj, score, res, ctx->slots[s].out,
+                                  jobs[s].fill_ms, *WK[s])))
                 break;
             h_lab += since(t);
         }
@@ -2731,8 +2799,9 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
         t_fill += since(t); t = clk::now();
         if ((rc = tb_collect(ctx, s, idx.size(), ctx->slots[s].out))) break;
         t_tbwait += since(t); t = clk::now();
-        if ((rc = label_batch(ctx, ph, hs, is_local, track, dev_of, si, sj, score, res, ctx->slots[s].out,
-                              jobs[s].fill_ms, walks)))
+        ctx->pass_off = poff[s];
+        if ((rc = label_batch(ctx, *PH[s], hs, is_local, track, dev_of, si, sj, score, res, ctx->slots[s].out,
+                              jobs[s].fill_ms, *WK[s])))
             break;
         t_label += since(t); t = clk::now();
         if (k + 1 < nsteps && (rc = trace(s ^ 1))) break;
@@ -2913,6 +2982,77 @@ extern "C" int gx_stage_pairs(gx_context* ctx, const uint8_t* const* s1, const s
     return GX_OK;
 }
 
+// GX_STAGED_ALTERNATE (gx.h): pass k over staged pairs k % 2 * H .. + H - 1.
+static int run_staged_alternate(gx_context* ctx, const std::vector<PairHost>& ph,
+                                const std::vector<std::pair<const uint8_t*, const uint8_t*>>& proc,
+                                const HostScores& hs, const Scores32& sc, int is_local, bool planes, bool track,
+                                bool want_sums, int passes, gx_result* out, double* fill_ms_out) {
+    const size_t P = ph.size(), H = P / 2;
+    if (P == 0 || P % 2) return fail(GX_EINVAL, "alternating sets: an even, non-zero number of staged pairs");
+    for (size_t p = 0; p < H; ++p)
+        if (ph[p].n != ph[p + H].n || ph[p].m != ph[p + H].m)
+            return fail(GX_EINVAL, "alternating sets: pair " + std::to_string(p) + " and " + std::to_string(p + H) +
+                                       " differ in shape");
+    const double bpc = planes ? ((!track && !getenv("GX_PLANES32") && d8_planes_ok(sc, is_local)) ? 3.0 : 12.0) : 0.0;
+    std::vector<PairHost> ph0(ph.begin(), ph.begin() + (long)H), ph1(ph.begin() + (long)H, ph.end());
+    if (plan_chunks(ctx, ph0, bpc).size() != 1) return fail(GX_EINVAL, "alternating sets must fit one chunk");
+    std::vector<std::pair<const uint8_t*, const uint8_t*>> pr0(proc.begin(), proc.begin() + (long)H),
+        pr1(proc.begin() + (long)H, proc.end());
+    std::vector<size_t> a1(ctx->st_off1.begin(), ctx->st_off1.begin() + (long)H),
+        a2(ctx->st_off2.begin(), ctx->st_off2.begin() + (long)H), b1(ctx->st_off1.begin() + (long)H, ctx->st_off1.end()),
+        b2(ctx->st_off2.begin() + (long)H, ctx->st_off2.end());
+    // checksum records in the order the fills write them: pass, then its set's pairs with an interior
+    std::vector<std::pair<int, size_t>> sum_order;
+    for (int k = 0; k < passes; ++k)
+        for (size_t p = 0; p < H; ++p)
+            if (ph[p].n >= 1 && ph[p].m >= 1) sum_order.emplace_back(k, (size_t)(k & 1) * H + p);
+    ctx->sums_host.clear();
+    if (want_sums && !sum_order.empty()) {
+        const size_t bytes = sum_order.size() * 3 * sizeof(unsigned long long);
+        if (ctx->sums_dev.cap < bytes) {
+            if (ctx->sums_dev.p) (void)hipFree(ctx->sums_dev.p);
+            ctx->sums_dev = DevBuf{};
+            HIPCHK(hipMalloc(&ctx->sums_dev.p, bytes));
+            ctx->sums_dev.cap = bytes;
+        }
+        HIPCHK(hipMemsetAsync(ctx->sums_dev.p, 0, bytes, ctx->stream));
+        ctx->sums_dst = (unsigned long long*)ctx->sums_dev.p;
+    }
+    std::vector<Walk> w0, w1;
+    PassSet alt{&ph1, &pr1, &b1, &b2, &w1, H};
+    ctx->pass_off = 0;
+    double fms = 0;
+    int rc = batch_core_steps(ctx, ph0, pr0, hs, sc, is_local, planes, track, passes, w0, &fms,
+                              (const uint8_t*)ctx->st_chars.p, &a1, &a2, &ctx->st_alpha, &alt);
+    ctx->last_chunks = 1;
+    const size_t filled = ctx->sums_dst ? (size_t)(ctx->sums_dst - (unsigned long long*)ctx->sums_dev.p) : 0;
+    ctx->sums_dst = nullptr;
+    if (rc) return rc;
+    if (want_sums) {
+        ctx->sums_host.assign((size_t)passes * P * 3, 0);
+        if (!sum_order.empty()) {
+            if (filled != sum_order.size() * 3)
+                return fail(GX_EHIP, "plane sums: " + std::to_string(filled / 3) + " pair records, expected " +
+                                         std::to_string(sum_order.size()));
+            std::vector<uint64_t> dev(filled);
+            HIPCHK(hipStreamSynchronize(ctx->stream));
+            HIPCHK(hipMemcpy(dev.data(), ctx->sums_dev.p, filled * sizeof(uint64_t), hipMemcpyDeviceToHost));
+            for (size_t r = 0; r < sum_order.size(); ++r)
+                for (int c = 0; c < 3; ++c)
+                    ctx->sums_host[((size_t)sum_order[r].first * P + sum_order[r].second) * 3 + c] = dev[r * 3 + c];
+        }
+    }
+    std::vector<Walk>& walks = ctx->walk_cache;
+    walks.resize(P);
+    for (size_t p = 0; p < H; ++p) {
+        if (p < w0.size()) std::swap(walks[p], w0[p]);
+        if (p < w1.size()) std::swap(walks[H + p], w1[p]);
+    }
+    for (size_t p = 0; p < P; ++p) out[p] = walks[p].res;
+    if (fill_ms_out) *fill_ms_out = fms;
+    return GX_OK;
+}
+
 extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int is_local, int keep_planes,
                                    uint32_t flags, int nsteps, gx_result* out, double* fill_ms_out) {
     if (!ctx || !out) return fail(GX_EINVAL, "NULL argument");
@@ -2943,6 +3083,7 @@ extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int
     ctx->pass_P = P;
     ctx->pass_off = 0;
     ctx->pass_k = 0;
+    if (wide && (flags & GX_STAGED_ALTERNATE)) return fail(GX_EINVAL, "alternating sets: not on the int64 fill");
     if (wide) {   // int64 fill: one synchronous pass at a time (a rare path, no pipelining or chunking)
         std::vector<Walk>& walks = ctx->walk_cache;
         const int passes = std::max(nsteps, 1);
@@ -2992,6 +3133,9 @@ extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int
     // checksum kernel (stream order, before the planes return to the pool)
     const bool want_sums = (flags & GX_STAGED_PLANE_SUMS) && keep_planes;
     const int passes = std::max(nsteps, 1);
+    if (flags & GX_STAGED_ALTERNATE)
+        return run_staged_alternate(ctx, ph, proc, hs, sc, is_local, keep_planes != 0, track, want_sums, passes, out,
+                                    fill_ms_out);
     // chunks: each runs its `passes` passes pipelined (pass k's labelling
     // beside pass k+1's fill); a step is still one pass over every pair
     const double bpc = keep_planes ? ((!track && !getenv("GX_PLANES32") && d8_planes_ok(sc, is_local)) ? 3.0 : 12.0)
@@ -3120,6 +3264,22 @@ extern "C" int gx_twin_admission_mode(const gx_scores* scores, int is_local, int
     const long long b = twin_bound(sc, band_waves, col_gap, is_local != 0);
     if (bound) *bound = b;
     return (sc.g <= 0 && sc.h <= 0 && b < kTwinBoundLimit) ? 1 : 0;
+}
+
+extern "C" int gx_plan_layout(const gx_scores* scores, int is_local, const int64_t* n, const int64_t* m,
+                              size_t npairs, int track, int grid_cap) {
+    if (!scores || !n || !m || npairs == 0) return -1;
+    int64_t nmax = 0, mmax = 0;
+    for (size_t p = 0; p < npairs; ++p) {
+        if (n[p] < 0 || m[p] < 0) return -1;
+        nmax = std::max(nmax, n[p]); mmax = std::max(mmax, m[p]);
+    }
+    HostScores hs;
+    Scores32 sc;
+    if (check_scores(scores, (size_t)nmax, (size_t)mmax, &hs, &sc, is_local, nullptr) != GX_OK) return -1;
+    std::vector<PairHost> ph(npairs);
+    for (size_t p = 0; p < npairs; ++p) ph[p] = PairHost{nullptr, nullptr, (size_t)n[p], (size_t)m[p]};
+    return fill_layout(ph, sc, grid_cap > 0 ? grid_cap : 256, track != 0);
 }
 
 extern "C" int gx_plane_bytes_per_cell(const gx_scores* scores, int is_local) {

@@ -29,6 +29,21 @@ __device__ __forceinline__ int shz(int src) {
 }
 __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
 
+// Counter reads and writes on a wave's hot path: relaxed workgroup-scope
+// atomics rather than volatile accesses, for which the compiler's memory
+// legalizer waits (s_waitcnt lgkmcnt(0)) right behind the access -- a
+// counter read at a group's start then exposed a full LDS round trip each
+// group (layout 3's core wave, ~10 % of a step).  Ordering against the data
+// is the writer's: an asm memory barrier between data and counter stores
+// (LDS executes one wave's operations in order).
+typedef __attribute__((address_space(3))) int lds_plain;
+__device__ __forceinline__ int lds_peek(lds_int* p) {
+    return __hip_atomic_load((lds_plain*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_post(lds_int* p, int v) {
+    __hip_atomic_store((lds_plain*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 __device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 

@@ -101,6 +101,7 @@ struct __attribute__((aligned(16))) PairRes {
 // Optional per-strip timeline (GX_TRACE_FILE): s_memrealtime ticks (100 MHz)
 // and spin iterations, for the diagnostic runs behind DESIGN.md's numbers.
 constexpr int kTraceQ = 7;   // progress stamps per strip (at k/8 of the sweep)
+constexpr int kTraceTL = 64; // layout 3: dense timeline stamps per strip (every 1,024 steps)
 struct __attribute__((aligned(16))) StripTrace {
     long long t_start;   // wave starts the strip
     long long t_first;   // first input sub-block available
@@ -109,6 +110,9 @@ struct __attribute__((aligned(16))) StripTrace {
     int wait_out;        // spin iterations waiting for ring space below
     long long clk;       // shader-clock ticks (s_memtime) from t_first to t_end
     long long t_q[kTraceQ];   // when the sweep passed k/8 of its steps (k = 1..7)
+    long long tl[kTraceTL];   // layout 3: when the core wave reached step 1024 k (a dense timeline)
+    long long tc[kTraceTL];   // ... and the shader clock (s_memtime) then
+    long long ts[kTraceTL];   // layout 3: when the side wave reached step 1024 k
 };
 
 struct __attribute__((aligned(16))) PairDev {   // 16-B multiple: the pinned staging puts PairRes (aligned 16) after P of these

@@ -29,6 +29,7 @@ GX_TABLE_PLANES = 1
 GX_TABLE_MATCHES = 2
 GX_ALIGN_MAX_CELL = 4
 GX_STAGED_PLANE_SUMS = 8
+GX_STAGED_ALTERNATE = 16   # gx.h: pass k runs the k % 2 half of the staged pairs
 
 # status codes (include/gx.h)
 _CODES = {0: "GX_OK", 1: "GX_EINVAL", 2: "GX_ESEQ", 3: "GX_ERANGE", 4: "GX_ENOMEM", 5: "GX_EHIP",
@@ -76,7 +77,7 @@ EXPORTED = ["gx_last_error", "gx_version", "gx_context_create", "gx_context_dest
             "gx_stage_pairs",
             "gx_run_staged", "gx_run_staged_steps", "gx_staged_plane_sums", "gx_staged_steps",
             "gx_staged_pass_results", "gx_fill_info", "gx_batch_chunks", "gx_fill_twin", "gx_fill_groups", "gx_plane_bytes_per_cell", "gx_twin_admission",
-            "gx_twin_admission_mode",
+            "gx_twin_admission_mode", "gx_plan_layout",
             "gx_fasta_load",
             "gx_config_load", "gx_format_alignment", "gx_format_table"]
 
@@ -131,6 +132,8 @@ def lib():
                                     ctypes.POINTER(ctypes.c_int64)]
     L.gx_twin_admission_mode.argtypes = [ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                          ctypes.POINTER(ctypes.c_int64)]
+    L.gx_plan_layout.argtypes = [ctypes.POINTER(CScores), ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
+                                 ctypes.POINTER(ctypes.c_int64), sz, ctypes.c_int, ctypes.c_int]
     L.gx_fasta_load.argtypes = [ctypes.c_char_p, vp, sz, vp, vp, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.gx_config_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(CScores)]
     L.gx_format_alignment.argtypes = [vp, sz, vp, sz, vp, sz, ctypes.POINTER(CResult), vp, sz, ctypes.POINTER(sz)]
@@ -295,6 +298,18 @@ def plane_bytes_per_cell(scores: "Scores", is_local: bool) -> int:
     if r < 0:
         raise GxError(3, "invalid scores")
     return r
+
+
+def plan_layout(scores: "Scores", is_local: bool, shapes: Seq[Tuple[int, int]], track: bool = False,
+                grid_cap: int = 0) -> int:
+    """The fill layout a launch of these (n, m) pair shapes would take
+    (gx_plan_layout; host rule only, no device): 0 anti-diagonal 128-row
+    strips, 1 the column step, 3 the skewed 64-row strips; -1 invalid."""
+    k = len(shapes)
+    n = (ctypes.c_int64 * max(k, 1))(*[a for a, _ in shapes])
+    m = (ctypes.c_int64 * max(k, 1))(*[b for _, b in shapes])
+    return lib().gx_plan_layout(ctypes.byref(scores.c()), int(bool(is_local)), n, m, k, int(bool(track)),
+                                int(grid_cap))
 
 
 def twin_admission(scores: "Scores", band_waves: int, col_gap: int = 0, is_local: bool = False) -> Tuple[bool, int]:
@@ -598,13 +613,16 @@ class StagedPairs:
         _check(lib().gx_stage_pairs(self.ctx.ptr, s1p, n, s2p, m, self.P))
 
     def run(self, scores: Scores, is_local: bool, keep_planes: bool = True, max_cell: bool = False,
-            steps: int = 1, plane_sums: bool = False):
+            steps: int = 1, plane_sums: bool = False, alternate: bool = False):
         """`steps` back-to-back passes (pipelined one pass deep when > 1) ->
         (the last pass's results, mean fill ms).  plane_sums: also checksum
-        every pass's score planes on the device (self.plane_sums())."""
+        every pass's score planes on the device (self.plane_sums()).
+        alternate: pass k runs the k % 2 half of the staged pairs
+        (GX_STAGED_ALTERNATE; the halves hold pairs of equal shapes)."""
         res = (CResult * self.P)()
         fms = ctypes.c_double(0)
-        flags = (GX_ALIGN_MAX_CELL if max_cell else 0) | (GX_STAGED_PLANE_SUMS if plane_sums else 0)
+        flags = ((GX_ALIGN_MAX_CELL if max_cell else 0) | (GX_STAGED_PLANE_SUMS if plane_sums else 0)
+                 | (GX_STAGED_ALTERNATE if alternate else 0))
         _check(lib().gx_run_staged_steps(self.ctx.ptr, ctypes.byref(scores.c()), int(is_local), int(keep_planes),
                                          flags, int(steps), res, ctypes.byref(fms)))
         return list(res), fms.value

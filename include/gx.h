@@ -202,6 +202,15 @@ int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int is_local, 
  * them as [pass][pair][3] (nsteps * npairs * 3 values).  Verification only. */
 #define GX_STAGED_PLANE_SUMS 8u
 int gx_staged_plane_sums(const gx_context* ctx, uint64_t* out, size_t cap, size_t* n_values);
+/* flags bit for gx_run_staged_steps: the staged pairs are two sets of equal
+ * size -- pairs 0 .. P/2-1 and P/2 .. P-1, pair p and p + P/2 of the same
+ * shape -- and pass k runs set k % 2 through the same pipeline, so that every
+ * pass's device buffers once held the other set's data (a pass that read a
+ * previous pass's planes or records would see different values).  Pass k's
+ * results, plane sums and (for the last pass of each set) walks land at its
+ * set's pair indices; the other set's row of pass k is zero.  The sets must
+ * fit one chunk (else GX_EINVAL).  Verification only. */
+#define GX_STAGED_ALTERNATE 16u
 /* The alignment (AlignedSequences.alignment) of staged pair `pair` from the
  * last pass of the last gx_run_staged(_steps) call; *n_steps = its length
  * (steps may be NULL to query it). */
@@ -255,6 +264,14 @@ int gx_twin_admission(const gx_scores* scores, int band_waves, int64_t col_gap, 
  * max(|h + g|, U) of the unshifted values and the floor's constants
  * (DESIGN.md 6.7).  Same returns as gx_twin_admission. */
 int gx_twin_admission_mode(const gx_scores* scores, int is_local, int band_waves, int64_t col_gap, int64_t* bound);
+/* The fill layout a launch of these pair shapes would take (host rule only,
+ * no device): 0 = anti-diagonal 128-row strips (batches), 1 = the column
+ * step, 3 = skewed 64-row strips (the latency layouts);
+ * `track` = an alignment_table call that keeps max_cell / matches_at_max
+ * (algo.rs:258-262, 279).  grid_cap = the device's CU count (0: 256).  -1 on
+ * invalid arguments.  Diagnostic; no reference counterpart. */
+int gx_plan_layout(const gx_scores* scores, int is_local, const int64_t* n, const int64_t* m, size_t npairs,
+                   int track, int grid_cap);
 
 /* ---- sequence.rs / config.rs mirrors ----------------------------------- */
 /* from_fasta (sequence.rs:45-95) on a file: records are appended to the

@@ -220,6 +220,37 @@ def test_plane_bytes_per_cell(gx, scores, local, monkeypatch):
     assert gx.plane_bytes_per_cell(gx.Scores(*scores), local) == 12
 
 
+@pytest.mark.parametrize("local", [False, True], ids=["global", "local"])
+def test_plan_layout(gx, local, monkeypatch):
+    """Host-only: the layout rule (gx_api.cpp fill_layout).  BASELINE configs
+    2 and 3 take the latency layouts; a wide batch takes layout 0; columns
+    past the 24-bit landing-column range of the 64-row strip layouts (the
+    skeleton holds E + 64 in 24 bits, gx_kernels.hip tb_chase_kernel; a
+    strip's int32 plane must stay inside one buffer descriptor) never take
+    layout 3 or the column step, forced or not."""
+    for k in ("GX_LAYOUT", "GX_CS2", "GX_BAND_WAVES"):
+        monkeypatch.delenv(k, raising=False)
+    sc = gx.Scores(1, -2, -1, -5)
+    covid, brca2 = (29903, 29882), (11382, 10346)
+    assert gx.plan_layout(sc, False, [covid]) == 3
+    assert gx.plan_layout(sc, True, [brca2]) == 1
+    assert gx.plan_layout(sc, local, [(64, 30000)]) == 3
+    assert gx.plan_layout(sc, local, [(30000, 30000)] * 80) == 0
+    big = (64, (1 << 24) - 100)
+    assert gx.plan_layout(sc, local, [big]) == 0
+    monkeypatch.setenv("GX_LAYOUT", "3")
+    assert gx.plan_layout(sc, local, [big]) == 0
+    assert gx.plan_layout(sc, local, [(64, (1 << 24) - 129)]) == 3
+    monkeypatch.setenv("GX_LAYOUT", "1")
+    assert gx.plan_layout(sc, local, [big]) == 0
+    # h > 0 (the folded gap opening needs h <= 0) and wide substitution scores
+    # (the ramp-up's virtual-column drift) keep layout 3 off
+    monkeypatch.setenv("GX_LAYOUT", "3")
+    assert gx.plan_layout(gx.Scores(1, -2, -1, 2), local, [covid]) != 3
+    assert gx.plan_layout(gx.Scores(1 << 23, -(1 << 23), -1, -5), local, [(4, 4)]) != 3
+    assert gx.plan_layout(gx.Scores(1 << 20, -(1 << 20), -1, -5), local, [(4, 4)]) == 3
+
+
 def test_display_log_lines():
     """display.rs:12-18 and 139-144: the Display and table renderings log the
     reference's info / warn lines on stderr under GX_LOG (CPU only: the

@@ -171,7 +171,7 @@ LAUNCHES = {
     "twin_w8_bytes": ({"GX_TWIN": "1", "GX_BAND_WAVES": "8", "GX_PLANES_W16": "0"}, (0, 8, 3)),
     "auto": ({}, None),
     "int32_planes": ({"GX_PLANES32": "1"}, (0, None, 12)),
-    # every buffer returned to the pool is poisoned: a pass that read the previous pass's data would fail
+    # every buffer the pool hands out is poisoned on its new user's stream: a pass that read the previous pass's data would fail
     "w15_poison": ({"GX_BAND_WAVES": "15", "GX_FILL_GRID": "16", "GX_POOL_POISON": "1"}, (0, 15, None)),
     "twin_poison": ({"GX_TWIN": "1", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "16", "GX_POOL_POISON": "1"}, (0, 15, 2)),
 }
@@ -211,6 +211,54 @@ def test_overlapped_bench_launch_30k(gx, ctx, monkeypatch, npairs, env):
     pairs = [_synth_pair(c["k"], 30000) for c in cases]
     info = _staged_check(gx, ctx, pairs, cases, steps=3)
     assert info["groups"] == 2 and info["twin"] == 1 and info["plane_bytes_per_cell"] == 2, info
+
+
+@pytest.mark.parametrize("poison", [True, False], ids=["poison", "plain"])
+def test_overlapped_alternating_sets(gx, ctx, monkeypatch, poison):
+    """The headline's overlapped two-group pipeline (groups == 2, twin plane
+    codes) over two different sets of 20 synthetic 30k pairs that alternate
+    pass by pass (GX_STAGED_ALTERNATE: pass k runs set k % 2), so that every
+    device buffer a pass takes from the pool last held the other set's planes
+    and records: a walk that read a later pass's planes, or a fill that
+    overwrote planes a walk still reads (the wait of group B's next fill on
+    the previous walk, gx_api.cpp batch_core_overlap), gives wrong results
+    here, where repeating one set would hide it.  With GX_POOL_POISON every
+    buffer is also filled with garbage on its new user's stream before use.
+    Every pass's plane checksums and results, and each set's last
+    alignments, against the oracle digests."""
+    monkeypatch.setenv("GX_TWIN", "1")
+    if poison:
+        monkeypatch.setenv("GX_POOL_POISON", "1")
+    cases = _synth(30000)[:40]
+    pairs = [_synth_pair(c["k"], 30000) for c in cases]
+    H = len(pairs) // 2
+    steps = 4
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, fill_ms = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=steps, plane_sums=True,
+                          alternate=True)
+    info = ctx.fill_info()
+    assert info["groups"] == 2 and info["twin"] == 1 and info["plane_bytes_per_cell"] == 2, info
+    assert fill_ms > 0
+    sums = st.plane_sums()
+    passes = st.pass_results()
+    assert sums.shape == (steps, len(pairs), 3) and len(passes) == steps
+    for k in range(steps):
+        for q in range(H):
+            p = (k % 2) * H + q
+            c = cases[p]
+            assert [int(x) for x in sums[k, p]] == [int(x) for x in c["plane_sums"]], (p, "pass", k)
+            _check_result(passes[k][p], None, c, (p, "pass", k))
+            other = passes[k][(1 - k % 2) * H + q]
+            assert other.score == 0 and other.n_steps == 0, (p, "pass", k, "the other set's row is empty")
+    for p, c in enumerate(cases):   # each set's last pass
+        _check_result(res[p], st.steps(p), c, (p, "last"))
+
+
+def test_alternating_sets_rejects_shapes(gx, ctx):
+    """GX_STAGED_ALTERNATE needs pair p and p + P/2 of one shape."""
+    st = gx.StagedPairs([(b"ACGT" * 10, b"ACGA" * 10), (b"ACGT" * 11, b"ACGA" * 10)], ctx=ctx)
+    with pytest.raises(gx.GxError):
+        st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=2, alternate=True)
 
 
 @pytest.mark.parametrize("L", [1024, 4096, 16384])

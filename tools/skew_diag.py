@@ -53,11 +53,15 @@ def main():
         cases = cases[:2]
     if os.environ.get("SKEW_DIAG_LONE"):   # (a lone strip: for experiment builds without pushes)
         cases = cases[:1]
+    if os.environ.get("SKEW_DIAG_FULL"):   # (the full 30k pair only)
+        cases = cases[-1:]
+    modes = (False,) if os.environ.get("SKEW_DIAG_GLOBAL") else (False, True)
+    keep = os.environ.get("SKEW_DIAG_OUT")  # (a directory: keep the trace CSVs)
     os.environ["GX_LAYOUT"] = "3"
     for W in widths:
         os.environ["GX_BAND_WAVES"] = str(W)
         for name, a, b in cases:
-            for local in (False, True):
+            for local in modes:
                 for _ in range(2):
                     _, r = gx.align_raw(a, b, sc, local, ctx=ctx, max_cell=False)
                 tr = os.path.join(tempfile.gettempdir(), f"skew_{W}_{name}_{int(local)}.csv")
@@ -69,6 +73,10 @@ def main():
                       f"({cells / max(r.fill_us, 1) / 1e3:.1f} GCUPS), traced fill {r2.fill_us} us, "
                       f"retrace {r.retrace_us} us", flush=True)
                 summarize(tr, len(b), W)
+                if keep:
+                    os.makedirs(keep, exist_ok=True)
+                    import shutil
+                    shutil.copy(tr, keep)
     ctx.close()
 
 
