@@ -19,7 +19,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
@@ -36,6 +38,8 @@ hipError_t launch_finalize(const PairDev* d_pairs, int npairs, const StripRes* d
 hipError_t launch_traceback(const TbDev* d_jobs, int njobs, int max_strips, bool w16, bool seq, hipStream_t st);
 hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t4, int lay, int gshift, int row0,
                          int rows, hipStream_t st);
+hipError_t launch_export_w16(const uint8_t* codes, int half, int which, int32_t* out, int n, int m, int t4, int h,
+                             int g, int floor_, int gshift, int row0, int rows, hipStream_t st);
 hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, int n, int m, int t4, int h, int g,
                             int floor_, int gshift, int row0, int rows, hipStream_t st);
 hipError_t launch_plane_sums(const PairDev* d_pairs, int npairs, int max_strips, int lay, int mode, int h, int g,
@@ -44,7 +48,7 @@ hipError_t launch_local_col(const PairDev* d_pairs, int npairs, PairRes* d_pres,
 hipError_t launch_fill_cs2(int W, bool local, bool planes, bool tbl, const PairDev* d_pairs, int npairs,
                            int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                            hipStream_t st);
-hipError_t launch_fill_skew(int W, bool local, bool planes, bool tbl, bool trace, const PairDev* d_pairs, int npairs,
+hipError_t launch_fill_skew(int W, bool local, bool planes, bool tbl, bool trace, bool track, const PairDev* d_pairs, int npairs,
                             int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                             hipStream_t st);
 hipError_t launch_skew_codes(const PairDev* d_pairs, int npairs, int mmax, Scores32 sc, bool tbl, hipStream_t st);
@@ -122,8 +126,13 @@ public:
     StepBuf() = default;
     StepBuf(const StepBuf& o) { *this = o; }
     StepBuf(StepBuf&& o) noexcept : p_(o.p_), n_(o.n_), cap_(o.cap_) { o.p_ = nullptr; o.n_ = o.cap_ = 0; }
-    StepBuf& operator=(const StepBuf& o) {
-        if (this != &o) { clear(); reserve(o.n_); if (o.n_) memcpy(p_, o.p_, o.n_ * sizeof(gx_step)); n_ = o.n_; }
+    StepBuf& operator=(const StepBuf& o) {   // (as std::vector: bad_alloc when the copy cannot be held)
+        if (this != &o) {
+            clear();
+            if (!reserve(o.n_)) throw std::bad_alloc();
+            if (o.n_) memcpy(p_, o.p_, o.n_ * sizeof(gx_step));
+            n_ = o.n_;
+        }
         return *this;
     }
     StepBuf& operator=(StepBuf&& o) noexcept {
@@ -141,9 +150,10 @@ public:
         p_ = q; cap_ = c;
         return true;
     }
-    void push_back(const gx_step& st) {
-        if (n_ == cap_) reserve(std::max<size_t>(16, 2 * cap_));
+    [[nodiscard]] bool push_back(const gx_step& st) {   // false: out of host memory (nothing appended)
+        if (n_ == cap_ && !reserve(std::max<size_t>(16, 2 * cap_))) return false;
         p_[n_++] = st;
+        return true;
     }
     size_t size() const { return n_; }
     size_t capacity() const { return cap_; }
@@ -244,6 +254,11 @@ struct WorkPool {
     }
 };
 
+struct HostScores {
+    int64_t sm, smm, g, h;
+    int64_t neg_inf;  // i64::MIN + |g + h|   (algo.rs:166)
+};
+
 struct gx_context {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -298,6 +313,14 @@ struct gx_context {
     size_t pass_off = 0, pass_P = 0;
     int pass_k = 0;
     std::vector<gx_result> pass_res;                 // [passes][staged pairs]
+    // GX_STAGED_KEEP_PLANES: the last pass's fill of a staged run, kept
+    // (device buffers included) for the tables gx_staged_table hands out.
+    // keep_capture: set while that pass runs; the pipelines then hold its
+    // job back from the pool and keep_job() takes it.
+    std::shared_ptr<struct KeptFill> kept;
+    bool keep_capture = false;
+    HostScores kept_hs{};
+    Scores32 kept_sc{};
 };
 
 static void* pinned_grow(PinnedBuf& b, size_t bytes) {
@@ -443,8 +466,13 @@ extern "C" int gx_context_trim(gx_context* ctx) {
     return GX_OK;
 }
 
+static void release_slots(gx_context* ctx);
 extern "C" void gx_context_destroy(gx_context* ctx) {
     if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipDeviceSynchronize();
+    release_slots(ctx);   // (into the pool, which the trim frees)
+    ctx->kept.reset();
     gx_context_trim(ctx);
     (void)hipSetDevice(ctx->device);
     if (ctx->st_chars.p) (void)hipFree(ctx->st_chars.p);
@@ -472,10 +500,6 @@ extern "C" void gx_context_destroy(gx_context* ctx) {
 // ---------------------------------------------------------------------------
 // scoring: exact-int32 guard (DESIGN.md "Integer range")
 
-struct HostScores {
-    int64_t sm, smm, g, h;
-    int64_t neg_inf;  // i64::MIN + |g + h|   (algo.rs:166)
-};
 
 static int64_t wadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
 static int64_t wmul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
@@ -728,13 +752,15 @@ struct PairHost {
 // and fewer than 2^24 - 128 columns: its skeleton holds E + 64 in the 24 bits
 // tb_chase_kernel decodes, and a strip's int32 plane (256 (m + 64) bytes)
 // must stay inside one buffer descriptor's 32-bit range.
-static bool skew_ok(const Scores32& sc, bool track, size_t mmax) {
+// Tracked fills (max_cell, matches_at_max) run on it too (round 5: the side
+// wave carries the first maximum and the LCS values); an LCS plane does not.
+static bool skew_ok(const Scores32& sc, bool lcs_plane, size_t mmax) {
     const long long g = sc.g;
     const long long s2 = std::max(std::llabs((long long)sc.sm - 2 * g), std::llabs((long long)sc.smm - 2 * g));
     const long long drift = 64LL * (std::llabs(g) + std::llabs((long long)sc.h) + s2);
-    return !track && sc.h <= 0 && drift < (1LL << 28) && mmax + 128 < (1u << 24);
+    return !lcs_plane && sc.h <= 0 && drift < (1LL << 28) && mmax + 128 < (1u << 24);
 }
-static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int grid_cap, bool track) {
+static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int grid_cap, bool track, bool lcs_plane) {
     const long long span = 65LL * (std::llabs((long long)sc.g) + std::llabs((long long)sc.h));
     size_t mmax = 0;
     long long strips64 = 0;
@@ -749,13 +775,14 @@ static int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int 
     // + 6.46 us global, 57.5 ns + 6.66 us local; the column step 113 ns +
     // 2.66 us (global), split for local fills 110 ns + 3.37 us
     const bool local = sc.floor_ == 0;
+    (void)track;
     double est1 = 0, est3 = 0;   // the launch's slowest pair on each layout (ns)
     for (const PairHost& h : ph) {
         const double S = (double)ceil_div((int)h.n, kStripRows1), m = (double)h.m;
         est1 = std::max(est1, local ? m * 110.0 + S * 3370.0 : m * 113.0 + S * 2660.0);
         est3 = std::max(est3, local ? m * 57.5 + S * 6660.0 : m * 50.0 + S * 6460.0);
     }
-    const bool sk_ok = skew_ok(sc, track, mmax);
+    const bool sk_ok = skew_ok(sc, lcs_plane, mmax);
     const int lat = sk_ok && (!cs_ok || est3 < est1) ? 3 : cs_ok ? 1 : 0;
     if (const char* e = getenv("GX_LAYOUT"); e && *e) {
         const int want = atoi(e);
@@ -812,6 +839,29 @@ static void job_release(gx_context* ctx, FillJob& j) {
     pool_put(ctx, j.progress); pool_put(ctx, j.sres); pool_put(ctx, j.pres); pool_put(ctx, j.pairs);
     pool_put(ctx, j.counter); pool_put(ctx, j.skel); pool_put(ctx, j.ccodes);
     pool_put(ctx, j.wrows); pool_put(ctx, j.wdesc); pool_put(ctx, j.wres_d);
+}
+
+// A staged run's last fill, kept for gx_staged_table (its buffers go back to
+// the pool when the run is replaced and the last table of it is freed; the
+// owner holds ctx->mu then).
+struct KeptFill {
+    gx_context* ctx = nullptr;
+    FillJob job;
+    std::vector<int> dev_of;   // staged pair -> its index in job.pd (-1: no interior, not filled)
+    ~KeptFill() { job_release(ctx, job); }
+};
+// The pipelines' release point for a pass's fill: the last pass of a
+// GX_STAGED_KEEP_PLANES run is held (*keep set) instead of released.
+static void release_or_hold(gx_context* ctx, FillJob& j, bool last_pass, bool* held) {
+    if (ctx->keep_capture && last_pass) { *held = true; return; }
+    job_release(ctx, j);
+}
+static void keep_job(gx_context* ctx, FillJob& j, const std::vector<int>& dev_of) {
+    auto k = std::make_shared<KeptFill>();
+    k->ctx = ctx;
+    k->dev_of = dev_of;
+    std::swap(k->job, j);
+    ctx->kept = std::move(k);
 }
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -922,7 +972,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                     bool lcs, FillJob& job, const uint8_t* chars_dev = nullptr,
                     const std::vector<size_t>* off1 = nullptr, const std::vector<size_t>* off2 = nullptr,
                     const SmallAlpha* alpha = nullptr, int slot = -1, bool collect = true) {
-    const int lay = fill_layout(ph, sc, fill_grid_cap(ctx->device), track || (lcs && planes));
+    const int lay = fill_layout(ph, sc, fill_grid_cap(ctx->device), track || (lcs && planes), lcs && planes);
     hipStream_t const fs = job.stream ? job.stream : ctx->stream;
     const int SR = strip_rows(lay);
     int total_strips = 0;
@@ -944,7 +994,9 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
     // value as V - (i + j) g (one add less per recurrence, gx_kernels.hip
     // cell; the local floor becomes -(i + j) g); the sub scores carry -2g
     Scores32 scl = sc;
-    const bool shift = ((lay == 0 || lay == 3) && !is_local && !track) || cs2;
+    // (layout 3's global recurrence always holds shifted values; its tracked
+    // fill compares them through a shifted threshold, gx_skew.hip track_step)
+    const bool shift = (lay == 3 && !is_local) || (lay == 0 && !is_local && !track) || cs2;
     scl.shift = shift ? 1 : 0;
     if (shift) { scl.sm = sc.sm - 2 * sc.g; scl.smm = sc.smm - 2 * sc.g; }
     job.shift = shift; job.g = sc.g;
@@ -1147,12 +1199,17 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
         d.progress = progress + gofs[p];
     }
     // layout 3 reads each lane's column symbols from an int32 copy (gx_skew.hip)
+    // (with score tables: four rows per pair, one per row symbol: the scores themselves)
     if (lay == 3) {
+        const size_t rows = tbl ? 4 : 1;
         size_t cc = 0;
-        for (size_t p = 0; p < P; ++p) cc += (size_t)job.pd[p].m + 192;
+        for (size_t p = 0; p < P; ++p) cc += rows * ((size_t)job.pd[p].m + 192);
         if ((rc = pool_get(ctx, cc * sizeof(int), &job.ccodes, fs))) return rc;
         cc = 0;
-        for (size_t p = 0; p < P; ++p) { job.pd[p].ccodes = (const int*)job.ccodes.p + cc; cc += (size_t)job.pd[p].m + 192; }
+        for (size_t p = 0; p < P; ++p) {
+            job.pd[p].ccodes = (const int*)job.ccodes.p + cc;
+            cc += rows * ((size_t)job.pd[p].m + 192);
+        }
     }
     const char* trace_file = slot < 0 ? getenv("GX_TRACE_FILE") : nullptr;
     DevBuf trace;
@@ -1220,7 +1277,7 @@ static int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*,
                               (const PairDev*)job.pairs.p, (int)P, (int)tw.size(), bands, counter,
                               (PairRes*)job.pres.p, (StripRes*)job.sres.p, scl, grid, fs));
     else if (bands > 0 && lay == 3)
-        HIPCHK(launch_fill_skew(W, is_local != 0, planes, tbl, trace.p != nullptr, (const PairDev*)job.pairs.p, (int)P, bands,
+        HIPCHK(launch_fill_skew(W, is_local != 0, planes, tbl, trace.p != nullptr, track, (const PairDev*)job.pairs.p, (int)P, bands,
                                 counter, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
     else if (bands > 0 && cs2)
         HIPCHK(launch_fill_cs2(W, is_local != 0, planes, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
@@ -1432,6 +1489,7 @@ struct gx_table {
     Scores32 sc;
     int is_local = 0;
     uint32_t flags = 0;
+    std::shared_ptr<KeptFill> share;   // gx_staged_table: the staged run's kept fill whose planes this table views
 };
 
 // What the start cell search needs from a fill's results (int32 or int64 fill).
@@ -1494,7 +1552,7 @@ static int label_boundary(const HostScores& hs, int is_local, const uint8_t* s1,
             return fail(GX_EPANIC, "Unexpected score during retrace: " + std::to_string(mx) + " at (" +
                                        std::to_string(i) + ", " + std::to_string(j) + ")");
         }
-        w.steps.push_back(st);
+        if (!w.steps.push_back(st)) return fail(GX_ENOMEM, "step buffer");
         const bool inone = di && i == 0, jnone = dj && j == 0;
         if (inone && jnone) break;
         i = inone ? 0 : i - (di ? 1 : 0);
@@ -1515,8 +1573,8 @@ static int label_walk(const HostScores& hs, int is_local, const uint8_t* s1, siz
     gx_result& r = w.res;
     uint64_t nmat = 0, nmis = 0, next = 0, nopen = 0;
     w.steps.clear();
-    w.steps.reserve(nmoves_hint + (size_t)si + (size_t)sj + 2);
-    bool done = false;
+    if (!w.steps.reserve(nmoves_hint + (size_t)si + (size_t)sj + 2)) return fail(GX_ENOMEM, "step buffer");
+    bool done = false, oom = false;
     // interior part, decided on the device
     src([&](uint8_t c) -> bool {
         gx_step st{};
@@ -1540,10 +1598,11 @@ static int label_walk(const HostScores& hs, int is_local, const uint8_t* s1, siz
             last = GX_DELETE;
             --i;
         }
-        w.steps.push_back(st);
+        if (!w.steps.push_back(st)) { oom = true; return false; }
         if (i == 0 && j == 0) { done = true; return false; }
         return true;
     });
+    if (oom) return fail(GX_ENOMEM, "step buffer");
     r.matches = nmat; r.mismatches = nmis; r.gap_extensions = next; r.opening_gaps = nopen;
     if (!done) {
         const int rc = label_boundary(hs, is_local, s1, n, s2, m, i, j, last, w);
@@ -1778,6 +1837,17 @@ static int run_traceback(gx_context* ctx, const FillJob& job, const std::vector<
 static void release_held(gx_context* ctx, int slot) {
     for (DevBuf& b : ctx->slots[slot].held) { pool_put(ctx, b); b = DevBuf{}; }
 }
+// After a pipeline drained (its streams and the copy stream synchronised),
+// or on its error path: every slot's traceback buffers and fill results block
+// back to the pool (a fill's held_pres is otherwise released only by its
+// fill_collect or the slot's next fill).
+static void release_slots(gx_context* ctx) {
+    (void)hipStreamSynchronize(ctx->cstream);
+    for (int k = 0; k < 4; ++k) {
+        release_held(ctx, k);
+        pool_put(ctx, ctx->slots[k].held_pres);
+    }
+}
 
 static int tb_collect(gx_context* ctx, int slot, size_t P, TbOut& out) {
     auto& s = ctx->slots[slot];
@@ -1938,13 +2008,17 @@ static int fetch_rows32(const gx_table* t, int which, size_t row0, size_t rows, 
     if (n == 0 || m == 0 || rows == 0) return GX_OK;
     const PairDev& d = t->job.pd[0];
     const int32_t* src = which == 0 ? d.pI : which == 1 ? d.pD : which == 2 ? d.pS : d.pL;
+    if (t->job.w16) src = which <= 2 ? d.pI : nullptr;   // (one code plane holds all three)
     if (!src) return fail(GX_EINVAL, "plane not kept: build the table with GX_TABLE_PLANES / GX_TABLE_MATCHES");
     gx_context* ctx = t->ctx;
     DevBuf tmp;
     int rc = pool_get(ctx, out.size() * sizeof(int32_t), &tmp);
     if (rc) return rc;
     hipError_t e;
-    if (t->job.d8)   // compact planes: rebuilt from the insert plane's running sum (+ this plane's x)
+    if (t->job.w16)   // twin plane codes (staged tables): this pair's half of the twin's code plane
+        e = launch_export_w16((const uint8_t*)d.pI, d.twin_half, which, (int32_t*)tmp.p, (int)n, (int)m, d.t4,
+                              t->sc.h, t->sc.g, t->sc.floor_, t->sc.g, (int)row0, (int)rows, ctx->stream);
+    else if (t->job.d8)   // compact planes: rebuilt from the insert plane's running sum (+ this plane's x)
         e = launch_export_d8((const uint8_t*)d.pI, which == 0 ? nullptr : (const uint8_t*)src, (int32_t*)tmp.p,
                              (int)n, (int)m, d.t4, t->sc.h, t->sc.g, t->sc.floor_, t->job.shift ? t->sc.g : 0,
                              (int)row0, (int)rows, ctx->stream);
@@ -2144,6 +2218,7 @@ extern "C" void gx_table_free(gx_table* t) {
     if (t->ctx) {
         std::lock_guard<std::mutex> lk(t->ctx->mu);
         job_release(t->ctx, t->job);
+        t->share.reset();   // (the kept fill's buffers go back to the pool with its last table)
     }
     delete t;
 }
@@ -2156,8 +2231,13 @@ static int copy_steps(const Walk& w, gx_step* steps, size_t cap) {
     return GX_OK;
 }
 
+extern "C" void gx_table_free(gx_table* t);
 extern "C" int gx_retrace(gx_table* t, int is_local, gx_step* steps, size_t cap, gx_result* out) {
     if (!t) return fail(GX_EINVAL, "table is NULL");
+    if (t->share) {   // (consumed whatever the return code, gx.h)
+        gx_table_free(t);
+        return fail(GX_EINVAL, "a staged table has no retrace (its alignment: gx_staged_steps)");
+    }
     gx_context* ctx = t->ctx;
     int rc = GX_OK;
     Walk w;
@@ -2430,8 +2510,16 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
     }
     const auto c2 = clk::now();
     if (fill_ms) *fill_ms = job.fill_ms;
-    job_release(ctx, job);
+    bool held = false;
+    if (rc) job_release(ctx, job);
+    else release_or_hold(ctx, job, true, &held);
     if (rc) return rc;
+    if (held) {
+        (void)hipStreamSynchronize(ctx->stream);
+        std::vector<int> kdev(P, -1);
+        for (size_t k = 0; k < idx.size(); ++k) kdev[idx[k]] = (int)k;
+        keep_job(ctx, job, kdev);
+    }
     struct PhaseLog {   // GX_LOG=debug: host-side phase times of the batch path
         clk::time_point c0, c1, c2;
         double fill_ms, tb_ms;
@@ -2555,8 +2643,7 @@ static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
         (void)hipStreamSynchronize(ctx->cstream);
         for (auto& j : jA) job_release(ctx, j);
         job_release(ctx, jB);
-        release_held(ctx, 0);
-        release_held(ctx, 1);
+        release_slots(ctx);
     };
     {   // both groups must take the twin fill without landing columns: decided before anything is enqueued
         FillJob pa, pb;
@@ -2692,6 +2779,8 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
     };
     // results of slot s's fill -> start cells -> its traceback queued; the fill
     // buffers return to the pool (their last user, the traceback, is queued)
+    int pl_pass = 0;
+    bool pl_held[2] = {false, false};
     auto trace = [&](int s) {
         int r = fill_collect(ctx, jobs[s]);
         if (r) return r;
@@ -2706,7 +2795,7 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
                             : TbStart{0, 0, 0};
         }
         r = run_traceback(ctx, jobs[s], starts, ctx->slots[s].out, s, false);
-        job_release(ctx, jobs[s]);
+        release_or_hold(ctx, jobs[s], pl_pass++ == nsteps - 1, &pl_held[s]);
         return r;
     };
     using clk = std::chrono::steady_clock;
@@ -2724,7 +2813,7 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
     // forces it from 16 pairs, GX_OVERLAP=0 turns it off)
     const char* ov = getenv("GX_OVERLAP");
     const bool ov_force = ov && !strcmp(ov, "1");
-    if (!track && planes && idx.size() >= 16 && (nmax_b >= 16384 || ov_force) &&
+    if (!track && planes && idx.size() >= 16 && (nmax_b >= 16384 || ov_force) && !ctx->keep_capture &&
         !(ov && !strcmp(ov, "0")) && (!is_local || idx.size() >= 64 || ov_force)) {
         const int orc = batch_core_overlap(ctx, ph, proc, hs, sc, is_local, planes, nsteps, walks, fill_ms, chars_dev, off1, off2,
                                            alpha, idx, alt);
@@ -2742,9 +2831,11 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
         // stream beside the next step's fill measured 1024 x 4k +6 % but made
         // 1024 x 1k 2.5x slower: the host's enqueue of the next fill stalled
         // behind the running walk.)
+        int tr_pass = 0;
+        bool held[2] = {false, false};
         auto trace_dev = [&](int s) {
             int r = run_traceback(ctx, jobs[s], starts, ctx->slots[s].out, s, false, true);
-            job_release(ctx, jobs[s]);   // stream order: later users come after the traceback
+            release_or_hold(ctx, jobs[s], tr_pass++ == nsteps - 1, &held[s]);   // stream order: later users come after the traceback
             return r;
         };
         auto results = [&](int s) {
@@ -2782,12 +2873,12 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
                     h_tbw / nsteps, h_res / nsteps, h_lab / nsteps);
         if (rc) {
             (void)hipStreamSynchronize(ctx->stream);
-            (void)hipStreamSynchronize(ctx->cstream);
             for (auto& j : jobs) job_release(ctx, j);
-            release_held(ctx, 0);
-            release_held(ctx, 1);
+            release_slots(ctx);
             return rc;
         }
+        for (int s = 0; s < 2; ++s)
+            if (held[s]) { (void)hipStreamSynchronize(ctx->stream); keep_job(ctx, jobs[s], dev_of); }
         if (fill_ms) *fill_ms = fsum / nsteps;
         return GX_OK;
     }
@@ -2814,12 +2905,12 @@ static int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
                 t_trace / nsteps);
     if (rc) {
         (void)hipStreamSynchronize(ctx->stream);
-        (void)hipStreamSynchronize(ctx->cstream);
         for (auto& j : jobs) job_release(ctx, j);
-        release_held(ctx, 0);
-        release_held(ctx, 1);
+        release_slots(ctx);
         return rc;
     }
+    for (int s = 0; s < 2; ++s)
+        if (pl_held[s]) { (void)hipStreamSynchronize(ctx->stream); keep_job(ctx, jobs[s], dev_of); }
     if (fill_ms) *fill_ms = fsum / nsteps;
     return GX_OK;
 }
@@ -3076,14 +3167,23 @@ extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int
     // every pass's results (label_batch records them; chunks set pass_off)
     struct PassRec {
         gx_context* c;
-        ~PassRec() { c->pass_rec = false; }
+        ~PassRec() { c->pass_rec = false; c->keep_capture = false; }
     } pass_guard{ctx};
+    ctx->kept.reset();   // (a previous run's kept planes: their tables hold their own reference)
+    if (flags & GX_STAGED_KEEP_PLANES) {
+        if (!keep_planes) return fail(GX_EINVAL, "GX_STAGED_KEEP_PLANES needs keep_planes");
+        if (flags & GX_STAGED_ALTERNATE) return fail(GX_EINVAL, "GX_STAGED_KEEP_PLANES with alternating sets");
+        ctx->keep_capture = true;
+        ctx->kept_hs = hs;
+        ctx->kept_sc = sc;
+    }
     ctx->pass_res.assign((size_t)std::max(nsteps, 1) * P, gx_result{});
     ctx->pass_rec = true;
     ctx->pass_P = P;
     ctx->pass_off = 0;
     ctx->pass_k = 0;
     if (wide && (flags & GX_STAGED_ALTERNATE)) return fail(GX_EINVAL, "alternating sets: not on the int64 fill");
+    if (wide && ctx->keep_capture) return fail(GX_EINVAL, "GX_STAGED_KEEP_PLANES: not on the int64 fill");
     if (wide) {   // int64 fill: one synchronous pass at a time (a rare path, no pipelining or chunking)
         std::vector<Walk>& walks = ctx->walk_cache;
         const int passes = std::max(nsteps, 1);
@@ -3141,6 +3241,7 @@ extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int
     const double bpc = keep_planes ? ((!track && !getenv("GX_PLANES32") && d8_planes_ok(sc, is_local)) ? 3.0 : 12.0)
                                    : 0.0;
     const auto chunks = plan_chunks(ctx, ph, bpc);
+    if (ctx->keep_capture && chunks.size() != 1) return fail(GX_EINVAL, "GX_STAGED_KEEP_PLANES needs one chunk");
     // the order in which the fills write their checksum records: chunk, pass, pair with an interior
     std::vector<std::pair<int, size_t>> sum_order;
     for (const auto& c : chunks)
@@ -3202,6 +3303,48 @@ extern "C" int gx_run_staged_steps(gx_context* ctx, const gx_scores* scores, int
     }
     for (size_t p = 0; p < P; ++p) out[p] = walks[p].res;
     if (fill_ms_out) *fill_ms_out = fms;
+    return GX_OK;
+}
+
+extern "C" int gx_staged_table(gx_context* ctx, size_t pair, gx_table** table_out) {
+    if (!ctx || !table_out) return fail(GX_EINVAL, "NULL argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    HIPCHK(hipSetDevice(ctx->device));
+    const std::shared_ptr<KeptFill> k = ctx->kept;
+    if (!k) return fail(GX_EINVAL, "no kept planes: run gx_run_staged_steps with GX_STAGED_KEEP_PLANES");
+    if (pair >= ctx->st_s1.size() || pair >= k->dev_of.size()) return fail(GX_EINVAL, "no such staged pair");
+    const size_t n = ctx->st_s1[pair].size(), m = ctx->st_s2[pair].size();
+    gx_table* t = new gx_table();
+    t->ctx = ctx;
+    t->is_local = k->job.local_on ? 1 : 0;
+    t->flags = GX_TABLE_PLANES;
+    t->hs = ctx->kept_hs;
+    t->sc = ctx->kept_sc;
+    t->s1 = ctx->st_s1[pair];
+    t->s2 = ctx->st_s2[pair];
+    int rc = processed_chars(t->s1.data(), n, t->s2.data(), m, 0, t->c1, t->c2);
+    if (rc) { delete t; return rc; }
+    // a view of the kept job: its flags and this pair's descriptor and
+    // results; the device buffers stay the kept job's (t->share), but for a
+    // descriptor block of its own (the plane checksum kernel reads it)
+    FillJob& j = t->job;
+    const FillJob& kj = k->job;
+    j.lay = kj.lay; j.W = kj.W; j.planes_on = kj.planes_on; j.d8 = kj.d8; j.shift = kj.shift; j.twin = kj.twin;
+    j.w16 = kj.w16; j.nocodes = kj.nocodes; j.noskel = kj.noskel; j.local_on = kj.local_on; j.g = kj.g;
+    j.fill_ms = kj.fill_ms; j.table = true;
+    const int q = k->dev_of[pair];
+    if (q >= 0) {
+        j.pd.assign(1, kj.pd[(size_t)q]);
+        j.res.assign(1, (size_t)q < kj.res.size() ? kj.res[(size_t)q] : PairRes{});
+        if ((rc = pool_get(ctx, sizeof(PairDev), &j.pairs))) { delete t; return rc; }
+        HIPCHK(hipMemcpy(j.pairs.p, &j.pd[0], sizeof(PairDev), hipMemcpyHostToDevice));
+    } else {
+        j.pd.assign(1, PairDev{});
+        j.pd[0].n = (int)n; j.pd[0].m = (int)m;
+        j.res.assign(1, PairRes{});
+    }
+    t->share = k;
+    *table_out = t;
     return GX_OK;
 }
 
@@ -3279,7 +3422,7 @@ extern "C" int gx_plan_layout(const gx_scores* scores, int is_local, const int64
     if (check_scores(scores, (size_t)nmax, (size_t)mmax, &hs, &sc, is_local, nullptr) != GX_OK) return -1;
     std::vector<PairHost> ph(npairs);
     for (size_t p = 0; p < npairs; ++p) ph[p] = PairHost{nullptr, nullptr, (size_t)n[p], (size_t)m[p]};
-    return fill_layout(ph, sc, grid_cap > 0 ? grid_cap : 256, track != 0);
+    return fill_layout(ph, sc, grid_cap > 0 ? grid_cap : 256, track != 0, false);
 }
 
 extern "C" int gx_plane_bytes_per_cell(const gx_scores* scores, int is_local) {

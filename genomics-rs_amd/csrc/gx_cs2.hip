@@ -181,9 +181,9 @@ __device__ __forceinline__ void cs2_core(const PairDev& P, const int s, const in
     StripTrace* const trace = P.trace;   // GX_TRACE_FILE diagnostics (tools/trace_summary.py)
     long long tr_start = 0, tr_first = 0, clk_first = 0;
     long long tr_q[kTraceQ] = {};
-    if (trace) tr_start = __builtin_amdgcn_s_memrealtime();
+    if (trace) tr_start = stamp_rt();
     const unsigned tr_win0 = wait_ge(wcnt_in, min(4, m) + 1, status);
-    if (trace) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
+    if (trace) { tr_first = stamp_rt(); clk_first = stamp_clk(); }
     Rec ra[4], rb[4];
     int psm;
     {
@@ -215,7 +215,7 @@ __device__ __forceinline__ void cs2_core(const PairDev& P, const int s, const in
         const int last_col = min(t0 + kSub, m);
         if (trace) {
             const int q = (int)((long long)t0 * (kTraceQ + 1) / (m + 1)) - 1;
-            if (q >= 0 && q < kTraceQ && tr_q[q] == 0) tr_q[q] = __builtin_amdgcn_s_memrealtime();
+            if (q >= 0 && q < kTraceQ && tr_q[q] == 0) tr_q[q] = stamp_rt();
         }
         if (has_consumer && last_col >= kRing) wait_ge(rcnt_out, last_col - kRing + 1, status);
         // staging slots free: group g reuses the slot of group g - KSB/4, so the
@@ -238,9 +238,9 @@ __device__ __forceinline__ void cs2_core(const PairDev& P, const int s, const in
     }
     if (trace && lane == 0) {
         StripTrace tr;
-        tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
+        tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = stamp_rt();
         tr.wait_in = (int)(tr_win0 + tr_wait_in); tr.wait_out = (int)tr_wait_sb;
-        tr.clk = __builtin_amdgcn_s_memtime() - clk_first;
+        tr.clk = stamp_clk() - clk_first;
         for (int q = 0; q < kTraceQ - 1; ++q) tr.t_q[q] = tr_q[q];
         // (t_q[kTraceQ - 1] belongs to the side wave: its own wait iterations)
         long long* d = &trace[s].t_start;

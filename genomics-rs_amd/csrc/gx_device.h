@@ -44,6 +44,23 @@ __device__ __forceinline__ void lds_post(lds_int* p, int v) {
     __hip_atomic_store((lds_plain*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// Trace stamps (GX_TRACE_FILE diagnostics): scalar-memory reads of the clocks.
+// They count on lgkmcnt out of order, so a stamp whose result is still in
+// flight when an LDS wait comes forces that wait to lgkmcnt(0) -- and the
+// compiler carries such an outstanding stamp through the whole strip loop.
+// Each stamp is therefore consumed on the spot (the asm use makes the
+// compiler wait for it there, on the traced path only).
+__device__ __forceinline__ long long stamp_rt() {
+    const long long v = __builtin_amdgcn_s_memrealtime();
+    asm volatile("" ::"s"(v));
+    return v;
+}
+__device__ __forceinline__ long long stamp_clk() {
+    const long long v = __builtin_amdgcn_s_memtime();
+    asm volatile("" ::"s"(v));
+    return v;
+}
+
 __device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -61,6 +78,19 @@ __device__ __forceinline__ unsigned wait_ge(lds_int* p, int v, int* status) {
         if (it > kSpinLimit) { __hip_atomic_store((gint*)status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
         if ((it & 4095u) == 4095u && __hip_atomic_load((gint*)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
         __builtin_amdgcn_s_sleep(1);
+    }
+    asm volatile("" ::: "memory");
+    return it;
+}
+
+// The same without the sleep between polls, for a wave alone on its SIMD
+// whose wait is on the critical path (layout 3's strip input): a poll is an
+// LDS round trip already, and s_sleep 1 adds 64 cycles to each.
+__device__ __forceinline__ unsigned wait_ge_tight(lds_int* p, int v, int* status) {
+    unsigned it = 0;
+    for (; *p < v; ++it) {
+        if (it > 4 * kSpinLimit) { __hip_atomic_store((gint*)status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
+        if ((it & 16383u) == 16383u && __hip_atomic_load((gint*)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
     }
     asm volatile("" ::: "memory");
     return it;

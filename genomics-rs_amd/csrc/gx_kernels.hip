@@ -30,6 +30,8 @@
 
 namespace gx {
 
+
+
 #ifndef GX_FILL_MIN_WAVES_TRACK
 #define GX_FILL_MIN_WAVES_TRACK 2
 #endif
@@ -500,7 +502,7 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     long long tr_start = 0, tr_first = 0, clk_first = 0;
     unsigned tr_wout = 0;
     long long tr_q[kTraceQ] = {};
-    if (tracing) tr_start = __builtin_amdgcn_s_memrealtime();
+    if (tracing) tr_start = stamp_rt();
     // column 0 of the row above seeds row A's top-left of column 1; columns
     // 1..4 feed the first step group
     w.tr_win += wait_ge(wcnt_in, min(4, m) + 1, status);
@@ -513,7 +515,7 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         st.a.Ltl = 0;
         read4(nxt, ring_in + ring_slot(1));
     }
-    if (tracing) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
+    if (tracing) { tr_first = stamp_rt(); clk_first = stamp_clk(); }
     const int T = m + kWave;                          // lane 63 pushes column m at step m + 63
     const bool rolled_only = (sc.dbg & 1) != 0;
     PendStore pend;
@@ -523,7 +525,7 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
         if (has_consumer && last_col >= kRing) tr_wout += wait_ge(rcnt_out, last_col - kRing + 1, status);
         if (tracing) {   // progress stamps at k/(kTraceQ+1) of the sweep
             const int q = (int)((long long)t0 * (kTraceQ + 1) / T) - 1;
-            if (q >= 0 && q < kTraceQ && tr_q[q] == 0) tr_q[q] = __builtin_amdgcn_s_memrealtime();
+            if (q >= 0 && q < kTraceQ && tr_q[q] == 0) tr_q[q] = stamp_rt();
         }
         const size_t sb_off = (size_t)(t0 >> 2) * kGroupInts;         // this sub-block's plane offset (ints)
         const bool full = (t0 >= kWave) && (t0 + kSub - 1 <= m - 1) && !rolled_only;
@@ -589,9 +591,9 @@ __device__ void compute_wave(const PairDev& P, const int s, const int lane, cons
     if (ok_b && ia + 1 == n) { pres->end_SM = st.b.SM; pres->end_E = st.b.E; }
     if (tracing && lane == 0) {
         StripTrace tr;
-        tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
+        tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = stamp_rt();
         tr.wait_in = (int)w.tr_win; tr.wait_out = (int)tr_wout;
-        tr.clk = __builtin_amdgcn_s_memtime() - clk_first;
+        tr.clk = stamp_clk() - clk_first;
         for (int q = 0; q < kTraceQ; ++q) tr.t_q[q] = tr_q[q];
         trace[s] = tr;
     }
@@ -868,7 +870,7 @@ __device__ void compute_wave_cs(const PairDev& P, const int s, const int lane, c
     long long tr_start = 0, tr_first = 0, clk_first = 0;
     unsigned tr_wout = 0;
     long long tr_q[kTraceQ] = {};
-    if (tracing) tr_start = __builtin_amdgcn_s_memrealtime();
+    if (tracing) tr_start = stamp_rt();
     w.tr_win += wait_ge(wcnt_in, min(4, m) + 1, status);
     Rec ra[4], rb[4];   // records of the current / next group (alternating)
     int psm, pl;
@@ -878,7 +880,7 @@ __device__ void compute_wave_cs(const PairDev& P, const int s, const int lane, c
         pl = 0;
         read4(ra, ring_in + ring_slot(1));
     }
-    if (tracing) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
+    if (tracing) { tr_first = stamp_rt(); clk_first = stamp_clk(); }
     CsPend pend;
     pend.voff = kNoStore;   // nothing pending before the first group
     // steps 0 .. m: step t computes column t + 1 and finishes E of column t,
@@ -888,7 +890,7 @@ __device__ void compute_wave_cs(const PairDev& P, const int s, const int lane, c
         if (has_consumer && last_col >= kRing) tr_wout += wait_ge(rcnt_out, last_col - kRing + 1, status);
         if (tracing) {
             const int q = (int)((long long)t0 * (kTraceQ + 1) / (m + 1)) - 1;
-            if (q >= 0 && q < kTraceQ && tr_q[q] == 0) tr_q[q] = __builtin_amdgcn_s_memrealtime();
+            if (q >= 0 && q < kTraceQ && tr_q[q] == 0) tr_q[q] = stamp_rt();
         }
         const uint32_t out_base = lds_addr(ring_out + ring_slot(t0 + 1));
         if (t0 + kSub < m) {   // step m - 1 (cell (., m)) and step m always run in a tail sub-block
@@ -938,9 +940,9 @@ __device__ void compute_wave_cs(const PairDev& P, const int s, const int lane, c
     if (ok && i == n) { pres->end_SM = st.fin_sm; pres->end_E = st.fin_E - 64; }
     if (tracing && lane == 0) {
         StripTrace tr;
-        tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
+        tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = stamp_rt();
         tr.wait_in = (int)w.tr_win; tr.wait_out = (int)tr_wout;
-        tr.clk = __builtin_amdgcn_s_memtime() - clk_first;
+        tr.clk = stamp_clk() - clk_first;
         for (int q = 0; q < kTraceQ; ++q) tr.t_q[q] = tr_q[q];
         trace[s] = tr;
     }
@@ -1394,7 +1396,7 @@ __global__ __launch_bounds__((1 + kSqHelp) * kWave) void tb_seq_kernel(const TbD
     lint* const ltbl = (lint*)(uintptr_t)lds_addr(tbl);
     int s = first, nrec = 0, cb = 0;
     int end_i = -1, end_j = -1;
-    long long clk0 = __builtin_amdgcn_s_memtime(), walk_clk = 0;   // (diagnostics: end_ij[3])
+    long long clk0 = stamp_clk(), walk_clk = 0;   // (diagnostics: end_ij[3])
     int nblk = 0;
     __syncthreads();
     for (int guard = 0; guard <= 2 * J.strips + 2; ++guard) {
@@ -1408,10 +1410,10 @@ __global__ __launch_bounds__((1 + kSqHelp) * kWave) void tb_seq_kernel(const TbD
             guint* const recs = (guint*)(J.recs + (size_t)s * J.srows);
             int nj;
             bool run_end;
-            const long long w0 = __builtin_amdgcn_s_memtime();
+            const long long w0 = stamp_clk();
             const int E = tb_walk_block<kSqWin, true>(J, s, vb, vb_top, R, ce, q0, (const lu32*)(uintptr_t)lds_addr(wbuf[cb]),
                                                       ltbl, lane, recs, nrec, nj, run_end);
-            walk_clk += __builtin_amdgcn_s_memtime() - w0;
+            walk_clk += stamp_clk() - w0;
             ++nblk;
             int done = 0;
             if (E < 0) {                  // on into the block above, in this strip
@@ -1440,7 +1442,7 @@ __global__ __launch_bounds__((1 + kSqHelp) * kWave) void tb_seq_kernel(const TbD
         end_j = ctl.done ? ctl.end_j : -1;
         J.end_ij[0] = end_i; J.end_ij[1] = end_j; J.end_ij[2] = end_i < 0 ? -1 : first;
         // cycles per block: all (high 16 bits) and the walk's (low 16)
-        const long long all = (__builtin_amdgcn_s_memtime() - clk0) / max(nblk, 1), wk = walk_clk / max(nblk, 1);
+        const long long all = (stamp_clk() - clk0) / max(nblk, 1), wk = walk_clk / max(nblk, 1);
         J.end_ij[3] = (int)((min(all, 65535LL) << 16) | min(wk, 65535LL));
     }
 }
@@ -1603,6 +1605,34 @@ __global__ void export_d8_kernel(const uint8_t* __restrict__ pI, const uint8_t* 
     }
 }
 
+// Export of the twin fill's plane codes (gx_fill_pk.hip w16_code, DESIGN.md
+// 4.4): one thread per row decodes this pair's 16-bit half of each dword,
+// rebuilds I(i, j) = (H(i, 0) + h) + sum (x_I' + g) and adds the plane's x_D
+// or x_S -- the decode of plane_sums_kernel mode 3.  `half` = the pair's half
+// (PairDev.twin_half), the code plane layout [strip][t/4][row-in-lane][lane][t%4]
+// dwords.  Rows row0 .. row0 + rows - 1 (each at least 1).
+__global__ void export_w16_kernel(const uint8_t* __restrict__ codes, int half, int which, int32_t* __restrict__ out,
+                                  int n, int m, int t4, int h, int g, int floor_, int gshift, int row0, int rows) {
+    const int r = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int i = r + row0;
+    if (r >= rows || i < 1 || i > n) return;
+    const int s = (i - 1) / kStripRows, rho = (i - 1) % kStripRows;
+    const int l = rho >> 1, hh = rho & 1;
+    const uint8_t* base = codes + (size_t)s * t4 * kTwinGroupBytes + (size_t)hh * (kTwinGroupBytes / 2) + (size_t)l * 16;
+    int I = max(h + i * g, floor_) + h;   // H(i, 0) + h, as the fill seeds it
+    int32_t* o = out + (size_t)r * (m + 1);
+    for (int j = 1; j <= m; ++j) {
+        const int t = j - 1 + l;
+        const uint32_t wd = *(const uint32_t*)(base + (size_t)(t >> 2) * kTwinGroupBytes + (size_t)(t & 3) * 4);
+        const uint32_t code = (0u - (wd >> (16 * half))) & 0xFFFFu;   // (stored negated)
+        const uint32_t q = code >> 4;                                  // x_S + 32 x_D (mod 2^12)
+        const int xS = (int)(q << 27) >> 27;                           // 5-bit signed
+        const int xD = (int)(((q - (uint32_t)xS) >> 5) << 25) >> 25;   // 7-bit signed
+        I += (int)(code & 15u) + gshift;                               // x_I - g stored
+        o[j] = which == 0 ? I : which == 1 ? I + xD : I + xS;
+    }
+}
+
 }  // namespace gx
 
 // ---- explicit launch wrappers (C++ linkage, used by gx_api.cpp) ----
@@ -1700,6 +1730,14 @@ hipError_t launch_export_d8(const uint8_t* pI, const uint8_t* px, int32_t* out, 
     if (n == 0 || m == 0 || rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(export_d8_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, pI, px, out, n, m, t4, h,
                        g, floor_, gshift, row0, rows);
+    return hipGetLastError();
+}
+
+hipError_t launch_export_w16(const uint8_t* codes, int half, int which, int32_t* out, int n, int m, int t4, int h,
+                             int g, int floor_, int gshift, int row0, int rows, hipStream_t st) {
+    if (n == 0 || m == 0 || rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(export_w16_kernel, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, st, codes, half, which, out,
+                       n, m, t4, h, g, floor_, gshift, row0, rows);
     return hipGetLastError();
 }
 

@@ -61,16 +61,23 @@ namespace gx {
 
 typedef __attribute__((address_space(3))) v4i lds_v4i;
 constexpr int kSkRingG = 64;     // ring groups per strip boundary (256 columns)
+constexpr int kSkHo = 8;         // core -> side hand-off ring depth (4-step groups)
 
 struct SkRing {                  // one strip boundary (see the file header)
     int dd[kSkRingG][4];
     int sm[kSkRingG][4];
 };
+struct SkHo {                    // one strip's core -> side ring: [group][S, D][lane] int4 (the side
+    int4 v[kSkHo][2][kWave];     // wave derives I from them: side_group)
+};
+struct SkMRing {                 // TRACK: one strip boundary's LCS values (max_matches, algo.rs:113-121), side to side
+    int m[kSkRingG][4];
+};
 __device__ __forceinline__ int sk_grp(int c) { return ((c + 3) >> 2) & (kSkRingG - 1); }
 __device__ __forceinline__ int sk_pos(int c) { return (c + 3) & 3; }
 
 // ---------------------------------------------------------------------------
-// the strip's two waves: shared pieces
+// core wave
 
 struct CoreState {               // cell (i, j-1) of the lane's row
     int I;                       // insert score
@@ -82,14 +89,14 @@ struct CoreState {               // cell (i, j-1) of the lane's row
 
 // One anti-diagonal step: cell (i, j), j = t - lane + 1.  (rdd, rsm) = lane
 // 0's cell above from the ring (0 in the other lanes); c2 = s2[j-1] (its symbol code * 8 with score
-// tables).  MASKED: act = false keeps the row at its last column.
+// tables).  MASKED (ramp-down): act = false keeps the row at its last column.
 template <bool LOCAL, bool TBL, bool MASKED>
 __device__ __forceinline__ void core_step(CoreState& st, const int rdd, const int rsm, const int c2, const bool act,
                                           const int c1v, const Scores32& sc, int& oI, int& oS, int& oD) {
     const int Dn = shz(st.Dd) + rdd;         // D(i, j): the delete successor of the cell above
     const int hu = shz(st.H) + rsm;          // score_max(i-1, j)  (rdd, rsm: 0 but in lane 0)
     const bool mt = c2 == c1v;               // sequence.rs:113-114
-    const int Sn = st.Hd + (TBL ? __builtin_amdgcn_sbfe(c1v, c2, 8) : (mt ? sc.sm : sc.smm));
+    const int Sn = st.Hd + (TBL ? c2 : (mt ? sc.sm : sc.smm));   // (TBL: c2 is the score of this row's symbol against s2[j-1])
     const int In = LOCAL ? max3i(st.I + sc.g, st.Hx, 0) : max(st.I, st.Hx);
     const int IS = max(In, Sn);
     const int Hn = max(IS, Dn);
@@ -104,200 +111,182 @@ __device__ __forceinline__ void core_step(CoreState& st, const int rdd, const in
     oI = In; oS = Sn; oD = Dn;
 }
 
-// What both waves of a strip need to step it: the ring above (lane 0 reads
-// it, the other lanes a zero block), the column symbols, flow control.
-struct StripIn {
+struct CoreCtx {
     __amdgpu_buffer_rsrc_t crs;  // the pair's int32 column symbols (PairDev.ccodes)
     uint32_t cvoff;              // 4 (64 - lane): this lane's column of step 0, less one
+    uint32_t push_base;          // LDS address; lane 63: the ring below's dd[0]; other lanes (or no consumer): their sink slot
+    uint32_t push_m16;           // lane 63: 16 (a ring group's bytes); other lanes: 0
+    lds_int* pcnt;               // wcnt_out (no consumer: a sink)
     uint32_t rd_base;            // LDS address; lane 0: the ring above's dd[0]; other lanes: a zero block
     uint32_t rd_m16;             // lane 0: 16; other lanes: 0
     const SkRing* rin;
+    SkRing* rout;
     lds_int* wcnt_in;            // columns the strip above published
-    lds_int* rcnt_in;            // ... of which this wave has read (the producer's flow control)
+    lds_int* rcnt_in;            // ... of which this strip has read (its flow control)
+    lds_int* wcnt_out;
+    lds_int* rcnt_out;
+    SkHo* ho;
+    lds_int* hcnt;               // hand-off groups written (core) / read (side), per sub-block
+    lds_int* bcnt;
+    v4i* hv_sub;                 // this lane's slot of the sub-block's first group (ho->v[(t0/4) % kSkHo][0][lane])
     int* status;
     int m, lane, c1;
-    unsigned tr_win;             // (diagnostics: spins waiting for the strip above)
+    int space_out, space_ho;     // rcnt_out / bcnt as read at the previous sub-block (lower bounds, core_sub)
+    bool push_on;
+    unsigned tr_win, tr_ho;      // (diagnostics: spins waiting for the strip above / for hand-off space)
+    long long* tl;               // (diagnostics: the strip's dense timeline, StripTrace.tl)
 };
 
 // Lane 0 reads ring group G (dd, then sm 1 KB on), the other lanes a zero block.
-__device__ __forceinline__ void read_grp(v4i (&r)[2], const StripIn& w, int G) {
+__device__ __forceinline__ void read_grp(v4i (&r)[2], const CoreCtx& w, int G) {
     const lds_v4i* p = (const lds_v4i*)(uintptr_t)(w.rd_base + __umul24((uint32_t)G, w.rd_m16));
     r[0] = p[0];
     r[1] = p[kSkRingG];
 }
 // This lane's column symbols of steps t .. t+3 (columns t-lane+1 ..).
-__device__ __forceinline__ int4 load_codes(const StripIn& w, int t) {
+__device__ __forceinline__ int4 load_codes(const CoreCtx& w, int t) {
     const v4i x = __builtin_amdgcn_raw_buffer_load_b128(w.crs, (int)w.cvoff, __builtin_amdgcn_readfirstlane(4 * t), 0);
     return make_int4(x[0], x[1], x[2], x[3]);
 }
-// The next group's ring record was read speculatively before the steps; if
-// the strip above had not published it yet (seen < need), wait and re-read it
-// into the same registers (one asm: no copies on the fast path).
-__device__ __forceinline__ void ring_catch_up(v4i (&nxt)[2], StripIn& w, const int seen, const int need, const int t) {
-    if (__builtin_amdgcn_readfirstlane(seen) < need) {
-        w.tr_win += wait_ge(w.wcnt_in, need, w.status);
-        const uint32_t a = w.rd_base + __umul24((uint32_t)sk_grp(t + 5), w.rd_m16);
-        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:%3\n\ts_waitcnt lgkmcnt(0)"
-                     : "+v"(nxt[0]), "+v"(nxt[1])
-                     : "v"(a), "i"(kSkRingG * 16)
-                     : "memory");
-    }
-}
-
-// Column 0 of the lane's row (algo.rs:204-211): I = S = neg_inf, D = h + i g,
-// score_max max(D, floor); global fills hold V - (i + 0) g.  Global fills:
-// lane l >= 1 starts at step 0 on virtual columns 1 - l .. 0 (no per-lane
-// masks in the ramp-up).  Its state starts at "minus infinity", so virtual
-// columns < 0 stay there and column 0 comes out of the recurrence exactly:
-// I = S = -inf, D''(i, 0) = max(D''(i-1, 0), H''(i-1, 0) + h) = h from lane
-// l-1, score_max = D (algo.rs:204-211).  Local fills keep the masked ramp-up
-// (their 0 floor lifts virtual cells).  Returns score_max(i, 0).
-template <bool LOCAL>
-__device__ __forceinline__ int strip_start(CoreState& st, const int i, const int lane, const Scores32& sc) {
-    const int D0 = sc.h + i * sc.g;
-    const int H0 = LOCAL ? max(D0, 0) : D0 - i * sc.g;
-    const bool virt = !LOCAL && lane > 0;
-    st.I = LOCAL ? kNeg : kNeg - i * sc.g;
-    st.H = virt ? kNeg : H0;
-    st.Hx = virt ? kNeg : H0 + (LOCAL ? sc.hg : sc.h);
-    st.Dd = virt ? kNeg : H0;                     // (lane 0: the successor D''(i+1, 0) = max(h, 2h) = h)
-    return H0;
-}
-
-// The groups' loop-carried registers (both waves).
-struct StripLoop {
-    v4i ra[2], rb[2];            // ring groups (current / next), alternating
-    int4 cc[4];                  // column symbols of the next four groups
-    long long tr_q[kTraceQ];     // (diagnostics: timeline stamps; core wave)
-};
-
-// Phases of a strip's sweep (one loop each, so that the loop-carried
-// registers keep their places across the back-edge: a merge of differently
-// allocated phases costs copies that wait for the symbol loads in flight).
-// Steps t = 0 .. T-1, T = m + 64; sub-blocks of 16 steps.
-//   ramp-up   t0 + 16 <= 64 and no lane past column m;
-//   steady    t0 >= 64, every lane inside columns 1..m;
-//   ramp-down the rest.
-__device__ __forceinline__ bool in_ramp(int t0, int m) { return t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1; }
-__device__ __forceinline__ bool in_steady(int t0, int m) { return t0 >= kWave && t0 + kSub - 1 <= m - 1; }
-
-// ---------------------------------------------------------------------------
-// core wave: the critical path (ring in, recurrence, push to the strip below)
-
-struct CoreCtx {
-    StripIn in;
-    uint32_t push_base;          // LDS address; lane 63: the ring below's dd[0]; other lanes (or no consumer): their sink slot
-    uint32_t push_m16;           // lane 63: 16 (a ring group's bytes); other lanes: 0
-    lds_int* pcnt;               // wcnt_out (no consumer: a sink)
-    SkRing* rout;
-    lds_int* wcnt_out;
-    lds_int* rcnt_out;           // the strip below's two readers (core, side; the I/O wave writes both)
-    lds_int* rcnt2_out;
-    bool push_on;
-    long long* tl;               // (diagnostics: the strip's dense timeline, StripTrace.tl)
-};
-
-// A group's push data stays allocated through the next group (pinned there),
-// so the next group's results never reuse registers an LDS store may still be
-// reading (which would cost a wait for that store: LDS reads store data after
-// issue).
-struct CorePend {
-    v4i v[2];                    // push dd, sm
-};
-__device__ __forceinline__ void pin(const CorePend& p) { asm volatile("" ::"v"(p.v[0]), "v"(p.v[1])); }
 
 // One 4-step group of the core wave.  MODE 0: every lane steps; 2: per-lane
 // selects (ramp-down of the strip holding row n: lanes past column m keep
 // their state; local ramp-up: lanes not started keep their column-0 state;
 // selects measured 72 ns a step against 100 for a branch per step); 3: the
 // ramp-down of every other global strip: every lane steps on into virtual
-// columns past m (nothing reads a lane's state after its column m: the
-// pushes stop at column m, the side wave masks its own state).  The
-// ramp-down is on the chain's critical path (a strip's last columns wait for
-// the strip above's), so it runs at the steady pace (30k pair 4.36 -> 4.05 ms).
-template <bool LOCAL, bool TBL, int MODE>
+// columns past m (nothing reads a lane's state after its column m: the pushes
+// stop at column m, the side wave masks its own state), pushes as in MODE 2.
+// The ramp-down is on the chain's critical path (a strip's last columns wait
+// for the strip above's), so it runs at the steady pace (30k pair 4.36 -> 4.05 ms).
+// A group's LDS store data (hand-off I, S, D; push dd, sm) stays allocated
+// through the next group (pinned there), so the next group's results never
+// reuse registers an LDS store may still be reading (which would cost a wait
+// for that store: LDS reads store data after issue).
+struct CorePend {
+    v4i v[4];                    // hand-off S, D; push dd, sm
+};
+__device__ __forceinline__ void pin(const CorePend& p) {
+    asm volatile("" ::"v"(p.v[0]), "v"(p.v[1]), "v"(p.v[2]), "v"(p.v[3]));
+}
+
+template <bool LOCAL, bool TBL, int MODE, int Q>
 __device__ __forceinline__ void core_group(CoreState& st, const v4i (&cur)[2], v4i (&nxt)[2], int4& cc, CoreCtx& w,
                                            const Scores32& sc, const int t, CorePend& mine, const CorePend& prev) {
-    StripIn& in = w.in;
-    const int need = min(t + 8, in.m) + 1;                     // columns of the next group: t+5 .. t+8
+    const int need = min(t + 8, w.m) + 1;                      // columns of the next group: t+5 .. t+8
+    const int seen_v = lds_peek(w.wcnt_in);
+    asm volatile("" ::: "memory");
+    read_grp(nxt, w, sk_grp(t + 5));
     const int pdd = st.Dd, psm = st.H;                         // lane 63: column t - 63 (the push below)
-    int oI, oS, oD, qdd[3], qsm[3], seen_v = 0;
+    int oI[4] = {}, oS[4] = {}, oD[4] = {}, qdd[3], qsm[3];
+    const int cd[4] = {cur[0][0], cur[0][1], cur[0][2], cur[0][3]};
+    const int cs[4] = {cur[1][0], cur[1][1], cur[1][2], cur[1][3]};
     const int c2[4] = {cc.x, cc.y, cc.z, cc.w};
 #pragma unroll
     for (int U = 0; U < 4; ++U) {
-        const int c = t + U - in.lane;                         // column - 1
-        const bool act = MODE == 2 ? (LOCAL ? (unsigned)c < (unsigned)in.m : c < in.m) : true;
-        core_step<LOCAL, TBL, MODE == 2>(st, cur[0][U], cur[1][U], c2[U], act, in.c1, sc, oI, oS, oD);
+        // MODE 2: selects per lane (global fills run the virtual columns <= 0
+        // too: only columns > m stop; local fills also hold lanes not started)
+        const int c = t + U - w.lane;   // column - 1
+        const bool act = MODE == 2 ? (LOCAL ? (unsigned)c < (unsigned)w.m : c < w.m) : true;
+        core_step<LOCAL, TBL, MODE == 2>(st, cd[U], cs[U], c2[U], act, w.c1, sc, oI[U], oS[U], oD[U]);
         if (U < 3) { qdd[U] = st.Dd; qsm[U] = st.H; }
-        if (U == 0) {
-            // the strip above's count, then the next group's ring record
-            // (speculative, ring_catch_up); issued after the first step, so
-            // that the wait for this group's record (read one group ago)
-            // does not also wait for this read
-            __builtin_amdgcn_sched_barrier(0);
-            seen_v = lds_peek(in.wcnt_in);
-            asm volatile("" ::: "memory");
-            read_grp(nxt, in, sk_grp(t + 5));
-        }
     }
     // the symbols of this group's steps four groups on, into the registers
-    // just consumed (loaded after the steps, so that the loop carries them in place)
-    cc = load_codes(in, t + 16);
+    // just consumed (loaded after the steps, so that the loop carries them
+    // in place)
+    cc = load_codes(w, t + 16);
+    // hand the group's cells to the side wave (slot t/4 mod kSkHo; the side
+    // wave has read the slot's previous group: checked per sub-block)
+    {
+        v4i* hv = w.hv_sub + Q * 2 * kWave;
+        mine.v[0] = v4i{oS[0], oS[1], oS[2], oS[3]};
+        mine.v[1] = v4i{oD[0], oD[1], oD[2], oD[3]};
+        hv[0] = mine.v[0];
+        hv[kWave] = mine.v[1];
+        asm volatile("" ::: "memory");                         // (the data stores stay before the count)
+        if (Q == 3) lds_post(w.hcnt, (t >> 2) + 1);            // (per sub-block; every lane, one value; LDS keeps the order)
+    }
     // lane 63 pushes ring group (t - 60) / 4: its columns t-63 .. t-60 (before
     // this group's step 0, after steps 0, 1, 2), then the count (same wave,
     // LDS in order).  Every lane writes (lanes 0..62 into a sink), so the
     // compiler sees and counts the stores: no exec change, no branch.
-    mine.v[0] = v4i{pdd, qdd[0], qdd[1], qdd[2]};
-    mine.v[1] = v4i{psm, qsm[0], qsm[1], qsm[2]};
-    if (MODE == 0 || (t >= 64 && t - 63 <= in.m)) {           // (full groups: always inside; no consumer: the sink)
+    mine.v[2] = v4i{pdd, qdd[0], qdd[1], qdd[2]};
+    mine.v[3] = v4i{psm, qsm[0], qsm[1], qsm[2]};
+    if (MODE == 0 || (t >= 64 && t - 63 <= w.m)) {            // (full groups: always inside; no consumer: all into the sink)
         lds_v4i* a = (lds_v4i*)(uintptr_t)(w.push_base + __umul24((uint32_t)sk_grp(t - 63), w.push_m16));
-        const int cnt = (MODE == 0 ? t - 60 : min(t - 60, in.m)) + 1;   // (MODE 0: t - 60 < m)
-        a[0] = mine.v[0];
-        a[kSkRingG] = mine.v[1];
-        asm volatile("" ::: "memory");                         // (the data stores stay before the count)
+        const int cnt = (MODE == 0 ? t - 60 : min(t - 60, w.m)) + 1;   // (MODE 0: t - 60 < m; 2, 3: the ramp-down)
+        a[0] = mine.v[2];
+        a[kSkRingG] = mine.v[3];
+        asm volatile("" ::: "memory");
         lds_post(w.pcnt, cnt);
     }
-    ring_catch_up(nxt, in, seen_v, need, t);
+    if (__builtin_amdgcn_readfirstlane(seen_v) < need) {       // the strip above was behind: wait, re-read
+        w.tr_win += wait_ge_tight(w.wcnt_in, need, w.status);
+        // re-read into the same registers and wait for it here (one asm: no
+        // copies on the fast path, nothing pending after the join)
+        const uint32_t a = w.rd_base + __umul24((uint32_t)sk_grp(t + 5), w.rd_m16);
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:%3\n\ts_waitcnt lgkmcnt(0)"
+                     : "+v"(nxt[0]), "+v"(nxt[1])
+                     : "v"(a), "i"(kSkRingG * 16)
+                     : "memory");
+    }
     pin(prev);
     __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool LOCAL, bool TBL, int MODE>
-__device__ __forceinline__ void core_sub(CoreState& st, StripLoop& L, CorePend (&pd)[2], CoreCtx& w,
-                                         const Scores32& sc, const int t0, const int T, const bool trace) {
-    // ring space below: both readers of the strip below have read what these
-    // pushes overwrite (the last group pushes columns up to t0 + 12 - 60)
-    const int last_col = min(t0 - 48, w.in.m);
+struct CoreLoop {                 // the core wave's loop-carried state besides CoreState
+    v4i ra[2], rb[2];            // ring groups (current / next), alternating
+    int4 cc[4];                  // column symbols of the next four groups
+    CorePend pa, pb;             // pinned store data, alternating
+    long long tr_q[kTraceQ];     // (diagnostics: timeline stamps)
+};
+
+// One 16-step sub-block: flow control, then four groups.
+template <bool LOCAL, bool TBL, int MODE, bool TRACE>
+__device__ __forceinline__ void core_sub(CoreState& st, CoreLoop& L, CoreCtx& w, const Scores32& sc, const int t0,
+                                         const int T, const bool trace) {
+    // ring space below: the strip below has read what these pushes
+    // overwrite (the last group pushes columns up to t0 + 12 - 60); hand-off
+    // space: the side wave has read this sub-block's slots' previous groups.
+    // Both checked against counts read one sub-block ago, so that no LDS
+    // round trip is waited for unless those fall short (the ring holds 256
+    // columns, the strip below reads ~72 behind; the side keeps up).
+    const int last_col = min(t0 - 48, w.m);
     if (w.push_on && last_col >= kSkRingG * 4 - 4) {
         const int v = last_col - (kSkRingG * 4 - 4) + 1;
-        wait_ge(w.rcnt_out, v, w.in.status);
-        wait_ge(w.rcnt2_out, v, w.in.status);
+        if (w.space_out < v) wait_ge(w.rcnt_out, v, w.status);
     }
-    if (trace) {
+    if (t0 >= 4 * kSkHo) {
+        const int v = (t0 >> 2) + 4 - kSkHo;
+        if (w.space_ho < v) w.tr_ho += wait_ge(w.bcnt, v, w.status);
+    }
+    if (w.push_on) w.space_out = lds_peek(w.rcnt_out);
+    w.space_ho = lds_peek(w.bcnt);
+    w.hv_sub = (v4i*)&w.ho->v[(t0 >> 2) & (kSkHo - 1)][0][w.lane];
+    if (TRACE && trace) {
         const int q = (int)((long long)t0 * (kTraceQ + 1) / T) - 1;
         const long long now = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
         for (int k = 0; k < kTraceQ; ++k)   // (constant indices: the stamps stay in registers)
             if (k >= 1 && k == q && L.tr_q[k] == 0) L.tr_q[k] = now;
         if (t0 == kWave) L.tr_q[0] = now;                  // (the end of the ramp-up)
-        if ((t0 & 1023) == 0 && (t0 >> 10) < kTraceTL && w.in.lane == 0) {
+        if ((t0 & 1023) == 0 && (t0 >> 10) < kTraceTL && w.lane == 0) {
             w.tl[t0 >> 10] = now;
             w.tl[kTraceTL + (t0 >> 10)] = __builtin_amdgcn_s_memtime();   // (StripTrace.tc follows tl)
         }
     }
-    core_group<LOCAL, TBL, MODE>(st, L.ra, L.rb, L.cc[0], w, sc, t0, pd[0], pd[1]);
-    core_group<LOCAL, TBL, MODE>(st, L.rb, L.ra, L.cc[1], w, sc, t0 + 4, pd[1], pd[0]);
-    core_group<LOCAL, TBL, MODE>(st, L.ra, L.rb, L.cc[2], w, sc, t0 + 8, pd[0], pd[1]);
-    core_group<LOCAL, TBL, MODE>(st, L.rb, L.ra, L.cc[3], w, sc, t0 + 12, pd[1], pd[0]);
+    core_group<LOCAL, TBL, MODE, 0>(st, L.ra, L.rb, L.cc[0], w, sc, t0, L.pa, L.pb);
+    core_group<LOCAL, TBL, MODE, 1>(st, L.rb, L.ra, L.cc[1], w, sc, t0 + 4, L.pb, L.pa);
+    core_group<LOCAL, TBL, MODE, 2>(st, L.ra, L.rb, L.cc[2], w, sc, t0 + 8, L.pa, L.pb);
+    core_group<LOCAL, TBL, MODE, 3>(st, L.rb, L.ra, L.cc[3], w, sc, t0 + 12, L.pb, L.pa);
     // every ring read up to column t0+20 (incl. the next group's) was issued before this store
     asm volatile("" ::: "memory");
-    lds_post(w.in.rcnt_in, min(t0 + kSub + 5, w.in.m + 1));
+    lds_post(w.rcnt_in, min(t0 + kSub + 5, w.m + 1));
 }
 
 // TRACE: a diagnostics build (GX_TRACE_FILE).  Its stamps are scalar-memory
 // instructions, which count on lgkmcnt out of order: any that may be in
-// flight make the compiler wait for lgkmcnt(0) at every LDS use, so the
-// stamps live only in their own instantiation.
+// flight make the compiler wait for lgkmcnt(0) at every LDS use (30k pair
+// 4.0 -> 3.8 ms without them), so the stamps live in their own instantiation.
 template <bool LOCAL, bool TBL, bool TRACE>
 __device__ void core_wave(const PairDev& P, const int s, const int lane, const Scores32& sc, CoreCtx& w,
                           PairRes* pres) {
@@ -305,18 +294,41 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
     const int i = s * kWave + lane + 1;          // this lane's row
     const bool ok = i <= n;
     StripTrace* const trace = TRACE ? P.trace : nullptr;
-    StripIn& in = w.in;
-    in.m = m; in.lane = lane; in.tr_win = 0;
+    w.m = m; w.lane = lane; w.tr_win = 0; w.tr_ho = 0;
+    w.space_out = w.space_ho = 0;
     w.tl = trace ? trace[s].tl : nullptr;
-    in.c1 = ok ? (int)P.c1[i - 1] : 0x1FF;       // 0x1FF never equals a byte
-    if (TBL) in.c1 = score_table(in.c1, sc);
+    w.c1 = ok ? (int)P.c1[i - 1] : 0x1FF;        // 0x1FF never equals a byte
+    // column 0 (algo.rs:204-211): I = S = neg_inf, D = h + i g, score_max
+    // max(D, floor); global fills hold V - (i + 0) g
+    // Global fills: lane l >= 1 starts at step 0 on virtual columns 1 - l .. 0
+    // (no per-lane masks in the ramp-up).  Its state starts at "minus
+    // infinity", so virtual columns < 0 stay there and column 0 comes out of
+    // the recurrence exactly: I = S = -inf, D''(i, 0) = max(D''(i-1, 0),
+    // H''(i-1, 0) + h) = h from lane l-1, score_max = D (algo.rs:204-211).
+    // Local fills keep the masked ramp-up (their 0 floor lifts virtual cells).
     CoreState st;
-    const int H0 = strip_start<LOCAL>(st, i, lane, sc);
-    in.crs = rsrc_of(uniform_ptr(P.ccodes), 4 * (m + 192));
-    in.cvoff = 4u * (uint32_t)(64 - lane);
+    int H0;                                       // score_max(i, 0) (shifted for global fills)
+    {
+        const int D0 = sc.h + i * sc.g;
+        H0 = LOCAL ? max(D0, 0) : D0 - i * sc.g;
+        const bool virt = !LOCAL && lane > 0;
+        st.I = LOCAL ? kNeg : kNeg - i * sc.g;
+        st.H = virt ? kNeg : H0;
+        st.Hx = virt ? kNeg : H0 + (LOCAL ? sc.hg : sc.h);
+        st.Dd = virt ? kNeg : H0;                 // (lane 0: the successor D''(i+1, 0) = max(h, 2h) = h)
+    }
+    {   // this lane's column inputs (skew_codes_kernel): with score tables
+        // (<= 4 symbols) the scores of its row's symbol against every column
+        // -- one of four int32 rows, so a step adds the loaded value -- else
+        // the column symbols themselves
+        const uint32_t row = 4u * (uint32_t)(m + 192);
+        const uint32_t k = TBL ? (uint32_t)sym_code(w.c1, sc) : 0u;   // (rows past n: symbol 0, never stored)
+        w.crs = rsrc_of(uniform_ptr(P.ccodes), (int)((TBL ? 4 : 1) * row));
+        w.cvoff = 4u * (uint32_t)(64 - lane) + k * row;
+    }
     if (w.push_on) {                              // column 0 of the bottom row: the next strip's first top-left
         if (lane == kWave - 1) {
-            w.rout->dd[0][3] = H0;                // (the delete successor of column 0: H0, see strip_start)
+            w.rout->dd[0][3] = H0;                // (the delete successor of column 0: H0, see above)
             w.rout->sm[0][3] = H0;
             asm volatile("" ::: "memory");
             *w.wcnt_out = 1;
@@ -324,46 +336,66 @@ __device__ void core_wave(const PairDev& P, const int s, const int lane, const S
     }
     long long tr_start = 0, tr_first = 0, clk_first = 0;
     if (trace) tr_start = __builtin_amdgcn_s_memrealtime();
-    in.tr_win += wait_ge(in.wcnt_in, min(4, m) + 1, in.status);
-    StripLoop L = {};
-    CorePend pd[2] = {};
+    w.tr_win += wait_ge(w.wcnt_in, min(4, m) + 1, w.status);
+    CoreLoop L = {};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) L.cc[q] = load_codes(in, 4 * q);
-    st.Hd = shr1(in.rin->sm[0][3], st.H);         // column 1's top-left: (64 s, 0) for lane 0, lane-1's column 0
+    for (int q = 0; q < 4; ++q) L.cc[q] = load_codes(w, 4 * q);
+    st.Hd = shr1(w.rin->sm[0][3], st.H);          // column 1's top-left: (64 s, 0) for lane 0, lane-1's column 0
     if (!LOCAL && lane > 0) st.Hd = kNeg;         // (virtual columns)
-    read_grp(L.ra, in, sk_grp(1));
+    read_grp(L.ra, w, sk_grp(1));
     if (trace) { tr_first = __builtin_amdgcn_s_memrealtime(); clk_first = __builtin_amdgcn_s_memtime(); }
     const int T = m + kWave;                      // lane 63 computes column m at step m + 62; pushes run to t = m + 63
+    // ramp-up (global: every lane steps, on virtual columns until its column
+    // 1 at step l; local: per-lane selects) while no lane passes column m;
+    // then every lane inside columns 1..m; then masked per lane.  One loop per
+    // phase, so that the loop-carried registers (ring groups, prefetched
+    // symbols, pinned store data) keep their places across the back-edge
+    // (a merge of differently allocated phases costs copies that wait for
+    // the symbol loads in flight).
     int t0 = 0;
-    if (!LOCAL)   // (virtual columns: every lane runs from step 0, see strip_start)
-        for (; t0 < T && in_ramp(t0, m); t0 += kSub) core_sub<LOCAL, TBL, 0>(st, L, pd, w, sc, t0, T, trace != nullptr);
-    for (; t0 < T && in_ramp(t0, m); t0 += kSub) core_sub<LOCAL, TBL, 2>(st, L, pd, w, sc, t0, T, trace != nullptr);
-    for (; t0 < T && in_steady(t0, m); t0 += kSub) core_sub<LOCAL, TBL, 0>(st, L, pd, w, sc, t0, T, trace != nullptr);
+    if (!LOCAL)   // (virtual columns: every lane runs from step 0, see the column-0 state above)
+        for (; t0 < T && t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1; t0 += kSub)
+            core_sub<LOCAL, TBL, 0, TRACE>(st, L, w, sc, t0, T, trace != nullptr);
+    for (; t0 < T && t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1; t0 += kSub)
+        core_sub<LOCAL, TBL, 2, TRACE>(st, L, w, sc, t0, T, trace != nullptr);
+    for (; t0 < T && t0 >= kWave && t0 + kSub - 1 <= m - 1; t0 += kSub)
+        core_sub<LOCAL, TBL, 0, TRACE>(st, L, w, sc, t0, T, trace != nullptr);
     if (!LOCAL && s + 1 < P.strips)               // (row n is in the last strip: its lane keeps column m's state)
-        for (; t0 < T; t0 += kSub) core_sub<LOCAL, TBL, 3>(st, L, pd, w, sc, t0, T, trace != nullptr);
-    for (; t0 < T; t0 += kSub) core_sub<LOCAL, TBL, 2>(st, L, pd, w, sc, t0, T, trace != nullptr);
+        for (; t0 < T; t0 += kSub)
+            core_sub<LOCAL, TBL, 3, TRACE>(st, L, w, sc, t0, T, trace != nullptr);
+    for (; t0 < T; t0 += kSub)
+        core_sub<LOCAL, TBL, 2, TRACE>(st, L, w, sc, t0, T, trace != nullptr);
     if (ok && i == n) pres->end_SM = st.H;        // score_max(n, m) (algo.rs:308, 331)
     if (trace && lane == 0) {
-        trace[s].t_start = tr_start;
-        trace[s].t_first = tr_first;
-        trace[s].t_end = __builtin_amdgcn_s_memrealtime();
-        trace[s].wait_in = (int)in.tr_win;
-        trace[s].clk = __builtin_amdgcn_s_memtime() - clk_first;
-        for (int q = 0; q < kTraceQ - 2; ++q) trace[s].t_q[q] = L.tr_q[q];
+        StripTrace tr;
+        tr.t_start = tr_start; tr.t_first = tr_first; tr.t_end = __builtin_amdgcn_s_memrealtime();
+        tr.wait_in = (int)w.tr_win;
+        tr.clk = __builtin_amdgcn_s_memtime() - clk_first;
+        for (int q = 0; q < kTraceQ; ++q) tr.t_q[q] = L.tr_q[q];
+        tr.t_q[kTraceQ - 2] = w.tr_ho;            // (layout 3: hand-off space waits; the side wave writes wait_out
+        trace[s].t_start = tr.t_start;            // and the last stamp, its own waits and end)
+        trace[s].t_first = tr.t_first;
+        trace[s].t_end = tr.t_end;
+        trace[s].wait_in = tr.wait_in;
+        trace[s].clk = tr.clk;
+        for (int q = 0; q < kTraceQ - 1; ++q) trace[s].t_q[q] = tr.t_q[q];
     }
 }
 
 // ---------------------------------------------------------------------------
-// side wave: the same recurrence from the same ring (a second reader), and
-// every output -- retrace bits, landing columns, planes, skeleton, the local
-// last maximum.  Recomputing costs the side about as many VALU as it saves the
-// core in LDS stores (the core handed each group's cells over in round 4: two
-// ds_write_b128 a group on the critical path, ~9 ns of a ~60 ns step).
+// side wave
 
 struct SideState {
+    int I, H;                    // insert score and score_max of (i, j-1) (I of (i, j) follows from them)
     int E, Ed;                   // landing column + 64 of (i, j-1) and of (i-1, j-1)
     uint32_t cI, cD;
     int lbest, lstep, lE;        // LOCAL: the row's last max of score_max (algo.rs:310-322)
+    // TRACK: max_matches of (i, j-1) and (i-1, j-1) (algo.rs:113-121, 250-256)
+    // and the row's FIRST maximum of score_max (algo.rs:258-262: strict <),
+    // held as thr = best - (i + j) g at the current column j for shifted
+    // (global) fills, so that a step compares its shifted value directly
+    int M, Md;
+    int thr, bstep, bl;
 };
 
 // Retrace bits and landing column of cell (i, j) from its I, S, D.
@@ -396,46 +428,98 @@ __device__ __forceinline__ void side_step(SideState& st, const int I, const int 
 }
 
 struct SideCtx {
-    StripIn in;
+    SkHo* ho;
+    lds_int* hcnt;
+    lds_int* bcnt;
+    int* status;
     uint32_t* codes;
     __amdgpu_buffer_rsrc_t rI, rD, rS;   // the strip's planes (offset in the VGPR; see gx_device.h bstore4)
     __amdgpu_buffer_rsrc_t skel_rsrc;    // skeleton row of this strip (bottom-row E + 64)
     uint32_t skel_voff;                  // lane 63: 0; other lanes: out of range
+    int m, lane;
+    int h, g, hg;                        // gap open / extend (global fills: shifted, g folded: g = 0)
+    unsigned tr_wait;                    // (diagnostics: spins waiting for the core wave)
     long long* ts;                       // (diagnostics: the side's dense timeline, StripTrace.ts)
+    // TRACK: the LCS rings (the strip above's side pushes its bottom row's
+    // values, lane 63 per 4-column group, as the core pushes dd / sm) and
+    // this lane's column symbols (PairDev.ccodes, raw bytes: tracked fills
+    // keep no score table)
+    uint32_t mrd_base, mrd_m16;          // LDS; lane 0: the ring above's m[0]; other lanes: the zero block
+    uint32_t mpush_base, mpush_m16;      // LDS; lane 63: the ring below's m[0]; other lanes / no consumer: a sink
+    lds_int* mw_in;                      // LCS columns the strip above published
+    lds_int* mr_in;                      // ... and this side has read
+    lds_int* mw_out;                     // (no consumer: a sink)
+    lds_int* mr_out;
+    bool mpush_on;
+    __amdgpu_buffer_rsrc_t crs;          // the column symbols
+    uint32_t cvoff;
+    int c1;                              // this row's symbol
+    int gs;                              // the shift per column of the tracked values (global: g; local: 0)
 };
 
-// One 4-step group of the side wave.  MODE 0: every lane inside columns
-// 1..m; 1 (global ramp-up): the recurrence runs every lane (virtual columns,
-// as the core), the landing columns only the lanes past column 0; 2: both
-// per lane (the recurrence as the core's MODE 2).
-template <bool LOCAL, bool TBL, bool PLANES, int MODE>
-__device__ __forceinline__ void side_group(CoreState& st, SideState& ss, const v4i (&cur)[2], v4i (&nxt)[2],
-                                           int4& cc, SideCtx& w, const Scores32& sc, const int t) {
-    StripIn& in = w.in;
-    const int need = min(t + 8, in.m) + 1;
-    int aI[4], aS[4], aD[4], e[4], seen_v = 0;
-    const int c2[4] = {cc.x, cc.y, cc.z, cc.w};
+// I(i, j) from the row's previous cell, as the core computes it (the core
+// hands over only S and D, one ds_write_b128 fewer per group on its path):
+// global (shifted, h <= 0) max(I, H + h); local max(I + g, H + h + g, 0).
+template <bool LOCAL, bool MASKED>
+__device__ __forceinline__ int side_insert(SideState& st, const SideCtx& w, const int S, const int D, const bool act) {
+    const int In = LOCAL ? max3i(st.I + w.g, st.H + w.hg, 0) : max(st.I, st.H + w.h);
+    const int Hn = max3i(In, S, D);
+    st.I = MASKED ? (act ? In : st.I) : In;
+    st.H = MASKED ? (act ? Hn : st.H) : Hn;
+    return In;
+}
+
+// TRACK: max_matches of cell (i, j) (algo.rs:250-256: max of the left's,
+// the one above's and the top-left's + is_match) and the row's first
+// maximum of score_max (algo.rs:258-262).  mu0: lane 0's value of the row
+// above from the LCS ring (the other lanes take lane l-1's by DPP); c2 the
+// column's symbol.
+template <bool MASKED>
+__device__ __forceinline__ void track_step(SideState& st, const SideCtx& w, const int H, const int mu0, const int c2,
+                                           const int t, const bool act) {
+    const int Mu = shr1(mu0, st.M);              // max_matches(i-1, j)
+    const int Mn = max3i(st.M, Mu, st.Md + (c2 == w.c1 ? 1 : 0));
+    st.Md = Mu;
+    const int thr = st.thr - w.gs;               // best - (i + j) g at this column
+    const bool nb = act && H > thr;
+    st.thr = nb ? H : (MASKED ? (act ? thr : st.thr) : thr);
+    st.bstep = nb ? t : st.bstep;
+    st.bl = nb ? Mn : st.bl;
+    st.M = MASKED ? (act ? Mn : st.M) : Mn;
+}
+
+template <bool LOCAL, bool PLANES, int MODE, bool TRACK>
+__device__ __forceinline__ void side_group(SideState& st, SideCtx& w, const int t, const int4 (&hv)[2],
+                                           const int4 mu, const int4 cc, int4& mpush) {
+    const int g = t >> 2;
+    const int4 vS = hv[0], vD = hv[1];
+    const int aS[4] = {vS.x, vS.y, vS.z, vS.w}, aD[4] = {vD.x, vD.y, vD.z, vD.w};
+    const int am[4] = {mu.x, mu.y, mu.z, mu.w}, ac[4] = {cc.x, cc.y, cc.z, cc.w};
+    int aI[4] = {0, 0, 0, 0};
+    int e[4], qm[4];
 #pragma unroll
     for (int U = 0; U < 4; ++U) {
-        const int c = t + U - in.lane;                         // column - 1
-        const bool ract = MODE == 2 ? (LOCAL ? (unsigned)c < (unsigned)in.m : c < in.m) : true;
-        const bool sact = MODE == 0 ? true : (unsigned)c < (unsigned)in.m;
-        core_step<LOCAL, TBL, MODE == 2>(st, cur[0][U], cur[1][U], c2[U], ract, in.c1, sc, aI[U], aS[U], aD[U]);
-        side_step<LOCAL, MODE != 0>(ss, aI[U], aS[U], aD[U], t + U, sact);
-        e[U] = ss.E;   // lane 63: E + 64 of its column t+U-62
-        if (U == 0) {   // (as core_group)
-            __builtin_amdgcn_sched_barrier(0);
-            seen_v = lds_peek(in.wcnt_in);
-            asm volatile("" ::: "memory");
-            read_grp(nxt, in, sk_grp(t + 5));
+        qm[U] = st.M;  // lane 63: max_matches of its column t+U-63 (the LCS push below)
+        if (MODE == 1) {
+            if (w.lane <= t + U) {
+                aI[U] = side_insert<LOCAL, false>(st, w, aS[U], aD[U], true);
+                if (TRACK) track_step<false>(st, w, max3i(aI[U], aS[U], aD[U]), am[U], ac[U], t + U, true);
+                side_step<LOCAL, false>(st, aI[U], aS[U], aD[U], t + U, true);
+            }
+        } else {
+            const bool act = MODE == 2 ? (unsigned)(t + U - w.lane) < (unsigned)w.m : true;
+            aI[U] = side_insert<LOCAL, MODE == 2>(st, w, aS[U], aD[U], act);
+            if (TRACK) track_step<MODE == 2>(st, w, max3i(aI[U], aS[U], aD[U]), am[U], ac[U], t + U, act);
+            side_step<LOCAL, MODE == 2>(st, aI[U], aS[U], aD[U], t + U, act);
         }
+        e[U] = st.E;   // lane 63: E + 64 of its column t+U-62
     }
-    cc = load_codes(in, t + 16);
+    if (TRACK) mpush = make_int4(qm[0], qm[1], qm[2], qm[3]);
     if (PLANES) {   // the group's cells, one dwordx4 per lane and plane
-        const uint32_t vo = (uint32_t)in.lane * 16u + (uint32_t)(t >> 2) * (kGroupInts1 * 4);
+        const uint32_t vo = (uint32_t)w.lane * 16u + (uint32_t)g * (kGroupInts1 * 4);
         bstore4(w.rI, vo, make_int4(aI[0], aI[1], aI[2], aI[3]));
-        bstore4(w.rS, vo, make_int4(aS[0], aS[1], aS[2], aS[3]));
-        bstore4(w.rD, vo, make_int4(aD[0], aD[1], aD[2], aD[3]));
+        bstore4(w.rS, vo, vS);
+        bstore4(w.rD, vo, vD);
     }
     // lane 63's landing columns (+64) of its columns t-62 .. t-59: the skeleton
     const int c0 = t - (kWave - 2);
@@ -445,38 +529,46 @@ __device__ __forceinline__ void side_group(CoreState& st, SideState& ss, const v
 #pragma unroll
         for (int U = 0; U < 4; ++U) {
             const int c = c0 + U;
-            skel_store(w.skel_rsrc, (c >= 1 && c <= in.m) ? w.skel_voff + 4u * (uint32_t)c : kSkelOff, e[U]);
+            skel_store(w.skel_rsrc, (c >= 1 && c <= w.m) ? w.skel_voff + 4u * (uint32_t)c : kSkelOff, e[U]);
         }
     }
-    ring_catch_up(nxt, in, seen_v, need, t);
-    __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool LOCAL, bool TBL, bool PLANES, int MODE, bool TRACE>
-__device__ __forceinline__ void side_sub(CoreState& st, SideState& ss, StripLoop& L, SideCtx& w, const Scores32& sc,
-                                         const int t0) {
-    if (TRACE && w.ts && (t0 & 1023) == 0 && (t0 >> 10) < kTraceTL && w.in.lane == 0) w.ts[t0 >> 10] = __builtin_amdgcn_s_memrealtime();
-    side_group<LOCAL, TBL, PLANES, MODE>(st, ss, L.ra, L.rb, L.cc[0], w, sc, t0);
-    side_group<LOCAL, TBL, PLANES, MODE>(st, ss, L.rb, L.ra, L.cc[1], w, sc, t0 + 4);
-    side_group<LOCAL, TBL, PLANES, MODE>(st, ss, L.ra, L.rb, L.cc[2], w, sc, t0 + 8);
-    side_group<LOCAL, TBL, PLANES, MODE>(st, ss, L.rb, L.ra, L.cc[3], w, sc, t0 + 12);
-    // codes[strip][t/16][lane]
-    gstore1(w.codes + (size_t)(t0 >> 4) * kWave + w.in.lane, (ss.cD << 16) | (ss.cI & 0xFFFFu));
-    asm volatile("" ::: "memory");
-    lds_post(w.in.rcnt_in, min(t0 + kSub + 5, w.in.m + 1));
+// One side group with its LCS traffic (TRACK): wait for and read the row
+// above's LCS values of the group's columns (lane 0: t+1 .. t+4), step, then
+// lane 63 pushes its columns t-63 .. t-60 and posts both counts.  Per group,
+// so that the sides' chain of LCS values lags no more per strip than the
+// cores' chain (a side waits for its core's sub-blocks; a longer lag would
+// accumulate strip by strip and stall the cores on hand-off space).
+template <bool LOCAL, bool PLANES, int MODE, bool TRACK>
+__device__ __forceinline__ void side_track_group(SideState& st, SideCtx& w, const int t, const int4 (&hv)[2],
+                                                 const int4 cc) {
+    int4 mu = make_int4(0, 0, 0, 0), mp;
+    if (TRACK) {
+        w.tr_wait += wait_ge(w.mw_in, min(t + 4, w.m) + 1, w.status);
+        const lds_v4i* a = (const lds_v4i*)(uintptr_t)(w.mrd_base + __umul24((uint32_t)sk_grp(t + 1), w.mrd_m16));
+        const v4i x = *a;
+        mu = make_int4(x[0], x[1], x[2], x[3]);
+        asm volatile("" ::: "memory");
+        lds_post(w.mr_in, min(t + 5, w.m + 1));
+    }
+    side_group<LOCAL, PLANES, MODE, TRACK>(st, w, t, hv, mu, cc, mp);
+    if (TRACK && t >= 64 && t - 63 <= w.m) {
+        lds_v4i* a = (lds_v4i*)(uintptr_t)(w.mpush_base + __umul24((uint32_t)sk_grp(t - 63), w.mpush_m16));
+        *a = v4i{mp.x, mp.y, mp.z, mp.w};
+        asm volatile("" ::: "memory");
+        lds_post(w.mw_out, min(t - 60, w.m) + 1);
+    }
 }
 
-template <bool LOCAL, bool TBL, bool PLANES, bool TRACE>
-__device__ void side_wave(const PairDev& P, const int s, const int lane, const Scores32& sc, SideCtx& w,
-                          const bool has_consumer, StripRes* sres, PairRes* pres) {
+template <bool LOCAL, bool PLANES, bool TRACE, bool TRACK>
+__device__ void side_wave(const PairDev& P, const int s, const int lane, SideCtx& w, const bool has_consumer,
+                          StripRes* sres, PairRes* pres) {
     const int n = P.n, m = P.m;
     const int i = s * kWave + lane + 1;
     const bool ok = i <= n;
-    StripIn& in = w.in;
-    in.m = m; in.lane = lane; in.tr_win = 0;
+    w.m = m; w.lane = lane; w.tr_wait = 0;
     w.ts = TRACE && P.trace ? P.trace[s].ts : nullptr;
-    in.c1 = ok ? (int)P.c1[i - 1] : 0x1FF;
-    if (TBL) in.c1 = score_table(in.c1, sc);
     if (PLANES) {
         const size_t strip_planes = (size_t)s * P.t4 * kGroupInts1;
         const int pbytes = P.t4 * kGroupInts1 * 4;   // one strip's plane
@@ -487,46 +579,121 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, const S
     w.codes = P.codes + (size_t)s * P.t16 * kWave;
     w.skel_rsrc = rsrc_of(uniform_ptr(P.skel + (size_t)s * P.skel_stride), has_consumer ? 4 * (m + 1) : 0);
     w.skel_voff = lane == kWave - 1 ? 0u : kSkelOff;
-    CoreState st;
-    (void)strip_start<LOCAL>(st, i, lane, sc);
-    SideState ss;
-    ss.E = 64 - (lane + 1);                       // column 0: the path reaches it at local row lane + 1
-    ss.Ed = shr1(64, ss.E);                       // column 1's top-left: (64 s, 0) for lane 0
-    ss.cI = 0; ss.cD = 0;
-    ss.lbest = ok ? INT_MIN : INT_MAX; ss.lstep = 0; ss.lE = 0;
-    in.crs = rsrc_of(uniform_ptr(P.ccodes), 4 * (m + 192));
-    in.cvoff = 4u * (uint32_t)(64 - lane);
-    in.tr_win += wait_ge(in.wcnt_in, min(4, m) + 1, in.status);
-    StripLoop L = {};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) L.cc[q] = load_codes(in, 4 * q);
-    st.Hd = shr1(in.rin->sm[0][3], st.H);
-    if (!LOCAL && lane > 0) st.Hd = kNeg;
-    read_grp(L.ra, in, sk_grp(1));
+    SideState st;
+    {   // column 0 (algo.rs:204-211), as the core starts it (core_wave)
+        const int D0 = w.h + i * w.g;
+        st.H = LOCAL ? max(D0, 0) : w.h;          // (global: shifted, D0 - i g = h)
+        st.I = LOCAL ? kNeg : kNeg - i * w.g;
+    }
+    st.E = 64 - (lane + 1);                       // column 0: the path reaches it at local row lane + 1
+    st.Ed = shr1(64, st.E);                       // column 1's top-left: (64 s, 0) for lane 0
+    st.cI = 0; st.cD = 0;
+    st.lbest = ok ? INT_MIN : INT_MAX; st.lstep = 0; st.lE = 0;
+    // TRACK: column 0 matches nothing (algo.rs:204-211: *_matches = 0); no maximum yet
+    // (INT_MIN + 2^29: the thresholds drift by (n + m) |g| < 2^28 and stay below every value)
+    st.M = 0; st.Md = 0;
+    st.thr = INT_MIN + (1 << 29); st.bstep = 0; st.bl = 0;
+    if (TRACK) {
+        w.c1 = ok ? (int)P.c1[i - 1] : 0x1FF;
+        w.crs = rsrc_of(uniform_ptr(P.ccodes), 4 * (m + 192));
+        w.cvoff = 4u * (uint32_t)(64 - lane);
+        if (w.mpush_on && lane == kWave - 1) {   // column 0 of the bottom row
+            ((lds_int*)(uintptr_t)w.mpush_base)[3] = 0;
+            asm volatile("" ::: "memory");
+            *w.mw_out = 1;
+        }
+    }
     const int T = m + kWave;
-    int t0 = 0;
-    if (!LOCAL)
-        for (; t0 < T && in_ramp(t0, m); t0 += kSub) side_sub<LOCAL, TBL, PLANES, 1, TRACE>(st, ss, L, w, sc, t0);
-    for (; t0 < T && in_ramp(t0, m); t0 += kSub) side_sub<LOCAL, TBL, PLANES, 2, TRACE>(st, ss, L, w, sc, t0);
-    for (; t0 < T && in_steady(t0, m); t0 += kSub) side_sub<LOCAL, TBL, PLANES, 0, TRACE>(st, ss, L, w, sc, t0);
-    for (; t0 < T; t0 += kSub) side_sub<LOCAL, TBL, PLANES, 2, TRACE>(st, ss, L, w, sc, t0);
+    int4 cc4[4] = {};
+    if (TRACK) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const v4i y = __builtin_amdgcn_raw_buffer_load_b128(w.crs, (int)w.cvoff, 16 * q, 0);
+            cc4[q] = make_int4(y[0], y[1], y[2], y[3]);
+        }
+    }
+    for (int t0 = 0; t0 < T; t0 += kSub) {
+        if (TRACE && w.ts && (t0 & 1023) == 0 && (t0 >> 10) < kTraceTL && lane == 0)
+            w.ts[t0 >> 10] = __builtin_amdgcn_s_memrealtime();
+        // TRACK: this lane's column symbols of the next sub-block (loaded one
+        // sub-block ahead), ring space below for this sub-block's LCS pushes
+        // (the last group pushes columns up to t0 + 12 - 60)
+        int4 cnx[4] = {};
+        if (TRACK) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const v4i y = __builtin_amdgcn_raw_buffer_load_b128(w.crs, (int)w.cvoff,
+                                                                    __builtin_amdgcn_readfirstlane(4 * (t0 + kSub + 4 * q)), 0);
+                cnx[q] = make_int4(y[0], y[1], y[2], y[3]);
+            }
+            const int last_col = min(t0 - 48, m);
+            if (w.mpush_on && last_col >= kSkRingG * 4 - 4)
+                wait_ge(w.mr_out, last_col - (kSkRingG * 4 - 4) + 1, w.status);
+        }
+        // the core publishes whole sub-blocks: read all four groups at once
+        w.tr_wait += wait_ge(w.hcnt, (t0 >> 2) + 4, w.status);
+        int4 sub[4][2];
+        {
+            const int4* hv = &w.ho->v[(t0 >> 2) & (kSkHo - 1)][0][lane];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) sub[q][k] = hv[(2 * q + k) * kWave];
+        }
+        asm volatile("" ::: "memory");
+        lds_post(w.bcnt, (t0 >> 2) + 4);          // (reads issued first: LDS keeps the order)
+        if (t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) side_track_group<LOCAL, PLANES, 1, TRACK>(st, w, t0 + 4 * q, sub[q], cc4[q]);
+        } else if (t0 >= kWave && t0 + kSub - 1 <= m - 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) side_track_group<LOCAL, PLANES, 0, TRACK>(st, w, t0 + 4 * q, sub[q], cc4[q]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) side_track_group<LOCAL, PLANES, 2, TRACK>(st, w, t0 + 4 * q, sub[q], cc4[q]);
+        }
+        if (TRACK) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) cc4[q] = cnx[q];
+        }
+        // codes[strip][t/16][lane]
+        gstore1(w.codes + (size_t)(t0 >> 4) * kWave + lane, (st.cD << 16) | (st.cI & 0xFFFFu));
+    }
+    int fbest = INT_MIN, fi = 0, fj = 0, fl = 0;
+    if (TRACK) {   // the strip's first max in row-major order: the lowest lane (earliest row) holding the largest
+        const int best = ok ? st.thr + (LOCAL ? 0 : (i + m) * w.gs) : INT_MIN;   // (the threshold at column m, unshifted)
+        int mx = best;
+        for (int off = 32; off > 0; off >>= 1) mx = max(mx, __shfl_xor(mx, off));
+        const unsigned long long fmask = __ballot(ok && best == mx);
+        const int fl_ = fmask ? (int)__builtin_ctzll(fmask) : 0;
+        fbest = mx; fi = s * kWave + fl_ + 1;
+        fj = __shfl(st.bstep, fl_) - fl_ + 1;
+        fl = __shfl(st.bl, fl_);
+    }
+    if (TRACK && !LOCAL && lane == 0) {
+        StripRes r{};
+        r.best = fbest; r.bi = fi; r.bj = fj; r.bl = fl;
+        r.lbest = INT_MIN;
+        sres[P.strip_base + s] = r;
+    }
     if (LOCAL) {   // the strip's last max: the highest lane (latest row) holding it
-        const int lb = ok ? ss.lbest : INT_MIN;
+        const int lb = ok ? st.lbest : INT_MIN;
         int lmx = lb;
         for (int off = 32; off > 0; off >>= 1) lmx = max(lmx, __shfl_xor(lmx, off));
         const unsigned long long lmask = __ballot(ok && lb == lmx);
         const int ll = lmask ? (63 - __clzll((long long)lmask)) : 0;
-        const int l_step = __shfl(ss.lstep, ll), l_E = __shfl(ss.lE, ll);
+        const int l_step = __shfl(st.lstep, ll), l_E = __shfl(st.lE, ll);
         if (lane == 0) {
             StripRes r{};
             r.best = INT_MIN;
+            if (TRACK) { r.best = fbest; r.bi = fi; r.bj = fj; r.bl = fl; }
             r.lbest = lmx; r.li = s * kWave + ll + 1; r.lj = l_step - ll + 1; r.lE = l_E - 64;
             sres[P.strip_base + s] = r;
         }
     }
-    if (ok && i == n) pres->end_E = ss.E - 64;   // landing column of cell (n, m)
+    if (ok && i == n) pres->end_E = st.E - 64;   // landing column of cell (n, m)
     if (TRACE && P.trace && lane == 0) {
-        P.trace[s].wait_out = (int)in.tr_win;
+        P.trace[s].wait_out = (int)w.tr_wait;
         P.trace[s].t_q[kTraceQ - 1] = __builtin_amdgcn_s_memrealtime();
     }
 }
@@ -545,19 +712,69 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, const S
 // (gx_api.cpp run_fill), so a granule is valid exactly once it was written by
 // this launch.  Stores and loads are 8-byte agent-scope (sc1: write-through,
 // L1 bypass).
-template <bool TBL>
+// TRACK: the LCS values of the bottom row travel the same way, one more
+// granule per column (the low word, valid bit 63) in the second half of the
+// band's feed row (a feed row holds 2 feed_stride granules, feed_stride > m).
+struct IoLcs {
+    SkMRing* ring0;
+    const SkMRing* ringW;
+    lds_int *mw0, *mr0, *mwW, *mrW;
+};
+template <bool TBL, bool TRACK>
 __device__ void io_wave_tag(const PairDev& P, const int lb, const int lane, const Scores32& sc, SkRing* ring0,
-                            const SkRing* ringW, lds_int* wcnt0, lds_int* rcnt0, lds_int* rcnt0b, lds_int* wcntW,
-                            lds_int* rcntW, lds_int* rcntWb, const bool do_out, int* status) {
+                            const SkRing* ringW, lds_int* wcnt0, lds_int* rcnt0, lds_int* wcntW, lds_int* rcntW,
+                            const bool do_out, int* status, const IoLcs& lc) {
     const int m = P.m;
     int in_next = 0, out_next = 0;
+    int min_next = TRACK ? 0 : m + 1, mout_next = TRACK ? 0 : m + 1;
     const gu64* feed_in = lb > 0 ? (const gu64*)(P.feed + (size_t)(lb - 1) * P.feed_stride) : nullptr;
     gu64* feed_out = do_out ? (gu64*)(P.feed + (size_t)lb * P.feed_stride) : nullptr;
     unsigned idle = 0;
-    while (in_next <= m || (do_out && out_next <= m)) {
+    while (in_next <= m || (do_out && out_next <= m) || min_next <= m || (do_out && mout_next <= m)) {
         bool moved = false;
+        if (TRACK && min_next <= m) {   // row 0's max_matches are 0 (algo.rs:213-220)
+            const int lim = min(m + 1, *lc.mr0 + kSkRingG * 4 - 4);
+            const int j = min_next + lane;
+            int v = 0;
+            bool valid = false;
+            if (j < lim) {
+                if (lb == 0) {
+                    valid = true;
+                } else {
+                    const unsigned long long gr =
+                        __hip_atomic_load(feed_in + P.feed_stride + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    valid = (gr >> 63) != 0;
+                    v = (int)(unsigned)gr;
+                }
+            }
+            const unsigned long long vm = __ballot(valid);
+            const int cnt = ~vm ? (int)__builtin_ctzll(~vm) : kWave;
+            if (cnt > 0) {
+                if (lane < cnt) lc.ring0->m[sk_grp(j)][sk_pos(j)] = v;
+                lds_wait();
+                if (lane == 0) *lc.mw0 = min_next + cnt;
+                min_next += cnt;
+                moved = true;
+            }
+        }
+        if (TRACK && do_out && mout_next <= m) {
+            const int chunk = min(*lc.mwW - mout_next, kWave);
+            if (chunk > 0) {
+                const int j = mout_next + lane;
+                int v = 0;
+                if (lane < chunk) v = lc.ringW->m[sk_grp(j)][sk_pos(j)];
+                lds_wait();
+                if (lane == 0) *lc.mrW = mout_next + chunk;
+                if (lane < chunk)
+                    __hip_atomic_store((gu64*)(feed_out + P.feed_stride + j),
+                                       (unsigned long long)(unsigned)v | (1ull << 63), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                mout_next += chunk;
+                moved = true;
+            }
+        }
         if (in_next <= m) {
-            const int lim = min(m + 1, min(*rcnt0, *rcnt0b) + kSkRingG * 4 - 4);   // ring slots both its readers have read
+            const int lim = min(m + 1, *rcnt0 + kSkRingG * 4 - 4);   // ring slots the strip has read
             const int j = in_next + lane;
             int dd = 0, sm = 0;
             bool valid = false;
@@ -600,7 +817,7 @@ __device__ void io_wave_tag(const PairDev& P, const int lb, const int lane, cons
                 int dd = 0, sm = 0;
                 if (lane < chunk) { dd = ringW->dd[sk_grp(j)][sk_pos(j)]; sm = ringW->sm[sk_grp(j)][sk_pos(j)]; }
                 lds_wait();
-                if (lane == 0) { *rcntW = out_next + chunk; *rcntWb = out_next + chunk; }   // ring slots free again
+                if (lane == 0) *rcntW = out_next + chunk;   // ring slots free again
                 if (lane < chunk) {
                     const unsigned long long gr = (unsigned long long)(unsigned)sm |
                                                   ((unsigned long long)(0x80000000u | ((unsigned)(dd - sm) & 0x7FFFFFFFu)) << 32);
@@ -630,26 +847,27 @@ __device__ void io_wave_tag(const PairDev& P, const int lb, const int lane, cons
 // I/O wave, which polls, shares one with a side wave); at W = 3 two core
 // waves share a SIMD with other waves.  Persistent workgroups take bands from the
 // host's band-major queue (gx_api.cpp run_fill), as fill_kernel does.
-// Ring k (k = 0 .. W) sits above strip k of the band: written by the strip
-// above's core wave (ring 0: the I/O wave), read by strip k's core and side
-// waves (ring W: by the I/O wave), each reader with its own read count.
-template <int W, bool LOCAL, bool PLANES, bool TBL, bool TRACE>
+template <int W, bool LOCAL, bool PLANES, bool TBL, bool TRACE, bool TRACK>
 __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const PairDev* __restrict__ pairs,
                                                                            const int npairs, const int total_bands,
                                                                            int* band_counter, StripRes* sres,
                                                                            PairRes* pres, const Scores32 sc) {
     __shared__ SkRing rings[W + 1];
-    __shared__ int wcnt[W + 1], rcnt[W + 1], rcnt2[W + 1];
+    __shared__ SkHo ho[W];
+    __shared__ int wcnt[W + 1], rcnt[W + 1], hcnt[W], bcnt[W];
+    __shared__ SkMRing mrings[TRACK ? W + 1 : 1];   // TRACK: the LCS rings (side to side)
+    __shared__ int mw[W + 1], mr[W + 1];
     __shared__ int band_sh;
     __shared__ int4 push_sink[2 * kWave];          // the core waves' lanes 0..62 push here (core_group)
     __shared__ int push_sink_cnt;
-    __shared__ int4 zero_blk[kSkRingG + 1];        // ... and both waves' lanes 1..63 read [0] and [64] (read_grp)
+    __shared__ int4 zero_blk[kSkRingG + 1];        // ... and their lanes 1..63 read [0] and [64] (read_grp)
     if (threadIdx.x <= kSkRingG) zero_blk[threadIdx.x] = make_int4(0, 0, 0, 0);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int lane = threadIdx.x & (kWave - 1);
     for (;;) {
         if (threadIdx.x == 0) band_sh = atomicAdd(band_counter, 1);
-        if (threadIdx.x < W + 1) { wcnt[threadIdx.x] = 0; rcnt[threadIdx.x] = 0; rcnt2[threadIdx.x] = 0; }
+        if (threadIdx.x < W + 1) { wcnt[threadIdx.x] = 0; rcnt[threadIdx.x] = 0; mw[threadIdx.x] = 0; mr[threadIdx.x] = 0; }
+        if (threadIdx.x < W) { hcnt[threadIdx.x] = 0; bcnt[threadIdx.x] = 0; }
         __syncthreads();
         const int b = __builtin_amdgcn_readfirstlane(band_sh);
         if (b >= total_bands) return;
@@ -661,52 +879,72 @@ __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const
         const int s = lb * W + k;
         const bool has_consumer = k == W - 1 ? (lb + 1 < P.bands) : (s + 1 < P.strips);
         if (wave == 0) {
-            io_wave_tag<TBL>(P, lb, lane, sc, &rings[0], &rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0],
-                             (lds_int*)&rcnt2[0], (lds_int*)&wcnt[W], (lds_int*)&rcnt[W], (lds_int*)&rcnt2[W],
-                             lb + 1 < P.bands, band_counter + 1);
-        } else if (s < P.strips) {
-            StripIn in;
-            in.rin = &rings[k];
-            in.wcnt_in = (lds_int*)&wcnt[k];
-            in.status = band_counter + 1;
-            in.rd_base = lds_addr(lane == 0 ? (const void*)rings[k].dd[0] : (const void*)zero_blk);
-            in.rd_m16 = lane == 0 ? 16 : 0;
-            if (wave <= W) {
+            const IoLcs lc{&mrings[0], &mrings[TRACK ? W : 0], (lds_int*)&mw[0], (lds_int*)&mr[0], (lds_int*)&mw[W],
+                           (lds_int*)&mr[W]};
+            io_wave_tag<TBL, TRACK>(P, lb, lane, sc, &rings[0], &rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0],
+                                    (lds_int*)&wcnt[W], (lds_int*)&rcnt[W], lb + 1 < P.bands, band_counter + 1, lc);
+        } else if (wave <= W) {
+            if (s < P.strips) {
                 CoreCtx w;
-                w.in = in;
-                w.in.rcnt_in = (lds_int*)&rcnt[k];
-                w.rout = &rings[k + 1];
-                w.wcnt_out = (lds_int*)&wcnt[k + 1];
-                w.rcnt_out = (lds_int*)&rcnt[k + 1];
-                w.rcnt2_out = (lds_int*)&rcnt2[k + 1];
+                w.rin = &rings[k]; w.rout = &rings[k + 1];
+                w.wcnt_in = (lds_int*)&wcnt[k]; w.rcnt_in = (lds_int*)&rcnt[k];
+                w.wcnt_out = (lds_int*)&wcnt[k + 1]; w.rcnt_out = (lds_int*)&rcnt[k + 1];
+                w.ho = &ho[k]; w.hcnt = (lds_int*)&hcnt[k]; w.bcnt = (lds_int*)&bcnt[k];
+                w.status = band_counter + 1;
                 w.push_on = has_consumer;
                 const bool pl = has_consumer && lane == kWave - 1;
                 w.push_base = lds_addr(pl ? (const void*)rings[k + 1].dd[0] : (const void*)&push_sink[lane]);
                 w.push_m16 = pl ? 16 : 0;
                 w.pcnt = has_consumer ? w.wcnt_out : (lds_int*)&push_sink_cnt;
+                w.rd_base = lds_addr(lane == 0 ? (const void*)rings[k].dd[0] : (const void*)zero_blk);
+                w.rd_m16 = lane == 0 ? 16 : 0;
                 core_wave<LOCAL, TBL, TRACE>(P, s, lane, sc, w, pres + p);
-            } else {
+            }
+        } else {
+            if (s < P.strips) {
                 SideCtx w;
-                w.in = in;
-                w.in.rcnt_in = (lds_int*)&rcnt2[k];
-                side_wave<LOCAL, TBL, PLANES, TRACE>(P, s, lane, sc, w, has_consumer, sres, pres + p);
+                w.ho = &ho[k]; w.hcnt = (lds_int*)&hcnt[k]; w.bcnt = (lds_int*)&bcnt[k];
+                w.status = band_counter + 1;
+                w.h = sc.h; w.g = sc.g; w.hg = sc.hg;
+                if (TRACK) {
+                    const int kk = TRACK ? k : 0;
+                    w.mrd_base = lds_addr(lane == 0 ? (const void*)mrings[kk].m[0] : (const void*)zero_blk);
+                    w.mrd_m16 = lane == 0 ? 16 : 0;
+                    w.mpush_on = has_consumer;
+                    const bool pl = has_consumer && lane == kWave - 1;
+                    w.mpush_base = lds_addr(pl ? (const void*)mrings[kk + 1].m[0] : (const void*)&push_sink[lane]);
+                    w.mpush_m16 = pl ? 16 : 0;
+                    w.mw_in = (lds_int*)&mw[k]; w.mr_in = (lds_int*)&mr[k];
+                    w.mw_out = has_consumer ? (lds_int*)&mw[k + 1] : (lds_int*)&push_sink_cnt;
+                    w.mr_out = (lds_int*)&mr[k + 1];
+                    w.gs = LOCAL ? 0 : sc.g;   // (global fills hold V - (i + j) g)
+                }
+                side_wave<LOCAL, PLANES, TRACE, TRACK>(P, s, lane, w, has_consumer, sres, pres + p);
             }
         }
         __syncthreads();
     }
 }
 
-// The column symbols of every pair as int32, 64 zeros on each side (the
-// steps where a lane is outside columns 1..m read them): index j - 1 + 64
-// holds s2[j-1], or its symbol code * 8 with score tables (Scores32.sym).
+// The column inputs of every pair as int32 rows of m + 192, 64 zeros before
+// and 128 after (the steps where a lane is outside columns 1..m read them):
+// index j - 1 + 64 holds s2[j-1], or with score tables (<= 4 symbols) four
+// such rows, row k the score of symbol k (Scores32.sym) against s2[j-1]
+// (sequence.rs:113-114; the launch's s - 2g for shifted fills).
 __global__ void skew_codes_kernel(const PairDev* __restrict__ pairs, const Scores32 sc, const int tbl) {
     const PairDev& P = pairs[blockIdx.y];
     const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (k >= P.m + 192) return;
+    const int row = P.m + 192;
+    if (k >= row) return;
     const int j = k - 64;
-    int v = 0;
-    if (j >= 0 && j < P.m) v = tbl ? sym_code(P.c2[j], sc) * 8 : (int)P.c2[j];
-    ((int*)P.ccodes)[k] = v;
+    const bool in = j >= 0 && j < P.m;
+    if (!tbl) {
+        ((int*)P.ccodes)[k] = in ? (int)P.c2[j] : 0;
+        return;
+    }
+    const int c = in ? sym_code(P.c2[j], sc) : -1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ((int*)P.ccodes)[(size_t)r * row + k] = in ? (c == r ? sc.sm : sc.smm) : 0;
 }
 hipError_t launch_skew_codes(const PairDev* d_pairs, int npairs, int mmax, Scores32 sc, bool tbl, hipStream_t st) {
     if (npairs <= 0) return hipSuccess;
@@ -715,47 +953,55 @@ hipError_t launch_skew_codes(const PairDev* d_pairs, int npairs, int mmax, Score
     return hipGetLastError();
 }
 
-template <int W, bool LOCAL, bool PLANES, bool TBL, bool TRACE>
+template <int W, bool LOCAL, bool PLANES, bool TBL, bool TRACE, bool TRACK>
 static hipError_t launch_skew_t(const PairDev* d_pairs, int npairs, int total_bands, int* d_counter, StripRes* d_sres,
                                 PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
-    hipLaunchKernelGGL((fill_skew_kernel<W, LOCAL, PLANES, TBL, TRACE>), dim3(grid), dim3((2 * W + 1) * kWave), 0, st,
-                       d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc);
+    hipLaunchKernelGGL((fill_skew_kernel<W, LOCAL, PLANES, TBL, TRACE, TRACK>), dim3(grid), dim3((2 * W + 1) * kWave), 0,
+                       st, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc);
     return hipGetLastError();
 }
 
-template <bool LO, bool PL, bool TB, bool TR, int W0, int... Ws>
+template <bool LO, bool PL, bool TB, bool TR, bool TK, int W0, int... Ws>
 static hipError_t launch_skew_w(int W, const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
                                 StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
     if (W == W0)
-        return launch_skew_t<W0, LO, PL, TB, TR>(d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc, grid, st);
+        return launch_skew_t<W0, LO, PL, TB, TR, TK>(d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc, grid,
+                                                     st);
     if constexpr (sizeof...(Ws) > 0)
-        return launch_skew_w<LO, PL, TB, TR, Ws...>(W, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc, grid,
-                                                    st);
+        return launch_skew_w<LO, PL, TB, TR, TK, Ws...>(W, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc,
+                                                        grid, st);
     return hipErrorInvalidValue;
 }
 
 // Band widths of layout 3 (must match gx_api.cpp skew_band_waves).  trace:
 // the diagnostics instantiation (PairDev.trace set; fills with planes only,
 // the others run untraced).
-hipError_t launch_fill_skew(int W, bool local, bool planes, bool tbl, bool trace, const PairDev* d_pairs, int npairs,
-                            int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
-                            hipStream_t st) {
-#define GX_SKEW_CASE(LO, PL, TB, TR)                                                                               \
-    if (local == LO && planes == PL && tbl == TB && (trace && PL) == TR)                                            \
-        return launch_skew_w<LO, PL, TB, TR, 1, 2, 3>(W, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres,  \
-                                                         sc, grid, st);
-    GX_SKEW_CASE(false, false, false, false)
-    GX_SKEW_CASE(false, false, true, false)
-    GX_SKEW_CASE(false, true, false, false)
-    GX_SKEW_CASE(false, true, true, false)
-    GX_SKEW_CASE(true, false, false, false)
-    GX_SKEW_CASE(true, false, true, false)
-    GX_SKEW_CASE(true, true, false, false)
-    GX_SKEW_CASE(true, true, true, false)
-    GX_SKEW_CASE(false, true, false, true)
-    GX_SKEW_CASE(false, true, true, true)
-    GX_SKEW_CASE(true, true, false, true)
-    GX_SKEW_CASE(true, true, true, true)
+// track: the first maximum + max_matches (alignment_table's max_cell and
+// matches_at_max, algo.rs:258-262, 279; no score tables, untraced).
+hipError_t launch_fill_skew(int W, bool local, bool planes, bool tbl, bool trace, bool track, const PairDev* d_pairs,
+                            int npairs, int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc,
+                            int grid, hipStream_t st) {
+    if (track && tbl) return hipErrorInvalidValue;
+#define GX_SKEW_CASE(LO, PL, TB, TR, TK)                                                                           \
+    if (local == LO && planes == PL && tbl == TB && (trace && PL && !track) == TR && track == TK)                   \
+        return launch_skew_w<LO, PL, TB, TR, TK, 1, 2, 3>(W, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, \
+                                                             sc, grid, st);
+    GX_SKEW_CASE(false, false, false, false, false)
+    GX_SKEW_CASE(false, false, true, false, false)
+    GX_SKEW_CASE(false, true, false, false, false)
+    GX_SKEW_CASE(false, true, true, false, false)
+    GX_SKEW_CASE(true, false, false, false, false)
+    GX_SKEW_CASE(true, false, true, false, false)
+    GX_SKEW_CASE(true, true, false, false, false)
+    GX_SKEW_CASE(true, true, true, false, false)
+    GX_SKEW_CASE(false, true, false, true, false)
+    GX_SKEW_CASE(false, true, true, true, false)
+    GX_SKEW_CASE(true, true, false, true, false)
+    GX_SKEW_CASE(true, true, true, true, false)
+    GX_SKEW_CASE(false, false, false, false, true)
+    GX_SKEW_CASE(false, true, false, false, true)
+    GX_SKEW_CASE(true, false, false, false, true)
+    GX_SKEW_CASE(true, true, false, false, true)
 #undef GX_SKEW_CASE
     return hipErrorInvalidValue;
 }

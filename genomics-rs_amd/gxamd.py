@@ -30,6 +30,7 @@ GX_TABLE_MATCHES = 2
 GX_ALIGN_MAX_CELL = 4
 GX_STAGED_PLANE_SUMS = 8
 GX_STAGED_ALTERNATE = 16   # gx.h: pass k runs the k % 2 half of the staged pairs
+GX_STAGED_KEEP_PLANES = 32   # gx.h: the last pass's planes stay on the device (gx_staged_table)
 
 # status codes (include/gx.h)
 _CODES = {0: "GX_OK", 1: "GX_EINVAL", 2: "GX_ESEQ", 3: "GX_ERANGE", 4: "GX_ENOMEM", 5: "GX_EHIP",
@@ -77,7 +78,7 @@ EXPORTED = ["gx_last_error", "gx_version", "gx_context_create", "gx_context_dest
             "gx_stage_pairs",
             "gx_run_staged", "gx_run_staged_steps", "gx_staged_plane_sums", "gx_staged_steps",
             "gx_staged_pass_results", "gx_fill_info", "gx_batch_chunks", "gx_fill_twin", "gx_fill_groups", "gx_plane_bytes_per_cell", "gx_twin_admission",
-            "gx_twin_admission_mode", "gx_plan_layout",
+            "gx_twin_admission_mode", "gx_plan_layout", "gx_staged_table",
             "gx_fasta_load",
             "gx_config_load", "gx_format_alignment", "gx_format_table"]
 
@@ -132,6 +133,7 @@ def lib():
                                     ctypes.POINTER(ctypes.c_int64)]
     L.gx_twin_admission_mode.argtypes = [ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int, ctypes.c_int64,
                                          ctypes.POINTER(ctypes.c_int64)]
+    L.gx_staged_table.argtypes = [vp, sz, ctypes.POINTER(vp)]
     L.gx_plan_layout.argtypes = [ctypes.POINTER(CScores), ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
                                  ctypes.POINTER(ctypes.c_int64), sz, ctypes.c_int, ctypes.c_int]
     L.gx_fasta_load.argtypes = [ctypes.c_char_p, vp, sz, vp, vp, vp, vp, sz, ctypes.POINTER(sz), ctypes.POINTER(sz)]
@@ -606,6 +608,7 @@ class StagedPairs:
         self.ctx = ctx or default_context()
         self.P = len(pairs)
         self._keep = [(_buf(a), _buf(b)) for a, b in pairs]
+        self._lens = [(len(a), len(b)) for a, b in pairs]
         s1p = (ctypes.c_void_p * self.P)(*[k[0][1] for k in self._keep])
         s2p = (ctypes.c_void_p * self.P)(*[k[1][1] for k in self._keep])
         n = (ctypes.c_size_t * self.P)(*[len(a) for a, _ in pairs])
@@ -613,19 +616,31 @@ class StagedPairs:
         _check(lib().gx_stage_pairs(self.ctx.ptr, s1p, n, s2p, m, self.P))
 
     def run(self, scores: Scores, is_local: bool, keep_planes: bool = True, max_cell: bool = False,
-            steps: int = 1, plane_sums: bool = False, alternate: bool = False):
+            steps: int = 1, plane_sums: bool = False, alternate: bool = False, keep: bool = False):
         """`steps` back-to-back passes (pipelined one pass deep when > 1) ->
         (the last pass's results, mean fill ms).  plane_sums: also checksum
         every pass's score planes on the device (self.plane_sums()).
         alternate: pass k runs the k % 2 half of the staged pairs
-        (GX_STAGED_ALTERNATE; the halves hold pairs of equal shapes)."""
+        (GX_STAGED_ALTERNATE; the halves hold pairs of equal shapes).
+        keep: the last pass's planes stay on the device (GX_STAGED_KEEP_PLANES)
+        for self.table(p)."""
         res = (CResult * self.P)()
         fms = ctypes.c_double(0)
         flags = ((GX_ALIGN_MAX_CELL if max_cell else 0) | (GX_STAGED_PLANE_SUMS if plane_sums else 0)
-                 | (GX_STAGED_ALTERNATE if alternate else 0))
+                 | (GX_STAGED_ALTERNATE if alternate else 0) | (GX_STAGED_KEEP_PLANES if keep else 0))
         _check(lib().gx_run_staged_steps(self.ctx.ptr, ctypes.byref(scores.c()), int(is_local), int(keep_planes),
                                          flags, int(steps), res, ctypes.byref(fms)))
         return list(res), fms.value
+
+    def table(self, pair: int) -> "AlignmentTable":
+        """Staged pair `pair`'s score planes from the last run(keep=True), as
+        an AlignmentTable (exports and checksums decode the batch format;
+        gx_staged_table).  Its alignment is self.steps(pair)."""
+        t = ctypes.c_void_p()
+        _check(lib().gx_staged_table(self.ctx.ptr, pair, ctypes.byref(t)))
+        (a, _), (b, _) = self._keep[pair]
+        n, m = self._lens[pair]
+        return AlignmentTable(t, bytes(a[:n]), bytes(b[:m]), GX_TABLE_PLANES)
 
     def plane_sums(self) -> np.ndarray:
         """uint64 [passes, pairs, 3] plane checksums of the last run(plane_sums=True)."""

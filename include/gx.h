@@ -211,6 +211,21 @@ int gx_staged_plane_sums(const gx_context* ctx, uint64_t* out, size_t cap, size_
  * set's pair indices; the other set's row of pass k is zero.  The sets must
  * fit one chunk (else GX_EINVAL).  Verification only. */
 #define GX_STAGED_ALTERNATE 16u
+/* flags bit for gx_run_staged_steps with keep_planes: the last pass's score
+ * planes stay on the device, in the format the batch launch stored them
+ * (twin plane codes 2 B/cell, compact bytes 3 B/cell or int32; DESIGN.md
+ * 4.2, 4.4), until the next staged run and the last gx_staged_table of them
+ * is freed.  One chunk only (else GX_EINVAL); such a run does not take the
+ * overlapped two-group pipeline, whose buffers alternate. */
+#define GX_STAGED_KEEP_PLANES 32u
+/* A table of staged pair `pair` from the last GX_STAGED_KEEP_PLANES run: the
+ * reference hands alignment_table's Array2 to its caller (algo.rs:172, 281),
+ * and this hands over a batch's planes the same way -- gx_table_info,
+ * gx_table_export, gx_table_export_plane, gx_table_export_rows and
+ * gx_table_plane_sums decode them to the reference's values.  Its alignment
+ * is the run's (gx_staged_steps): gx_retrace returns GX_EINVAL.  Free with
+ * gx_table_free. */
+int gx_staged_table(gx_context* ctx, size_t pair, gx_table** table_out);
 /* The alignment (AlignedSequences.alignment) of staged pair `pair` from the
  * last pass of the last gx_run_staged(_steps) call; *n_steps = its length
  * (steps may be NULL to query it). */

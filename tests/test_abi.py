@@ -233,6 +233,7 @@ def test_plan_layout(gx, local, monkeypatch):
     sc = gx.Scores(1, -2, -1, -5)
     covid, brca2 = (29903, 29882), (11382, 10346)
     assert gx.plan_layout(sc, False, [covid]) == 3
+    assert gx.plan_layout(sc, False, [covid], track=True) == 3   # (tracked fills too, since round 5)
     assert gx.plan_layout(sc, True, [brca2]) == 1
     assert gx.plan_layout(sc, local, [(64, 30000)]) == 3
     assert gx.plan_layout(sc, local, [(30000, 30000)] * 80) == 0

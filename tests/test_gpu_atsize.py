@@ -77,7 +77,8 @@ def test_large_table_plane_sums(gx, ctx, monkeypatch, case, tracked, layout):
     anti-diagonal layout, whose untracked tables keep compact byte planes;
     cs1 / cs2 = the column step as one wave per strip / as the split core +
     side waves (gx_cs2.hip, untracked fills only); skew = layout 3
-    (gx_skew.hip, untracked fills; tracked ones fall back to the column step)."""
+    (gx_skew.hip; tracked fills carry the first maximum and the LCS values in
+    the side waves)."""
     if layout == "lay0":
         monkeypatch.setenv("GX_LAYOUT", "0")
     if layout in ("cs1", "cs2"):
@@ -95,7 +96,7 @@ def test_large_table_plane_sums(gx, ctx, monkeypatch, case, tracked, layout):
     if layout in ("cs1", "cs2"):
         assert info["layout"] == (2 if layout == "cs2" and not tracked else 1), info
     if layout == "skew":
-        assert info["layout"] == (1 if tracked else 3), info
+        assert info["layout"] == 3, info   # (tracked fills too, since round 5)
     assert table.plane_sums() == [int(x) for x in c["plane_sums"]], (c["name"], info)
     if tracked:
         assert mam == c["matches_at_max"] and table.info()["max_cell"] == tuple(c["max_cell"])

@@ -60,6 +60,48 @@ def test_skew_edge_sizes(gx, ctx, oracle, launch, is_local):
                 _same(steps, r, oracle.align(a, b, t, is_local=is_local), (n, m, alpha, t))
 
 
+@pytest.mark.parametrize("is_local", [False, True], ids=["global", "local"])
+def test_skew_tracked(gx, ctx, oracle, launch, is_local):
+    """Tracked fills on layout 3 (round 5): alignment_table's max_cell -- the
+    FIRST maximum of score_max in row-major order, strict < (algo.rs:258-262)
+    -- and matches_at_max, the max_matches field there (algo.rs:250-256, 279,
+    carried by the side waves and, across bands, by the I/O waves' LCS
+    granules), with the alignment, at every edge size, two alphabets (AC:
+    dense ties between maxima), both scoring configurations."""
+    rng = random.Random(71 + is_local)
+    for n, m in SIZES:
+        for alpha in (b"ACGT", b"AC"):
+            a = bytes(rng.choice(alpha) for _ in range(n))
+            b = bytes(rng.choice(alpha) for _ in range(m))
+            for t in (CONFIG_SCORES, TEST_SCORES):
+                steps, r = gx.align_raw(a, b, gx.Scores(*t), is_local, ctx=ctx, max_cell=True)
+                assert ctx.fill_info()["layout"] == 3, ctx.fill_info()
+                o = oracle.align(a, b, t, is_local=is_local)
+                _same(steps, r, o, (n, m, alpha, t))
+                assert (r.max_cell_i, r.max_cell_j, r.matches_at_max) == (*o.max_cell, o.matches_at_max), \
+                    (n, m, alpha, t)
+
+
+def test_skew_tracked_table(gx, ctx, oracle, monkeypatch):
+    """alignment_table (the drop-in call with max_cell / matches_at_max, as
+    INTEGRATION.md binds it) on layout 3: every exported cell value and the
+    tracked outputs against the oracle, reverse_sequences both ways."""
+    monkeypatch.setenv("GX_LAYOUT", "3")
+    rng = random.Random(5)
+    for n, m, rev in ((200, 333, False), (333, 200, True), (129, 640, False)):
+        a = "".join(rng.choice("ACGT") for _ in range(n))
+        b = "".join(rng.choice("ACGT") for _ in range(m))
+        for is_local in (False, True):
+            cont = gx.SequenceContainer([gx.Sequence("a", a), gx.Sequence("b", b)])
+            table, mam = gx.alignment_table(cont, gx.Scores(*CONFIG_SCORES), is_local, rev, ctx=ctx, max_cell=True)
+            assert ctx.fill_info()["layout"] == 3, ctx.fill_info()
+            o = oracle.align(a.encode(), b.encode(), CONFIG_SCORES, is_local=is_local, rev=rev, want_planes=True)
+            assert mam == o.matches_at_max and table.info()["max_cell"] == o.max_cell, (n, m, rev, is_local)
+            for k in range(3):
+                assert np.array_equal(table.plane(k), o.planes[k]), (n, m, rev, is_local, k)
+            table.free()
+
+
 @pytest.mark.parametrize("scores,layout", [((1, -2, -1, -5), 3), ((2, -3, -2, -4), 3), ((5, -4, 0, -10), 3),
                                            ((1, -1, -1, 0), 3), ((3, 1, -1, -2), 3), ((1, -2, 1, -3), 3),
                                            ((2, -1, -1, 3), 1), ((1, -1, 0, 2), 1)])

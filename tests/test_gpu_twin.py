@@ -374,3 +374,46 @@ def test_twin_overlapped_global(gx, ctx, oracle, monkeypatch, launch_env):
             r = passes[k][p]
             assert (r.score, r.matches, r.mismatches, r.gap_extensions, r.opening_gaps, r.n_steps) == want, (p, k)
         assert _steps_list(st.steps(p)) == o.alignment(), (p, len(a), len(b))
+
+
+@pytest.mark.parametrize("variant", ["twin_codes", "byte_planes", "int32", "local_twin"])
+def test_staged_table_export(gx, ctx, oracle, monkeypatch, variant):
+    """The batch formats handed over as tables (gx_staged_table): a staged
+    run keeps its last pass's planes on the device (GX_STAGED_KEEP_PLANES)
+    and each pair's table exports, row by row, the reference's I, D, S planes
+    (algo.rs:172, 281) -- decoded from the twin fill's 2-B plane codes (the
+    headline's format), the byte planes, or int32 -- equal to the oracle's
+    whole planes; plane checksums too.  Rows cover the strip and twin-half
+    boundaries; pairs of unequal shapes so twins mix lengths."""
+    env = {"twin_codes": {"GX_TWIN": "1"}, "byte_planes": {"GX_TWIN": "0"}, "int32": {"GX_PLANES32": "1"},
+           "local_twin": {"GX_TWIN": "1", "GX_OVERLAP": "0"}}[variant]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    local = variant == "local_twin"
+    rng = np.random.default_rng(17)
+    pairs = []
+    for k in range(24):
+        n = int(rng.integers(200, 700)) if k % 3 else 640
+        m = int(rng.integers(200, 700)) if k % 3 else 512
+        a = bytes(rng.choice(list(b"ACGT"), n))
+        b = bytearray(a[:m] if m <= n else a + bytes(rng.choice(list(b"ACGT"), m - n)))
+        for _ in range(m // 10):   # related pairs: long local alignments for the local variant
+            b[int(rng.integers(0, m))] = int(rng.choice(list(b"ACGT")))
+        pairs.append((a, bytes(b)))
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, _ = st.run(gx.Scores(*CONFIG_SCORES), local, keep_planes=True, steps=2, keep=True)
+    info = ctx.fill_info()
+    want_bpc = {"twin_codes": 2, "byte_planes": 3, "int32": 12, "local_twin": 2}[variant]
+    assert info["plane_bytes_per_cell"] == want_bpc and info["layout"] == 0, info
+    for p in (0, 1, 5, 12, 23):
+        a, b = pairs[p]
+        o = oracle.align(a, b, CONFIG_SCORES, is_local=local, want_planes=True)
+        assert res[p].score == o.score, p
+        t = st.table(p)
+        for which in range(3):
+            got = np.concatenate([t.rows(which, r0, min(200, len(a) + 1 - r0)) for r0 in range(0, len(a) + 1, 200)])
+            assert np.array_equal(got, o.planes[which]), (variant, p, which)
+        t.free()
+    with pytest.raises(gx.GxError):   # the staged run's alignment is gx_staged_steps; a staged table has no retrace
+        gx.retrace(gx.SequenceContainer([gx.Sequence("a", pairs[0][0].decode()), gx.Sequence("b", pairs[0][1].decode())]),
+                   st.table(0), local)
