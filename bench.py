@@ -283,26 +283,30 @@ def fasta_pair(gx, which: str):
     return cont.sequences[0].sequence.encode(), cont.sequences[1].sequence.encode()
 
 
-def config_record(gx, ctx, which: str, steps: int):
+def config_record(gx, ctx, which: str, steps: int, tracked: bool = False):
     """BASELINE configs 2 (Covid_Wuhan x Covid_USA-CA4, global) and 3 (Human x
     Mouse BRCA2, local): the reference's align call (main.rs:143-150), one pair
     per call, resident in HBM, with int32 score planes and traceback, `steps`
     timed passes (bench.py's own clock), then one untimed pass with device
     plane checksums compared with tests/golden/large_digests.json (score,
-    statistics, alignment sha256, the three plane checksums)."""
+    statistics, alignment sha256, the three plane checksums).  tracked: the
+    fill also keeps alignment_table's running max cell and matches_at_max
+    (algo.rs:258-262, 279), as the drop-in alignment_table call does; both are
+    checked too."""
     a, b = fasta_pair(gx, which)
     local = which == "brca2"
     scores = gx.Scores(*SCORES)
     st = gx.StagedPairs([(a, b)], ctx=ctx)
-    st.run(scores, local, True)
+    st.run(scores, local, True, max_cell=tracked)
     t0 = time.perf_counter()
-    res, fms = st.run(scores, local, True, steps=steps)
+    res, fms = st.run(scores, local, True, steps=steps, max_cell=tracked)
     el = time.perf_counter() - t0
     finfo = ctx.fill_info()
     cells = len(a) * len(b)
     out = {"workload": f"{'Covid_Wuhan x Covid_USA-CA4' if which == 'covid' else 'Human x Mouse BRCA2 cds'} "
                        f"({len(a)}x{len(b)}), {'local SW' if local else 'global NW'}, scores {SCORES}, "
-                       f"{plane_desc(finfo['plane_bytes_per_cell'])}",
+                       f"{plane_desc(finfo['plane_bytes_per_cell'])}"
+                       + (", max cell + matches_at_max tracked (alignment_table)" if tracked else ""),
            "gcups": round(cells * steps / el / 1e9, 3), "ms_per_step": round(el / steps * 1e3, 3),
            "fill_ms_avg": round(fms, 3), "fill_gcups": round(cells / (fms * 1e-3) / 1e9, 3), "steps": steps,
            "fill_launch": finfo}
@@ -314,15 +318,20 @@ def config_record(gx, ctx, which: str, steps: int):
     with open(os.path.join(ROOT, "tests", "golden", "large_digests.json")) as f:
         gold = {c["name"]: c for c in json.load(f)["cases"]}
     g = gold["brca2/local" if local else "covid_wuhan_usa/global"]
-    res, _ = st.run(scores, local, True, plane_sums=True)
+    res, _ = st.run(scores, local, True, plane_sums=True, max_cell=tracked)
+    if ctx.fill_info() != finfo:
+        raise RuntimeError(f"{which}: the parity pass took a different launch: {ctx.fill_info()} != {finfo}")
     sums = [int(x) for x in st.plane_sums()[0, 0]]
     r = res[0]
     ok = (r.score == g["score"] and [r.matches, r.mismatches, r.gap_extensions, r.opening_gaps] == g["stats"]
           and r.n_steps == g["n_steps"] and alignment_sha256(st.steps(0)) == g["alignment_sha256"]
           and sums == [int(x) for x in g["plane_sums"]])
+    if tracked:
+        ok = ok and [r.max_cell_i, r.max_cell_j] == list(g["max_cell"]) and r.matches_at_max == g["matches_at_max"]
     if not ok:
         raise RuntimeError(f"{which}: result differs from tests/golden/large_digests.json")
-    out["parity"] = {"bit_exact": True, "fields": "score, statistics, alignment sha256, I/D/S plane checksums",
+    out["parity"] = {"bit_exact": True, "fields": "score, statistics, alignment sha256, I/D/S plane checksums"
+                                                  + (", max cell, matches_at_max" if tracked else ""),
                      "source": "tests/golden/large_digests.json (oracle)"}
     return out
 
@@ -406,7 +415,18 @@ def allvsall_share(gx, rank: int, world: int):
     pairs = gx.all_pairs(len(seqs), with_self=False)
     w = [float(len(seqs[i])) * len(seqs[j]) for i, j in pairs]
     mine = gx.lpt_partition(w, world)[rank]
-    return [(seqs[pairs[p][0]], seqs[pairs[p][1]]) for p in mine], int(sum(w))
+    return [(seqs[pairs[p][0]], seqs[pairs[p][1]]) for p in mine], int(sum(w)), [tuple(pairs[p]) for p in mine]
+
+
+def allvsall_digests(ij):
+    """{pair index on this rank: oracle digest} for the rank's all-vs-all
+    pairs (tests/golden/allvsall_digests.json: score, statistics, alignment
+    sha256, plane checksums per genome pair i, j), and the file's path."""
+    path = os.path.join(ROOT, "tests", "golden", "allvsall_digests.json")
+    with open(path) as f:
+        d = json.load(f)
+    by = {(c["i"], c["j"]): c for c in d["cases"]}
+    return {p: by[tuple(x)] for p, x in enumerate(ij) if tuple(x) in by}, os.path.relpath(path, ROOT)
 
 
 def plane_desc(bytes_per_cell: int) -> str:
@@ -498,6 +518,12 @@ def verify_against_golden(staged, ctx, scores, is_local, keep_planes, rank: int,
     mine, src = golden_digests(rank, P, L, related)
     if is_local or not mine:
         return 0, src, None
+    return verify_passes(staged, ctx, scores, is_local, keep_planes, mine, src, rank, P, timed_info, passes)
+
+
+def verify_passes(staged, ctx, scores, is_local, keep_planes, mine, src, rank: int, P: int, timed_info: dict,
+                  passes: int):
+    """verify_against_golden's check for digests `mine` ({pair index: digest})."""
     staged.run(scores, is_local, keep_planes, steps=passes, plane_sums=keep_planes)
     info = ctx.fill_info()
     if info != timed_info:
@@ -525,28 +551,39 @@ def simulate_world(args, gx, ctx):
     scores = gx.Scores(*SCORES)
     strong = args.workload == "allvsall"
 
+    checked = [0, 0]
+
     def shard(r, w):
         if strong:
-            return allvsall_share(gx, r, w)[0]
+            pr, _, ij = allvsall_share(gx, r, w)
+            return pr, ij
         P = args.pairs_per_gpu or 8
-        return rank_pairs(r, P, args.length)
+        return rank_pairs(r, P, args.length), None
 
-    def timed(pairs):
+    def timed(pairs, ij):
         st = gx.StagedPairs(pairs, ctx=ctx)
         keep = args.planes if strong else not args.no_planes
         st.run(scores, False, keep)
         t0 = time.perf_counter()
         st.run(scores, False, keep, steps=args.steps)
-        return (time.perf_counter() - t0) / args.steps * 1e3
+        ms = (time.perf_counter() - t0) / args.steps * 1e3
+        if strong and not args.no_verify:
+            # every timed pass of the shard against the oracle digests
+            mine, _ = allvsall_digests(ij)
+            if len(mine) != len(pairs):
+                raise RuntimeError("all-vs-all pairs without an oracle digest")
+            checked[0] += check_passes(st.pass_results(), mine, 0, 0, "simulated shard") * len(mine)
+            checked[1] += len(mine)
+        return ms
 
     per = []
     for r in range(W):
-        pr = shard(r, W)
+        pr, ij = shard(r, W)
         per.append({"rank": r, "pairs": len(pr), "cells": sum(len(a) * len(b) for a, b in pr),
-                    "ms_per_step": round(timed(pr), 3)})
+                    "ms_per_step": round(timed(pr, ij), 3)})
         log(f"simulated rank {r}/{W}: {per[-1]}")
-    full = shard(0, 1)
-    t1 = timed(full)
+    full, ij1 = shard(0, 1)
+    t1 = timed(full, ij1)
     cells1 = sum(len(a) * len(b) for a, b in full)
     tmax = max(p["ms_per_step"] for p in per)
     cells_w = sum(p["cells"] for p in per)
@@ -562,6 +599,9 @@ def simulate_world(args, gx, ctx):
                       "efficiency": round(eff, 4),
                       "basis": "each rank's shard timed alone on one MI355X; N-GPU step = slowest shard "
                                "(no data-path collective)"},
+        "parity": ({"pair_passes_checked": checked[0], "pairs_checked": checked[1], "bit_exact": True,
+                    "fields": "score, statistics, alignment length of every pair, every timed pass",
+                    "source": "tests/golden/allvsall_digests.json (oracle)"} if strong and checked[1] else None),
         "steps": args.steps}), flush=True)
 
 
@@ -628,8 +668,9 @@ def main():
     if P is None:
         pb = 0 if args.no_planes else gx.plane_bytes_per_cell(scores, args.local)
         P = max(1, min(MAX_DEFAULT_PAIRS, int(PLANE_BUDGET // (max(pb, 3) * L * (L + 64)))))
+    ij = None
     if args.workload == "allvsall":
-        pairs, n_total = allvsall_share(gx, rank, world)
+        pairs, n_total, ij = allvsall_share(gx, rank, world)
         P = len(pairs)
         keep_planes = args.planes
         args.single_pair_steps = 0
@@ -677,6 +718,11 @@ def main():
         mine, _ = golden_digests(rank, P, L, args.related)
         if mine:
             timed_checked = check_passes(timed_passes, mine, rank, P, "timed passes")
+    elif args.workload == "allvsall" and not args.local and not args.no_verify:
+        mine, _ = allvsall_digests(ij)
+        if len(mine) != P:
+            raise RuntimeError(f"{P - len(mine)} of this rank's all-vs-all pairs have no oracle digest")
+        timed_checked = check_passes(timed_passes, mine, rank, P, "timed passes")
     else:   # no digests: every pass must at least agree with the last
         for k, row in enumerate(timed_passes):
             if [(r.score, r.n_steps, r.matches) for r in row] != [(r.score, r.n_steps, r.matches) for r in res]:
@@ -786,6 +832,25 @@ def main():
                                  f"{finfo['groups']} fill group(s) per pass"
                                  + (", the overlapped two-group pipeline" if finfo.get('groups') == 2 else "")
                                  + "); plane checksums of every pass, alignment sha256 of the last"}
+    if args.workload == "allvsall" and not args.local and not args.no_verify:
+        # every pair of this rank's share against the oracle digests of the 45
+        # genome pairs (tests/golden/allvsall_digests.json); gathered over ranks
+        vpasses = 2 if args.steps >= 2 else 1
+        mine, src = allvsall_digests(ij)
+        checked, src, _ = verify_passes(staged, ctx, scores, False, keep_planes, mine, src, rank, P, finfo, vpasses)
+        pairs_total = P
+        if dist is not None:
+            import torch
+            t = torch.tensor([checked, P], dtype=torch.int64, device="cuda")
+            dist.all_reduce(t)
+            checked, pairs_total = int(t[0].item()), int(t[1].item())
+        out["parity"] = {"pairs_checked": checked, "pairs_total": pairs_total, "bit_exact": True,
+                         "fields": "score, statistics, alignment sha256" + (", I/D/S plane checksums" if keep_planes
+                                                                            else ""),
+                         "source": src, "timed_passes_checked": timed_checked,
+                         "timed_pass_fields": "score, statistics, alignment length of every pair, every timed pass",
+                         "pass": f"{vpasses} extra untimed pipelined passes through the timed call's launch "
+                                 f"(fill_info identical); plane checksums of every pass, alignment sha256 of the last"}
     if world == 1 and keep_planes and bytes_per_cell == 2 and args.no_plane_steps > 0:
         # the same batch with the per-pair byte planes (3 B/cell, the table format)
         os.environ["GX_PLANES_W16"] = "0"
@@ -843,6 +908,9 @@ def main():
         # BASELINE configs 2 and 3, the drop-in single-pair align calls, timed here
         out["config2"] = config_record(gx, ctx, "covid", args.config_steps)
         out["config3"] = config_record(gx, ctx, "brca2", args.config_steps)
+        # the same calls with alignment_table's max cell + matches_at_max kept
+        out["config2_tracked"] = config_record(gx, ctx, "covid", args.config_steps, tracked=True)
+        out["config3_tracked"] = config_record(gx, ctx, "brca2", args.config_steps, tracked=True)
     if world == 1 and args.workload == "synthetic" and args.local_batch_steps > 0 and not args.local:
         out["local_batch"] = local_batch_record(gx, ctx, args.local_batch_steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
