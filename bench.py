@@ -8,7 +8,7 @@ DNA pairs (BASELINE.json metric), 1..8 GPUs, one process per GPU.
 A STEP is one pass of the hot path over one batch: for each of the P
 synthetic 30k x 30k pairs resident on this GPU, the full-table fill that
 writes the three score planes (alignment_table, algo.rs:151-282; stored as
-exact per-cell byte differences when the scores allow it, gx_api.cpp
+exact per-cell byte differences when the scores allow it, gx_api_plan.cpp
 d8_planes_ok, else int32) plus
 the traceback (retrace, algo.rs:287-441) down to the labelled alignment on
 the host.  Inputs are staged in HBM before the timed region; the K timed

@@ -486,7 +486,7 @@ static hipError_t launch_cs2_w(int W, const PairDev* d_pairs, int npairs, int to
     }
 }
 
-// Band widths instantiated (must match gx_api.cpp kCs2Widths).
+// Band widths instantiated (must match gx_api_plan.cpp kCs2Widths).
 hipError_t launch_fill_cs2(int W, bool local, bool planes, bool tbl, const PairDev* d_pairs, int npairs,
                            int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                            hipStream_t st) {

@@ -156,7 +156,7 @@ __device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 }
 
 // Compact planes (plane mode 3, layout 0, global untracked launches whose
-// scores pass the host's range proof, gx_api.cpp d8_planes_ok): per cell one
+// scores pass the host's range proof, gx_api_plan.cpp d8_planes_ok): per cell one
 // signed byte each of
 //     x_I = I(i,j) - I(i,j-1),  x_S = S(i,j) - I(i,j),  x_D = D(i,j) - I(i,j)
 // in the int32 plane layout with bytes for ints (4 steps of a row = one dword

@@ -20,7 +20,7 @@
 //     need converting; the blocks it pushes carry that same base;
 //   * the I/O wave converts the band's bottom row back to int32 for HBM.
 // The host admits a launch only when the worst-case spread of a band's values
-// around the inherited bases stays below 2^15 (gx_api.cpp twin_width).
+// around the inherited bases stays below 2^15 (gx_api_plan.cpp twin_width).
 // Comparisons and max are exact on values within 2^15 of each other, so the
 // codes, landing columns, planes and results equal the int32 fill's.
 #include "gx_device.h"
@@ -138,7 +138,7 @@ struct PkScores {
 // Twin plane code (PLANES == 2, 2 B per cell): the three differences of a
 // cell in one 16-bit word, code = x_I + 16 x_S + 512 x_D (mod 2^16), x_I in
 // [0, 15] (shifted: I'' - I''(j-1)), x_S = S - I in [-16, 15], x_D = D - I in
-// [-64, 63] (gx_api.cpp w16_ok checks the ranges); both pairs' codes of a
+// [-64, 63] (gx_api_plan.cpp w16_ok checks the ranges); both pairs' codes of a
 // cell in one dword, as the halves already hold them.  Two v_pk_mad_u16 and
 // three v_pk_sub_i16 per two cells (the byte format: three SDWA per cell).
 // Small-alphabet twins (TBL, the launch's <= 4 symbols in Scores32.sym): a
@@ -182,7 +182,7 @@ struct LanePk {
 // LOCAL (Smith-Waterman, algo.rs:231-248 with is_local): plain (unshifted)
 // values, relative to per-block bases like the global twin's (neighbouring
 // local values differ by at most max(|h + g|, U) as global ones do, the 0
-// floor keeps every inequality: gx_api.cpp twin_bound), so the 0 floor of
+// floor keeps every inequality: gx_api_plan.cpp twin_bound), so the 0 floor of
 // score_max is one v_pk_max_u16 against k.Z, the biased relative zero of the
 // current bases (-B per half, clamped to -2^15: a base above 2^15 lies more
 // than the admission bound above every value of the band, whose floor then

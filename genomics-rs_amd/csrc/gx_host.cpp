@@ -12,7 +12,7 @@
 
 #include "../../include/gx.h"
 
-int gx_internal_fail(int code, const std::string& msg);  // gx_api.cpp (shared gx_last_error state)
+int gx_internal_fail(int code, const std::string& msg);  // gx_api_context.cpp (shared gx_last_error state)
 
 namespace {
 int hfail(int code, const std::string& m) { return gx_internal_fail(code, m); }

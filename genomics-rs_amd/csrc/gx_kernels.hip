@@ -1635,7 +1635,7 @@ __global__ void export_w16_kernel(const uint8_t* __restrict__ codes, int half, i
 
 }  // namespace gx
 
-// ---- explicit launch wrappers (C++ linkage, used by gx_api.cpp) ----
+// ---- explicit launch wrappers (C++ linkage, used by gx_api_fill.cpp and the table exports) ----
 namespace gx {
 
 template <int W, bool LOCAL, int PLANES, bool TRACK, bool LCSP, bool TBL>

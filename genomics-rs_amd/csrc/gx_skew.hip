@@ -709,7 +709,7 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, SideCtx
 // dd - sm lies in [h + g, max(g, 0)] (Ddn = max(Dn, H + h) with Dn <= H; local:
 // the floor and + g), so one granule holds sm (low word) and (dd - sm) in 31
 // bits under a valid bit (bit 63).  The feed rows are zeroed before the launch
-// (gx_api.cpp run_fill), so a granule is valid exactly once it was written by
+// (gx_api_fill.cpp run_fill), so a granule is valid exactly once it was written by
 // this launch.  Stores and loads are 8-byte agent-scope (sc1: write-through,
 // L1 bypass).
 // TRACK: the LCS values of the bottom row travel the same way, one more
@@ -846,7 +846,7 @@ __device__ void io_wave_tag(const PairDev& P, const int lb, const int lane, cons
 // round-robin, so at W = 2 the two core waves have SIMDs of their own (the
 // I/O wave, which polls, shares one with a side wave); at W = 3 two core
 // waves share a SIMD with other waves.  Persistent workgroups take bands from the
-// host's band-major queue (gx_api.cpp run_fill), as fill_kernel does.
+// host's band-major queue (gx_api_fill.cpp run_fill), as fill_kernel does.
 template <int W, bool LOCAL, bool PLANES, bool TBL, bool TRACE, bool TRACK>
 __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const PairDev* __restrict__ pairs,
                                                                            const int npairs, const int total_bands,
@@ -973,7 +973,7 @@ static hipError_t launch_skew_w(int W, const PairDev* d_pairs, int npairs, int t
     return hipErrorInvalidValue;
 }
 
-// Band widths of layout 3 (must match gx_api.cpp skew_band_waves).  trace:
+// Band widths of layout 3 (must match gx_api_plan.cpp skew_band_waves).  trace:
 // the diagnostics instantiation (PairDev.trace set; fills with planes only,
 // the others run untraced).
 // track: the first maximum + max_matches (alignment_table's max_cell and

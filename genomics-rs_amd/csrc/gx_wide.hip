@@ -1,6 +1,6 @@
 // gx_wide.hip -- the wide (int64) fill: alignment_table (algo.rs:151-282) in
 // the reference's own integer type, for jobs outside the exact-int32 range of
-// the main fill (gx_api.cpp check_scores: score magnitudes above 2^24, |score|
+// the main fill (gx_api_plan.cpp check_scores: score magnitudes above 2^24, |score|
 // bounds above 2^28, the g < 0 < h configurations whose boundary arithmetic
 // wraps, sequences longer than 2^26).  Every add wraps modulo 2^64 exactly as
 // the reference's release build does (i64 overflow is not checked there), and

@@ -452,7 +452,7 @@ def alignment_table(sequence_container: SequenceContainer, scores: Scores, is_lo
 
     max_cell=False skips the running max cell and matches_at_max (returned as
     0): the untracked fill, whose score planes are kept in the compact
-    byte format (gx_api.cpp d8_planes_ok) when the table is built on layout 0."""
+    byte format (gx_api_plan.cpp d8_planes_ok) when the table is built on layout 0."""
     a, b = _first_two(sequence_container)
     if len(sequence_container.sequences) > 2:   # algo.rs:161-163
         _log.warning("More than two sequences found. Only the first two will be used.")

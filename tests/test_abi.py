@@ -222,7 +222,7 @@ def test_plane_bytes_per_cell(gx, scores, local, monkeypatch):
 
 @pytest.mark.parametrize("local", [False, True], ids=["global", "local"])
 def test_plan_layout(gx, local, monkeypatch):
-    """Host-only: the layout rule (gx_api.cpp fill_layout).  BASELINE configs
+    """Host-only: the layout rule (gx_api_plan.cpp fill_layout).  BASELINE configs
     2 and 3 take the latency layouts; a wide batch takes layout 0; columns
     past the 24-bit landing-column range of the 64-row strip layouts (the
     skeleton holds E + 64 in 24 bits, gx_kernels.hip tb_chase_kernel; a

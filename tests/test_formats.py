@@ -1,7 +1,7 @@
 """CPU checks of the compact plane formats' arithmetic:
 the twin plane code of gx_fill_pk.hip (w16_code) and its decoder in
 plane_sums_kernel (mode 3) are exact over the whole admitted range, and the
-admission bounds of gx_api.cpp (d8_planes_ok, w16_ok) hold for the default
+admission bounds of gx_api_plan.cpp (d8_planes_ok, w16_ok) hold for the default
 scores.  Pure integer arithmetic: no GPU, no library call."""
 import numpy as np
 
@@ -47,6 +47,6 @@ def test_default_scores_fit_both_formats():
 
 
 def test_shifted_score_tables_fit_a_byte():
-    # gx_api.cpp twin_tbl: the score tables hold s - 2g for match and mismatch
+    # gx_api_fill.cpp twin_tbl: the score tables hold s - 2g for match and mismatch
     sm, smm, g = 1, -2, -1
     assert 0 <= sm - 2 * g <= 255 and 0 <= smm - 2 * g <= 255

@@ -200,7 +200,7 @@ def test_bench_launch_synthetic_30k(gx, ctx, monkeypatch, launch):
 @pytest.mark.parametrize("npairs,env", [(20, {"GX_TWIN": "1"}), (80, {})], ids=["20_twin", "80_default"])
 def test_overlapped_bench_launch_30k(gx, ctx, monkeypatch, npairs, env):
     """The launch the headline times: synthetic 30k pairs through the
-    overlapped two-group pipeline (gx_api.cpp batch_core_overlap), three
+    overlapped two-group pipeline (gx_api_batch.cpp batch_core_overlap), three
     passes -- 20 pairs with the twin fill forced (group A's 4 pairs alone
     would not fill the grid and take the scalar fill, so the pipeline would
     not run by default) and the bench's whole 80-pair batch under the default
@@ -222,7 +222,7 @@ def test_overlapped_alternating_sets(gx, ctx, monkeypatch, poison):
     device buffer a pass takes from the pool last held the other set's planes
     and records: a walk that read a later pass's planes, or a fill that
     overwrote planes a walk still reads (the wait of group B's next fill on
-    the previous walk, gx_api.cpp batch_core_overlap), gives wrong results
+    the previous walk, gx_api_batch.cpp batch_core_overlap), gives wrong results
     here, where repeating one set would hide it.  With GX_POOL_POISON every
     buffer is also filled with garbage on its new user's stream before use.
     Every pass's plane checksums and results, and each set's last

@@ -181,10 +181,10 @@ def test_exported_planes_and_cells(gx, ctx, oracle, n, m, is_local):
 def test_untracked_table_planes(gx, ctx, oracle, scores, is_local):
     """Tables built without the max-cell tracking: on layout 0 their
     score planes are stored as per-cell byte differences when the scores pass
-    the range proof (gx_api.cpp d8_planes_ok; (30, -30, -10, -40) does not and
+    the range proof (gx_api_plan.cpp d8_planes_ok; (30, -30, -10, -40) does not and
     (1, -2, 1, -3), (2, -1, 1, -4) have g > 0, all keep int32 planes).  On
     layout 1 a local fill with g > 0 must not take the split column step
-    (gx_api.cpp cs2_enabled: its 0 floor is applied after the delete chain's
+    (gx_api_plan.cpp cs2_enabled: its 0 floor is applied after the delete chain's
     prefix max, exact only for g <= 0), even where GX_CS2=1 asks for it.  Every exported plane
     value equals the oracle's, including dense-tie and long-match inputs that
     push the differences towards the proof's bounds."""

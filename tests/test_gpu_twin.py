@@ -41,7 +41,7 @@ def _twin_pairs(seed, shapes, per_shape=2, alphas=(b"ACGT", b"AC", b"ACGTN", b"A
 @pytest.fixture(autouse=True)
 def _force_twin(monkeypatch):
     """The batches here are small: force the twin fill (by default it runs
-    only for band queues of >= 2.5 rounds, gx_api.cpp run_fill)."""
+    only for band queues of >= 2.5 rounds, gx_api_fill.cpp run_fill)."""
     monkeypatch.setenv("GX_TWIN", "1")
 
 
@@ -245,7 +245,7 @@ def test_twin_pairs_by_shape(gx, ctx, oracle, monkeypatch):
         assert res[p].score == o.score and _steps_list(st.steps(p)) == o.alignment(), p
 
 
-# ---- the int16 admission bound where it binds (gx_api.cpp twin_width) ------
+# ---- the int16 admission bound where it binds (gx_api_plan.cpp twin_width) ------
 # Inputs that push the twin fill's values hardest (tests/test_twin_bound.py
 # measures their spreads against the rule on the CPU) at the widest scores
 # each band width admits; every plane cell of a table filled by the twin
@@ -343,7 +343,7 @@ def test_twin_auto_selection(gx, ctx, oracle, monkeypatch, kind):
 @pytest.mark.parametrize("launch_env", ["auto", "w4_grid3"])
 def test_twin_overlapped_global(gx, ctx, oracle, monkeypatch, launch_env):
     """The headline's launch shape: a long-pair global batch through the
-    overlapped two-group pipeline (gx_api.cpp batch_core_overlap: group A's
+    overlapped two-group pipeline (gx_api_batch.cpp batch_core_overlap: group A's
     fill of pass k+1 beside pass k's walk into a second A buffer, group B's
     fill of pass k+1 waiting on the device for pass k's walk before it reuses
     B's buffers).  20 mixed shapes, three passes: every pass's plane

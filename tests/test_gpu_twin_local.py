@@ -48,7 +48,7 @@ def _check(gx, ctx, oracle, pairs, scores, steps=1, twin=1):
 
 
 def _w16_ok(scores):
-    """gx_api.cpp w16_ok: the twin plane codes' field ranges."""
+    """gx_api_plan.cpp w16_ok: the twin plane codes' field ranges."""
     sm, smm, g, h = scores
     a = h + g
     U = max(0, max(sm, smm) - a)
@@ -75,7 +75,7 @@ def _planted(rng, n, m, core, al=b"ACGT"):
 
 
 # (scores, twin fill expected): the local twin needs the twin plane codes'
-# ranges (gx_api.cpp w16_ok: x_I - g in [0, 15] ...); (2, -3, -2, -4) and
+# ranges (gx_api_plan.cpp w16_ok: x_I - g in [0, 15] ...); (2, -3, -2, -4) and
 # (5, -4, 0, -10) exceed them and run the scalar local fill
 @pytest.mark.parametrize("scores,twin", [(CONFIG_SCORES, 1), ((2, -3, -1, -4), 1), ((3, -2, -1, -3), 1),
                                          ((1, -1, 0, 0), 1), ((3, -3, -1, -1), 1), ((2, -3, -2, -4), 0),
@@ -183,7 +183,7 @@ def test_local_twin_64k_related(gx, ctx, monkeypatch):
 
 def test_local_twin_overlapped(gx, ctx, oracle, monkeypatch):
     """A long-pair local batch (>= 16 pairs, n >= 16,384) takes the overlapped
-    two-group pipeline (gx_api.cpp batch_core_overlap): each pass's walk runs
+    two-group pipeline (gx_api_batch.cpp batch_core_overlap): each pass's walk runs
     beside the next pass's fill and reads its start cells (the last maxima,
     finalize_kernel's PairRes) on the device.  Three passes, every result of
     every pass against the oracle."""

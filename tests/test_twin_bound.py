@@ -1,4 +1,4 @@
-"""CPU: the twin fill's int16 admission rule (gx_api.cpp twin_width /
+"""CPU: the twin fill's int16 admission rule (gx_api_plan.cpp twin_width /
 gx_twin_admission) against brute-force spreads measured with the oracle.
 
 The twin fill (genomics-rs_amd/csrc/gx_fill_pk.hip) keeps every value of a
