@@ -11,6 +11,16 @@ for sub in ("oracle", "genomics-rs_amd"):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# Hardware queues per process for the GPU tests (read when HIP initialises,
+# before any test touches the device).  The library's pipelines put fills,
+# walks and copies on up to five streams; with HIP's default of 4 queues two
+# of them share a queue, which orders their work as if it were one stream
+# and hides missing stream waits.  With 8 every stream has a queue of its own
+# (tests/test_gpu_atsize.py test_overlapped_alternating_sets fails on a build
+# without the overlapped pipeline's walk wait only then:
+# profiles/r05_mutation_nowait.txt).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 FASTA = os.path.join(GOLDEN, "fasta")
 COMPARISON = os.path.join(GOLDEN, "comparison_data")

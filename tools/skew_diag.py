@@ -62,16 +62,21 @@ def main():
         os.environ["GX_BAND_WAVES"] = str(W)
         for name, a, b in cases:
             for local in modes:
+                # (int32 score planes, as the drop-in table call and bench.py's
+                # config records keep them: the traced instantiation has planes)
+                st = gx.StagedPairs([(a, b)], ctx=ctx)
                 for _ in range(2):
-                    _, r = gx.align_raw(a, b, sc, local, ctx=ctx, max_cell=False)
+                    res, fms = st.run(sc, local, True)
+                r = res[0]
                 tr = os.path.join(tempfile.gettempdir(), f"skew_{W}_{name}_{int(local)}.csv")
                 os.environ["GX_TRACE_FILE"] = tr
-                _, r2 = gx.align_raw(a, b, sc, local, ctx=ctx, max_cell=False)
+                _, fms2 = st.run(sc, local, True)
                 del os.environ["GX_TRACE_FILE"]
                 cells = len(a) * len(b)
-                print(f"W={W} {name} {'local' if local else 'global'}: fill {r.fill_us} us "
-                      f"({cells / max(r.fill_us, 1) / 1e3:.1f} GCUPS), traced fill {r2.fill_us} us, "
-                      f"retrace {r.retrace_us} us", flush=True)
+                fus = fms * 1e3
+                print(f"W={W} {name} {'local' if local else 'global'}: fill {fus:.0f} us "
+                      f"({cells / max(fus, 1) / 1e3:.1f} GCUPS), traced fill {fms2 * 1e3:.0f} us, "
+                      f"retrace {r.retrace_us} us; {ctx.fill_info()}", flush=True)
                 summarize(tr, len(b), W)
                 if keep:
                     os.makedirs(keep, exist_ok=True)
