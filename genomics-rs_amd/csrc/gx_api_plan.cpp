@@ -272,16 +272,24 @@ int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int grid_ca
     const bool cs_ok = span < (1LL << 29) && mmax + 128 < (1u << 24);   // landing keys hold E + 64 in 24 bits
     // a pair's fill time ~ m x (a strip's pace per column) + S x (a strip's
     // start lag), fitted per layout on a lone 64-row strip and on the
-    // BASELINE pairs (round 4, profiles/r04_layout_fit.json): layout 3 50 ns
-    // + 6.46 us global, 57.5 ns + 6.66 us local; the column step 113 ns +
-    // 2.66 us (global), split for local fills 110 ns + 3.37 us
+    // BASELINE pairs: untracked (round 4, profiles/r04_layout_fit.json)
+    // layout 3 50 ns + 6.46 us global, 57.5 ns + 6.66 us local; the column
+    // step 113 ns + 2.66 us (global), split for local fills 110 ns + 3.37 us.
+    // Tracked fills (round 5, profiles/r05_tracked_layouts.txt: the side wave
+    // carries the first maximum and the LCS values and sets the pace) layout
+    // 3 113 ns + 12.1 us, the tracked column step 146 ns + 3.45 us, both
+    // modes: layout 3 only for short pairs (n below about a quarter of m)
     const bool local = sc.floor_ == 0;
-    (void)track;
     double est1 = 0, est3 = 0;   // the launch's slowest pair on each layout (ns)
     for (const PairHost& h : ph) {
         const double S = (double)ceil_div((int)h.n, kStripRows1), m = (double)h.m;
-        est1 = std::max(est1, local ? m * 110.0 + S * 3370.0 : m * 113.0 + S * 2660.0);
-        est3 = std::max(est3, local ? m * 57.5 + S * 6660.0 : m * 50.0 + S * 6460.0);
+        if (track) {
+            est1 = std::max(est1, m * 146.0 + S * 3450.0);
+            est3 = std::max(est3, m * 113.0 + S * 12100.0);
+        } else {
+            est1 = std::max(est1, local ? m * 110.0 + S * 3370.0 : m * 113.0 + S * 2660.0);
+            est3 = std::max(est3, local ? m * 57.5 + S * 6660.0 : m * 50.0 + S * 6460.0);
+        }
     }
     const bool sk_ok = skew_ok(sc, lcs_plane, mmax);
     const int lat = sk_ok && (!cs_ok || est3 < est1) ? 3 : cs_ok ? 1 : 0;

@@ -3,7 +3,8 @@ the synthetic 30k pair and BASELINE configs 2 (Covid, global) and 3 (BRCA2,
 local), per band width / layout, min and median of the fill's HIP-event time.
 
     python tools/skew_bench.py [runs] [W ...]     (default 7 runs, W = 2)
-    env SKEW_BENCH_LAYOUTS="3 1" picks the layouts (default: 3)
+    env SKEW_BENCH_LAYOUTS="3 1" picks the layouts (default: 3); SKEW_BENCH_TRACK=1 times
+    the tracked fill (max cell + matches_at_max) with int32 score planes instead
 """
 import os
 import statistics
@@ -44,9 +45,16 @@ def main():
             os.environ["GX_BAND_WAVES"] = str(W)
             for name, a, b, local in cases:
                 t = []
-                for _ in range(runs + 1):
-                    _, r = gx.align_raw(a, b, sc, local, ctx=ctx, max_cell=False)
-                    t.append(r.fill_us)
+                if os.environ.get("SKEW_BENCH_TRACK"):   # tracked fill with int32 planes (the drop-in table call)
+                    st = gx.StagedPairs([(a, b)], ctx=ctx)
+                    for _ in range(runs + 1):
+                        _, fms = st.run(sc, local, True, max_cell=True)
+                        t.append(int(fms * 1e3))
+                    del st
+                else:
+                    for _ in range(runs + 1):
+                        _, r = gx.align_raw(a, b, sc, local, ctx=ctx, max_cell=False)
+                        t.append(r.fill_us)
                 t = t[1:]
                 cells = len(a) * len(b)
                 info = ctx.fill_info()
