@@ -402,9 +402,13 @@ int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
                                                                      (int)dph[q].m, 0};
         // the walk stays on the fill's stream: the fill's buffers return to
         // the pool right behind it (stream-ordered reuse).  (A walk on its own
-        // stream beside the next step's fill measured 1024 x 4k +6 % but made
-        // 1024 x 1k 2.5x slower: the host's enqueue of the next fill stalled
-        // behind the running walk.)
+        // stream beside the next step's fill, its buffers released once the
+        // walk is collected, measured in round 5 (tools/walk_stream_sweep.sh,
+        // 3 alternating runs a size): 1024 x 1k 0.99 -> 1.06 ms a step,
+        // 1024 x 4k 8.35 -> 8.17, 128 x 16k 17.5 -> 17.6: the walk and the
+        // fill slow each other down on shared CUs (fill 0.56 -> 0.67 ms beside
+        // a walk stretched from 0.30 to 0.82), and the host's labelling then
+        // leaves the device idle between pairs of steps.)
         int tr_pass = 0;
         bool held[2] = {false, false};
         auto trace_dev = [&](int s) {
