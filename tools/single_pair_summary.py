@@ -20,7 +20,7 @@ SIZES = {"covid": (29903, 29882), "brca2": (11382, 10346)}
 
 def fill_row(path):
     with open(path) as f:
-        rows = [r for r in csv.DictReader(f) if "fill" in r["Name"] and "codes" not in r["Name"]]
+        rows = [r for r in csv.DictReader(f) if "gx::fill" in r["Name"]]
     r = max(rows, key=lambda r: float(r["TotalDurationNs"]))
     return {"kernel": r["Name"][:100], "calls": int(r["Calls"]), "avg_ms": round(float(r["AverageNs"]) / 1e6, 4),
             "min_ms": round(float(r["MinNs"]) / 1e6, 4), "max_ms": round(float(r["MaxNs"]) / 1e6, 4)}
@@ -32,7 +32,7 @@ def pmc(d):
     per = {}
     for kname, disp, ctr, val, dur in c.execute(
             "select kernel_name, dispatch_id, counter_name, value, duration from counters_collection"):
-        if "fill" in kname and "codes" not in kname:
+        if "gx::fill" in kname:   # (not the runtime's __amd_rocclr_fillBufferAligned memsets)
             per.setdefault(disp, {"duration_ns": dur, "kernel": kname})[ctr] = val
     disps = sorted(per)[1:] or sorted(per)
     keys = [k for k in per[disps[0]] if k != "kernel"]
