@@ -277,7 +277,7 @@ int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int grid_ca
     // step 113 ns + 2.66 us (global), split for local fills 110 ns + 3.37 us.
     // Tracked fills (round 5, profiles/r05_tracked_layouts.txt: the side wave
     // carries the first maximum and the LCS values and sets the pace) layout
-    // 3 113 ns + 12.1 us, the tracked column step 146 ns + 3.45 us, both
+    // 3 104 ns + 11.9 us, the tracked column step 146 ns + 3.45 us, both
     // modes: layout 3 only for short pairs (n below about a quarter of m)
     const bool local = sc.floor_ == 0;
     double est1 = 0, est3 = 0;   // the launch's slowest pair on each layout (ns)
@@ -285,7 +285,7 @@ int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int grid_ca
         const double S = (double)ceil_div((int)h.n, kStripRows1), m = (double)h.m;
         if (track) {
             est1 = std::max(est1, m * 146.0 + S * 3450.0);
-            est3 = std::max(est3, m * 113.0 + S * 12100.0);
+            est3 = std::max(est3, m * 104.0 + S * 11900.0);
         } else {
             est1 = std::max(est1, local ? m * 110.0 + S * 3370.0 : m * 113.0 + S * 2660.0);
             est3 = std::max(est3, local ? m * 57.5 + S * 6660.0 : m * 50.0 + S * 6460.0);

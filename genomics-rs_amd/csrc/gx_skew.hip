@@ -455,6 +455,7 @@ struct SideCtx {
     uint32_t cvoff;
     int c1;                              // this row's symbol
     int gs;                              // the shift per column of the tracked values (global: g; local: 0)
+    v4i mu_next;                         // lane 0: the next group's LCS ring values, read one group ahead
 };
 
 // I(i, j) from the row's previous cell, as the core computes it (the core
@@ -540,17 +541,30 @@ __device__ __forceinline__ void side_group(SideState& st, SideCtx& w, const int 
 // so that the sides' chain of LCS values lags no more per strip than the
 // cores' chain (a side waits for its core's sub-blocks; a longer lag would
 // accumulate strip by strip and stall the cores on hand-off space).
+// Lane 0: LCS ring group G of the strip above (the other lanes read the zero block).
+__device__ __forceinline__ v4i side_mread(const SideCtx& w, int G) {
+    return *(const lds_v4i*)(uintptr_t)(w.mrd_base + __umul24((uint32_t)G, w.mrd_m16));
+}
+
 template <bool LOCAL, bool PLANES, int MODE, bool TRACK>
 __device__ __forceinline__ void side_track_group(SideState& st, SideCtx& w, const int t, const int4 (&hv)[2],
                                                  const int4 cc) {
     int4 mu = make_int4(0, 0, 0, 0), mp;
+    // TRACK: the group's LCS inputs (columns t+1 .. t+4) were read one group
+    // ago and checked then; the next group's are read now against a count
+    // peeked now and checked at the end of the group (a re-read only if the
+    // strip above was behind), so no LDS round trip waits on the path (as
+    // the core reads its ring, core_group)
+    int need = 0, seen = 0;
     if (TRACK) {
-        w.tr_wait += wait_ge(w.mw_in, min(t + 4, w.m) + 1, w.status);
-        const lds_v4i* a = (const lds_v4i*)(uintptr_t)(w.mrd_base + __umul24((uint32_t)sk_grp(t + 1), w.mrd_m16));
-        const v4i x = *a;
+        const v4i x = w.mu_next;
         mu = make_int4(x[0], x[1], x[2], x[3]);
+        need = min(t + 8, w.m) + 1;
+        seen = lds_peek(w.mw_in);
         asm volatile("" ::: "memory");
-        lds_post(w.mr_in, min(t + 5, w.m + 1));
+        w.mu_next = side_mread(w, sk_grp(t + 5));
+        asm volatile("" ::: "memory");
+        lds_post(w.mr_in, min(t + 5, w.m + 1));   // (the ring's 252-column window keeps t+5 .. t+8 in place)
     }
     side_group<LOCAL, PLANES, MODE, TRACK>(st, w, t, hv, mu, cc, mp);
     if (TRACK && t >= 64 && t - 63 <= w.m) {
@@ -558,6 +572,10 @@ __device__ __forceinline__ void side_track_group(SideState& st, SideCtx& w, cons
         *a = v4i{mp.x, mp.y, mp.z, mp.w};
         asm volatile("" ::: "memory");
         lds_post(w.mw_out, min(t - 60, w.m) + 1);
+    }
+    if (TRACK && __builtin_amdgcn_readfirstlane(seen) < need) {   // the strip above was behind: wait, re-read
+        w.tr_wait += wait_ge(w.mw_in, need, w.status);
+        w.mu_next = side_mread(w, sk_grp(t + 5));
     }
 }
 
@@ -605,6 +623,10 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, SideCtx
     }
     const int T = m + kWave;
     int4 cc4[4] = {};
+    if (TRACK) {   // the first group's LCS inputs (side_track_group reads one group ahead)
+        w.tr_wait += wait_ge(w.mw_in, min(4, m) + 1, w.status);
+        w.mu_next = side_mread(w, sk_grp(1));
+    }
     if (TRACK) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
