@@ -135,12 +135,15 @@ struct PkScores {
     uint32_t ng, na, Z;      // local (unshifted values): -g, -(h + g) (>= 0), and the biased zero of the floor
 };
 
-// Twin plane code (PLANES == 2, 2 B per cell): the three differences of a
-// cell in one 16-bit word, code = x_I + 16 x_S + 512 x_D (mod 2^16), x_I in
-// [0, 15] (shifted: I'' - I''(j-1)), x_S = S - I in [-16, 15], x_D = D - I in
-// [-64, 63] (gx_api_plan.cpp w16_ok checks the ranges); both pairs' codes of a
-// cell in one dword, as the halves already hold them.  Two v_pk_mad_u16 and
-// three v_pk_sub_i16 per two cells (the byte format: three SDWA per cell).
+// Twin plane code (PLANES == 2, 2 B per cell): a cell's two differences in
+// one 16-bit word, code = x_S + 32 x_D (mod 2^16), x_S = S - I in [-16, 15],
+// x_D = D - I in [-64, 63] (gx_api_plan.cpp w16_ok checks the ranges); both
+// pairs' codes of a cell in one dword, as the halves already hold them.  I
+// itself is not stored: it follows from the row's previous cell, I(i, j) =
+// I(i, j-1) + g + max(0, max(x_S, x_D)(i, j-1) + h) (local: then max(., 0)),
+// the insert recurrence of algo.rs:231-236 (cell_pk), which every decoder
+// replays along the row (round 5; the x_I field of the earlier format cost a
+// third v_pk_mad_u16 per two cells).
 // Small-alphabet twins (TBL, the launch's <= 4 symbols in Scores32.sym): a
 // row's score table (byte k: the shifted match score if c1 is symbol k, else
 // the shifted mismatch score, both in [0, 255]) and a column's selector for
@@ -155,12 +158,13 @@ __device__ __forceinline__ uint32_t perm_selector(int code0, int code1) {
     return (uint32_t)code0 | 0x0C00u | ((uint32_t)(4 + code1) << 16) | 0x0C000000u;
 }
 
-// Stored negated: -code = 527 I + I(j-1) - 16 S - 512 D (mod 2^16), three
-// v_pk_mad_u16 on the cell's values directly instead of three differences and
-// two mads; the offset-binary bias cancels (527 + 1 - 16 - 512 = 0).  The
-// decoders (gx_kernels.hip w16_word_of, plane_sums_kernel) negate it back.
+// code = S + 32 D - 33 I (mod 2^16): two v_pk_mad_u16 on the cell's values
+// directly; the offset-binary bias cancels (1 + 32 - 33 = 0).  Decoders:
+// gx_kernels.hip w16_word_of, plane_sums_kernel, export_w16_kernel,
+// local_col_kernel.  (Iold: unused since the format dropped x_I.)
 __device__ __forceinline__ uint32_t w16_code(uint32_t I, uint32_t D, uint32_t S, uint32_t Iold) {
-    return pmad(D, 0xFE00FE00u, pmad(S, 0xFFF0FFF0u, pmad(I, 0x020F020Fu, Iold)));
+    (void)Iold;
+    return pmad(I, 0xFFDFFFDFu, pmad(D, 0x00200020u, S));
 }
 
 // One row of a lane, both pairs: the cell left of the one being computed.

@@ -1151,6 +1151,21 @@ __global__ void tb_chase_kernel(const TbDev* __restrict__ jobs) {
 // row are rebuilt; the walk (tb_strip_kernel) never uses a word outside them
 // once its rows have converged (every path cell lies in that range).  One
 // block of 128 threads per strip, one thread per row.
+// A twin plane code (gx_fill_pk.hip w16_code: x_S + 32 x_D mod 2^16, this
+// pair's 16-bit half) -> x_S = S - I (5-bit signed), x_D = D - I (7-bit signed).
+__device__ __forceinline__ void w16_decode(uint32_t code16, int& xS, int& xD) {
+    xS = (int)(code16 << 27) >> 27;
+    xD = (int)(short)(unsigned short)(code16 - (uint32_t)xS) >> 5;
+}
+// The format stores no x_I: I(i, j) from I(i, j-1) and the previous cell's
+// max(x_S, x_D) -- the fill's insert recurrence, algo.rs:231-236 --
+// I + g + max(0, m + h), local max(that, 0).  A row starts at I(i, 0) =
+// H(i, 0) + h with m = -h (global) or 0 (local), as the fill seeds it.
+__device__ __forceinline__ int w16_next_I(int I, int mprev, int h, int g, bool local) {
+    const int v = I + g + max(0, mprev + h);
+    return local ? max(v, 0) : v;
+}
+
 // The code word (cD << 16 | cI, first step in bit 15) of 16 steps of one row
 // from its four 4-step groups of twin plane codes (this pair's half `sh`).
 __device__ __forceinline__ uint32_t w16_word_of(const uint4 (&w4)[4], const int sh) {
@@ -1160,10 +1175,8 @@ __device__ __forceinline__ uint32_t w16_word_of(const uint4 (&w4)[4], const int 
         const uint32_t wk[4] = {w4[g].x, w4[g].y, w4[g].z, w4[g].w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t code = (0u - (wk[k] >> sh)) & 0xFFFFu;   // (stored negated, gx_fill_pk.hip w16_code)
-            const uint32_t r = code >> 4;                               // x_S + 32 x_D (mod 2^12)
-            const int xS = (int)(r << 27) >> 27;                        // 5-bit signed
-            const int xD = (int)(((r - (uint32_t)xS) >> 5) << 25) >> 25;   // 7-bit signed
+            int xS, xD;
+            w16_decode((wk[k] >> sh) & 0xFFFFu, xS, xD);
             cI = (cI << 1) | (uint32_t)(xS < 0);
             cD = (cD << 1) | (uint32_t)(xD > max(0, xS));
         }
@@ -1482,7 +1495,9 @@ __global__ __launch_bounds__(64) void plane_sums_kernel(const PairDev* __restric
         const int half = d.twin_half;      // the twin's two pairs share its code plane
         const uint8_t* base = (const uint8_t*)d.pI + (size_t)s * d.t4 * kTwinGroupBytes +
                               (size_t)hh * (kTwinGroupBytes / 2) + (size_t)lane * 16;
+        const bool local = floor_ == 0;
         int I = max(h + i * g, floor_) + h;             // H(i, 0) + h, as the fill seeds it
+        int mp = local ? 0 : -h;                        // (its max(S, D) - I)
         for (int q = 0; q < d.t4; ++q) {
             uint4 w4 = make_uint4(0u, 0u, 0u, 0u);
             if (row_ok) w4 = *(const uint4*)(base + (size_t)q * kTwinGroupBytes);
@@ -1491,12 +1506,10 @@ __global__ __launch_bounds__(64) void plane_sums_kernel(const PairDev* __restric
             for (int k = 0; k < 4; ++k) {
                 const int j = 4 * q + k - l + 1;
                 if (!row_ok || j < 1 || j > d.m) continue;
-                const uint32_t code = (0u - (wk[k] >> (16 * half))) & 0xFFFFu;   // (stored negated, w16_code)
-                const int xI = (int)(code & 15u);
-                const uint32_t r = code >> 4;                       // x_S + 32 x_D (mod 2^12)
-                const int xS = (int)(r << 27) >> 27;                // 5-bit signed
-                const int xD = (int)(((r - (uint32_t)xS) >> 5) << 25) >> 25;   // 7-bit signed
-                I += xI + gshift;                                   // shifted fills store x_I - g
+                int xS, xD;
+                w16_decode((wk[k] >> (16 * half)) & 0xFFFFu, xS, xD);
+                I = w16_next_I(I, mp, h, g, local);
+                mp = max(xS, xD);
                 const long long vI = I, vD = I + xD, vS = I + xS;
                 const unsigned long long w = wi + (unsigned long long)j * 0x85EBCA77ull;
                 sI += (unsigned long long)vI * w;
@@ -1607,8 +1620,8 @@ __global__ void export_d8_kernel(const uint8_t* __restrict__ pI, const uint8_t* 
 
 // Export of the twin fill's plane codes (gx_fill_pk.hip w16_code, DESIGN.md
 // 4.4): one thread per row decodes this pair's 16-bit half of each dword,
-// rebuilds I(i, j) = (H(i, 0) + h) + sum (x_I' + g) and adds the plane's x_D
-// or x_S -- the decode of plane_sums_kernel mode 3.  `half` = the pair's half
+// replays I(i, j) along the row (w16_next_I) and adds the plane's x_D or x_S
+// -- the decode of plane_sums_kernel mode 3.  `half` = the pair's half
 // (PairDev.twin_half), the code plane layout [strip][t/4][row-in-lane][lane][t%4]
 // dwords.  Rows row0 .. row0 + rows - 1 (each at least 1).
 __global__ void export_w16_kernel(const uint8_t* __restrict__ codes, int half, int which, int32_t* __restrict__ out,
@@ -1619,16 +1632,18 @@ __global__ void export_w16_kernel(const uint8_t* __restrict__ codes, int half, i
     const int s = (i - 1) / kStripRows, rho = (i - 1) % kStripRows;
     const int l = rho >> 1, hh = rho & 1;
     const uint8_t* base = codes + (size_t)s * t4 * kTwinGroupBytes + (size_t)hh * (kTwinGroupBytes / 2) + (size_t)l * 16;
+    const bool local = floor_ == 0;
+    (void)gshift;
     int I = max(h + i * g, floor_) + h;   // H(i, 0) + h, as the fill seeds it
+    int mp = local ? 0 : -h;              // (its max(S, D) - I)
     int32_t* o = out + (size_t)r * (m + 1);
     for (int j = 1; j <= m; ++j) {
         const int t = j - 1 + l;
         const uint32_t wd = *(const uint32_t*)(base + (size_t)(t >> 2) * kTwinGroupBytes + (size_t)(t & 3) * 4);
-        const uint32_t code = (0u - (wd >> (16 * half))) & 0xFFFFu;   // (stored negated)
-        const uint32_t q = code >> 4;                                  // x_S + 32 x_D (mod 2^12)
-        const int xS = (int)(q << 27) >> 27;                           // 5-bit signed
-        const int xD = (int)(((q - (uint32_t)xS) >> 5) << 25) >> 25;   // 7-bit signed
-        I += (int)(code & 15u) + gshift;                               // x_I - g stored
+        int xS, xD;
+        w16_decode((wd >> (16 * half)) & 0xFFFFu, xS, xD);
+        I = w16_next_I(I, mp, h, g, local);
+        mp = max(xS, xD);
         o[j] = which == 0 ? I : which == 1 ? I + xD : I + xS;
     }
 }
@@ -1757,10 +1772,13 @@ hipError_t launch_export(const int32_t* plane, int32_t* out, int n, int m, int t
 // score_max only; finalize_kernel has picked the last row holding the pair's
 // maximum (PairRes.lmax_i, lmax_val).  This finds that row's LAST column
 // holding it (the reference's row-major max_by, algo.rs:310-322) from the twin
-// plane codes: I(i, j) = I(i, 0) + sum (x_I' + g), I(i, 0) = H(i, 0) + h = h
-// (local), score_max = I + max(0, x_S, x_D).  One wave per
-// pair: each lane decodes a chunk of the row, an exclusive scan of the chunk
-// sums gives every lane its starting I, and the highest matching column wins.
+// plane codes: I(i, j) = max(I(i, j-1) + d_j, 0) with d_j = g + max(0,
+// m(i, j-1) + h), m = max(x_S, x_D) of the previous cell (w16_next_I; I(i, 0)
+// = H(i, 0) + h = h, m = 0), score_max = I + max(0, x_S, x_D).
+// One wave per pair: each lane takes a chunk of the row; the maps x -> max(x
+// + A, B) that the chunks apply to I compose (max(max(x + A1, B1) + A2, B2)
+// = max(x + A1 + A2, max(B1 + A2, B2))), so an exclusive scan of them gives
+// every lane its starting I, and the highest matching column wins.
 __global__ __launch_bounds__(64) void local_col_kernel(const PairDev* __restrict__ pairs, PairRes* __restrict__ pres,
                                                       const int h, const int g) {
     const PairDev d = pairs[blockIdx.x];
@@ -1773,28 +1791,38 @@ __global__ __launch_bounds__(64) void local_col_kernel(const PairDev* __restrict
                           (size_t)l * 16;
     const int sh = 16 * d.twin_half;
     const int C = (d.m + kWave - 1) / kWave, j0 = lane * C + 1, j1 = min(d.m, j0 + C - 1);
-    auto code_at = [&](int j, int& xI, int& xS, int& xD) {
+    auto code_at = [&](int j, int& xS, int& xD) {
         const int t = j + l - 1;   // the step at which this row computes column j (anti-diagonal skew)
         const uint32_t w = *(const uint32_t*)(base + (size_t)(t >> 2) * kTwinGroupBytes + (size_t)(t & 3) * 4);
-        const uint32_t code = (0u - (w >> sh)) & 0xFFFFu;   // (stored negated, gx_fill_pk.hip w16_code)
-        xI = (int)(code & 15u);
-        const uint32_t q = code >> 4;
-        xS = (int)(q << 27) >> 27;
-        xD = (int)(((q - (uint32_t)xS) >> 5) << 25) >> 25;
+        w16_decode((w >> sh) & 0xFFFFu, xS, xD);
     };
-    int sum = 0;
-    for (int j = j0; j <= j1; ++j) { int a, b, c; code_at(j, a, b, c); sum += a + g; }
-    int pre = sum;   // inclusive scan over the lanes
-    for (int o = 1; o < kWave; o <<= 1) {
-        const int v = __shfl_up(pre, o);
-        if (lane >= o) pre += v;
-    }
-    int I = h + pre - sum, last = 0;
+    constexpr int kLow = INT_MIN / 4;   // "no floor yet" (far below every value, no overflow when shifted)
+    int mp0 = 0;                        // m of the cell before the chunk (column 0: 0)
+    if (j0 >= 2 && j0 <= j1) { int a, b; code_at(j0 - 1, a, b); mp0 = max(a, b); }
+    int A = 0, B = kLow, mp = mp0;      // the chunk's map x -> max(x + A, B)
     for (int j = j0; j <= j1; ++j) {
-        int a, b, c;
-        code_at(j, a, b, c);
-        I += a + g;
-        if (I + max(0, max(b, c)) == target) last = j;
+        int a, b;
+        code_at(j, a, b);
+        const int dj = g + max(0, mp + h);
+        A += dj; B = max(B + dj, 0);
+        mp = max(a, b);
+    }
+    // exclusive scan of the maps over the lanes (earlier chunks first)
+    int SA = A, SB = B;                 // inclusive: this chunk after all earlier ones
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int pa = __shfl_up(SA, o), pb = __shfl_up(SB, o);
+        if (lane >= o) { SB = max(pb + SA, SB); SA = pa + SA; }
+    }
+    int EA = __shfl_up(SA, 1), EB = __shfl_up(SB, 1);   // exclusive
+    if (lane == 0) { EA = 0; EB = kLow; }
+    int I = max(h + EA, EB), last = 0;
+    mp = mp0;
+    for (int j = j0; j <= j1; ++j) {
+        int a, b;
+        code_at(j, a, b);
+        I = w16_next_I(I, mp, h, g, true);
+        mp = max(a, b);
+        if (I + max(0, max(a, b)) == target) last = j;
     }
     for (int o = 32; o > 0; o >>= 1) last = max(last, __shfl_xor(last, o));
     if (lane == 0) r->lmax_j = last;
