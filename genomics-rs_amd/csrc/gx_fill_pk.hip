@@ -169,7 +169,7 @@ __device__ __forceinline__ uint32_t w16_code(uint32_t I, uint32_t D, uint32_t S,
 
 // One row of a lane, both pairs: the cell left of the one being computed.
 struct RowPk {
-    uint32_t I, SD, Dd, SMp, SMtl;   // insert, max(sub, delete), delete successor, score_max + sm'', SMp(i-1, j-1)
+    uint32_t I, Hx, Dd, SMp, SMtl;   // insert, score_max + h (local + g), delete successor, score_max + sm'', SMp(i-1, j-1)
     uint32_t cI, cD;                 // code bit-planes, negated (16 steps, one per half; pcode)
     uint32_t E, Etl;                 // landing columns (int16 per half)
     uint32_t lb;                     // local: the largest score_max along the row (biased)
@@ -203,8 +203,13 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
                                         const PkScores& k,
                                         uint32_t& oI, uint32_t& oD, uint32_t& oS, uint32_t& oIold) {
     const uint32_t Ig = LOCAL ? st.I - k.ng : st.I;                // (biased halves: no borrow across them)
-    const uint32_t In = LOCAL ? pmaxu(pmaxu(Ig, st.SD - k.na), k.Z)   // max(I + g, max(S,D) + h + g, 0)
-                              : pmaxu(st.I, st.SD - k.nh);          // max(I, max(S,D) + h)   (algo.rs:231-236)
+    // the gap terms fold onto score_max H = max(I, S, D) (h <= 0: I + h never
+    // wins against I, nor D + h against D): I' = max(I, H + h) and D(i+1) =
+    // max(D, H + h) share Hx = H + h, one subtraction and one max fewer per
+    // cell pair than max(S, D) + h and max(I, S) + h (round 5; local: + g and
+    // the 0 floor, algo.rs:231-243)
+    const uint32_t In = LOCAL ? pmaxu(pmaxu(Ig, st.Hx), k.Z)         // max(I + g, H + h + g, 0)
+                              : pmaxu(st.I, st.Hx);                 // max(I, H + h)   (algo.rs:231-236)
     // SM(i-1,j-1) + s''  (algo.rs:245-248).  TBL: c1/c1h are the row's score
     // tables of the two pairs (byte k: s_match'' if the row's char is symbol
     // k, else s_mismatch''; SM is then kept without the s_match'' offset) and
@@ -215,9 +220,9 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
     const uint32_t Dn = dd_in;                                     // (algo.rs:238-243, from the row above)
     const uint32_t IS = pmaxu(In, Sn);
     const uint32_t SMn = pmaxu(IS, Dn);
-    const uint32_t SDn = pmaxu(Sn, Dn);
-    const uint32_t Ddn = LOCAL ? pmaxu(pmaxu(IS - k.na, Dn - k.ng), k.Z)   // D(i+1, j), local
-                               : pmaxu(IS - k.nh, Dn);             // D(i+1, j)
+    const uint32_t Hxn = LOCAL ? SMn - k.na : SMn - k.nh;          // (biased halves: no borrow across them)
+    const uint32_t Ddn = LOCAL ? pmaxu(pmaxu(Hxn, Dn - k.ng), k.Z)   // D(i+1, j), local
+                               : pmaxu(Hxn, Dn);                   // D(i+1, j)
     // retrace priority S > I > D (algo.rs:351-400): m1 = I beats S, m2 = D beats both
     // (NOE: no landing columns -- the twin fill without a skeleton, whose
     // traceback walks the strips in sequence, tb_seq_kernel; with no code
@@ -232,11 +237,11 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
     if (LOCAL)      // the row's largest score_max (its last column: local_col_kernel, from the plane codes)
         st.lb = pmaxu(st.lb, MASKED ? bfi(act, SMn, k.Z) : SMn);
     if (MASKED) {   // act: 0xFFFF in each half whose pair has this column
-        st.I = bfi(act, In, st.I); st.SD = bfi(act, SDn, st.SD); st.Dd = bfi(act, Ddn, st.Dd);
+        st.I = bfi(act, In, st.I); st.Hx = bfi(act, Hxn, st.Hx); st.Dd = bfi(act, Ddn, st.Dd);
         st.SMp = bfi(act, SMpn, st.SMp);
         if (!NOE) st.E = bfi(act, En, st.E);
     } else {
-        st.I = In; st.SD = SDn; st.Dd = Ddn; st.SMp = SMpn;
+        st.I = In; st.Hx = Hxn; st.Dd = Ddn; st.SMp = SMpn;
         if (!NOE) st.E = En;
     }
     if (CODES) { st.cI = cIn; st.cD = cDn; }
@@ -444,7 +449,7 @@ __device__ __forceinline__ void fold_lb(RowPk& r, int (&mx)[2], int B0, int B1) 
 
 // Shift every value of the lane state to new bases (delta = new - old).
 __device__ __forceinline__ void rebase_row(RowPk& r, uint32_t dpk) {
-    r.I = psubs(r.I, dpk); r.SD = psubs(r.SD, dpk); r.Dd = psubs(r.Dd, dpk);
+    r.I = psubs(r.I, dpk); r.Hx = psubs(r.Hx, dpk); r.Dd = psubs(r.Dd, dpk);
     r.SMp = psubs(r.SMp, dpk); r.SMtl = psubs(r.SMtl, dpk);
 }
 __device__ __forceinline__ void rebase(LanePk& st, uint32_t dpk) {
@@ -472,7 +477,7 @@ __device__ __forceinline__ void init_row_pk(RowPk& rs, const Scores32& sc, int B
     rs.lb = 0;
     if (LOCAL) {
         rs.I = pk2(sc.h - B0, sc.h - B1) ^ kBias2;
-        rs.SD = pk2(sc.h - B0, sc.h - B1) ^ kBias2;
+        rs.Hx = pk2(sc.hg - B0, sc.hg - B1) ^ kBias2;   // H(i, 0) + h + g = h + g
         rs.Dd = pk2(-B0, -B1) ^ kBias2;
         rs.SMp = padds(pk2(-B0, -B1) ^ kBias2, k.smp);
         rs.SMtl = 0;
@@ -480,7 +485,7 @@ __device__ __forceinline__ void init_row_pk(RowPk& rs, const Scores32& sc, int B
         return;
     }
     rs.I = pk2(2 * sc.h - B0, 2 * sc.h - B1) ^ kBias2;
-    rs.SD = pk2(sc.h - B0, sc.h - B1) ^ kBias2;
+    rs.Hx = pk2(2 * sc.h - B0, 2 * sc.h - B1) ^ kBias2;   // H''(i, 0) + h = 2h
     rs.Dd = pk2(sc.h - B0, sc.h - B1) ^ kBias2;
     rs.SMp = padds(pk2(sc.h - B0, sc.h - B1) ^ kBias2, k.smp);
     rs.SMtl = 0;
