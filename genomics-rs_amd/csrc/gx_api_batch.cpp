@@ -136,11 +136,14 @@ static int batch_core(gx_context* ctx, const std::vector<PairHost>& ph,
 // and results are those of the last pass; *fill_ms is the mean fill time.
 // Overlapped pipeline for a global untracked batch on the twin fill without
 // landing columns (the sequential strip walk, tb_seq_kernel, ~5 ms for a 30k
-// pair, uses a few CUs): the pairs are split into a small group A (about a
-// fifth) and the rest, B, each filled by its own launch on its own stream.
+// pair, uses a few CUs): the pairs are split into group A (half of them;
+// local batches a fifth) and group B, each filled by its own launch on its
+// own stream.
 // Step k's walk (stream tstream, after both fills) then runs beside step k+1's
 // group-A fill, whose plane codes go to a second A buffer (two A buffers, one
-// B buffer: the device holds P + |A| pairs' planes); step k+1's group-B fill
+// B buffer: the device holds P + |A| <= 1.5 P pairs' planes, <= 3 B a cell
+// of twin codes, within the 3.25 B a cell the chunk plan budgets for a pair
+// of a compact-plane batch); step k+1's group-B fill
 // waits on the device for step k's walk before it reuses B's buffers.  Only
 // buffers no pending work uses go back to the pool (a walk's fills after it
 // was collected; B's before its next fill, which waits for the walk that
@@ -155,7 +158,16 @@ static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
                               const std::vector<size_t>* off2, const SmallAlpha& alpha,
                               const std::vector<size_t>& idx, const PassSet* alt) {
     const size_t P = ph.size(), Q = idx.size();
-    const size_t G = std::max<size_t>(2, (Q / 5) & ~(size_t)1);   // group A: about a fifth, even (twins)
+    // group A: half the pairs (global), even (twins).  Two equal launches
+    // fill the chip better than a small A beside a large B: 80 x 30k, fill ms
+    // a pass by A's pairs 8 / 16 / 24 / 32 / 40 = 33.7 / 29.9 / 29.0 / 27.0 /
+    // 26.5 (the one-launch pass 27.8); all-vs-all with planes 20.4 -> 17.0 ms,
+    // 1024 x 16k 100.4 -> 99.4.  Local batches keep a fifth (64 related local
+    // pairs 26.9 ms against 27.9 at half; profiles/r05_overlap_split.txt).
+    // GX_OVERLAP_A sets A's pair count.
+    size_t G = std::max<size_t>(2, (is_local ? Q / 5 : Q / 2) & ~(size_t)1);
+    if (const char* e = getenv("GX_OVERLAP_A"); e && atoi(e) >= 2 && (size_t)atoi(e) + 2 <= Q)
+        G = (size_t)atoi(e) & ~(size_t)1;
     std::vector<size_t> gi[2];
     gi[0].assign(idx.begin(), idx.begin() + (long)G);
     gi[1].assign(idx.begin() + (long)G, idx.end());
