@@ -208,7 +208,10 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
         if ((rc = pool_get(ctx, chars_bytes, &job.chars, fs))) return rc;
     }
     if (planes && (rc = pool_get(ctx, plane_elems * plane_esz * nplanes, &job.planes, fs))) return rc;
-    if (codes && (rc = pool_get(ctx, code_elems * sizeof(uint32_t), &job.codes, fs))) return rc;
+    // (no code-word buffer for a fill that stores none: 0.25 B a cell, 21 GB of
+    // a 20-pair 64k chunk, which the overlapped pipeline's second A group needs)
+    const bool want_codes = codes && !job.nocodes;
+    if (want_codes && (rc = pool_get(ctx, code_elems * sizeof(uint32_t), &job.codes, fs))) return rc;
     if ((rc = pool_get(ctx, std::max<size_t>(skel_elems, 1) * sizeof(int), &job.skel, fs))) return rc;
     if ((rc = pool_get(ctx, std::max<size_t>(feed_recs, 1) * sizeof(Rec), &job.feed, fs))) return rc;
     if ((rc = pool_get(ctx, std::max(strips, 1) * sizeof(StripRes), &job.sres, fs))) return rc;
@@ -265,7 +268,7 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
         d.pD = (planes && !w16) ? plane_at(1) : nullptr;
         d.pS = (planes && !w16) ? plane_at(2) : nullptr;
         d.pL = (planes && lcs) ? plane_at(3) : nullptr;
-        d.codes = codes ? (uint32_t*)job.codes.p + co[p] : nullptr;
+        d.codes = want_codes ? (uint32_t*)job.codes.p + co[p] : nullptr;
         d.skel = (int*)job.skel.p + so[p];
         d.feed = (Rec*)job.feed.p + fo[p];
         d.progress = progress + gofs[p];

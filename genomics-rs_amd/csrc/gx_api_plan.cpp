@@ -446,6 +446,12 @@ std::vector<std::pair<size_t, size_t>> plan_chunks(gx_context* ctx, const std::v
                                                    double plane_bpc) {
     const double budget = chunk_budget(ctx);
     auto out = plan_chunks_within(ph, plane_bpc, budget);
+    if (const char* e = getenv("GX_LOG"); e && !strcmp(e, "debug")) {
+        size_t fr = 0, tot = 0;
+        (void)hipMemGetInfo(&fr, &tot);
+        fprintf(stderr, "[gx DEBUG] chunk plan: %zu pairs, %.2f B/cell, budget %.3e B (free %zu of %zu, %zu cached) -> %zu chunks\n",
+                ph.size(), plane_bpc, budget, fr, tot, ctx->free_list.size(), out.size());
+    }
     if (out.size() > 1) {
         double total = 0;
         for (size_t p = 0; p < ph.size(); ++p)

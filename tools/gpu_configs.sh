@@ -8,7 +8,9 @@ rm -rf "$O" && mkdir -p "$O"
 run() {   # name, bench args
   timeout -k 10 400 python bench.py "${@:2}" --no-cpu-baseline --int32-steps 0 --no-plane-steps 0 \
       > "$O/$1.json" 2> "$O/$1.err" || { echo BENCH_FAIL $1; tail -20 "$O/$1.err"; exit 1; }
-  python3 -c "import json,sys;d=json.load(open('$O/$1.json'));r=d['roofline'];h=r.get('hbm',r);print('$1',d['value'],'GCUPS','fill_ms',r['fill_ms_avg'],'ms/step',d['ms_per_step'],'frac',r['frac'],r['unit'],'hbm',h['frac'],'chunks',d['fill_launch'].get('chunks'),'parity',d.get('parity',{}).get('pairs_checked'))"
+  python3 -c "import json,sys;d=json.load(open('$O/$1.json'))
+if 'roofline' not in d: print('$1', d.get('predicted'), 'parity', d.get('parity', {}).get('pair_passes_checked')); sys.exit()
+r=d['roofline'];h=r.get('hbm',r);print('$1',d['value'],'GCUPS','fill_ms',r['fill_ms_avg'],'ms/step',d['ms_per_step'],'frac',r['frac'],r['unit'],'hbm',h['frac'],'chunks',d['fill_launch'].get('chunks'),'parity',d.get('parity',{}).get('pairs_checked'))"
 }
 run config2_covid --workload covid
 run config3_brca2 --workload brca2
