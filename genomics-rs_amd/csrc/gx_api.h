@@ -470,6 +470,8 @@ std::vector<std::pair<int, int>> twin_table(const std::vector<PairHost>& ph, lon
 int twin_width(const std::vector<PairHost>& ph, const std::vector<std::pair<int, int>>& tw, const Scores32& sc,
                int is_local, bool track, bool lcs, int lay, bool planes, bool d8, int W_want,
                bool long_ok = false);
+double pair_device_bytes(size_t n, size_t m, double plane_bpc);   // one pair's device bytes in a batch
+double chunk_budget(gx_context* ctx);                             // device bytes one chunk may use
 std::vector<std::pair<size_t, size_t>> plan_chunks(gx_context* ctx, const std::vector<PairHost>& ph,
                                                    double plane_bpc);
 

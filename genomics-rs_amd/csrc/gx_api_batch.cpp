@@ -165,7 +165,9 @@ static int batch_core_overlap(gx_context* ctx, const std::vector<PairHost>& ph,
     // 1024 x 16k 100.4 -> 99.4.  Local batches keep a fifth (64 related local
     // pairs 26.9 ms against 27.9 at half; profiles/r05_overlap_split.txt).
     // GX_OVERLAP_A sets A's pair count.
-    size_t G = std::max<size_t>(2, (is_local ? Q / 5 : Q / 2) & ~(size_t)1);
+    // (half rounded up: a chunked batch's 19- and 20-pair chunks then both
+    // split 10 + 9 / 10 + 10 and reuse the same cached plane buffers)
+    size_t G = std::max<size_t>(2, (is_local ? Q / 5 : (Q + 1) / 2) & ~(size_t)1);
     if (const char* e = getenv("GX_OVERLAP_A"); e && atoi(e) >= 2 && (size_t)atoi(e) + 2 <= Q)
         G = (size_t)atoi(e) & ~(size_t)1;
     std::vector<size_t> gi[2];
@@ -351,7 +353,7 @@ int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
             alpha.add(dproc[q].first, dph[q].n);
             alpha.add(dproc[q].second, dph[q].m);
         }
-    FillJob jobs[2];
+    FillJob jobs[3];
     std::vector<PairRes> res(P, PairRes{});
     std::vector<TbStart> starts(idx.size());
     std::vector<uint64_t> si(P), sj(P);
@@ -359,10 +361,11 @@ int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
     std::vector<int> dev_of(P, -1);
     for (size_t q = 0; q < idx.size(); ++q) dev_of[idx[q]] = (int)q;
     double fsum = 0;
-    auto fill = [&](int s) {   // slot s = the pass's parity = its pair set
-        return run_fill(ctx, dproc_s[s], dph_s[s], sc, is_local, planes, track, false, jobs[s], chars_dev,
-                        chars_dev ? &o1_s[s] : nullptr, chars_dev ? &o2_s[s] : nullptr, &alpha, s, false);
+    auto fill_at = [&](int s, int v) {   // slot s (pinned staging, events, job), pair set v
+        return run_fill(ctx, dproc_s[v], dph_s[v], sc, is_local, planes, track, false, jobs[s], chars_dev,
+                        chars_dev ? &o1_s[v] : nullptr, chars_dev ? &o2_s[v] : nullptr, &alpha, s, false);
     };
+    auto fill = [&](int s) { return fill_at(s, s); };   // slot s = the pass's parity = its pair set
     // results of slot s's fill -> start cells -> its traceback queued; the fill
     // buffers return to the pool (their last user, the traceback, is queued)
     int pl_pass = 0;
@@ -421,9 +424,45 @@ int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
         // fill slow each other down on shared CUs (fill 0.56 -> 0.67 ms beside
         // a walk stretched from 0.30 to 0.82), and the host's labelling then
         // leaves the device idle between pairs of steps.)
+        //
+        // Three slots in flight: pass k+2's fill and walk are queued before
+        // the host waits for pass k's records, so the record copy (4.3 MB on
+        // a 1024 x 1k pass, ~0.22 ms on the copy engine after the walk) and
+        // the labelling (~0.52 ms) of pass k run beside passes k+1 and k+2 on
+        // the device.  One slot ahead, the next fill was queued only after
+        // the labelling: the device sat idle ~0.2 ms a pass (rocprofv3
+        // timeline, 1024 x 1k).  A slot's pinned buffers are rewritten when
+        // pass k+3 is queued, after pass k was labelled; its device
+        // descriptor caches on the fill stream, in stream order.
         int tr_pass = 0;
-        bool held[2] = {false, false};
+        bool held[3] = {false, false, false};
+        // the walk on its own stream beside the next pass's fill, when the
+        // two more passes' fill buffers this holds (a walk keeps its fill's
+        // buffers until it is collected) fit the free HBM as it is -- not by
+        // evicting the pool's cached buffers, whose re-allocation costs far
+        // more (hipMalloc of an 86 GB plane buffer ~2.4 s: a 4-pair 64k batch
+        // that evicted them cost the next 1024 x 64k batch 7 s).  1024 x 1k
+        // 0.94 -> 0.84 ms a pass, 1024 x 4k 7.93 -> 7.57 (tools/walk_prio_ab.sh).
+        // (With one slot ahead it was slower: the labelling, not the device,
+        // then set the pace.)  GX_TB_OWN_STREAM=0 keeps the walk on the fill's
+        // stream.
+        bool wstream = !ctx->keep_capture && !(getenv("GX_TB_OWN_STREAM") && !strcmp(getenv("GX_TB_OWN_STREAM"), "0"));
+        if (wstream) {
+            double need = 0;
+            for (const PairHost& h : dph) need += pair_device_bytes(h.n, h.m, 2.0);
+            size_t fr = 0, tot = 0;
+            wstream = hipMemGetInfo(&fr, &tot) == hipSuccess && 2.0 * need <= (double)fr - 4.0 * (1ull << 30);
+        }
+        if (wstream && !ctx->tstream && hipStreamCreateWithFlags(&ctx->tstream, hipStreamNonBlocking) != hipSuccess)
+            return fail(GX_EHIP, "walk stream");
+        bool jheld[3] = {false, false, false};
         auto trace_dev = [&](int s) {
+            if (wstream) {   // the walk on its own stream; the fill's buffers held until it is collected
+                if (hipStreamWaitEvent(ctx->tstream, ctx->slots[s].fdone, 0) != hipSuccess) return fail(GX_EHIP, "walk stream wait");
+                jheld[s] = true;
+                return run_traceback(ctx, std::vector<const FillJob*>{&jobs[s]}, starts, ctx->slots[s].out, s, false, true,
+                                     ctx->tstream);
+            }
             int r = run_traceback(ctx, jobs[s], starts, ctx->slots[s].out, s, false, true);
             release_or_hold(ctx, jobs[s], tr_pass++ == nsteps - 1, &held[s]);   // stream order: later users come after the traceback
             return r;
@@ -440,19 +479,24 @@ int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
         using clk = std::chrono::steady_clock;
         const auto t_all = clk::now();
         double h_enq = 0, h_tbw = 0, h_res = 0, h_lab = 0;   // host time per phase (GX_LOG=debug)
-        if (!(rc = fill(0))) rc = trace_dev(0);
+        int queued = 0;   // passes whose fill and walk are queued
         for (int k = 0; k < nsteps && !rc; ++k) {
-            const int s = k & 1;
+            const int s = k % 3, v = k & 1;
             auto t = clk::now();
-            if (k + 1 < nsteps && ((rc = fill(s ^ 1)) || (rc = trace_dev(s ^ 1)))) break;
+            while (!rc && queued < std::min(nsteps, k + 3)) {
+                const int q = queued++;
+                if (!(rc = fill_at(q % 3, q & 1))) rc = trace_dev(q % 3);
+            }
+            if (rc) break;
             h_enq += since(t); t = clk::now();
             if ((rc = tb_collect(ctx, s, idx.size(), ctx->slots[s].out))) break;
             h_tbw += since(t); t = clk::now();
             if ((rc = results(s))) break;
+            if (jheld[s]) { job_release(ctx, jobs[s]); jheld[s] = false; }   // its walk has ended
             h_res += since(t); t = clk::now();
-            ctx->pass_off = poff[s];
-            if ((rc = label_batch(ctx, *PH[s], hs, is_local, track, dev_of, si, sj, score, res, ctx->slots[s].out,
-                                  jobs[s].fill_ms, *WK[s])))
+            ctx->pass_off = poff[v];
+            if ((rc = label_batch(ctx, *PH[v], hs, is_local, track, dev_of, si, sj, score, res, ctx->slots[s].out,
+                                  jobs[s].fill_ms, *WK[v])))
                 break;
             h_lab += since(t);
         }
@@ -463,11 +507,12 @@ int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
                     h_tbw / nsteps, h_res / nsteps, h_lab / nsteps);
         if (rc) {
             (void)hipStreamSynchronize(ctx->stream);
+            if (ctx->tstream) (void)hipStreamSynchronize(ctx->tstream);
             for (auto& j : jobs) job_release(ctx, j);
             release_slots(ctx);
             return rc;
         }
-        for (int s = 0; s < 2; ++s)
+        for (int s = 0; s < 3; ++s)
             if (held[s]) { (void)hipStreamSynchronize(ctx->stream); keep_job(ctx, jobs[s], dev_of); }
         if (fill_ms) *fill_ms = fsum / nsteps;
         return GX_OK;

@@ -75,10 +75,17 @@ static int pool_take(gx_context* ctx, size_t bytes, DevBuf* out) {
         const DevBuf& b = ctx->free_list[k];
         if (b.cap >= bytes && b.cap < best) { best = b.cap; bi = (int)k; }
     }
-    // a large request does not take a cached buffer more than twice its size
-    // (that buffer may fit a later, larger request of the same launch)
-    if (bi >= 0 && bytes >= ((size_t)1 << 30) && best > 2 * bytes) bi = -1;
+    // no request takes a cached buffer of 1 GiB or more that is over twice
+    // its size (that buffer may fit a later, larger request of the same
+    // launch; 1024 x 64k chunks ran out of HBM when the 0.7 GB skeleton and
+    // hand-off requests of an overlapped pass took the two 34 GB plane
+    // buffers a smaller batch had left cached.  A tighter 1.25x made the
+    // chunks' alternating 86 / 69 / 95 GB plane requests miss and re-map the
+    // HBM: 1024 x 64k fill 2.0 -> 4.8 s a pass)
+    if (bi >= 0 && best >= ((size_t)1 << 30) && best / 2 > bytes) bi = -1;
     if (bi >= 0) {
+        if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug") && bytes >= ((size_t)1 << 30))
+            fprintf(stderr, "[gx DEBUG] pool hit: %zu B from a cached %zu B\n", bytes, best);
         *out = ctx->free_list[bi];
         ctx->free_list.erase(ctx->free_list.begin() + bi);
         return GX_OK;
@@ -98,7 +105,10 @@ static int pool_take(gx_context* ctx, size_t bytes, DevBuf* out) {
         e = hipMalloc(&p, bytes);
         if (e != hipSuccess) {
             (void)hipGetLastError();
-            return fail(GX_ENOMEM, "hipMalloc(" + std::to_string(bytes) + " B) failed");
+            size_t fr = 0, tot = 0;
+            (void)hipMemGetInfo(&fr, &tot);
+            return fail(GX_ENOMEM, "hipMalloc(" + std::to_string(bytes) + " B) failed (" + std::to_string(fr) +
+                                       " B free of " + std::to_string(tot) + ")");
         }
     }
     out->p = p;
@@ -134,8 +144,17 @@ extern "C" int gx_context_create(int device, gx_context** out) {
     HIPCHK(hipSetDevice(device));
     gx_context* c = new gx_context();
     c->device = device;
+    // every stream of the context up front, in this order: HIP maps streams
+    // onto its hardware queues (GPU_MAX_HW_QUEUES, 4 by default) round robin
+    // at creation, and two streams on one queue run in order.  Created on
+    // first use instead, the walk stream of a short batch ahead of the second
+    // fill stream put that stream on the fill stream's queue: a later
+    // overlapped batch (1024 x 64k) then ran its two fill groups and the walk
+    // in series, fill 1.9 -> 5.4 s a pass.
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->tstream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
     HIPCHK(hipEventCreate(&c->ev2));

@@ -402,14 +402,14 @@ int twin_width(const std::vector<PairHost>& ph, const std::vector<std::pair<int,
 // Device bytes a fill + traceback of pair (n, m) holds: score planes
 // (plane_bpc per cell), traceback codes (0.25 B/cell), skeleton and hand-off
 // rows, traceback records.
-static double pair_device_bytes(size_t n, size_t m, double plane_bpc) {
+double pair_device_bytes(size_t n, size_t m, double plane_bpc) {
     const double cells = (double)(n + 128) * (double)(m + 64);
     return cells * (plane_bpc + 0.25) + 64.0 * (double)(m + 64) * (double)(n / 64 + 2) / 8.0 + 65536.0;
 }
 
 // Budget for one chunk: GX_CHUNK_BYTES if set, else the free device memory
 // plus the context's cached buffers, less 4 GiB of headroom.
-static double chunk_budget(gx_context* ctx) {
+double chunk_budget(gx_context* ctx) {
     if (const char* e = getenv("GX_CHUNK_BYTES"); e && *e) return atof(e);
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 64e9;

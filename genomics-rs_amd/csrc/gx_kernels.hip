@@ -1401,6 +1401,13 @@ __global__ __launch_bounds__((1 + kSqHelp) * kWave) void tb_seq_kernel(const TbD
         return;
     }
     const int first = (i - 1) / J.srows;
+    // the walker wave issues ahead of its helpers and of a fill sharing the
+    // CU (the walk runs beside the next pass's fill): 1024 x 1k 0.84 -> 0.83
+    // ms a pass with the walk on its own stream, 0.94 -> 0.90 without
+    // (tools/walk_prio_ab.sh)
+#ifndef GX_TB_NOPRIO
+    if (wave == 0) __builtin_amdgcn_s_setprio(3);
+#endif
     // block 0 of the walk: its window from every wave
     int vb = (i - 1) / kTbRows, R = (i - 1) % kTbRows, ce = j;
     int q0 = max(((ce - 1 + tb_lot(J, tb_rho(J, vb, R))) >> 4) - (kSqWin - 1), 0);

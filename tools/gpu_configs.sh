@@ -21,8 +21,8 @@ run config4_allvsall_planes --workload allvsall --planes
 run config4_sim8 --workload allvsall --simulate-world 8
 # config 5 as stated: 1024 pairs per length (batches beyond the free HBM run
 # in chunks through the same buffers; 16k: 825 GB, 64k: 13 TB of compact planes)
-run config5_L1024 --length 1024 --pairs-per-gpu 1024 --single-pair-steps 0
-run config5_L4096 --length 4096 --pairs-per-gpu 1024 --single-pair-steps 0
+run config5_L1024 --length 1024 --pairs-per-gpu 1024 --single-pair-steps 0 --steps 20
+run config5_L4096 --length 4096 --pairs-per-gpu 1024 --single-pair-steps 0 --steps 20
 run config5_L16384 --length 16384 --pairs-per-gpu 1024 --single-pair-steps 0 --steps 3 --warmup 1
 run config5_L65536 --length 65536 --pairs-per-gpu 1024 --single-pair-steps 0 --steps 2 --warmup 1
 echo CONFIGS_DONE
