@@ -110,6 +110,21 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
             for (const auto& t : tw) selfs += t.first == t.second;
             if (4 * selfs > tw.size() + 3) Wt = 0;
         }
+        // 7-wave bands, two workgroups per CU (16 waves: the twin fill's 128
+        // VGPRs allow four a SIMD; 8-wave bands fit one), for global batches
+        // of long pairs with >= 1.25 such bands per workgroup of that grid:
+        // the CU then holds two independent band pipelines.  80 x 30k (each
+        // overlapped group 680 bands on 512 workgroups) fill 26.8 -> 24.6 ms a
+        // pass (2,616 -> 2,852 GCUPS), 1024 x 16k (1,216) 99.5 -> 95.0;
+        // slower with fewer bands (all-vs-all with planes, 374-408: 16.7 ->
+        // 18.5 ms), for the local twin (64 related 30k pairs 1,852 -> 1,359
+        // GCUPS) and beside the many walks of short batches
+        // (profiles/r05_w7_sweep.txt)
+        if (Wt == 8 && !is_local && long_ok && !getenv("GX_BAND_WAVES") && min_strips >= 200) {
+            long long b7 = 0;
+            for (const auto& t : tw) b7 += ceil_div(ceil_div((int)std::max(ph[t.first].n, ph[t.second].n), SR), 7);
+            if (4 * b7 >= 5LL * 2 * fill_grid_cap(ctx->device)) Wt = 7;
+        }
     }
     const bool twin = Wt > 0;
     job.twin = twin;

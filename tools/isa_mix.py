@@ -4,7 +4,7 @@ blocks holding the compact-plane byte inserts), from a device-only assembly
 build of gx_kernels.hip:
 
     python tools/isa_mix.py [kernel-name-regex]   (default: the bench's W=15 compact-plane kernel)
-    python tools/isa_mix.py twin                  (the twin fill, gx_fill_pk.hip, W=8, twin plane codes, score tables, no code words, no skeleton: PLANES 30)
+    python tools/isa_mix.py twin|twin7            (the twin fill, gx_fill_pk.hip, W=8, twin plane codes, score tables, no code words, no skeleton: PLANES 30)
 
 Compiles to /tmp/gx_isa/ (about 2 minutes) unless GX_ISA_S names an existing .s.
 A twin group holds 16 cells per lane (4 steps x 2 rows x 2 pairs)."""
@@ -17,8 +17,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pat = sys.argv[1] if len(sys.argv) > 1 else r"_ZN2gx11fill_kernelILi15ELb0ELi2ELb1ELb0ELb0ELb1ELi0E"
 src, cells = "gx_kernels", 8
-if pat == "twin":
-    pat, src, cells = r"_ZN2gx14fill_pk_kernelILi8ELi30E", "gx_fill_pk", 16
+if pat in ("twin", "twin7"):   # twin7: the 7-wave bands the headline batch takes (two workgroups per CU)
+    pat, src, cells = r"_ZN2gx14fill_pk_kernelILi%sELi30E" % ("7" if pat == "twin7" else "8"), "gx_fill_pk", 16
 s_path = os.environ.get("GX_ISA_S")
 if not s_path:
     os.makedirs("/tmp/gx_isa", exist_ok=True)
