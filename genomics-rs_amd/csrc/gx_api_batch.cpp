@@ -485,7 +485,11 @@ int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
             auto t = clk::now();
             while (!rc && queued < std::min(nsteps, k + 3)) {
                 const int q = queued++;
-                if (!(rc = fill_at(q % 3, q & 1))) rc = trace_dev(q % 3);
+                if ((rc = fill_at(q % 3, q & 1))) break;
+                // two fill workgroups a CU (7-wave bands, run_fill) leave the
+                // walks no room beside the fill: the walk stays on its stream
+                if (q == 0 && ctx->last_W == 7) wstream = false;
+                rc = trace_dev(q % 3);
             }
             if (rc) break;
             h_enq += since(t); t = clk::now();

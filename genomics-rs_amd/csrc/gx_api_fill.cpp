@@ -112,15 +112,18 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
         }
         // 7-wave bands, two workgroups per CU (16 waves: the twin fill's 128
         // VGPRs allow four a SIMD; 8-wave bands fit one), for global batches
-        // of long pairs with >= 1.25 such bands per workgroup of that grid:
-        // the CU then holds two independent band pipelines.  80 x 30k (each
-        // overlapped group 680 bands on 512 workgroups) fill 26.8 -> 24.6 ms a
-        // pass (2,616 -> 2,852 GCUPS), 1024 x 16k (1,216) 99.5 -> 95.0;
-        // slower with fewer bands (all-vs-all with planes, 374-408: 16.7 ->
-        // 18.5 ms), for the local twin (64 related 30k pairs 1,852 -> 1,359
-        // GCUPS) and beside the many walks of short batches
+        // of pairs of >= 32 strips (4,096 rows) with >= 1.25 such bands per
+        // workgroup of that grid: the CU then holds two independent band
+        // pipelines.  80 x 30k (each overlapped group 680 bands on 512
+        // workgroups) fill 26.8 -> 24.6 ms a pass (2,616 -> 2,852 GCUPS),
+        // 1024 x 16k (1,216) 99.5 -> 95.0, 1024 x 4k 7.59 -> 6.78 ms a pass and
+        // 8k 26.7 -> 23.9 (with the walk on the fill's stream: beside the
+        // fill, 1,024 walks found no room on the CUs, 4k once 72 ms a pass;
+        // batch_core_steps); slower with fewer bands (all-vs-all with planes,
+        // 374-408: 16.7 -> 18.5 ms), for 2k pairs (2.25 -> 2.38 ms) and for
+        // the local twin (64 related 30k pairs 1,852 -> 1,359 GCUPS)
         // (profiles/r05_w7_sweep.txt)
-        if (Wt == 8 && !is_local && long_ok && !getenv("GX_BAND_WAVES") && min_strips >= 200) {
+        if (Wt == 8 && !is_local && long_ok && !getenv("GX_BAND_WAVES") && min_strips >= 32) {
             long long b7 = 0;
             for (const auto& t : tw) b7 += ceil_div(ceil_div((int)std::max(ph[t.first].n, ph[t.second].n), SR), 7);
             if (4 * b7 >= 5LL * 2 * fill_grid_cap(ctx->device)) Wt = 7;
