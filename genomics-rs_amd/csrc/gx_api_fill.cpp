@@ -349,8 +349,11 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
     // layout 3 hands band rows over in tagged granules (gx_skew.hip io_wave_tag): valid once written
     if (lay == 3 && feed_recs > 0) HIPCHK(hipMemsetAsync(job.feed.p, 0, feed_recs * sizeof(Rec), fs));
     HIPCHK(hipMemsetAsync(job.pres.p, 0, res_bytes + 64 + prog_bytes, fs));
-    // twin workgroups: as many per CU as fit 16 waves (the twin kernels hold
-    // up to 128 VGPRs: 4 waves per SIMD)
+    // twin workgroups: as many per CU as fit 16 waves (the global twin fill
+    // holds 96 VGPRs, the local one 149: 5 and 3 waves a SIMD by registers;
+    // 16 measured best for the global fill: 8-wave bands two a CU, 18
+    // waves, 30.4 ms a headline pass against 25.4 at 7-wave bands two a CU
+    // and 29.2 at 4-wave bands four a CU, profiles/r05_w7_sweep.txt)
     const int per_cu = (twin && !getenv("GX_FILL_GRID")) ? std::max(1, 16 / (Wf + 1)) : 1;
     const int grid = std::min(bands, fill_grid_cap(ctx->device) * per_cu);
     if (const char* lg = getenv("GX_LOG"); lg && !strcmp(lg, "debug"))
