@@ -429,9 +429,10 @@ def allvsall_digests(ij):
     return {p: by[tuple(x)] for p, x in enumerate(ij) if tuple(x) in by}, os.path.relpath(path, ROOT)
 
 
-def plane_desc(bytes_per_cell: int) -> str:
-    if bytes_per_cell == 2:
-        return "score planes (exact per-cell 16-bit codes of the three differences, 2 B/cell) + traceback"
+def plane_desc(bytes_per_cell) -> str:
+    if bytes_per_cell == 1.5:
+        return ("score planes (exact per-cell 12-bit codes of the differences S - I, D - I; I replayed along the "
+                "row; 1.5 B/cell) + traceback")
     if bytes_per_cell == 3:
         return "score planes (exact per-cell byte differences, 3 B/cell) + traceback"
     return f"score planes (int32, {bytes_per_cell} B/cell) + traceback"
@@ -442,6 +443,69 @@ def rank_pairs(rank: int, pairs_per_rank: int, length: int, related: bool = Fals
     data-path collective; every rank generates its own inputs)."""
     gen = related_pair if related else synth_pair
     return [gen(rank * pairs_per_rank + p, length) for p in range(pairs_per_rank)]
+
+
+# Inputs of a multi-GPU run above this many bytes are synthesised by each rank
+# itself instead of scattered from rank 0 (config 5 at 1024 x 64k x 8 ranks
+# would be 1 GB of sequences generated on one host thread)
+SCATTER_MAX_BYTES = 1 << 30
+
+
+def scatter_inputs(dist, rank: int, world: int, workload: str, P: int, L: int, related: bool, device: str):
+    """North star: "RCCL over xGMI used only to scatter pairs and gather
+    scores".  Rank 0 holds the job's inputs -- the 10 comparison_data genomes
+    (config 4; read from FASTA on rank 0 only) or every rank's synthetic pairs
+    -- and sends them to all ranks with gxamd._broadcast_bytes_list (three
+    broadcasts: count, lengths, packed bytes; RCCL over xGMI for device =
+    "cuda", gloo on CPU tensors in tests); each rank keeps its share: its LPT
+    share of the 45 pairs, or pairs r*P .. r*P+P-1.  Untimed (before the
+    timed region, which starts with the inputs resident in HBM).  Returns
+    (pairs, all ranks' cells, (i, j) of each pair or None, info)."""
+    import gxamd as gx
+    t0 = time.perf_counter()
+    ij = None
+    if workload == "allvsall":
+        seqs = None
+        if rank == 0:
+            cont = gx.SequenceContainer()
+            d = os.path.join(ROOT, "tests", "golden", "comparison_data")
+            for f in sorted(os.listdir(d)):
+                if f.endswith(".fasta"):
+                    cont.from_fasta(os.path.join(d, f))
+            seqs = [x.sequence.encode() for x in cont.sequences]
+        seqs = gx._broadcast_bytes_list(dist, seqs, device)
+        allp = gx.all_pairs(len(seqs), with_self=False)
+        w = [float(len(seqs[i])) * len(seqs[j]) for i, j in allp]
+        mine = gx.lpt_partition(w, world)[rank]
+        pairs = [(seqs[allp[p][0]], seqs[allp[p][1]]) for p in mine]
+        ij = [tuple(allp[p]) for p in mine]
+        n_total, nbytes = int(sum(w)), sum(len(x) for x in seqs)
+        what = f"the {len(seqs)} comparison_data genomes; each rank keeps its LPT share of the {len(allp)} pairs"
+    else:
+        if 2 * L * P * world > SCATTER_MAX_BYTES:
+            pairs = rank_pairs(rank, P, L, related)
+            cells = sum(len(a) * len(b) for a, b in pairs)
+            return pairs, cells * world, None, {"mode": "local synthesis", "bytes": 0, "ms": 0.0,
+                                                "reason": f"inputs above {SCATTER_MAX_BYTES} B: each rank "
+                                                          f"synthesises its own shard"}
+        items = None
+        if rank == 0:
+            items = [x for r in range(world) for a, b in rank_pairs(r, P, L, related) for x in (a, b)]
+        items = gx._broadcast_bytes_list(dist, items, device)
+        mine = items[2 * P * rank: 2 * P * (rank + 1)]
+        pairs = [(mine[2 * k], mine[2 * k + 1]) for k in range(P)]
+        n_total = sum(len(items[2 * k]) * len(items[2 * k + 1]) for k in range(P * world))
+        nbytes = sum(len(x) for x in items)
+        what = f"{P * world} synthetic pairs; each rank keeps pairs r*{P} .. r*{P}+{P - 1}"
+    if device == "cuda":
+        import torch
+        torch.cuda.synchronize()
+    dist.barrier()
+    ms = (time.perf_counter() - t0) * 1e3
+    return pairs, n_total, ij, {"mode": "scatter from rank 0", "bytes": int(nbytes), "ms": round(ms, 3),
+                                "collective": "3 broadcasts (count, lengths, packed bytes) from rank 0, "
+                                              + ("RCCL over xGMI" if device == "cuda" else "gloo"),
+                                "inputs": what}
 
 
 def combine_over_ranks(dist, elapsed: float, rows, device: str):
@@ -669,7 +733,17 @@ def main():
         pb = 0 if args.no_planes else gx.plane_bytes_per_cell(scores, args.local)
         P = max(1, min(MAX_DEFAULT_PAIRS, int(PLANE_BUDGET // (max(pb, 3) * L * (L + 64)))))
     ij = None
-    if args.workload == "allvsall":
+    scatter = None
+    if world > 1 and args.workload in ("allvsall", "synthetic"):
+        # the inputs come from rank 0 (north_star: RCCL scatters the pairs)
+        pairs, n_total, ij, scatter = scatter_inputs(dist, rank, world, args.workload, P, L, args.related, "cuda")
+        if args.workload == "allvsall":
+            P = len(pairs)
+            keep_planes = args.planes
+            args.single_pair_steps = 0
+        else:
+            keep_planes = not args.no_planes
+    elif args.workload == "allvsall":
         pairs, n_total, ij = allvsall_share(gx, rank, world)
         P = len(pairs)
         keep_planes = args.planes
@@ -769,7 +843,7 @@ def main():
         # launches; "launch" figures are per pass, the time is the fill
         # pipeline's per pass, the PMC profile the same kernel run one launch a pass
         hbm["fill_launches_per_pass"] = 2
-    if valu is not None and keep_planes and bytes_per_cell in (2, 3):
+    if valu is not None and keep_planes and bytes_per_cell in (1.5, 3):
         # compact planes / twin codes: the fill is bound by VALU issue, not HBM -- lane-ops
         # per launch (VALU/cell x cells, SQ_INSTS_VALU profile) over the live
         # fill time, against the probe-measured ceiling at the fill's mix
@@ -810,6 +884,8 @@ def main():
         "fill_gcups_per_gpu": round(cells_rank / (avg_fill_ms * 1e-3) / 1e9, 3),
         "traceback_us_pair0": int(np.mean(tb_us)),
     }
+    if scatter is not None:
+        out["scatter"] = scatter
     if args.workload == "synthetic" and not args.no_verify:
         vpasses = 2 if args.steps >= 2 else 1
         checked, src, vinfo = verify_against_golden(staged, ctx, scores, args.local, keep_planes, rank, P, L,
@@ -851,7 +927,7 @@ def main():
                          "timed_pass_fields": "score, statistics, alignment length of every pair, every timed pass",
                          "pass": f"{vpasses} extra untimed pipelined passes through the timed call's launch "
                                  f"(fill_info identical); plane checksums of every pass, alignment sha256 of the last"}
-    if world == 1 and keep_planes and bytes_per_cell == 2 and args.no_plane_steps > 0:
+    if world == 1 and keep_planes and bytes_per_cell == 1.5 and args.no_plane_steps > 0:
         # the same batch with the per-pair byte planes (3 B/cell, the table format)
         os.environ["GX_PLANES_W16"] = "0"
         try:
@@ -863,7 +939,7 @@ def main():
         out["byte_planes"] = {"fill_ms_avg": round(fms3, 3),
                               "fill_gcups_per_gpu": round(cells_rank / (fms3 * 1e-3) / 1e9, 3),
                               "steps": args.no_plane_steps, "fill_launch": fi3}
-    if world == 1 and keep_planes and bytes_per_cell in (2, 3) and args.int32_steps > 0:
+    if world == 1 and keep_planes and bytes_per_cell in (1.5, 3) and args.int32_steps > 0:
         # the same batch with int32 score planes (12 B/cell, the HBM-bound
         # format of SURVEY 8(d)); batches beyond the free HBM run in chunks
         os.environ["GX_PLANES32"] = "1"

@@ -56,7 +56,10 @@ hipError_t launch_fill_cs2(int W, bool local, bool planes, bool tbl, const PairD
                            hipStream_t st);
 hipError_t launch_fill_skew(int W, bool local, bool planes, bool tbl, bool trace, bool track, const PairDev* d_pairs, int npairs,
                             int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
-                            hipStream_t st);
+                            int lcs_blocks, hipStream_t st);
+int skew_lcs_blocks(int W, int n, int m);
+hipError_t launch_skew_max_col(const PairDev* d_pairs, int npairs, int mmax, PairRes* d_pres, int gshift, hipStream_t st);
+bool skew_traced(bool planes, bool trace, bool track);
 hipError_t launch_skew_codes(const PairDev* d_pairs, int npairs, int mmax, Scores32 sc, bool tbl, hipStream_t st);
 hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int npairs, int ntwins, int total_bands,
                           int* d_counter, PairRes* d_pres, StripRes* d_sres, Scores32 sc, int grid, hipStream_t st);
@@ -286,6 +289,7 @@ struct gx_context {
         std::vector<char> fdesc_last;
     } slots[4];   // 0, 1: pipelined steps by parity (overlapped batches: group A's fills and the walks); 2, 3: group B's fills
     int last_lay = 0, last_W = 0, last_pbytes = 0;   // the last fill launch (gx_fill_info)
+    int last_pbits = 0;                              // ... its plane bits per cell (gx_fill_plane_bits)
     int last_chunks = 1;                             // chunks of the last staged / batch call
     int last_twin = 0;                               // the last fill was the twin (packed 16-bit) fill
     int last_groups = 1;                             // fill launches per pass of the last staged / batch call
@@ -318,6 +322,8 @@ struct PairHost {
 struct FillJob {
     // device buffers (owned by the job until released)
     DevBuf chars, planes, codes, skel, feed, progress, sres, pres, pairs, counter, ccodes;
+    DevBuf lcs;                    // layout-3 tracked fills: LCS masks, hand-offs and bit rows (gx_lcs.h)
+    bool lcs_rows = false;         // max_matches lives in PairDev.lbits (not in an LCS plane)
     bool pairs_borrowed = false;   // pairs is a pipeline slot's cached descriptor block (not pooled)
     bool pres_held = false;        // pres is held by its pipeline slot until fill_collect
     std::vector<PairDev> pd;

@@ -396,7 +396,9 @@ int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
     // (long pairs only: a short pair's walk is short; and both groups must
     // fill the grid on the twin fill, or the attempt falls back.  1024 x 4k:
     // 14.9 ms a step overlapped against 10.8 plain; 1024 x 16k 116.8 against
-    // 145: profiles/r04_config5_*.json, r02k_config5_*.json)
+    // 145, measured in round 4 (those records were replaced by the round-5
+    // ones on the same rule, profiles/r05_config5_*.json; the plain-pipeline
+    // side: profiles/r02k_config5_*.json))
     // (local batches from 64 pairs: at 32 related 30k pairs the split launches
     // fill worse than the walk they hide, 27.2 vs 21.6 ms a step; GX_OVERLAP=1
     // forces it from 16 pairs, GX_OVERLAP=0 turns it off)

@@ -18,7 +18,7 @@ void job_release(gx_context* ctx, FillJob& j) {
     pool_put(ctx, j.chars); pool_put(ctx, j.planes); pool_put(ctx, j.codes); pool_put(ctx, j.feed);
     pool_put(ctx, j.progress); pool_put(ctx, j.sres); pool_put(ctx, j.pres); pool_put(ctx, j.pairs);
     pool_put(ctx, j.counter); pool_put(ctx, j.skel); pool_put(ctx, j.ccodes);
-    pool_put(ctx, j.wrows); pool_put(ctx, j.wdesc); pool_put(ctx, j.wres_d);
+    pool_put(ctx, j.wrows); pool_put(ctx, j.wdesc); pool_put(ctx, j.wres_d); pool_put(ctx, j.lcs);
 }
 
 // The pipelines' release point for a pass's fill: the last pass of a
@@ -72,12 +72,15 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
     scl.shift = shift ? 1 : 0;
     if (shift) { scl.sm = sc.sm - 2 * sc.g; scl.smm = sc.smm - 2 * sc.g; }
     job.shift = shift; job.g = sc.g;
-    // small-alphabet score table: untracked fill (global or local), <= 4 symbols, scores in a signed byte
-    const bool tbl = alpha && alpha->n <= 4 && !track && scl.sm >= -128 && scl.sm <= 127 &&
+    // small-alphabet score table: <= 4 symbols, scores in a signed byte; untracked fills (global or
+    // local), and tracked ones on layout 3 (whose max_matches comes from the LCS rows, not the fill)
+    const bool tbl = alpha && alpha->n <= 4 && (!track || lay == 3) && scl.sm >= -128 && scl.sm <= 127 &&
                      scl.smm >= -128 && scl.smm <= 127 && !getenv("GX_NO_SCORE_TABLE");
     if (tbl)
         for (int k = 0; k < 4; ++k) scl.sym[k] = alpha->sym[k];
     job.planes_on = planes; job.lcs_on = lcs; job.track_on = track;
+    // layout 3 keeps max_matches as bit-parallel LCS rows beside the fill (gx_lcs.h), never as a plane
+    job.lcs_rows = lay == 3 && track;
     const bool d8 = planes && lay == 0 && !track && d8_planes_ok(sc, is_local);
     job.d8 = d8;
     // twin fill: half as many band jobs (each carries two pairs); the band
@@ -155,7 +158,8 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
     const size_t plane_esz = d8 ? 1 : sizeof(int32_t);
     job.W = Wf;
     ctx->last_lay = cs2 ? 2 : lay; ctx->last_W = Wf;
-    ctx->last_pbytes = planes ? (w16 ? 2 : (int)(plane_esz * 3)) : 0;
+    ctx->last_pbytes = planes ? (w16 ? 2 : (int)(plane_esz * 3)) : 0;   // (twin codes: 1.5, reported rounded up)
+    ctx->last_pbits = planes ? (w16 ? 12 : (int)(plane_esz * 24)) : 0;
     const size_t P = ph.size();
     if (job.plan_only) { job.twin = twin; return GX_OK; }
     job.pd.assign(P, PairDev{});
@@ -221,7 +225,7 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
     job.total_bands = bands;
     job.total_strips = strips;
     int rc;
-    const int nplanes = w16 ? 1 : lcs ? 4 : 3;
+    const int nplanes = w16 ? 1 : (lcs && !job.lcs_rows) ? 4 : 3;
     if (!chars_dev) {
         if ((rc = pool_get(ctx, chars_bytes, &job.chars, fs))) return rc;
     }
@@ -285,7 +289,7 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
         d.pI = planes ? plane_at(0) : nullptr;
         d.pD = (planes && !w16) ? plane_at(1) : nullptr;
         d.pS = (planes && !w16) ? plane_at(2) : nullptr;
-        d.pL = (planes && lcs) ? plane_at(3) : nullptr;
+        d.pL = (planes && lcs && !job.lcs_rows) ? plane_at(3) : nullptr;
         d.codes = want_codes ? (uint32_t*)job.codes.p + co[p] : nullptr;
         d.skel = (int*)job.skel.p + so[p];
         d.feed = (Rec*)job.feed.p + fo[p];
@@ -304,7 +308,44 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
             cc += rows * ((size_t)job.pd[p].m + 192);
         }
     }
+    // layout-3 tracked fills: per pair the masks 256 x (lwords + 128) (zeroed) and the bit rows
+    // strips x lcs_steps(lwords) x 64 words, filled by the launch's leading LCS workgroups (gx_lcs.h)
+    int lcs_blocks = 0;
+    // (GX_LCS=0, diagnostics only: no LCS workgroups, so matches_at_max is
+    // not computed -- the timing of the fill without them)
+    if (const char* e = getenv("GX_LCS"); e && !strcmp(e, "0")) job.lcs_rows = false;
+    if (job.lcs_rows) {
+        std::vector<size_t> zo(P), ro(P);
+        size_t zbytes = 0, rbytes = 0;
+        for (size_t p = 0; p < P; ++p) {
+            PairDev& d = job.pd[p];
+            d.lwords = ceil_div(d.m, kLcsBits);
+            // sweeping workgroups (GX_LCS_WAVES, GX_LCS_WGS override: diagnostics)
+            const int nwg = getenv("GX_LCS_WGS") ? std::max(1, atoi(getenv("GX_LCS_WGS"))) : skew_lcs_blocks(W, d.n, d.m);
+            d.lcs_waves = (getenv("GX_LCS_WAVES") ? atoi(getenv("GX_LCS_WAVES")) : 0) | (nwg << 8);   // (0: all that fit)
+            d.lcs_base = lcs_blocks;
+            lcs_blocks += nwg;
+            const size_t feed_words = (size_t)ceil_div(d.n, kWave) * lcs_steps(d.lwords);   // (x2: tagged halves)
+            zo[p] = zbytes; zbytes += (256 * ((size_t)d.lwords + 2 * kLcsMaskPad) + 2 * feed_words) * sizeof(unsigned long long);
+            ro[p] = rbytes;
+            rbytes += feed_words * kWave * sizeof(unsigned long long);
+        }
+        if ((rc = pool_get(ctx, zbytes + rbytes, &job.lcs, fs))) return rc;
+        for (size_t p = 0; p < P; ++p) {
+            PairDev& d = job.pd[p];
+            d.lmask = (unsigned long long*)((char*)job.lcs.p + zo[p]);
+            d.llink = d.lmask + 256 * ((size_t)d.lwords + 2 * kLcsMaskPad);
+            d.lbits = (unsigned long long*)((char*)job.lcs.p + zbytes + ro[p]);
+        }
+        HIPCHK(hipMemsetAsync(job.lcs.p, 0, zbytes, fs));
+    }
     const char* trace_file = slot < 0 ? getenv("GX_TRACE_FILE") : nullptr;
+    if (trace_file && *trace_file && lay == 3 && !skew_traced(planes, true, track)) {
+        // (layout 3 has traced instantiations for untracked fills with planes only: no file of zero stamps)
+        fprintf(stderr, "[gx WARN] GX_TRACE_FILE: this layout-3 launch (planes %d, tracked %d) runs untraced; no trace written\n",
+                planes ? 1 : 0, track ? 1 : 0);
+        trace_file = nullptr;
+    }
     DevBuf trace;
     if (trace_file && *trace_file) {
         if ((rc = pool_get(ctx, (size_t)std::max(strips, 1) * sizeof(StripTrace), &trace, fs))) return rc;
@@ -373,8 +414,10 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
                               (const PairDev*)job.pairs.p, (int)P, (int)tw.size(), bands, counter,
                               (PairRes*)job.pres.p, (StripRes*)job.sres.p, scl, grid, fs));
     else if (bands > 0 && lay == 3)
-        HIPCHK(launch_fill_skew(W, is_local != 0, planes, tbl, trace.p != nullptr, track, (const PairDev*)job.pairs.p, (int)P, bands,
-                                counter, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
+        HIPCHK(launch_fill_skew(W, is_local != 0, planes, tbl, trace.p != nullptr, track, (const PairDev*)job.pairs.p, (int)P,
+                                // (GX_LCS_ALONE=1, diagnostics only: the LCS workgroups without the fill, to time them)
+                                getenv("GX_LCS_ALONE") && lcs_blocks ? 0 : bands,
+                                counter, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, lcs_blocks, fs));
     else if (bands > 0 && cs2)
         HIPCHK(launch_fill_cs2(W, is_local != 0, planes, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
                                counter, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
@@ -391,6 +434,14 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
     if (bands > 0 && (track || is_local))
         HIPCHK(launch_finalize((const PairDev*)job.pairs.p, (int)P, (const StripRes*)job.sres.p,
                                (PairRes*)job.pres.p, fs));
+    // tracked layout-3 fills with planes track each row's largest value only:
+    // the first column holding the maximum from the planes, then matches_at_max
+    if (bands > 0 && lay == 3 && track && planes) {
+        int mmax = 0;
+        for (size_t p = 0; p < P; ++p) mmax = std::max(mmax, job.pd[p].m);
+        HIPCHK(launch_skew_max_col((const PairDev*)job.pairs.p, (int)P, mmax, (PairRes*)job.pres.p,
+                                   is_local ? 0 : sc.g, fs));
+    }
     // the local twin fill tracks each row's maximum only: the last column of
     // the chosen row from its plane codes (gx_kernels.hip local_col_kernel)
     if (bands > 0 && twin && is_local)
@@ -488,7 +539,7 @@ int run_fill_wide(gx_context* ctx, const std::vector<std::pair<const uint8_t*, c
     lcs = lcs && planes;
     track = track || lcs;
     job.planes_on = planes; job.lcs_on = lcs; job.track_on = track;
-    ctx->last_lay = 1; ctx->last_W = 1; ctx->last_pbytes = planes ? 24 : 0;
+    ctx->last_lay = 1; ctx->last_W = 1; ctx->last_pbytes = planes ? 24 : 0; ctx->last_pbits = planes ? 192 : 0;
     job.pd.assign(P, PairDev{});
     job.wd.assign(P, WideDev{});
     size_t chars = 0, codes = 0, skel = 0, rows = 0, cells = 0;

@@ -171,18 +171,21 @@ bool d8_planes_ok(const Scores32& sc, int is_local) {
     return lo >= -128 && hi <= 127;
 }
 
-// Twin plane codes (gx_fill_pk.hip w16_code): x_I - g in [0, U - a - g] must
-// fit 4 unsigned bits, x_S in [smin - U, smax - 2a] 5 signed bits and x_D in
-// [2a - U, U - 2a] 7 signed bits (the bounds of d8_planes_ok); the default
-// scores give [0, 14], [-9, 13], [-19, 19].  GX_PLANES_W16=0 keeps the byte
-// format.
+// Twin plane codes (gx_fill_pk.hip w16_code: code = x_S + 32 x_D, of which
+// the record keeps 12 bits, gx_device.h w12_pack; the format holds no x_I,
+// which every decoder replays along the row): x_S in [smin - U, smax - 2a]
+// must fit the low 5 bits (signed) and x_D in [2a - U, U - 2a] the other 7
+// (w16_decode), the bounds of d8_planes_ok; the default scores give [-9, 13]
+// and [-19, 19].  (Until round 5 an insert difference x_I - g in
+// [0, U - a - g] had a 4-bit field too; tests/test_formats.py restates the
+// codec.)  GX_PLANES_W16=0 keeps the byte format.
 bool w16_ok(const Scores32& sc) {
     if (sc.g > 0 || sc.h > 0 || getenv("GX_PLANES32")) return false;
     if (const char* e = getenv("GX_PLANES_W16"); e && !strcmp(e, "0")) return false;
-    const long long g = sc.g, a = (long long)sc.h + sc.g;
+    const long long a = (long long)sc.h + sc.g;
     const long long smax = std::max(sc.sm, sc.smm), smin = std::min(sc.sm, sc.smm);
     const long long U = std::max(0LL, smax - a);
-    return U - a - g <= 15 && smin - U >= -16 && smax - 2 * a <= 15 && 2 * a - U >= -64 && U - 2 * a <= 63;
+    return smin - U >= -16 && smax - 2 * a <= 15 && 2 * a - U >= -64 && U - 2 * a <= 63;
 }
 
 // The split column step (gx_cs2.hip) replaces layout 1's one-wave strips for
@@ -253,13 +256,14 @@ int cs2_band_waves(int total_strips, int grid_cap) {
 // and fewer than 2^24 - 128 columns: its skeleton holds E + 64 in the 24 bits
 // tb_chase_kernel decodes, and a strip's int32 plane (256 (m + 64) bytes)
 // must stay inside one buffer descriptor's 32-bit range.
-// Tracked fills (max_cell, matches_at_max) run on it too (round 5: the side
-// wave carries the first maximum and the LCS values); an LCS plane does not.
-bool skew_ok(const Scores32& sc, bool lcs_plane, size_t mmax) {
+// Tracked fills (max_cell, matches_at_max) run on it too (round 6: the side
+// wave carries the first maximum, the launch's leading workgroups the LCS
+// as bit rows, gx_lcs.h; GX_TABLE_MATCHES exports rebuild *_matches from them).
+bool skew_ok(const Scores32& sc, bool /*lcs_plane*/, size_t mmax) {
     const long long g = sc.g;
     const long long s2 = std::max(std::llabs((long long)sc.sm - 2 * g), std::llabs((long long)sc.smm - 2 * g));
     const long long drift = 64LL * (std::llabs(g) + std::llabs((long long)sc.h) + s2);
-    return !lcs_plane && sc.h <= 0 && drift < (1LL << 28) && mmax + 128 < (1u << 24);
+    return sc.h <= 0 && drift < (1LL << 28) && mmax + 128 < (1u << 24);
 }
 int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int grid_cap, bool track, bool lcs_plane) {
     const long long span = 65LL * (std::llabs((long long)sc.g) + std::llabs((long long)sc.h));
@@ -275,17 +279,18 @@ int fill_layout(const std::vector<PairHost>& ph, const Scores32& sc, int grid_ca
     // BASELINE pairs: untracked (round 4, profiles/r04_layout_fit.json)
     // layout 3 50 ns + 6.46 us global, 57.5 ns + 6.66 us local; the column
     // step 113 ns + 2.66 us (global), split for local fills 110 ns + 3.37 us.
-    // Tracked fills (round 5, profiles/r05_tracked_layouts.txt: the side wave
-    // carries the first maximum and the LCS values and sets the pace) layout
-    // 3 104 ns + 11.9 us, the tracked column step 146 ns + 3.45 us, both
-    // modes: layout 3 only for short pairs (n below about a quarter of m)
+    // Tracked fills: the tracked column step 146 ns + 3.45 us (round 5,
+    // profiles/r05_tracked_layouts.txt); layout 3 at its untracked pace since
+    // round 6 (the side wave keeps only the first maximum, the LCS runs as
+    // bit rows in workgroups of their own, gx_lcs.h; before, the side wave's
+    // LCS chain set a 104 ns + 11.9 us pace)
     const bool local = sc.floor_ == 0;
     double est1 = 0, est3 = 0;   // the launch's slowest pair on each layout (ns)
     for (const PairHost& h : ph) {
         const double S = (double)ceil_div((int)h.n, kStripRows1), m = (double)h.m;
         if (track) {
             est1 = std::max(est1, m * 146.0 + S * 3450.0);
-            est3 = std::max(est3, m * 104.0 + S * 11900.0);
+            est3 = std::max(est3, local ? m * 57.5 + S * 6660.0 : m * 50.0 + S * 6460.0);
         } else {
             est1 = std::max(est1, local ? m * 110.0 + S * 3370.0 : m * 113.0 + S * 2660.0);
             est3 = std::max(est3, local ? m * 57.5 + S * 6660.0 : m * 50.0 + S * 6460.0);

@@ -344,6 +344,7 @@ extern "C" int gx_staged_steps(const gx_context* ctx, size_t pair, gx_step* step
 extern "C" int gx_batch_chunks(const gx_context* ctx) { return ctx ? ctx->last_chunks : -1; }
 extern "C" int gx_fill_twin(const gx_context* ctx) { return ctx ? ctx->last_twin : -1; }
 extern "C" int gx_fill_groups(const gx_context* ctx) { return ctx ? ctx->last_groups : -1; }
+extern "C" int gx_fill_plane_bits(const gx_context* ctx) { return ctx ? ctx->last_pbits : -1; }
 
 extern "C" int gx_fill_info(const gx_context* ctx, int* layout, int* band_waves, int* plane_bytes_per_cell) {
     if (!ctx) return fail(GX_EINVAL, "context is NULL");

@@ -111,6 +111,38 @@ static int fetch_plane32(const gx_table* t, int which, std::vector<int32_t>& out
     return fetch_rows32(t, which, 0, t->s1.size() + 1, out);
 }
 
+// max_matches of the interior cells of rows row0 .. row0 + rows - 1,
+// row-major rows x (m+1) (row 0 and column 0: 0), from a layout-3 fill's LCS
+// bit rows (gx_lcs.h): LM(i, j) = j - popcount(V_i & (2^j - 1)).
+static int fetch_lcs_rows(const gx_table* t, size_t row0, size_t rows, std::vector<int32_t>& out) {
+    const size_t n = t->s1.size(), m = t->s2.size();
+    out.assign(rows * (m + 1), 0);
+    const PairDev& d = t->job.pd[0];
+    if (n == 0 || m == 0 || rows == 0) return GX_OK;
+    if (!d.lbits || d.lwords <= 0) return fail(GX_EINVAL, "LCS rows not kept: build the table with GX_TABLE_MATCHES");
+    const size_t i0 = std::max<size_t>(row0, 1), i1 = std::min(row0 + rows, n + 1);
+    if (i1 <= i0) return GX_OK;
+    // (the rows' strips: bits[strip][step][lane], gx_lcs.h lcs_word_index)
+    const size_t s0 = (i0 - 1) / kWave, s1 = (i1 - 2) / kWave + 1, T = (size_t)lcs_steps(d.lwords);
+    std::vector<unsigned long long> bits((s1 - s0) * T * kWave);
+    HIPCHK(hipMemcpy(bits.data(), d.lbits + s0 * T * kWave, bits.size() * sizeof(unsigned long long),
+                     hipMemcpyDeviceToHost));
+    const size_t base = s0 * T * kWave;
+    for (size_t i = i0; i < i1; ++i) {
+        int32_t* o = &out[(i - row0) * (m + 1)];
+        int32_t ones = 0;
+        for (size_t j = 1; j <= m; ++j) {
+            const unsigned long long wv = bits[lcs_word_index((int)i, (int)((j - 1) / kLcsBits), d.lwords) - base];
+            ones += (int32_t)((wv >> ((j - 1) % kLcsBits)) & 1u);
+            o[j] = (int32_t)j - ones;
+        }
+    }
+    return GX_OK;
+}
+static int fetch_lcs_plane(const gx_table* t, std::vector<int32_t>& out) {
+    return fetch_lcs_rows(t, 0, t->s1.size() + 1, out);
+}
+
 // The int64 fill's planes: rows row0 .. row0 + rows - 1 of plane `which`
 // (0-2; 3 = the LCS plane) as int64, rows x (m+1) (column 0 and row 0 undefined).
 static int fetch_rows_wide(const gx_table* t, int which, size_t row0, size_t rows, std::vector<int64_t>& out) {
@@ -146,13 +178,19 @@ static int export_rows(const gx_table* t, int which, size_t row0, size_t rows, i
     const size_t m = t->s2.size();
     std::vector<int32_t> p32;
     std::vector<int64_t> p64;
-    int rc = t->job.wide ? fetch_rows_wide(t, which, row0, rows, p64) : fetch_rows32(t, which, row0, rows, p32);
+    if (which == 3 && !t->job.lcs_on)
+        return fail(GX_EINVAL, "max_matches not kept: build the table with GX_TABLE_MATCHES");
+    int rc = t->job.wide ? fetch_rows_wide(t, which, row0, rows, p64)
+             : (which == 3 && t->job.lcs_rows) ? fetch_lcs_rows(t, row0, rows, p32)
+                                               : fetch_rows32(t, which, row0, rows, p32);
     if (rc) return rc;
     for (size_t r = 0; r < rows; ++r) {
         const size_t i = row0 + r;
         for (size_t j = 0; j <= m; ++j) {
             int64_t v;
-            if (i == 0 || j == 0) {
+            if (which == 3 && (i == 0 || j == 0)) {
+                v = 0;   // (boundary cells match nothing, algo.rs:195-220)
+            } else if (i == 0 || j == 0) {
                 int64_t I, D, S;
                 boundary_cell(t->hs, i, j, &I, &D, &S);
                 v = which == 0 ? I : which == 1 ? D : S;
@@ -178,7 +216,8 @@ extern "C" int gx_table_export_plane(const gx_table* t, int which, int64_t* out,
 extern "C" int gx_table_export_rows(const gx_table* t, int which, size_t row0, size_t rows, int64_t* out,
                                     size_t out_cells) {
     if (!t || (!out && rows)) return fail(GX_EINVAL, "NULL argument");
-    if (which < 0 || which > 2) return fail(GX_EINVAL, "which must be 0 (insert), 1 (delete) or 2 (sub)");
+    if (which < 0 || which > 3)
+        return fail(GX_EINVAL, "which must be 0 (insert), 1 (delete), 2 (sub) or 3 (max_matches)");
     const size_t n = t->s1.size(), m = t->s2.size();
     if (row0 > n + 1 || rows > n + 1 - row0) return fail(GX_EINVAL, "row range outside the table");
     if (out_cells < rows * (m + 1)) return fail(GX_ECAP, "out too small");
@@ -251,7 +290,7 @@ extern "C" int gx_table_export(const gx_table* t, gx_cell* out, size_t out_cells
     }
     std::vector<int32_t> pI, pD, pS, pL;
     if ((rc = fetch_plane32(t, 0, pI)) || (rc = fetch_plane32(t, 1, pD)) || (rc = fetch_plane32(t, 2, pS))) return rc;
-    if (have_l && (rc = fetch_plane32(t, 3, pL))) return rc;
+    if (have_l && (rc = t->job.lcs_rows ? fetch_lcs_plane(t, pL) : fetch_plane32(t, 3, pL))) return rc;
     auto L = [&](size_t i, size_t j) -> uint64_t {
         if (i == 0 || j == 0 || !have_l) return 0;
         return (uint64_t)pL[i * (m + 1) + j];

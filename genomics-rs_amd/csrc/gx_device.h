@@ -340,4 +340,41 @@ __device__ __forceinline__ void cs_push63(uint32_t base, unsigned long long m63,
 
 constexpr uint32_t kNoStore = 0xFFFFFFF0u;   // past every strip plane's range: the store is dropped
 
+// Twin plane codes, 12 bits a cell.  The fill computes each
+// step's dword d_k = code_A | code_B << 16 (the twin's two pairs; a code is
+// x_S + 32 x_D mod 2^16, of which the low 12 bits decode exactly while x_D
+// fits 7 signed bits).  A lane's four steps of one row pack into 12 B:
+//   w0 = the codes' low bytes of steps 0, 1 [A0, B0, A1, B1]
+//   w1 = those of steps 2, 3                [A2, B2, A3, B3]
+//   w2 = the high nibbles: byte k = nibble of w0's byte k | nibble of w1's byte k << 4
+// four v_perm_b32, a shift and a v_bfi_b32 (1.5 B a cell instead of 2: the
+// plane stores were a third of the headline fill's time).
+__device__ __forceinline__ void w12_pack(const uint32_t d0, const uint32_t d1, const uint32_t d2, const uint32_t d3,
+                                         uint32_t& w0, uint32_t& w1, uint32_t& w2) {
+    w0 = __builtin_amdgcn_perm(d1, d0, 0x06040200u);
+    w1 = __builtin_amdgcn_perm(d3, d2, 0x06040200u);
+    const uint32_t n01 = __builtin_amdgcn_perm(d1, d0, 0x07050301u), n23 = __builtin_amdgcn_perm(d3, d2, 0x07050301u);
+    w2 = (n01 & 0x0F0F0F0Fu) | ((n23 << 4) & 0xF0F0F0F0u);
+}
+// The four steps' dwords (code_A | code_B << 16, 12 bits each) of a record.
+__device__ __forceinline__ uint4 w12_unpack(const uint32_t w0, const uint32_t w1, const uint32_t w2) {
+    const uint32_t n = (w2 >> 4) & 0x0F0F0F0Fu;
+    uint4 d;
+    d.x = __builtin_amdgcn_perm(w2, w0, 0x05010400u) & 0x0FFF0FFFu;
+    d.y = __builtin_amdgcn_perm(w2, w0, 0x07030602u) & 0x0FFF0FFFu;
+    d.z = __builtin_amdgcn_perm(n, w1, 0x05010400u);
+    d.w = __builtin_amdgcn_perm(n, w1, 0x07030602u);
+    return d;
+}
+// A record at `rec` (4-byte aligned, global memory).
+__device__ __forceinline__ uint4 w12_load(const uint8_t* rec) {
+    const __attribute__((address_space(1))) uint32_t* p = (const __attribute__((address_space(1))) uint32_t*)rec;
+    return w12_unpack(p[0], p[1], p[2]);   // (one global_load_dwordx3)
+}
+// Byte offset of the record of row-in-strip rho (lane rho / 2, row-in-lane
+// rho % 2) in 4-step group G of strip s, for strips of t4 groups.
+__device__ __forceinline__ size_t w12_rec_off(const int s, const int t4, const int G, const int rho) {
+    return ((size_t)s * t4 + G) * kTwinGroupBytes + (size_t)(rho & 1) * (kTwinGroupBytes / 2) + (size_t)(rho >> 1) * kTwinRec;
+}
+
 }  // namespace gx

@@ -399,11 +399,26 @@ __device__ __forceinline__ void group4_pk(LanePk& st, Rec (&nxt)[4], WavePk& w, 
             skel_store4(w.skel_rsrc, w.skel_voff + 4u * (uint32_t)(col0 + 1), (int)e0, (int)e1, (int)e2, (int)st.b.E);
     }
     if ((PLANES & 3) == 2) {
-        // twin plane codes: per strip [group][row][lane][step] dwords (2 KB a group)
-        const uint32_t v = (uint32_t)G4 * kTwinGroupBytes + (uint32_t)w.lane * 16u;
+        // twin plane codes: per strip [group][row][lane] 12-B records (1.5 KB a
+        // group; gx_device.h w12_pack), one dwordx3 per row and lane
         const auto r = rsrc_of(w.pI[0] + sb_off * (kTwinGroupBytes / kGroupInts), 4 * kTwinGroupBytes);
-        bstore4(r, v, make_int4((int)wc[0][0], (int)wc[0][1], (int)wc[0][2], (int)wc[0][3]));
-        bstore4(r, v + kTwinGroupBytes / 2, make_int4((int)wc[1][0], (int)wc[1][1], (int)wc[1][2], (int)wc[1][3]));
+        const uint32_t v = (uint32_t)G4 * kTwinGroupBytes + (uint32_t)w.lane * kTwinRec;
+        typedef int v3i __attribute__((ext_vector_type(3)));
+#pragma unroll
+        for (int row = 0; row < 2; ++row) {
+            uint32_t w0, w1, w2;
+#ifdef GX_DIAG_NO_PACK   // (timing only: the codes computed, neither packed nor stored)
+            asm volatile("" ::"v"(wc[row][0]), "v"(wc[row][1]), "v"(wc[row][2]), "v"(wc[row][3]));
+            continue;
+#endif
+            w12_pack(wc[row][0], wc[row][1], wc[row][2], wc[row][3], w0, w1, w2);
+#ifndef GX_DIAG_NO_PLANES
+            __builtin_amdgcn_raw_buffer_store_b96(v3i{(int)w0, (int)w1, (int)w2}, r,
+                                                  (int)(v + (uint32_t)row * (kTwinGroupBytes / 2)), 0, GX_PLANE_AUX);
+#else
+            asm volatile("" ::"v"(w0), "v"(w1), "v"(w2));
+#endif
+        }
     }
     if ((PLANES & 3) == 1) {
         // compact planes of both pairs (bytes_step): x_I = I - I(j-1) (shifted:
@@ -506,7 +521,7 @@ __device__ void compute_wave_pk(const PairDev& P0, const PairDev& P1, const int 
     const int ia = s * kStripRows + kRowsPerLane * lane + 1;
     WavePk w;
     {
-        // bytes per compact plane per strip (PLANES 2: the twin's one code plane, 2 KB a group)
+        // bytes per compact plane per strip (PLANES 2: the twin's one code plane, 1.5 KB a group)
         const size_t strip_planes = (size_t)s * P0.t4 * ((PLANES & 3) == 2 ? kTwinGroupBytes : kGroupInts);
         w.pI[0] = (PLANES & 3) ? (uint8_t*)P0.pI + strip_planes : nullptr;
         w.pD[0] = (PLANES & 3) == 1 ? (uint8_t*)P0.pD + strip_planes : nullptr;

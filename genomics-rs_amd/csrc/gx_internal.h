@@ -17,6 +17,7 @@
 //       k = t%16 bit 31-k = "delete beats insert and sub", bit 15-k = "insert
 //       beats sub"; decode D ? 2 : I ? 1 : 0)
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 namespace gx {
@@ -35,9 +36,12 @@ constexpr int kStripRows = kWave * kRowsPerLane;   // 128 rows per strip
 // Plane layout (ints): plane[strip][t/4][row-in-lane][lane][t%4]; one 4-step
 // group of one row is 1 KiB contiguous per wave.
 constexpr int kGroupInts = kRowsPerLane * kWave * 4;
-// twin plane codes (gx_fill_pk.hip PLANES 2): one 2-B code per cell, both
-// pairs of a twin in one dword; a 4-step group of a strip = [row][lane][step]
-constexpr int kTwinGroupBytes = kRowsPerLane * kWave * 4 * 4;
+// twin plane codes (gx_fill_pk.hip PLANES 2): one 12-bit code per cell and
+// pair (round 6; 16 bits before), a lane's 4 steps of one row for both pairs
+// of a twin in a 12-B record (gx_device.h w12_pack); a 4-step group of a
+// strip = [row][lane] records
+constexpr int kTwinRec = 12;
+constexpr int kTwinGroupBytes = kRowsPerLane * kWave * kTwinRec;
 // Column-step layout (layout 1): 64-row strips, lane l owns row 64s + l + 1,
 // step t = column t + 1 for every lane (no skew); planes
 // plane[strip][t/4][lane][t%4] (1 KiB per wave per plane every 4 columns),
@@ -81,6 +85,18 @@ struct Scores32 {
 struct __attribute__((aligned(16))) Rec {
     int dd, sm, c2, l;
 };
+
+// Bit-parallel LCS rows of layout-3 tracked fills (gx_lcs.h): a word holds
+// kLcsBits columns (bit k of word w: column kLcsBits w + k + 1); steps a strip of the sweep takes
+// for rows of `words` words (a multiple of 32, the sweep's unrolling: lane 63
+// finishes word words - 1 at step words + 62), and the index (in words) of word w of row i (1-based)
+// in PairDev.lbits, [strip][step][lane].
+constexpr int kLcsBits = 64;
+constexpr int kLcsMaskPad = 64;         // zero words before (and after) each mask row
+constexpr int lcs_steps(int words) { return (words + 64 + 31) & ~31; }
+constexpr size_t lcs_word_index(int i, int w, int words) {
+    return ((size_t)((i - 1) / 64) * (size_t)lcs_steps(words) + (size_t)(w + (i - 1) % 64)) * 64 + (size_t)((i - 1) % 64);
+}
 
 struct __attribute__((aligned(16))) StripRes {
     int best, bi, bj, bl;      // first max of score_max in row-major order + LCS there
@@ -139,6 +155,16 @@ struct __attribute__((aligned(16))) PairDev {   // 16-B multiple: the pinned sta
     int twin_half;       // twin fill: this pair's 16-bit half (0 low, 1 high) in its twin's shared buffers
     const int* ccodes;   // layout 3: the column symbols as int32 (code * 8 with score tables), 64 zeros
                          // before and after (index j - 1 + 64 for column j; gx_skew.hip)
+    // layout-3 tracked fills: max_matches as bit-parallel LCS rows (gx_lcs.h),
+    // computed beside the fill by the launch's leading workgroups
+    unsigned long long* lbits;   // row i's LCS difference bits V_i (bit k of word w: column 63 w + k + 1),
+                                 // [strip][step][lane] (gx_lcs.h lcs_word_index)
+    unsigned long long* lmask;   // [256][lwords + 128] match masks of each byte against s2 (zeroed before the launch)
+    unsigned long long* llink;   // [strips][lcs_steps][2] the strips' bottom rows, tagged halves (zeroed before the launch)
+    int lwords;                  // words per bit row, ceil(m / kLcsBits); 0 = no LCS rows
+    int lcs_waves;               // sweeping waves per LCS workgroup | (the pair's LCS workgroups << 8)
+    int lcs_base;                // the pair's first LCS workgroup (blockIdx.x)
+    int lcs_pad[3];
 };
 static_assert(sizeof(PairDev) % 16 == 0, "PairDev staging keeps the PairRes that follow it 16-B aligned");
 

@@ -27,6 +27,7 @@
 
 #include "gx_device.h"
 #include "gx_io.h"
+#include "gx_lcs.h"
 
 namespace gx {
 
@@ -1033,12 +1034,31 @@ __global__ void finalize_kernel(const PairDev* __restrict__ pairs, const StripRe
         fs = min(fs, __shfl_xor(fs, off));
         lsel = max(lsel, __shfl_xor(lsel, off));
     }
+    // matches_at_max = max_matches(max_cell) (algo.rs:279): from the fill's
+    // LCS field, or from the LCS bit rows of a layout-3 launch (gx_lcs.h):
+    // LM(i, j) = j - popcount(V_i & (2^j - 1))
+    int mam = 0;
+    if (fs != INT_MAX) {
+        const StripRes r = sres[P.strip_base + fs];
+        mam = r.bl;
+        if (P.lwords > 0 && P.lbits && r.bj > 0) {   // (bj = 0: layout 3 finds the column later, skew_max_col_kernel)
+            int ones = 0;
+            for (int w = lane; w * kLcsBits < r.bj; w += kWave) {   // (64 columns a word, gx_lcs.h)
+                unsigned long long x = P.lbits[lcs_word_index(r.bi, w, P.lwords)];
+                const int rem = r.bj - w * kLcsBits;
+                if (rem < kLcsBits) x &= (1ull << rem) - 1ull;
+                ones += __popcll(x);
+            }
+            for (int off = 32; off > 0; off >>= 1) ones += __shfl_xor(ones, off);
+            mam = r.bj - ones;
+        }
+    }
     if (lane == 0) {
         PairRes& o = pres[p];
         o.max_val = mx; o.lmax_val = lmx; o.nstrips = P.strips;
         if (fs != INT_MAX) {
             const StripRes r = sres[P.strip_base + fs];
-            o.max_i = r.bi; o.max_j = r.bj; o.mam = r.bl;
+            o.max_i = r.bi; o.max_j = r.bj > 0 ? r.bj : INT_MAX; o.mam = mam;
         } else {
             o.max_i = 0; o.max_j = 0; o.mam = 0;
         }
@@ -1151,11 +1171,12 @@ __global__ void tb_chase_kernel(const TbDev* __restrict__ jobs) {
 // row are rebuilt; the walk (tb_strip_kernel) never uses a word outside them
 // once its rows have converged (every path cell lies in that range).  One
 // block of 128 threads per strip, one thread per row.
-// A twin plane code (gx_fill_pk.hip w16_code: x_S + 32 x_D mod 2^16, this
-// pair's 16-bit half) -> x_S = S - I (5-bit signed), x_D = D - I (7-bit signed).
-__device__ __forceinline__ void w16_decode(uint32_t code16, int& xS, int& xD) {
-    xS = (int)(code16 << 27) >> 27;
-    xD = (int)(short)(unsigned short)(code16 - (uint32_t)xS) >> 5;
+// A twin plane code (gx_fill_pk.hip w16_code: x_S + 32 x_D, of which the
+// record keeps the low 12 bits, gx_device.h w12_pack; this pair's half of a
+// step's dword) -> x_S = S - I (5-bit signed), x_D = D - I (7-bit signed).
+__device__ __forceinline__ void w16_decode(uint32_t code, int& xS, int& xD) {
+    xS = (int)(code << 27) >> 27;
+    xD = (int)((code - (uint32_t)xS) << 20) >> 25;
 }
 // The format stores no x_I: I(i, j) from I(i, j-1) and the previous cell's
 // max(x_S, x_D) -- the fill's insert recurrence, algo.rs:231-236 --
@@ -1183,16 +1204,16 @@ __device__ __forceinline__ uint32_t w16_word_of(const uint4 (&w4)[4], const int 
     }
     return (cD << 16) | cI;
 }
-// Address of row rho's 4-step group G of strip s in the twin code plane.
-__device__ __forceinline__ const uint4* w16_group(const TbDev& J, int s, int G, int rho) {
-    return (const uint4*)(J.w16 + ((size_t)s * J.t4 + G) * kTwinGroupBytes + (size_t)(rho & 1) * (kTwinGroupBytes / 2) +
-                          (size_t)(rho >> 1) * 16);
+// Row rho's 4-step group G of strip s in the twin code plane: the four
+// steps' dwords (gx_device.h w12_load).
+__device__ __forceinline__ uint4 w16_group(const TbDev& J, int s, int G, int rho) {
+    return w12_load(J.w16 + w12_rec_off(s, J.t4, G, rho));
 }
 // Code word q of row rho of strip s, derived from the twin plane codes.
 __device__ __forceinline__ uint32_t w16_word(const TbDev& J, int s, int q, int rho) {
     uint4 w4[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) w4[g] = *w16_group(J, s, 4 * q + g, rho);
+    for (int g = 0; g < 4; ++g) w4[g] = w16_group(J, s, 4 * q + g, rho);
     return w16_word_of(w4, 16 * J.w16_half);
 }
 
@@ -1207,14 +1228,14 @@ __global__ __launch_bounds__(128) void tb_w16_codes_kernel(const TbDev* __restri
     j_lo = max(j_lo, 1);
     const int rho = threadIdx.x, lane = rho >> 1, hh = rho & 1;
     const int q_lo = (j_lo - 1 + lane) >> 4, q_hi = min((j_hi - 1 + lane) >> 4, J.t16 - 1);
-    const uint8_t* base = J.w16 + (size_t)s * J.t4 * kTwinGroupBytes + (size_t)hh * (kTwinGroupBytes / 2) +
-                          (size_t)lane * 16;
+    (void)hh;
+    const uint8_t* base = J.w16 + w12_rec_off(s, J.t4, 0, rho);
     const int sh = 16 * J.w16_half;
     guint* const out = (guint*)(J.codes + (size_t)s * J.t16 * kStripRows + rho);
     for (int q = q_lo; q <= q_hi; ++q) {
         uint4 w4[4];
 #pragma unroll
-        for (int g = 0; g < 4; ++g) w4[g] = *(const uint4*)(base + (size_t)(4 * q + g) * kTwinGroupBytes);
+        for (int g = 0; g < 4; ++g) w4[g] = w12_load(base + (size_t)(4 * q + g) * kTwinGroupBytes);
         out[(size_t)q * kStripRows] = w16_word_of(w4, sh);
     }
 }
@@ -1381,7 +1402,7 @@ __device__ __forceinline__ void tb_seq_window(const TbDev& J, const int vb, cons
     for (int u = 0; u < kPer; ++u) {
         const int q = min(q0 + hw + u * kSqHelp, J.t16 - 1);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) w4[u][g] = *w16_group(J, s, 4 * q + g, rho);
+        for (int g = 0; g < 4; ++g) w4[u][g] = w16_group(J, s, 4 * q + g, rho);
     }
 #pragma unroll
     for (int u = 0; u < kPer; ++u) lw[(hw + u * kSqHelp) * kWave + lane] = w16_word_of(w4[u], sh);
@@ -1500,14 +1521,13 @@ __global__ __launch_bounds__(64) void plane_sums_kernel(const PairDev* __restric
     const size_t row0 = (size_t)s * d.t4 * gints + (lay ? (size_t)lane * 4 : (size_t)hh * kWave * 4 + (size_t)lane * 4);
     if (mode == 3) {   // twin plane codes (gx_fill_pk.hip w16_code): this pair's half of each dword
         const int half = d.twin_half;      // the twin's two pairs share its code plane
-        const uint8_t* base = (const uint8_t*)d.pI + (size_t)s * d.t4 * kTwinGroupBytes +
-                              (size_t)hh * (kTwinGroupBytes / 2) + (size_t)lane * 16;
+        const uint8_t* base = (const uint8_t*)d.pI + w12_rec_off(s, d.t4, 0, 2 * lane + hh);
         const bool local = floor_ == 0;
         int I = max(h + i * g, floor_) + h;             // H(i, 0) + h, as the fill seeds it
         int mp = local ? 0 : -h;                        // (its max(S, D) - I)
         for (int q = 0; q < d.t4; ++q) {
             uint4 w4 = make_uint4(0u, 0u, 0u, 0u);
-            if (row_ok) w4 = *(const uint4*)(base + (size_t)q * kTwinGroupBytes);
+            if (row_ok) w4 = w12_load(base + (size_t)q * kTwinGroupBytes);
             const uint32_t wk[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -1638,15 +1658,18 @@ __global__ void export_w16_kernel(const uint8_t* __restrict__ codes, int half, i
     if (r >= rows || i < 1 || i > n) return;
     const int s = (i - 1) / kStripRows, rho = (i - 1) % kStripRows;
     const int l = rho >> 1, hh = rho & 1;
-    const uint8_t* base = codes + (size_t)s * t4 * kTwinGroupBytes + (size_t)hh * (kTwinGroupBytes / 2) + (size_t)l * 16;
+    (void)hh;
+    const uint8_t* base = codes + w12_rec_off(s, t4, 0, rho);
     const bool local = floor_ == 0;
     (void)gshift;
     int I = max(h + i * g, floor_) + h;   // H(i, 0) + h, as the fill seeds it
     int mp = local ? 0 : -h;              // (its max(S, D) - I)
     int32_t* o = out + (size_t)r * (m + 1);
+    uint4 rec = make_uint4(0u, 0u, 0u, 0u);
     for (int j = 1; j <= m; ++j) {
         const int t = j - 1 + l;
-        const uint32_t wd = *(const uint32_t*)(base + (size_t)(t >> 2) * kTwinGroupBytes + (size_t)(t & 3) * 4);
+        if (j == 1 || (t & 3) == 0) rec = w12_load(base + (size_t)(t >> 2) * kTwinGroupBytes);
+        const uint32_t wd = (t & 3) == 0 ? rec.x : (t & 3) == 1 ? rec.y : (t & 3) == 2 ? rec.z : rec.w;
         int xS, xD;
         w16_decode((wd >> (16 * half)) & 0xFFFFu, xS, xD);
         I = w16_next_I(I, mp, h, g, local);
@@ -1794,13 +1817,14 @@ __global__ __launch_bounds__(64) void local_col_kernel(const PairDev* __restrict
     const int i = __builtin_amdgcn_readfirstlane(r->lmax_i), target = __builtin_amdgcn_readfirstlane(r->lmax_val);
     if (i < 1 || i > d.n || d.m < 1 || !d.pI) return;
     const int s = (i - 1) / kStripRows, rr = (i - 1) % kStripRows, l = rr >> 1, hh = rr & 1;
-    const uint8_t* base = (const uint8_t*)d.pI + (size_t)s * d.t4 * kTwinGroupBytes + (size_t)hh * (kTwinGroupBytes / 2) +
-                          (size_t)l * 16;
+    (void)hh;
+    const uint8_t* base = (const uint8_t*)d.pI + w12_rec_off(s, d.t4, 0, rr);
     const int sh = 16 * d.twin_half;
     const int C = (d.m + kWave - 1) / kWave, j0 = lane * C + 1, j1 = min(d.m, j0 + C - 1);
     auto code_at = [&](int j, int& xS, int& xD) {
         const int t = j + l - 1;   // the step at which this row computes column j (anti-diagonal skew)
-        const uint32_t w = *(const uint32_t*)(base + (size_t)(t >> 2) * kTwinGroupBytes + (size_t)(t & 3) * 4);
+        const uint4 rec = w12_load(base + (size_t)(t >> 2) * kTwinGroupBytes);
+        const uint32_t w = (t & 3) == 0 ? rec.x : (t & 3) == 1 ? rec.y : (t & 3) == 2 ? rec.z : rec.w;
         w16_decode((w >> sh) & 0xFFFFu, xS, xD);
     };
     constexpr int kLow = INT_MIN / 4;   // "no floor yet" (far below every value, no overflow when shifted)

@@ -56,6 +56,7 @@
 #include "gx_internal.h"
 
 #include "gx_device.h"
+#include "gx_lcs.h"
 
 namespace gx {
 
@@ -69,9 +70,6 @@ struct SkRing {                  // one strip boundary (see the file header)
 };
 struct SkHo {                    // one strip's core -> side ring: [group][S, D][lane] int4 (the side
     int4 v[kSkHo][2][kWave];     // wave derives I from them: side_group)
-};
-struct SkMRing {                 // TRACK: one strip boundary's LCS values (max_matches, algo.rs:113-121), side to side
-    int m[kSkRingG][4];
 };
 __device__ __forceinline__ int sk_grp(int c) { return ((c + 3) >> 2) & (kSkRingG - 1); }
 __device__ __forceinline__ int sk_pos(int c) { return (c + 3) & 3; }
@@ -390,12 +388,12 @@ struct SideState {
     int E, Ed;                   // landing column + 64 of (i, j-1) and of (i-1, j-1)
     uint32_t cI, cD;
     int lbest, lstep, lE;        // LOCAL: the row's last max of score_max (algo.rs:310-322)
-    // TRACK: max_matches of (i, j-1) and (i-1, j-1) (algo.rs:113-121, 250-256)
-    // and the row's FIRST maximum of score_max (algo.rs:258-262: strict <),
+    // TRACK: the row's FIRST maximum of score_max (algo.rs:258-262: strict <),
     // held as thr = best - (i + j) g at the current column j for shifted
     // (global) fills, so that a step compares its shifted value directly
-    int M, Md;
-    int thr, bstep, bl;
+    // (max_matches is not carried here: the bit-parallel LCS rows of the
+    // launch's leading workgroups, gx_lcs.h)
+    int thr, bstep;
 };
 
 // Retrace bits and landing column of cell (i, j) from its I, S, D.
@@ -440,22 +438,7 @@ struct SideCtx {
     int h, g, hg;                        // gap open / extend (global fills: shifted, g folded: g = 0)
     unsigned tr_wait;                    // (diagnostics: spins waiting for the core wave)
     long long* ts;                       // (diagnostics: the side's dense timeline, StripTrace.ts)
-    // TRACK: the LCS rings (the strip above's side pushes its bottom row's
-    // values, lane 63 per 4-column group, as the core pushes dd / sm) and
-    // this lane's column symbols (PairDev.ccodes, raw bytes: tracked fills
-    // keep no score table)
-    uint32_t mrd_base, mrd_m16;          // LDS; lane 0: the ring above's m[0]; other lanes: the zero block
-    uint32_t mpush_base, mpush_m16;      // LDS; lane 63: the ring below's m[0]; other lanes / no consumer: a sink
-    lds_int* mw_in;                      // LCS columns the strip above published
-    lds_int* mr_in;                      // ... and this side has read
-    lds_int* mw_out;                     // (no consumer: a sink)
-    lds_int* mr_out;
-    bool mpush_on;
-    __amdgpu_buffer_rsrc_t crs;          // the column symbols
-    uint32_t cvoff;
-    int c1;                              // this row's symbol
-    int gs;                              // the shift per column of the tracked values (global: g; local: 0)
-    v4i mu_next;                         // lane 0: the next group's LCS ring values, read one group ahead
+    int gs;                              // TRACK: the shift per column of the tracked values (global: g; local: 0)
 };
 
 // I(i, j) from the row's previous cell, as the core computes it (the core
@@ -470,52 +453,51 @@ __device__ __forceinline__ int side_insert(SideState& st, const SideCtx& w, cons
     return In;
 }
 
-// TRACK: max_matches of cell (i, j) (algo.rs:250-256: max of the left's,
-// the one above's and the top-left's + is_match) and the row's first
-// maximum of score_max (algo.rs:258-262).  mu0: lane 0's value of the row
-// above from the LCS ring (the other lanes take lane l-1's by DPP); c2 the
-// column's symbol.
-template <bool MASKED>
-__device__ __forceinline__ void track_step(SideState& st, const SideCtx& w, const int H, const int mu0, const int c2,
-                                           const int t, const bool act) {
-    const int Mu = shr1(mu0, st.M);              // max_matches(i-1, j)
-    const int Mn = max3i(st.M, Mu, st.Md + (c2 == w.c1 ? 1 : 0));
-    st.Md = Mu;
-    const int thr = st.thr - w.gs;               // best - (i + j) g at this column
+// TRACK: the row's first maximum of score_max (algo.rs:258-262), H that of
+// cell (i, j) at step t.  COL: with its column (a compare and two selects);
+// without (fills that keep their planes), the row's largest value only --
+// thr = max(thr - g, H), two instructions a cell (local: one) -- and
+// skew_max_col_kernel finds the first column holding it in the one row that
+// finalize_kernel picks, from the planes (the side wave sets a tracked
+// fill's pace: 30k pair 4.87 ms with the column against 4.25 untracked).
+template <bool MASKED, bool LOCAL, bool COL>
+__device__ __forceinline__ void track_step(SideState& st, const SideCtx& w, const int H, const int t, const bool act) {
+#ifdef GX_DIAG_NO_TRACK_STEP
+    return;   // (timing only: the tracked fill without its per-cell tracking)
+#endif
+    const int thr = LOCAL ? st.thr : st.thr - w.gs;   // best - (i + j) g at this column
+    if (!COL) {
+        st.thr = MASKED ? (act ? max(thr, H) : st.thr) : max(thr, H);
+        return;
+    }
     const bool nb = act && H > thr;
     st.thr = nb ? H : (MASKED ? (act ? thr : st.thr) : thr);
     st.bstep = nb ? t : st.bstep;
-    st.bl = nb ? Mn : st.bl;
-    st.M = MASKED ? (act ? Mn : st.M) : Mn;
 }
 
 template <bool LOCAL, bool PLANES, int MODE, bool TRACK>
-__device__ __forceinline__ void side_group(SideState& st, SideCtx& w, const int t, const int4 (&hv)[2],
-                                           const int4 mu, const int4 cc, int4& mpush) {
+__device__ __forceinline__ void side_group(SideState& st, SideCtx& w, const int t, const int4 (&hv)[2]) {
     const int g = t >> 2;
     const int4 vS = hv[0], vD = hv[1];
     const int aS[4] = {vS.x, vS.y, vS.z, vS.w}, aD[4] = {vD.x, vD.y, vD.z, vD.w};
-    const int am[4] = {mu.x, mu.y, mu.z, mu.w}, ac[4] = {cc.x, cc.y, cc.z, cc.w};
     int aI[4] = {0, 0, 0, 0};
-    int e[4], qm[4];
+    int e[4];
 #pragma unroll
     for (int U = 0; U < 4; ++U) {
-        qm[U] = st.M;  // lane 63: max_matches of its column t+U-63 (the LCS push below)
         if (MODE == 1) {
             if (w.lane <= t + U) {
                 aI[U] = side_insert<LOCAL, false>(st, w, aS[U], aD[U], true);
-                if (TRACK) track_step<false>(st, w, max3i(aI[U], aS[U], aD[U]), am[U], ac[U], t + U, true);
+                if (TRACK) track_step<false, LOCAL, !PLANES>(st, w, max3i(aI[U], aS[U], aD[U]), t + U, true);
                 side_step<LOCAL, false>(st, aI[U], aS[U], aD[U], t + U, true);
             }
         } else {
             const bool act = MODE == 2 ? (unsigned)(t + U - w.lane) < (unsigned)w.m : true;
             aI[U] = side_insert<LOCAL, MODE == 2>(st, w, aS[U], aD[U], act);
-            if (TRACK) track_step<MODE == 2>(st, w, max3i(aI[U], aS[U], aD[U]), am[U], ac[U], t + U, act);
+            if (TRACK) track_step<MODE == 2, LOCAL, !PLANES>(st, w, max3i(aI[U], aS[U], aD[U]), t + U, act);
             side_step<LOCAL, MODE == 2>(st, aI[U], aS[U], aD[U], t + U, act);
         }
         e[U] = st.E;   // lane 63: E + 64 of its column t+U-62
     }
-    if (TRACK) mpush = make_int4(qm[0], qm[1], qm[2], qm[3]);
     if (PLANES) {   // the group's cells, one dwordx4 per lane and plane
         const uint32_t vo = (uint32_t)w.lane * 16u + (uint32_t)g * (kGroupInts1 * 4);
         bstore4(w.rI, vo, make_int4(aI[0], aI[1], aI[2], aI[3]));
@@ -532,50 +514,6 @@ __device__ __forceinline__ void side_group(SideState& st, SideCtx& w, const int 
             const int c = c0 + U;
             skel_store(w.skel_rsrc, (c >= 1 && c <= w.m) ? w.skel_voff + 4u * (uint32_t)c : kSkelOff, e[U]);
         }
-    }
-}
-
-// One side group with its LCS traffic (TRACK): wait for and read the row
-// above's LCS values of the group's columns (lane 0: t+1 .. t+4), step, then
-// lane 63 pushes its columns t-63 .. t-60 and posts both counts.  Per group,
-// so that the sides' chain of LCS values lags no more per strip than the
-// cores' chain (a side waits for its core's sub-blocks; a longer lag would
-// accumulate strip by strip and stall the cores on hand-off space).
-// Lane 0: LCS ring group G of the strip above (the other lanes read the zero block).
-__device__ __forceinline__ v4i side_mread(const SideCtx& w, int G) {
-    return *(const lds_v4i*)(uintptr_t)(w.mrd_base + __umul24((uint32_t)G, w.mrd_m16));
-}
-
-template <bool LOCAL, bool PLANES, int MODE, bool TRACK>
-__device__ __forceinline__ void side_track_group(SideState& st, SideCtx& w, const int t, const int4 (&hv)[2],
-                                                 const int4 cc) {
-    int4 mu = make_int4(0, 0, 0, 0), mp;
-    // TRACK: the group's LCS inputs (columns t+1 .. t+4) were read one group
-    // ago and checked then; the next group's are read now against a count
-    // peeked now and checked at the end of the group (a re-read only if the
-    // strip above was behind), so no LDS round trip waits on the path (as
-    // the core reads its ring, core_group)
-    int need = 0, seen = 0;
-    if (TRACK) {
-        const v4i x = w.mu_next;
-        mu = make_int4(x[0], x[1], x[2], x[3]);
-        need = min(t + 8, w.m) + 1;
-        seen = lds_peek(w.mw_in);
-        asm volatile("" ::: "memory");
-        w.mu_next = side_mread(w, sk_grp(t + 5));
-        asm volatile("" ::: "memory");
-        lds_post(w.mr_in, min(t + 5, w.m + 1));   // (the ring's 252-column window keeps t+5 .. t+8 in place)
-    }
-    side_group<LOCAL, PLANES, MODE, TRACK>(st, w, t, hv, mu, cc, mp);
-    if (TRACK && t >= 64 && t - 63 <= w.m) {
-        lds_v4i* a = (lds_v4i*)(uintptr_t)(w.mpush_base + __umul24((uint32_t)sk_grp(t - 63), w.mpush_m16));
-        *a = v4i{mp.x, mp.y, mp.z, mp.w};
-        asm volatile("" ::: "memory");
-        lds_post(w.mw_out, min(t - 60, w.m) + 1);
-    }
-    if (TRACK && __builtin_amdgcn_readfirstlane(seen) < need) {   // the strip above was behind: wait, re-read
-        w.tr_wait += wait_ge(w.mw_in, need, w.status);
-        w.mu_next = side_mread(w, sk_grp(t + 5));
     }
 }
 
@@ -607,51 +545,13 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, SideCtx
     st.Ed = shr1(64, st.E);                       // column 1's top-left: (64 s, 0) for lane 0
     st.cI = 0; st.cD = 0;
     st.lbest = ok ? INT_MIN : INT_MAX; st.lstep = 0; st.lE = 0;
-    // TRACK: column 0 matches nothing (algo.rs:204-211: *_matches = 0); no maximum yet
-    // (INT_MIN + 2^29: the thresholds drift by (n + m) |g| < 2^28 and stay below every value)
-    st.M = 0; st.Md = 0;
-    st.thr = INT_MIN + (1 << 29); st.bstep = 0; st.bl = 0;
-    if (TRACK) {
-        w.c1 = ok ? (int)P.c1[i - 1] : 0x1FF;
-        w.crs = rsrc_of(uniform_ptr(P.ccodes), 4 * (m + 192));
-        w.cvoff = 4u * (uint32_t)(64 - lane);
-        if (w.mpush_on && lane == kWave - 1) {   // column 0 of the bottom row
-            ((lds_int*)(uintptr_t)w.mpush_base)[3] = 0;
-            asm volatile("" ::: "memory");
-            *w.mw_out = 1;
-        }
-    }
+    // TRACK: no maximum yet (INT_MIN + 2^29: the thresholds drift by
+    // (n + m) |g| < 2^28 and stay below every value)
+    st.thr = INT_MIN + (1 << 29); st.bstep = 0;
     const int T = m + kWave;
-    int4 cc4[4] = {};
-    if (TRACK) {   // the first group's LCS inputs (side_track_group reads one group ahead)
-        w.tr_wait += wait_ge(w.mw_in, min(4, m) + 1, w.status);
-        w.mu_next = side_mread(w, sk_grp(1));
-    }
-    if (TRACK) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const v4i y = __builtin_amdgcn_raw_buffer_load_b128(w.crs, (int)w.cvoff, 16 * q, 0);
-            cc4[q] = make_int4(y[0], y[1], y[2], y[3]);
-        }
-    }
     for (int t0 = 0; t0 < T; t0 += kSub) {
         if (TRACE && w.ts && (t0 & 1023) == 0 && (t0 >> 10) < kTraceTL && lane == 0)
             w.ts[t0 >> 10] = __builtin_amdgcn_s_memrealtime();
-        // TRACK: this lane's column symbols of the next sub-block (loaded one
-        // sub-block ahead), ring space below for this sub-block's LCS pushes
-        // (the last group pushes columns up to t0 + 12 - 60)
-        int4 cnx[4] = {};
-        if (TRACK) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const v4i y = __builtin_amdgcn_raw_buffer_load_b128(w.crs, (int)w.cvoff,
-                                                                    __builtin_amdgcn_readfirstlane(4 * (t0 + kSub + 4 * q)), 0);
-                cnx[q] = make_int4(y[0], y[1], y[2], y[3]);
-            }
-            const int last_col = min(t0 - 48, m);
-            if (w.mpush_on && last_col >= kSkRingG * 4 - 4)
-                wait_ge(w.mr_out, last_col - (kSkRingG * 4 - 4) + 1, w.status);
-        }
         // the core publishes whole sub-blocks: read all four groups at once
         w.tr_wait += wait_ge(w.hcnt, (t0 >> 2) + 4, w.status);
         int4 sub[4][2];
@@ -666,22 +566,18 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, SideCtx
         lds_post(w.bcnt, (t0 >> 2) + 4);          // (reads issued first: LDS keeps the order)
         if (t0 + kSub <= kWave && t0 + kSub - 1 <= m - 1) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) side_track_group<LOCAL, PLANES, 1, TRACK>(st, w, t0 + 4 * q, sub[q], cc4[q]);
+            for (int q = 0; q < 4; ++q) side_group<LOCAL, PLANES, 1, TRACK>(st, w, t0 + 4 * q, sub[q]);
         } else if (t0 >= kWave && t0 + kSub - 1 <= m - 1) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) side_track_group<LOCAL, PLANES, 0, TRACK>(st, w, t0 + 4 * q, sub[q], cc4[q]);
+            for (int q = 0; q < 4; ++q) side_group<LOCAL, PLANES, 0, TRACK>(st, w, t0 + 4 * q, sub[q]);
         } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) side_track_group<LOCAL, PLANES, 2, TRACK>(st, w, t0 + 4 * q, sub[q], cc4[q]);
-        }
-        if (TRACK) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) cc4[q] = cnx[q];
+            for (int q = 0; q < 4; ++q) side_group<LOCAL, PLANES, 2, TRACK>(st, w, t0 + 4 * q, sub[q]);
         }
         // codes[strip][t/16][lane]
         gstore1(w.codes + (size_t)(t0 >> 4) * kWave + lane, (st.cD << 16) | (st.cI & 0xFFFFu));
     }
-    int fbest = INT_MIN, fi = 0, fj = 0, fl = 0;
+    int fbest = INT_MIN, fi = 0, fj = 0, fl = 0;   // (fl: max_matches there, from the LCS rows: finalize_kernel)
     if (TRACK) {   // the strip's first max in row-major order: the lowest lane (earliest row) holding the largest
         const int best = ok ? st.thr + (LOCAL ? 0 : (i + m) * w.gs) : INT_MIN;   // (the threshold at column m, unshifted)
         int mx = best;
@@ -689,8 +585,7 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, SideCtx
         const unsigned long long fmask = __ballot(ok && best == mx);
         const int fl_ = fmask ? (int)__builtin_ctzll(fmask) : 0;
         fbest = mx; fi = s * kWave + fl_ + 1;
-        fj = __shfl(st.bstep, fl_) - fl_ + 1;
-        fl = __shfl(st.bl, fl_);
+        fj = PLANES ? 0 : __shfl(st.bstep, fl_) - fl_ + 1;   // (0: the column is found later, skew_max_col_kernel)
     }
     if (TRACK && !LOCAL && lane == 0) {
         StripRes r{};
@@ -734,67 +629,17 @@ __device__ void side_wave(const PairDev& P, const int s, const int lane, SideCtx
 // (gx_api_fill.cpp run_fill), so a granule is valid exactly once it was written by
 // this launch.  Stores and loads are 8-byte agent-scope (sc1: write-through,
 // L1 bypass).
-// TRACK: the LCS values of the bottom row travel the same way, one more
-// granule per column (the low word, valid bit 63) in the second half of the
-// band's feed row (a feed row holds 2 feed_stride granules, feed_stride > m).
-struct IoLcs {
-    SkMRing* ring0;
-    const SkMRing* ringW;
-    lds_int *mw0, *mr0, *mwW, *mrW;
-};
-template <bool TBL, bool TRACK>
+template <bool TBL>
 __device__ void io_wave_tag(const PairDev& P, const int lb, const int lane, const Scores32& sc, SkRing* ring0,
                             const SkRing* ringW, lds_int* wcnt0, lds_int* rcnt0, lds_int* wcntW, lds_int* rcntW,
-                            const bool do_out, int* status, const IoLcs& lc) {
+                            const bool do_out, int* status) {
     const int m = P.m;
     int in_next = 0, out_next = 0;
-    int min_next = TRACK ? 0 : m + 1, mout_next = TRACK ? 0 : m + 1;
     const gu64* feed_in = lb > 0 ? (const gu64*)(P.feed + (size_t)(lb - 1) * P.feed_stride) : nullptr;
     gu64* feed_out = do_out ? (gu64*)(P.feed + (size_t)lb * P.feed_stride) : nullptr;
     unsigned idle = 0;
-    while (in_next <= m || (do_out && out_next <= m) || min_next <= m || (do_out && mout_next <= m)) {
+    while (in_next <= m || (do_out && out_next <= m)) {
         bool moved = false;
-        if (TRACK && min_next <= m) {   // row 0's max_matches are 0 (algo.rs:213-220)
-            const int lim = min(m + 1, *lc.mr0 + kSkRingG * 4 - 4);
-            const int j = min_next + lane;
-            int v = 0;
-            bool valid = false;
-            if (j < lim) {
-                if (lb == 0) {
-                    valid = true;
-                } else {
-                    const unsigned long long gr =
-                        __hip_atomic_load(feed_in + P.feed_stride + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    valid = (gr >> 63) != 0;
-                    v = (int)(unsigned)gr;
-                }
-            }
-            const unsigned long long vm = __ballot(valid);
-            const int cnt = ~vm ? (int)__builtin_ctzll(~vm) : kWave;
-            if (cnt > 0) {
-                if (lane < cnt) lc.ring0->m[sk_grp(j)][sk_pos(j)] = v;
-                lds_wait();
-                if (lane == 0) *lc.mw0 = min_next + cnt;
-                min_next += cnt;
-                moved = true;
-            }
-        }
-        if (TRACK && do_out && mout_next <= m) {
-            const int chunk = min(*lc.mwW - mout_next, kWave);
-            if (chunk > 0) {
-                const int j = mout_next + lane;
-                int v = 0;
-                if (lane < chunk) v = lc.ringW->m[sk_grp(j)][sk_pos(j)];
-                lds_wait();
-                if (lane == 0) *lc.mrW = mout_next + chunk;
-                if (lane < chunk)
-                    __hip_atomic_store((gu64*)(feed_out + P.feed_stride + j),
-                                       (unsigned long long)(unsigned)v | (1ull << 63), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                mout_next += chunk;
-                moved = true;
-            }
-        }
         if (in_next <= m) {
             const int lim = min(m + 1, *rcnt0 + kSkRingG * 4 - 4);   // ring slots the strip has read
             const int j = in_next + lane;
@@ -869,16 +714,19 @@ __device__ void io_wave_tag(const PairDev& P, const int lb, const int lane, cons
 // I/O wave, which polls, shares one with a side wave); at W = 3 two core
 // waves share a SIMD with other waves.  Persistent workgroups take bands from the
 // host's band-major queue (gx_api_fill.cpp run_fill), as fill_kernel does.
+// TRACK: the first lcs_blocks workgroups (one per pair) compute the pairs'
+// LCS rows instead (gx_lcs.h); they come first so that they are dispatched
+// with the fill and run beside it, and nothing waits for them but the
+// kernels after the launch.
 template <int W, bool LOCAL, bool PLANES, bool TBL, bool TRACE, bool TRACK>
 __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const PairDev* __restrict__ pairs,
                                                                            const int npairs, const int total_bands,
                                                                            int* band_counter, StripRes* sres,
-                                                                           PairRes* pres, const Scores32 sc) {
+                                                                           PairRes* pres, const Scores32 sc,
+                                                                           const int lcs_blocks) {
     __shared__ SkRing rings[W + 1];
     __shared__ SkHo ho[W];
     __shared__ int wcnt[W + 1], rcnt[W + 1], hcnt[W], bcnt[W];
-    __shared__ SkMRing mrings[TRACK ? W + 1 : 1];   // TRACK: the LCS rings (side to side)
-    __shared__ int mw[W + 1], mr[W + 1];
     __shared__ int band_sh;
     __shared__ int4 push_sink[2 * kWave];          // the core waves' lanes 0..62 push here (core_group)
     __shared__ int push_sink_cnt;
@@ -886,9 +734,18 @@ __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const
     if (threadIdx.x <= kSkRingG) zero_blk[threadIdx.x] = make_int4(0, 0, 0, 0);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const int lane = threadIdx.x & (kWave - 1);
+    if (TRACK && (int)blockIdx.x < lcs_blocks) {   // an LCS workgroup (gx_lcs.h)
+        const int blk = (int)blockIdx.x;
+        int p = 0;
+        while (p + 1 < npairs && pairs[p + 1].lcs_base <= blk) ++p;
+        p = __builtin_amdgcn_readfirstlane(p);
+        const PairDev& P = pairs[p];
+        lcs_workgroup(P, blk - P.lcs_base, P.lcs_waves >> 8, wave, 2 * W + 1, lane, (char*)ho, sizeof(ho), band_counter + 1);
+        return;
+    }
     for (;;) {
         if (threadIdx.x == 0) band_sh = atomicAdd(band_counter, 1);
-        if (threadIdx.x < W + 1) { wcnt[threadIdx.x] = 0; rcnt[threadIdx.x] = 0; mw[threadIdx.x] = 0; mr[threadIdx.x] = 0; }
+        if (threadIdx.x < W + 1) { wcnt[threadIdx.x] = 0; rcnt[threadIdx.x] = 0; }
         if (threadIdx.x < W) { hcnt[threadIdx.x] = 0; bcnt[threadIdx.x] = 0; }
         __syncthreads();
         const int b = __builtin_amdgcn_readfirstlane(band_sh);
@@ -901,10 +758,8 @@ __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const
         const int s = lb * W + k;
         const bool has_consumer = k == W - 1 ? (lb + 1 < P.bands) : (s + 1 < P.strips);
         if (wave == 0) {
-            const IoLcs lc{&mrings[0], &mrings[TRACK ? W : 0], (lds_int*)&mw[0], (lds_int*)&mr[0], (lds_int*)&mw[W],
-                           (lds_int*)&mr[W]};
-            io_wave_tag<TBL, TRACK>(P, lb, lane, sc, &rings[0], &rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0],
-                                    (lds_int*)&wcnt[W], (lds_int*)&rcnt[W], lb + 1 < P.bands, band_counter + 1, lc);
+            io_wave_tag<TBL>(P, lb, lane, sc, &rings[0], &rings[W], (lds_int*)&wcnt[0], (lds_int*)&rcnt[0],
+                             (lds_int*)&wcnt[W], (lds_int*)&rcnt[W], lb + 1 < P.bands, band_counter + 1);
         } else if (wave <= W) {
             if (s < P.strips) {
                 CoreCtx w;
@@ -928,24 +783,60 @@ __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const
                 w.ho = &ho[k]; w.hcnt = (lds_int*)&hcnt[k]; w.bcnt = (lds_int*)&bcnt[k];
                 w.status = band_counter + 1;
                 w.h = sc.h; w.g = sc.g; w.hg = sc.hg;
-                if (TRACK) {
-                    const int kk = TRACK ? k : 0;
-                    w.mrd_base = lds_addr(lane == 0 ? (const void*)mrings[kk].m[0] : (const void*)zero_blk);
-                    w.mrd_m16 = lane == 0 ? 16 : 0;
-                    w.mpush_on = has_consumer;
-                    const bool pl = has_consumer && lane == kWave - 1;
-                    w.mpush_base = lds_addr(pl ? (const void*)mrings[kk + 1].m[0] : (const void*)&push_sink[lane]);
-                    w.mpush_m16 = pl ? 16 : 0;
-                    w.mw_in = (lds_int*)&mw[k]; w.mr_in = (lds_int*)&mr[k];
-                    w.mw_out = has_consumer ? (lds_int*)&mw[k + 1] : (lds_int*)&push_sink_cnt;
-                    w.mr_out = (lds_int*)&mr[k + 1];
-                    w.gs = LOCAL ? 0 : sc.g;   // (global fills hold V - (i + j) g)
-                }
+                w.gs = LOCAL ? 0 : sc.g;   // TRACK: global fills hold V - (i + j) g
                 side_wave<LOCAL, PLANES, TRACE, TRACK>(P, s, lane, w, has_consumer, sres, pres + p);
             }
         }
         __syncthreads();
     }
+}
+
+// Tracked layout-3 fills that keep their planes track each row's largest
+// score_max only (track_step): finalize_kernel picks the first row holding
+// the maximum (max_i, max_val) and leaves max_j = INT_MAX; this finds the
+// first column of that row with score_max == max_val (algo.rs:258-262: the
+// first maximum in row-major order) from the row's I, D, S planes (shifted
+// for global fills: score_max = max(I, D, S) + (i + j) g), one thread per
+// column, atomicMin.  Then skew_mam_kernel: matches_at_max = max_matches
+// there from the LCS rows (algo.rs:279; gx_lcs.h).
+__global__ void skew_max_col_kernel(const PairDev* __restrict__ pairs, PairRes* pres, const int gshift) {
+    const PairDev& P = pairs[blockIdx.y];
+    PairRes* const r = pres + blockIdx.y;
+    const int i = r->max_i, j = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
+    if (i < 1 || i > P.n || j > P.m || !P.pI) return;
+    const int s = (i - 1) / kWave, lane = (i - 1) % kWave, t = j - 1 + lane;
+    const size_t o = (size_t)s * P.t4 * kGroupInts1 + (size_t)(t >> 2) * kGroupInts1 + (size_t)lane * 4 + (t & 3);
+    const int H = max3i(P.pI[o], P.pD[o], P.pS[o]) + (i + j) * gshift;
+    if (H == r->max_val) atomicMin(&r->max_j, j);
+}
+__global__ void skew_mam_kernel(const PairDev* __restrict__ pairs, PairRes* pres) {
+    const PairDev& P = pairs[blockIdx.x];
+    PairRes* const r = pres + blockIdx.x;
+    const int lane = threadIdx.x;
+    const int i = r->max_i, j = r->max_j;
+    if (i < 1 || i > P.n || j < 1 || j > P.m) return;
+    int mam = 0;
+    if (P.lwords > 0 && P.lbits) {   // LM(i, j) = j - popcount(V_i & (2^j - 1))
+        int ones = 0;
+        for (int w = lane; w * kLcsBits < j; w += kWave) {   // (64 columns a word, gx_lcs.h)
+            unsigned long long x = P.lbits[lcs_word_index(i, w, P.lwords)];
+            const int rem = j - w * kLcsBits;
+            if (rem < kLcsBits) x &= (1ull << rem) - 1ull;
+            ones += __popcll(x);
+        }
+        for (int off = 32; off > 0; off >>= 1) ones += __shfl_xor(ones, off);
+        mam = j - ones;
+    }
+    if (lane == 0) r->mam = mam;
+}
+hipError_t launch_skew_max_col(const PairDev* d_pairs, int npairs, int mmax, PairRes* d_pres, int gshift, hipStream_t st) {
+    if (npairs <= 0 || mmax <= 0) return hipSuccess;
+    hipLaunchKernelGGL(skew_max_col_kernel, dim3((unsigned)((mmax + 255) / 256), (unsigned)npairs), dim3(256), 0, st,
+                       d_pairs, d_pres, gshift);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(skew_mam_kernel, dim3((unsigned)npairs), dim3(kWave), 0, st, d_pairs, d_pres);
+    return hipGetLastError();
 }
 
 // The column inputs of every pair as int32 rows of m + 192, 64 zeros before
@@ -977,37 +868,52 @@ hipError_t launch_skew_codes(const PairDev* d_pairs, int npairs, int mmax, Score
 
 template <int W, bool LOCAL, bool PLANES, bool TBL, bool TRACE, bool TRACK>
 static hipError_t launch_skew_t(const PairDev* d_pairs, int npairs, int total_bands, int* d_counter, StripRes* d_sres,
-                                PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
-    hipLaunchKernelGGL((fill_skew_kernel<W, LOCAL, PLANES, TBL, TRACE, TRACK>), dim3(grid), dim3((2 * W + 1) * kWave), 0,
-                       st, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc);
+                                PairRes* d_pres, Scores32 sc, int grid, int lcs_blocks, hipStream_t st) {
+    hipLaunchKernelGGL((fill_skew_kernel<W, LOCAL, PLANES, TBL, TRACE, TRACK>), dim3(grid + (TRACK ? lcs_blocks : 0)),
+                       dim3((2 * W + 1) * kWave), 0, st, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc,
+                       TRACK ? lcs_blocks : 0);
     return hipGetLastError();
 }
 
 template <bool LO, bool PL, bool TB, bool TR, bool TK, int W0, int... Ws>
 static hipError_t launch_skew_w(int W, const PairDev* d_pairs, int npairs, int total_bands, int* d_counter,
-                                StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid, hipStream_t st) {
+                                StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid, int lcs_blocks,
+                                hipStream_t st) {
     if (W == W0)
         return launch_skew_t<W0, LO, PL, TB, TR, TK>(d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc, grid,
-                                                     st);
+                                                     lcs_blocks, st);
     if constexpr (sizeof...(Ws) > 0)
         return launch_skew_w<LO, PL, TB, TR, TK, Ws...>(W, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, sc,
-                                                        grid, st);
+                                                        grid, lcs_blocks, st);
     return hipErrorInvalidValue;
 }
 
+// LCS workgroups of a tracked launch (gx_lcs.h): sweeping waves a workgroup
+// (all of them, as many as the LDS of the fill's core -> side rings holds
+// rings for), and enough workgroups that about T / 64 + 1 strips are swept
+// at once -- a strip starts ~71 steps after the one above, so that many
+// keep up with the dependence chain -- and no more than the strips.
+int skew_lcs_sweep(int W) { return std::min(2 * W + 1, lcs_max_sweep((size_t)W * sizeof(SkHo))); }
+int skew_lcs_blocks(int W, int n, int m) {
+    const int T = lcs_steps(ceil_div(m, kLcsBits)), S = ceil_div(n, kWave);
+    const int waves = std::min(S, ceil_div(T, 64) + 1);
+    return std::max(1, std::min(8, ceil_div(waves, std::max(1, skew_lcs_sweep(W)))));
+}
+
 // Band widths of layout 3 (must match gx_api_plan.cpp skew_band_waves).  trace:
-// the diagnostics instantiation (PairDev.trace set; fills with planes only,
-// the others run untraced).
-// track: the first maximum + max_matches (alignment_table's max_cell and
-// matches_at_max, algo.rs:258-262, 279; no score tables, untraced).
+// the diagnostics instantiation (PairDev.trace set; untracked fills with
+// planes only, the others run untraced).
+// track: the first maximum (alignment_table's max_cell, algo.rs:258-262)
+// in the side waves, and max_matches as LCS rows in lcs_blocks leading
+// workgroups (gx_lcs.h; matches_at_max, algo.rs:279, by finalize_kernel).
+bool skew_traced(bool planes, bool trace, bool track) { return trace && planes && !track; }
 hipError_t launch_fill_skew(int W, bool local, bool planes, bool tbl, bool trace, bool track, const PairDev* d_pairs,
                             int npairs, int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc,
-                            int grid, hipStream_t st) {
-    if (track && tbl) return hipErrorInvalidValue;
+                            int grid, int lcs_blocks, hipStream_t st) {
 #define GX_SKEW_CASE(LO, PL, TB, TR, TK)                                                                           \
-    if (local == LO && planes == PL && tbl == TB && (trace && PL && !track) == TR && track == TK)                   \
+    if (local == LO && planes == PL && tbl == TB && skew_traced(planes, trace, track) == TR && track == TK)         \
         return launch_skew_w<LO, PL, TB, TR, TK, 1, 2, 3>(W, d_pairs, npairs, total_bands, d_counter, d_sres, d_pres, \
-                                                             sc, grid, st);
+                                                             sc, grid, lcs_blocks, st);
     GX_SKEW_CASE(false, false, false, false, false)
     GX_SKEW_CASE(false, false, true, false, false)
     GX_SKEW_CASE(false, true, false, false, false)
@@ -1024,6 +930,10 @@ hipError_t launch_fill_skew(int W, bool local, bool planes, bool tbl, bool trace
     GX_SKEW_CASE(false, true, false, false, true)
     GX_SKEW_CASE(true, false, false, false, true)
     GX_SKEW_CASE(true, true, false, false, true)
+    GX_SKEW_CASE(false, false, true, false, true)
+    GX_SKEW_CASE(false, true, true, false, true)
+    GX_SKEW_CASE(true, false, true, false, true)
+    GX_SKEW_CASE(true, true, true, false, true)
 #undef GX_SKEW_CASE
     return hipErrorInvalidValue;
 }

@@ -77,7 +77,7 @@ EXPORTED = ["gx_last_error", "gx_version", "gx_context_create", "gx_context_dest
             "gx_table_plane_sums", "gx_retrace", "gx_table_free", "gx_align", "gx_align_batch", "gx_align_batch_multi",
             "gx_stage_pairs",
             "gx_run_staged", "gx_run_staged_steps", "gx_staged_plane_sums", "gx_staged_steps",
-            "gx_staged_pass_results", "gx_fill_info", "gx_batch_chunks", "gx_fill_twin", "gx_fill_groups", "gx_plane_bytes_per_cell", "gx_twin_admission",
+            "gx_staged_pass_results", "gx_fill_info", "gx_batch_chunks", "gx_fill_twin", "gx_fill_groups", "gx_fill_plane_bits", "gx_plane_bytes_per_cell", "gx_twin_admission",
             "gx_twin_admission_mode", "gx_plan_layout", "gx_staged_table",
             "gx_fasta_load",
             "gx_config_load", "gx_format_alignment", "gx_format_table"]
@@ -128,6 +128,8 @@ def lib():
     L.gx_batch_chunks.argtypes = [vp]
     L.gx_fill_twin.argtypes = [vp]
     L.gx_fill_groups.argtypes = [vp]
+    if hasattr(L, "gx_fill_plane_bits"):   # (absent from pre-12-bit builds run for A/B timing)
+        L.gx_fill_plane_bits.argtypes = [vp]
     L.gx_plane_bytes_per_cell.argtypes = [ctypes.POINTER(CScores), ctypes.c_int]
     L.gx_twin_admission.argtypes = [ctypes.POINTER(CScores), ctypes.c_int, ctypes.c_int64,
                                     ctypes.POINTER(ctypes.c_int64)]
@@ -347,7 +349,9 @@ class Context:
         """The last fill launch: layout, band width, score-plane bytes per cell (gx_fill_info)."""
         v = [ctypes.c_int() for _ in range(3)]
         _check(lib().gx_fill_info(self.ptr, *[ctypes.byref(x) for x in v]))
-        return {"layout": v[0].value, "band_waves": v[1].value, "plane_bytes_per_cell": v[2].value,
+        bits = lib().gx_fill_plane_bits(self.ptr) if hasattr(lib(), "gx_fill_plane_bits") else 8 * v[2].value
+        return {"layout": v[0].value, "band_waves": v[1].value,
+                "plane_bytes_per_cell": bits // 8 if bits % 8 == 0 else bits / 8,   # (twin codes: 1.5)
                 "chunks": lib().gx_batch_chunks(self.ptr), "twin": lib().gx_fill_twin(self.ptr),
                 "groups": lib().gx_fill_groups(self.ptr)}
 

@@ -133,8 +133,10 @@ int gx_table_export_plane(const gx_table* t, int which, int64_t* out, size_t out
 
 /* Rows row0 .. row0+rows-1 of one score plane as int64, row-major rows x (m+1)
  * (a slice of the table: a 30k x 30k plane is 7.2 GB as int64).  Row 0 and
- * column 0 are the reference's boundary cells (algo.rs:195-220).  No
- * reference counterpart (the reference materialises the whole Array2). */
+ * column 0 are the reference's boundary cells (algo.rs:195-220).  which = 3:
+ * max_matches of each cell (AlignmentCell::max_matches, algo.rs:113-121; 0 on
+ * the boundary), for tables built with GX_TABLE_MATCHES.  No reference
+ * counterpart (the reference materialises the whole Array2). */
 int gx_table_export_rows(const gx_table* t, int which, size_t row0, size_t rows, int64_t* out, size_t out_cells);
 
 /* Checksums of the three score planes, computed on the device from the
@@ -240,9 +242,14 @@ int gx_staged_pass_results(const gx_context* ctx, gx_result* out, size_t cap, si
  * untracked single pairs), band width (strips per workgroup) and
  * score-plane bytes written per cell (0: none, 12: int32 planes, 3: compact
  * planes -- per-cell byte differences, decoded exactly by the exports, 2:
- * the twin fill's plane codes -- the three differences in one 16-bit word,
- * DESIGN.md 4.4, batches only).  No reference counterpart (measurement only). */
+ * the twin fill's plane codes -- 12 bits a cell since round 6, DESIGN.md
+ * 4.4, batches only; reported rounded up: gx_fill_plane_bits gives the exact
+ * figure).  No reference counterpart (measurement only). */
 int gx_fill_info(const gx_context* ctx, int* layout, int* band_waves, int* plane_bytes_per_cell);
+/* Score-plane bits written per cell by the last fill launch (0, 12: twin
+ * plane codes, 24: compact bytes, 96: int32 planes, 192: int64 planes), or
+ * -1 without a context.  No reference counterpart (measurement only). */
+int gx_fill_plane_bits(const gx_context* ctx);
 /* Chunks of the last gx_run_staged(_steps) / gx_align_batch call: a batch
  * whose device footprint (planes, codes, skeleton) exceeds the free HBM runs
  * as contiguous chunks of pairs through the same device buffers

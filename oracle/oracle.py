@@ -208,3 +208,50 @@ def fasta_parse(data: bytes):
     for r in range(k):
         res.append((ob[int(no[r]):int(no[r] + nl[r])], ob[int(so[r]):int(so[r] + sl[r])]))
     return res
+
+
+def processed_bytes(s1: bytes, s2: bytes, rev: bool = False):
+    """The bytes is_match compares (sequence.rs:102-115) as int arrays, None
+    (an index past the end, incl. the usize wrap of len - i) as -1: row k of
+    the table (k = i - 1) reads s1[len(s2) - k], column k reads s2[len(s1) - k]
+    when rev, else s1[k] / s2[k]."""
+    a = np.frombuffer(s1, np.uint8).astype(np.int32)
+    b = np.frombuffer(s2, np.uint8).astype(np.int32)
+    if not rev:
+        return a, b
+    n, m = len(a), len(b)
+    c1 = np.full(n, -1, np.int32)
+    c2 = np.full(m, -1, np.int32)
+    for k in range(n):
+        if k <= m and m - k < n:
+            c1[k] = a[m - k]
+    for k in range(m):
+        if k <= n and n - k < m:
+            c2[k] = b[n - k]
+    return c1, c2
+
+
+def lcs_rows(s1: bytes, s2: bytes, rows, rev: bool = False) -> dict:
+    """max_matches(cell(i, j)) for every i in `rows` (a dict i -> int32 row
+    of m + 1 values): the recurrence of algo.rs:250-256 (max of
+    max_matches(i, j-1), max_matches(i-1, j), max_matches(i-1, j-1) +
+    is_match), 0 on row 0 and column 0 (algo.rs:195-220).  Row by row in
+    numpy: L(i, j) = max over k <= j of max(L(i-1, k), L(i-1, k-1) + is_match),
+    the prefix max carrying the L(i, j-1) term."""
+    c1, c2 = processed_bytes(s1, s2, rev)
+    want = set(int(i) for i in rows)
+    out = {}
+    prev = np.zeros(len(c2) + 1, np.int32)
+    if 0 in want:
+        out[0] = prev.copy()
+    top = max(want) if want else 0
+    for i in range(1, top + 1):
+        mt = (c2 == c1[i - 1]).astype(np.int32)
+        t = np.maximum(prev[1:], prev[:-1] + mt)
+        cur = np.empty_like(prev)
+        cur[0] = 0
+        np.maximum.accumulate(t, out=cur[1:])
+        prev = cur
+        if i in want:
+            out[i] = cur.copy()
+    return out

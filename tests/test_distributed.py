@@ -57,6 +57,65 @@ def test_two_ranks_shard_and_reduce():
     assert not set(out[0][3]) & set(out[1][3])
 
 
+def _scatter_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "genomics-rs_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    import bench as b
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    for workload, P, L in (("synthetic", 3, 300), ("allvsall", 0, 0)):
+        pairs, n_total, ij, info = b.scatter_inputs(dist, rank, world, workload, P, L, False, "cpu")
+        # the rest of bench.py's path with a stand-in for the GPU aligner:
+        # per-pair rows, max-over-ranks time, rank-ordered gather
+        rows = [[len(x) * 7 + len(y), len(x) + len(y), sum(x) % 1000] for x, y in pairs]
+        t, gathered = b.combine_over_ranks(dist, 1.0 + rank, rows, "cpu")
+        out[workload] = (pairs, n_total, ij, info, t, gathered)
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_inputs_scattered_from_rank0():
+    """bench.py's multi-GPU path (world 2, gloo on CPU tensors; RCCL over
+    xGMI on the GPU box): rank 0 builds the inputs and broadcasts them
+    (scatter_inputs), each rank keeps exactly the shard the local path would
+    have built -- synthetic pairs r*P .. r*P+P-1, the LPT share of the 45
+    comparison-genome pairs -- then the per-pair rows are gathered and the
+    time is the max over ranks.  The line's scatter record counts the bytes."""
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "genomics-rs_amd"))
+    import gxamd as gx
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        out = sorted((q.get(timeout=240) for _ in range(2)), key=lambda x: x[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for rank, o in out:
+        pairs, n_total, ij, info, t, gathered = o["synthetic"]
+        assert pairs == bench.rank_pairs(rank, 3, 300)
+        assert n_total == 2 * 3 * 300 * 300 and ij is None and t == 2.0
+        assert info["mode"] == "scatter from rank 0" and info["bytes"] == 2 * 3 * 2 * 300 and "gloo" in info["collective"]
+        want = [[(len(x) * 7 + len(y), len(x) + len(y), sum(x) % 1000) for x, y in bench.rank_pairs(r, 3, 300)]
+                for r in range(2)]
+        assert gathered == want
+        pairs, n_total, ij, info, t, gathered = o["allvsall"]
+        local_pairs, local_total, local_ij = bench.allvsall_share(gx, rank, 2)
+        assert pairs == local_pairs and n_total == local_total and ij == local_ij
+        assert info["bytes"] == sum(len(a) for a in {x for p in bench.allvsall_share(gx, 0, 1)[0] for x in p})
+    # the two ranks' all-vs-all shares are disjoint and cover the 45 pairs
+    both = out[0][1]["allvsall"][2] + out[1][1]["allvsall"][2]
+    assert sorted(both) == sorted(gx.all_pairs(10, with_self=False))
+
+
 def test_single_process_combine_is_identity():
     t, g = bench.combine_over_ranks(None, 3.5, [[1, 2, 3]], "cpu")
     assert t == 3.5 and g == [[(1, 2, 3)]]

@@ -184,7 +184,7 @@ def test_all_vs_all_planes_match_oracle(gx, ctx, monkeypatch, twin):
     st = gx.StagedPairs(pairs, ctx=ctx)
     res, _ = st.run(gx.Scores(*g["scores"]), False, keep_planes=True, steps=1, plane_sums=True)
     info = ctx.fill_info()
-    assert info["plane_bytes_per_cell"] == (2 if twin == "auto" else 3) and info["twin"] == (1 if twin == "auto" else 0), info
+    assert info["plane_bytes_per_cell"] == (1.5 if twin == "auto" else 3) and info["twin"] == (1 if twin == "auto" else 0), info
     sums = st.plane_sums()
     for p, c in enumerate(g["cases"]):
         assert [int(x) for x in sums[0, p]] == c["plane_sums"], (c["i"], c["j"])

@@ -106,6 +106,41 @@ def test_large_table_plane_sums(gx, ctx, monkeypatch, case, tracked, layout):
     assert len(aln.alignment) == c["n_steps"] and _digest(aln._steps) == c["alignment_sha256"]
 
 
+@pytest.mark.parametrize("case", range(4), ids=[c["name"] for c in _large_cases()])
+def test_large_tracked_lcs_rows(gx, ctx, oracle, case):
+    """The drop-in alignment_table with max_cell / matches_at_max and the
+    full-cell export flag at configs 2 and 3 (round 6): the default launch
+    puts them on layout 3, whose max_matches are LCS bit rows beside the fill
+    (gx_lcs.h).  matches_at_max and max_cell against large_digests.json, the
+    score matrix against its checksums, and max_matches of row slices (first
+    rows, the middle, the last rows, every column) against the LCS recurrence
+    (algo.rs:250-256) restated row by row in numpy (oracle.lcs_rows)."""
+    c = _large_cases()[case]
+    a, b = _large_inputs()[c["name"].split("/")[0]]
+    n, m = len(a), len(b)
+    cont = gx.SequenceContainer([gx.Sequence("a", a.decode()), gx.Sequence("b", b.decode())])
+    table, mam = gx.alignment_table(cont, gx.Scores(*c["scores"]), c["is_local"], False, ctx=ctx, max_cell=True,
+                                    flags=gx.GX_TABLE_MATCHES)
+    info = ctx.fill_info()
+    assert info["layout"] == 3, info
+    assert mam == c["matches_at_max"] and table.info()["max_cell"] == tuple(c["max_cell"])
+    assert table.plane_sums() == [int(x) for x in c["plane_sums"]]
+    slices = [(0, 40), (n // 2 - 20, 41), (n - 39, 40)]
+    want = set()
+    for r0, k in slices:
+        want.update(range(r0, r0 + k))
+    want.add(c["max_cell"][0])
+    L = oracle.lcs_rows(a, b, want)
+    for r0, k in slices:
+        got = table.rows(3, r0, k)
+        for r in range(k):
+            assert np.array_equal(got[r], L[r0 + r]), (c["name"], r0 + r)
+    assert L[c["max_cell"][0]][c["max_cell"][1]] == mam
+    aln = gx.retrace(cont, table, c["is_local"])
+    assert aln.score == c["score"] and len(aln.alignment) == c["n_steps"]
+    assert _digest(aln._steps) == c["alignment_sha256"]
+
+
 def _host_fold(table, n, m, chunk=1024):
     """Weighted plane sums folded on the host from exported int64 rows."""
     sums = [np.uint64(0)] * 3
@@ -166,15 +201,15 @@ LAUNCHES = {
     # the scalar fill's headline instantiation: 15-strip bands, compact byte planes, band-major queue;
     # a grid of 8 workgroups makes the 64 bands run in 8 rounds with HBM hand-offs between them
     "w15_grid8": ({"GX_TWIN": "0", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "8"}, (0, 15, 3)),
-    # the bench's headline launch: the twin fill at 8-strip bands, 2-B twin plane codes
-    "twin_w8_grid8": ({"GX_TWIN": "1", "GX_BAND_WAVES": "8", "GX_FILL_GRID": "8"}, (0, 8, 2)),
+    # the bench's headline launch: the twin fill at 8-strip bands, 12-bit twin plane codes
+    "twin_w8_grid8": ({"GX_TWIN": "1", "GX_BAND_WAVES": "8", "GX_FILL_GRID": "8"}, (0, 8, 1.5)),
     # the twin fill with per-pair byte planes (the table format)
     "twin_w8_bytes": ({"GX_TWIN": "1", "GX_BAND_WAVES": "8", "GX_PLANES_W16": "0"}, (0, 8, 3)),
     "auto": ({}, None),
     "int32_planes": ({"GX_PLANES32": "1"}, (0, None, 12)),
     # every buffer the pool hands out is poisoned on its new user's stream: a pass that read the previous pass's data would fail
     "w15_poison": ({"GX_BAND_WAVES": "15", "GX_FILL_GRID": "16", "GX_POOL_POISON": "1"}, (0, 15, None)),
-    "twin_poison": ({"GX_TWIN": "1", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "16", "GX_POOL_POISON": "1"}, (0, 15, 2)),
+    "twin_poison": ({"GX_TWIN": "1", "GX_BAND_WAVES": "15", "GX_FILL_GRID": "16", "GX_POOL_POISON": "1"}, (0, 15, 1.5)),
 }
 
 
@@ -211,7 +246,7 @@ def test_overlapped_bench_launch_30k(gx, ctx, monkeypatch, npairs, env):
     cases = _synth(30000)[:npairs]
     pairs = [_synth_pair(c["k"], 30000) for c in cases]
     info = _staged_check(gx, ctx, pairs, cases, steps=3)
-    assert info["groups"] == 2 and info["twin"] == 1 and info["plane_bytes_per_cell"] == 2, info
+    assert info["groups"] == 2 and info["twin"] == 1 and info["plane_bytes_per_cell"] == 1.5, info
 
 
 @pytest.mark.parametrize("poison", [True, False], ids=["poison", "plain"])
@@ -238,7 +273,7 @@ def test_overlapped_alternating_sets(gx, ctx, monkeypatch, poison):
     res, fill_ms = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=steps, plane_sums=True,
                           alternate=True)
     info = ctx.fill_info()
-    assert info["groups"] == 2 and info["twin"] == 1 and info["plane_bytes_per_cell"] == 2, info
+    assert info["groups"] == 2 and info["twin"] == 1 and info["plane_bytes_per_cell"] == 1.5, info
     assert fill_ms > 0
     sums = st.plane_sums()
     passes = st.pass_results()
@@ -299,7 +334,7 @@ def test_chunked_bench_launch(gx, ctx, monkeypatch, variant):
     pairs = [_synth_pair(c["k"], 30000) for c in cases]
     info = _staged_check(gx, ctx, pairs, cases, steps=2)
     assert info["chunks"] == 2, info
-    assert info["plane_bytes_per_cell"] in ((2, 3) if variant == "compact" else (12,)), info
+    assert info["plane_bytes_per_cell"] in ((1.5, 3) if variant == "compact" else (12,)), info
 
 
 def test_config5_1k_chunked(gx, ctx, monkeypatch):

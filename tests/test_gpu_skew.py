@@ -85,21 +85,73 @@ def test_skew_tracked(gx, ctx, oracle, launch, is_local):
 def test_skew_tracked_table(gx, ctx, oracle, monkeypatch):
     """alignment_table (the drop-in call with max_cell / matches_at_max, as
     INTEGRATION.md binds it) on layout 3: every exported cell value and the
-    tracked outputs against the oracle, reverse_sequences both ways."""
+    tracked outputs against the oracle, reverse_sequences both ways.  With
+    GX_TABLE_MATCHES (round 6) the full 48-B cells: the *_matches fields come
+    from the LCS bit rows of the launch's leading workgroups (gx_lcs.h),
+    insert = LM(i, j-1), delete = LM(i-1, j), sub = LM(i-1, j-1) + is_match on
+    the processed bytes (algo.rs:250-256, sequence.rs:102-115)."""
     monkeypatch.setenv("GX_LAYOUT", "3")
     rng = random.Random(5)
-    for n, m, rev in ((200, 333, False), (333, 200, True), (129, 640, False)):
+    for n, m, rev in ((200, 333, False), (333, 200, True), (129, 640, False), (70, 129, True)):
         a = "".join(rng.choice("ACGT") for _ in range(n))
         b = "".join(rng.choice("ACGT") for _ in range(m))
         for is_local in (False, True):
-            cont = gx.SequenceContainer([gx.Sequence("a", a), gx.Sequence("b", b)])
-            table, mam = gx.alignment_table(cont, gx.Scores(*CONFIG_SCORES), is_local, rev, ctx=ctx, max_cell=True)
-            assert ctx.fill_info()["layout"] == 3, ctx.fill_info()
-            o = oracle.align(a.encode(), b.encode(), CONFIG_SCORES, is_local=is_local, rev=rev, want_planes=True)
-            assert mam == o.matches_at_max and table.info()["max_cell"] == o.max_cell, (n, m, rev, is_local)
-            for k in range(3):
-                assert np.array_equal(table.plane(k), o.planes[k]), (n, m, rev, is_local, k)
-            table.free()
+            for flags in (0, gx.GX_TABLE_PLANES | gx.GX_TABLE_MATCHES):
+                cont = gx.SequenceContainer([gx.Sequence("a", a), gx.Sequence("b", b)])
+                table, mam = gx.alignment_table(cont, gx.Scores(*CONFIG_SCORES), is_local, rev, ctx=ctx,
+                                                max_cell=True, flags=flags or gx.GX_TABLE_PLANES)
+                assert ctx.fill_info()["layout"] == 3, ctx.fill_info()
+                o = oracle.align(a.encode(), b.encode(), CONFIG_SCORES, is_local=is_local, rev=rev, want_planes=True,
+                                 want_lcs=True)
+                tag = (n, m, rev, is_local, flags)
+                assert mam == o.matches_at_max and table.info()["max_cell"] == o.max_cell, tag
+                for k in range(3):
+                    assert np.array_equal(table.plane(k), o.planes[k]), (tag, k)
+                if flags:
+                    cells = table.export()
+                    L = o.lcs.astype(np.int64)
+                    c1, c2 = oracle.processed_bytes(a.encode(), b.encode(), rev)
+                    mt = (c1[:, None] == c2[None, :]).astype(np.int64)
+                    assert np.array_equal(cells["insert_matches"][1:, 1:], L[1:, :-1]), tag
+                    assert np.array_equal(cells["delete_matches"][1:, 1:], L[:-1, 1:]), tag
+                    assert np.array_equal(cells["sub_matches"][1:, 1:], L[:-1, :-1] + mt), tag
+                    for f in ("insert_matches", "delete_matches", "sub_matches"):
+                        assert not cells[f][0, :].any() and not cells[f][:, 0].any(), (tag, f)
+                    assert np.array_equal(table.rows(3, 0, n + 1), L), tag
+                table.free()
+
+
+# rows / columns around the LCS units' edges (128 words = 8,192 columns a
+# unit, 2W + 1 units a workgroup: 40,960 columns at W = 2) and the 32-row
+# carry hand-offs between units
+LCS_SHAPES = [(1, 8193), (31, 8192), (32, 8191), (33, 16385), (64, 24577), (65, 40961), (40, 50000), (97, 100)]
+
+
+@pytest.mark.parametrize("n,m", LCS_SHAPES)
+def test_skew_lcs_rows(gx, ctx, oracle, monkeypatch, n, m):
+    """max_matches of every cell (table rows, which = 3) and matches_at_max
+    of tracked layout-3 tables whose LCS rows span several units and LCS
+    workgroups, for DNA (score tables in the core), a 6-letter alphabet and
+    reverse_sequences (None == None past the ends), at band widths 2 and 1
+    (1: three units a workgroup)."""
+    rng = random.Random(n * 7 + m)
+    for alpha, rev, bw in ((b"ACGT", False, "2"), (b"ACDEFG", True, "2"), (b"AC", False, "1")):
+        monkeypatch.setenv("GX_LAYOUT", "3")
+        monkeypatch.setenv("GX_BAND_WAVES", bw)
+        a = bytes(rng.choice(alpha) for _ in range(n))
+        b = bytes(rng.choice(alpha) for _ in range(m))
+        cont = gx.SequenceContainer([gx.Sequence("a", a.decode()), gx.Sequence("b", b.decode())])
+        table, mam = gx.alignment_table(cont, gx.Scores(*CONFIG_SCORES), False, rev, ctx=ctx, max_cell=True,
+                                        flags=gx.GX_TABLE_MATCHES)
+        assert ctx.fill_info()["layout"] == 3, ctx.fill_info()
+        o = oracle.align(a, b, CONFIG_SCORES, rev=rev)
+        tag = (n, m, alpha, rev, bw)
+        assert mam == o.matches_at_max and table.info()["max_cell"] == o.max_cell, tag
+        L = oracle.lcs_rows(a, b, range(n + 1), rev=rev)
+        got = table.rows(3, 0, n + 1)
+        for i in range(n + 1):
+            assert np.array_equal(got[i], L[i]), (tag, i)
+        table.free()
 
 
 @pytest.mark.parametrize("scores,layout", [((1, -2, -1, -5), 3), ((2, -3, -2, -4), 3), ((5, -4, 0, -10), 3),

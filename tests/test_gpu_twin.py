@@ -74,7 +74,7 @@ def test_twin_staged_planes(gx, ctx, oracle, launch, monkeypatch, fmt):
     st = gx.StagedPairs(pairs, ctx=ctx)
     res, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=3, plane_sums=True)
     info = ctx.fill_info()
-    assert info["twin"] == 1 and info["plane_bytes_per_cell"] == (2 if fmt == "codes" else 3), info
+    assert info["twin"] == 1 and info["plane_bytes_per_cell"] == (1.5 if fmt == "codes" else 3), info
     sums = st.plane_sums()
     for p, (a, b) in enumerate(pairs):
         o = oracle.align_lean(a, b, CONFIG_SCORES)
@@ -163,7 +163,7 @@ def test_twin_mixed_shapes(gx, ctx, oracle, monkeypatch, odd):
     st = gx.StagedPairs(pairs, ctx=ctx)
     res, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=2, plane_sums=True)
     info = ctx.fill_info()
-    assert info["twin"] == 1 and info["plane_bytes_per_cell"] == 2, info
+    assert info["twin"] == 1 and info["plane_bytes_per_cell"] == 1.5, info
     sums = st.plane_sums()
     for p, (a, b) in enumerate(pairs):
         o = oracle.align_lean(a, b, CONFIG_SCORES)
@@ -362,7 +362,7 @@ def test_twin_overlapped_global(gx, ctx, oracle, monkeypatch, launch_env):
     st = gx.StagedPairs(pairs, ctx=ctx)
     res, _ = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=steps, plane_sums=True)
     info = ctx.fill_info()
-    assert info["groups"] == 2 and info["twin"] == 1 and info["plane_bytes_per_cell"] == 2, info
+    assert info["groups"] == 2 and info["twin"] == 1 and info["plane_bytes_per_cell"] == 1.5, info
     sums = st.plane_sums()
     passes = st.pass_results()
     assert len(passes) == steps
@@ -381,7 +381,7 @@ def test_staged_table_export(gx, ctx, oracle, monkeypatch, variant):
     """The batch formats handed over as tables (gx_staged_table): a staged
     run keeps its last pass's planes on the device (GX_STAGED_KEEP_PLANES)
     and each pair's table exports, row by row, the reference's I, D, S planes
-    (algo.rs:172, 281) -- decoded from the twin fill's 2-B plane codes (the
+    (algo.rs:172, 281) -- decoded from the twin fill's 12-bit plane codes (the
     headline's format), the byte planes, or int32 -- equal to the oracle's
     whole planes; plane checksums too.  Rows cover the strip and twin-half
     boundaries; pairs of unequal shapes so twins mix lengths."""
@@ -403,7 +403,7 @@ def test_staged_table_export(gx, ctx, oracle, monkeypatch, variant):
     st = gx.StagedPairs(pairs, ctx=ctx)
     res, _ = st.run(gx.Scores(*CONFIG_SCORES), local, keep_planes=True, steps=2, keep=True)
     info = ctx.fill_info()
-    want_bpc = {"twin_codes": 2, "byte_planes": 3, "int32": 12, "local_twin": 2}[variant]
+    want_bpc = {"twin_codes": 1.5, "byte_planes": 3, "int32": 12, "local_twin": 1.5}[variant]
     assert info["plane_bytes_per_cell"] == want_bpc and info["layout"] == 0, info
     for p in (0, 1, 5, 12, 23):
         a, b = pairs[p]

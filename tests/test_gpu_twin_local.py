@@ -48,11 +48,13 @@ def _check(gx, ctx, oracle, pairs, scores, steps=1, twin=1):
 
 
 def _w16_ok(scores):
-    """gx_api_plan.cpp w16_ok: the twin plane codes' field ranges."""
+    """gx_api_plan.cpp w16_ok: the twin plane codes' field ranges (DESIGN.md
+    4.4): x_S in 5 signed bits, x_D in 7 (12-bit codes; the format holds no
+    x_I since round 5)."""
     sm, smm, g, h = scores
     a = h + g
     U = max(0, max(sm, smm) - a)
-    return (U - a - g <= 15 and min(sm, smm) - U >= -16 and max(sm, smm) - 2 * a <= 15 and 2 * a - U >= -64
+    return (g <= 0 and h <= 0 and min(sm, smm) - U >= -16 and max(sm, smm) - 2 * a <= 15 and 2 * a - U >= -64
             and U - 2 * a <= 63)
 
 
@@ -75,10 +77,12 @@ def _planted(rng, n, m, core, al=b"ACGT"):
 
 
 # (scores, twin fill expected): the local twin needs the twin plane codes'
-# ranges (gx_api_plan.cpp w16_ok: x_I - g in [0, 15] ...); (2, -3, -2, -4) and
-# (5, -4, 0, -10) exceed them and run the scalar local fill
+# ranges (gx_api_plan.cpp w16_ok: x_S in [-16, 15], x_D in [-64, 63]);
+# (2, -3, -2, -4), whose insert difference (16) overflowed the pre-round-6
+# rule's 4-bit x_I field, now takes it; (5, -4, 0, -10) (x_S down to -19)
+# still runs the scalar local fill
 @pytest.mark.parametrize("scores,twin", [(CONFIG_SCORES, 1), ((2, -3, -1, -4), 1), ((3, -2, -1, -3), 1),
-                                         ((1, -1, 0, 0), 1), ((3, -3, -1, -1), 1), ((2, -3, -2, -4), 0),
+                                         ((1, -1, 0, 0), 1), ((3, -3, -1, -1), 1), ((2, -3, -2, -4), 1),
                                          ((5, -4, 0, -10), 0)])
 def test_local_twin_planted_cores(gx, ctx, oracle, monkeypatch, scores, twin):
     """A planted shared core per pair (a long local alignment inside the
