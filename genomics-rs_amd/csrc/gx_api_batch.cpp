@@ -460,10 +460,17 @@ int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
         bool jheld[3] = {false, false, false};
         auto trace_dev = [&](int s) {
             if (wstream) {   // the walk on its own stream; the fill's buffers held until it is collected
+#ifndef GX_MUT_NO_FDONE_WAIT   // (mutation build only: tests/test_gpu_atsize.py must catch its absence)
                 if (hipStreamWaitEvent(ctx->tstream, ctx->slots[s].fdone, 0) != hipSuccess) return fail(GX_EHIP, "walk stream wait");
+#endif
                 jheld[s] = true;
-                return run_traceback(ctx, std::vector<const FillJob*>{&jobs[s]}, starts, ctx->slots[s].out, s, false, true,
-                                     ctx->tstream);
+                const int r = run_traceback(ctx, std::vector<const FillJob*>{&jobs[s]}, starts, ctx->slots[s].out, s, false,
+                                            true, ctx->tstream);
+#ifdef GX_MUT_EARLY_RELEASE   // (mutation build only: the fill's buffers back to the pool while the walk may read them)
+                job_release(ctx, jobs[s]);
+                jheld[s] = false;
+#endif
+                return r;
             }
             int r = run_traceback(ctx, jobs[s], starts, ctx->slots[s].out, s, false, true);
             release_or_hold(ctx, jobs[s], tr_pass++ == nsteps - 1, &held[s]);   // stream order: later users come after the traceback

@@ -322,13 +322,14 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
             d.lwords = ceil_div(d.m, kLcsBits);
             // sweeping workgroups (GX_LCS_WAVES, GX_LCS_WGS override: diagnostics)
             const int nwg = getenv("GX_LCS_WGS") ? std::max(1, atoi(getenv("GX_LCS_WGS"))) : skew_lcs_blocks(W, d.n, d.m);
-            d.lcs_waves = (getenv("GX_LCS_WAVES") ? atoi(getenv("GX_LCS_WAVES")) : 0) | (nwg << 8);   // (0: all that fit)
+            d.lcs_waves = (getenv("GX_LCS_WAVES") ? atoi(getenv("GX_LCS_WAVES")) : 0) | (nwg << 8) |   // (0: all that fit)
+                          (lcs ? 1 << 16 : 0);   // every row (the matches planes of a table) or the strips' last
             d.lcs_base = lcs_blocks;
             lcs_blocks += nwg;
             const size_t feed_words = (size_t)ceil_div(d.n, kWave) * lcs_steps(d.lwords);   // (x2: tagged halves)
             zo[p] = zbytes; zbytes += (256 * ((size_t)d.lwords + 2 * kLcsMaskPad) + 2 * feed_words) * sizeof(unsigned long long);
             ro[p] = rbytes;
-            rbytes += feed_words * kWave * sizeof(unsigned long long);
+            rbytes += feed_words * (lcs ? kWave : 1) * sizeof(unsigned long long);
         }
         if ((rc = pool_get(ctx, zbytes + rbytes, &job.lcs, fs))) return rc;
         for (size_t p = 0; p < P; ++p) {

@@ -119,7 +119,8 @@ static int fetch_lcs_rows(const gx_table* t, size_t row0, size_t rows, std::vect
     out.assign(rows * (m + 1), 0);
     const PairDev& d = t->job.pd[0];
     if (n == 0 || m == 0 || rows == 0) return GX_OK;
-    if (!d.lbits || d.lwords <= 0) return fail(GX_EINVAL, "LCS rows not kept: build the table with GX_TABLE_MATCHES");
+    if (!d.lbits || d.lwords <= 0 || !((d.lcs_waves >> 16) & 1))
+        return fail(GX_EINVAL, "LCS rows not kept: build the table with GX_TABLE_MATCHES");
     const size_t i0 = std::max<size_t>(row0, 1), i1 = std::min(row0 + rows, n + 1);
     if (i1 <= i0) return GX_OK;
     // (the rows' strips: bits[strip][step][lane], gx_lcs.h lcs_word_index)

@@ -1041,17 +1041,8 @@ __global__ void finalize_kernel(const PairDev* __restrict__ pairs, const StripRe
     if (fs != INT_MAX) {
         const StripRes r = sres[P.strip_base + fs];
         mam = r.bl;
-        if (P.lwords > 0 && P.lbits && r.bj > 0) {   // (bj = 0: layout 3 finds the column later, skew_max_col_kernel)
-            int ones = 0;
-            for (int w = lane; w * kLcsBits < r.bj; w += kWave) {   // (64 columns a word, gx_lcs.h)
-                unsigned long long x = P.lbits[lcs_word_index(r.bi, w, P.lwords)];
-                const int rem = r.bj - w * kLcsBits;
-                if (rem < kLcsBits) x &= (1ull << rem) - 1ull;
-                ones += __popcll(x);
-            }
-            for (int off = 32; off > 0; off >>= 1) ones += __shfl_xor(ones, off);
-            mam = r.bj - ones;
-        }
+        if (P.lwords > 0 && P.lbits && r.bj > 0)   // (bj = 0: layout 3 finds the column later, skew_max_col_kernel)
+            mam = lcs_matches(P, r.bi, r.bj, lane);
     }
     if (lane == 0) {
         PairRes& o = pres[p];

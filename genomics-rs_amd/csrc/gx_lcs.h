@@ -123,6 +123,7 @@ __device__ __forceinline__ void lcs_workgroup(const PairDev& P, const int wg, co
     const uint8_t* const c1 = uni_ptr(P.c1);
     const uint8_t* const c2 = uni_ptr(P.c2);
     const int lw = __builtin_amdgcn_readfirstlane(P.lcs_waves) & 0xFF;
+    const bool full = (__builtin_amdgcn_readfirstlane(P.lcs_waves) >> 16) & 1;   // every row, or the strips' last only
     int ns = lw > 0 && lw < nwave ? lw : nwave;
     ns = min(ns, lcs_max_sweep(lds_bytes));
     int* const pub = (int*)lds;                  // [wave] steps of its strips published (q T + t)
@@ -175,7 +176,8 @@ __device__ __forceinline__ void lcs_workgroup(const PairDev& P, const int wg, co
 #endif
         const int qT = q * T;
         const __amdgpu_buffer_rsrc_t brs =
-            rsrc_of(uni_ptr(bits + (size_t)s * T * kWave), __builtin_amdgcn_readfirstlane(T * kWave * 8));
+            full ? rsrc_of(uni_ptr(bits + (size_t)s * T * kWave), __builtin_amdgcn_readfirstlane(T * kWave * 8))
+                 : rsrc_of(uni_ptr(bits + (size_t)s * T), __builtin_amdgcn_readfirstlane(T * 8));
         const gu64* const fin = (const gu64*)(feed + (size_t)(s > 0 ? s - 1 : 0) * T * 2);
         gu64* const fout = (gu64*)(feed + (size_t)s * T * 2);
         uint32_t c = 0, vl = ~0u, vh = ~0u;   // the carry; this lane's word of the previous step
@@ -268,12 +270,15 @@ __device__ __forceinline__ void lcs_workgroup(const PairDev& P, const int wg, co
                 vl = ol[7]; vh = oh[7];
             }
 #ifndef GX_DIAG_LCS_NOSTORE   // (timing only: no bit rows)
-#ifdef GX_DIAG_LCS_CKPT
-            if (lane == kWave - 1)
-#endif
+            if (full) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
-                __builtin_amdgcn_raw_buffer_store_b64(v2i{(int)ol[k], (int)oh[k]}, brs, (int)(lane * 8), (t0 + k) * kWave * 8, 0);
+                for (int k = 0; k < 8; ++k)
+                    __builtin_amdgcn_raw_buffer_store_b64(v2i{(int)ol[k], (int)oh[k]}, brs, (int)(lane * 8), (t0 + k) * kWave * 8, 0);
+            } else if (lane == kWave - 1) {   // (the strip's bottom row: lcs_matches restarts from it)
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    __builtin_amdgcn_raw_buffer_store_b64(v2i{(int)ol[k], (int)oh[k]}, brs, 0, (t0 + k) * 8, 0);
+            }
 #endif
             // lane 63 passes its words of steps t0 .. t0 + 7 down
             if (hbm_out) {
@@ -321,6 +326,83 @@ __device__ __forceinline__ void lcs_workgroup(const PairDev& P, const int wg, co
             group(t0 + 24, mD, fD, mC, fC);
         }
     }
+}
+
+// LM(i, j) = max_matches of cell (i, j) (algo.rs:279 matches_at_max), one
+// wave (all 64 lanes, wave-uniform i, j): from the stored row when the sweep
+// kept every row, otherwise by sweeping strip (i - 1) / 64 again from the
+// bottom row of the strip above (which the sweep keeps: bits[strip][step],
+// word w at step w + 63) up to row i's word (j - 1) / 64 -- a few hundred
+// steps of one wave, against the 64x traffic of keeping every row.
+__device__ __forceinline__ int lcs_matches(const PairDev& P, const int i, const int j, const int lane) {
+    const int wd = __builtin_amdgcn_readfirstlane(P.lwords);
+    if (wd <= 0 || !P.lbits || i < 1 || j < 1) return 0;
+    const unsigned long long* const bits = uni_ptr(P.lbits);
+    const int T = lcs_steps(wd);
+    const int wj = (j + kLcsBits - 1) / kLcsBits;   // words of row i that count
+    int ones = 0;
+    if ((__builtin_amdgcn_readfirstlane(P.lcs_waves) >> 16) & 1) {
+        for (int w = lane; w < wj; w += kWave) {
+            unsigned long long x = bits[lcs_word_index(i, w, wd)];
+            const int rem = j - w * kLcsBits;
+            if (rem < kLcsBits) x &= (1ull << rem) - 1ull;
+            ones += __popcll(x);
+        }
+    } else {
+        const int s = (i - 1) / kWave, li = (i - 1) % kWave;
+        const int ws = wd + 2 * kLcsMaskPad;
+        const int r = s * kWave + lane + 1;
+        const int b = r <= P.n ? (int)P.c1[r - 1] : 0;
+        const uint32_t vb = (uint32_t)(b * ws + kLcsMaskPad - lane) * 8u;
+        const __amdgpu_buffer_rsrc_t mrs = rsrc_of(uni_ptr(P.lmask), __builtin_amdgcn_readfirstlane(256 * ws * 8));
+        typedef int v2i __attribute__((ext_vector_type(2)));
+        const unsigned long long* const above = bits + (size_t)(s > 0 ? s - 1 : 0) * T;
+        const int tend = li + wj;   // steps: lane li finishes word wj - 1 at step tend - 1
+        auto top_at = [&](int t0) -> unsigned long long {   // lane k < 8: the row above's word t0 + k
+            return s > 0 && lane < 8 ? above[min(t0 + lane + 63, T - 1)] : ~0ull;
+        };
+        v2i mn[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) mn[k] = __builtin_amdgcn_raw_buffer_load_b64(mrs, (int)vb, k * 8, 0);
+        unsigned long long tn = top_at(0);
+        uint32_t c = 0, vl = ~0u, vh = ~0u;
+        for (int t0 = 0; t0 < tend; t0 += 8) {
+            uint32_t mlo[8], mhi[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { mlo[k] = (uint32_t)mn[k][0]; mhi[k] = (uint32_t)mn[k][1]; }
+            const unsigned long long tc = tn;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) mn[k] = __builtin_amdgcn_raw_buffer_load_b64(mrs, (int)vb, (t0 + 8 + k) * 8, 0);
+            tn = top_at(t0 + 8);
+            uint32_t ol[8], oh[8];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint32_t a[4], bh[4], ml[4], mh[4], o1[4], o2[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    a[k] = __builtin_amdgcn_readlane((uint32_t)tc, 4 * h + k);
+                    bh[k] = __builtin_amdgcn_readlane((uint32_t)(tc >> 32), 4 * h + k);
+                    ml[k] = mlo[4 * h + k]; mh[k] = mhi[4 * h + k];
+                }
+                lcs_block4(a, bh, ml, mh, o1, o2, vl, vh, c);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) { ol[4 * h + k] = o1[k]; oh[4 * h + k] = o2[k]; }
+                vl = o1[3]; vh = o2[3];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int w = t0 + k - lane;   // this lane's word of step t0 + k
+                if (lane == li && w >= 0 && w < wj) {
+                    unsigned long long x = ((unsigned long long)oh[k] << 32) | ol[k];
+                    const int rem = j - w * kLcsBits;
+                    if (rem < kLcsBits) x &= (1ull << rem) - 1ull;
+                    ones += __popcll(x);
+                }
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) ones += __shfl_xor(ones, off);
+    return j - ones;
 }
 
 }  // namespace gx

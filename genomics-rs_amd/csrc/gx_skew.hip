@@ -740,7 +740,7 @@ __global__ __launch_bounds__((2 * W + 1) * kWave, 1) void fill_skew_kernel(const
         while (p + 1 < npairs && pairs[p + 1].lcs_base <= blk) ++p;
         p = __builtin_amdgcn_readfirstlane(p);
         const PairDev& P = pairs[p];
-        lcs_workgroup(P, blk - P.lcs_base, P.lcs_waves >> 8, wave, 2 * W + 1, lane, (char*)ho, sizeof(ho), band_counter + 1);
+        lcs_workgroup(P, blk - P.lcs_base, (P.lcs_waves >> 8) & 0xFF, wave, 2 * W + 1, lane, (char*)ho, sizeof(ho), band_counter + 1);
         return;
     }
     for (;;) {
@@ -815,18 +815,7 @@ __global__ void skew_mam_kernel(const PairDev* __restrict__ pairs, PairRes* pres
     const int lane = threadIdx.x;
     const int i = r->max_i, j = r->max_j;
     if (i < 1 || i > P.n || j < 1 || j > P.m) return;
-    int mam = 0;
-    if (P.lwords > 0 && P.lbits) {   // LM(i, j) = j - popcount(V_i & (2^j - 1))
-        int ones = 0;
-        for (int w = lane; w * kLcsBits < j; w += kWave) {   // (64 columns a word, gx_lcs.h)
-            unsigned long long x = P.lbits[lcs_word_index(i, w, P.lwords)];
-            const int rem = j - w * kLcsBits;
-            if (rem < kLcsBits) x &= (1ull << rem) - 1ull;
-            ones += __popcll(x);
-        }
-        for (int off = 32; off > 0; off >>= 1) ones += __shfl_xor(ones, off);
-        mam = j - ones;
-    }
+    const int mam = lcs_matches(P, i, j, lane);   // LM(i, j) (gx_lcs.h)
     if (lane == 0) r->mam = mam;
 }
 hipError_t launch_skew_max_col(const PairDev* d_pairs, int npairs, int mmax, PairRes* d_pres, int gshift, hipStream_t st) {

@@ -290,6 +290,60 @@ def test_overlapped_alternating_sets(gx, ctx, monkeypatch, poison):
         _check_result(res[p], st.steps(p), c, (p, "last"))
 
 
+SHORT_PIPELINES = {
+    # 2 x 512 pairs of 1k: the walk on its own stream beside the next passes' fills (fill buffers held
+    # until the walk is collected, gx_api_batch.cpp trace_dev)
+    "1k_walk_stream": (1024, 512, lambda W: W != 7),
+    # 2 x 32 pairs of 4k on the twin fill at 7-wave bands (forced: 32 pairs alone take the scalar
+    # fill), two workgroups a CU as at 1024 x 4k, so the walk stays on the fill's stream
+    "4k_w7_fill_stream": (4096, 32, lambda W: W == 7),
+}
+
+
+@pytest.mark.parametrize("poison", [False, True], ids=["plain", "poison"])
+@pytest.mark.parametrize("shape", sorted(SHORT_PIPELINES))
+def test_short_pipeline_alternating_sets(gx, ctx, monkeypatch, shape, poison):
+    """The three-slot short-batch pipeline (gx_api_batch.cpp, global
+    untracked batches too short for the overlapped two-group launch: three
+    passes in flight, the walk on its own stream when it fits) over two
+    different sets of synthetic pairs that alternate pass by pass
+    (GX_STAGED_ALTERNATE), five passes: every buffer a pass takes from the
+    pool -- planes, records, descriptors, pinned staging -- last held the
+    other set's data, so a walk that ran before its fill finished (no wait on
+    the slot's fdone event), or a fill buffer returned to the pool while its
+    walk still reads it, gives wrong results here (with GX_POOL_POISON the
+    buffers are also filled with garbage on their new user's stream).  Every
+    pass's plane checksums and results, and each set's last alignments,
+    against the oracle digests (tests/golden/synthetic_L{1024,4096}.json)."""
+    L, H, w_ok = SHORT_PIPELINES[shape]
+    if L == 4096:
+        monkeypatch.setenv("GX_TWIN", "1")
+        monkeypatch.setenv("GX_BAND_WAVES", "7")
+    if poison:
+        monkeypatch.setenv("GX_POOL_POISON", "1")
+    cases = _synth(L)[:2 * H]
+    assert len(cases) == 2 * H
+    pairs = [_synth_pair(c["k"], L) for c in cases]
+    steps = 5
+    st = gx.StagedPairs(pairs, ctx=ctx)
+    res, fill_ms = st.run(gx.Scores(*CONFIG_SCORES), False, keep_planes=True, steps=steps, plane_sums=True,
+                          alternate=True)
+    info = ctx.fill_info()
+    assert info.get("groups", 1) == 1 and w_ok(info["band_waves"]), info
+    assert fill_ms > 0
+    sums = st.plane_sums()
+    passes = st.pass_results()
+    assert sums.shape == (steps, len(pairs), 3) and len(passes) == steps
+    for k in range(steps):
+        for q in range(H):
+            p = (k % 2) * H + q
+            c = cases[p]
+            assert [int(x) for x in sums[k, p]] == [int(x) for x in c["plane_sums"]], (shape, p, "pass", k)
+            _check_result(passes[k][p], None, c, (shape, p, "pass", k))
+    for p, c in enumerate(cases):   # each set's last pass
+        _check_result(res[p], st.steps(p), c, (shape, p, "last"))
+
+
 def test_alternating_sets_rejects_shapes(gx, ctx):
     """GX_STAGED_ALTERNATE needs pair p and p + P/2 of one shape."""
     st = gx.StagedPairs([(b"ACGT" * 10, b"ACGA" * 10), (b"ACGT" * 11, b"ACGA" * 10)], ctx=ctx)
