@@ -237,6 +237,8 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
     if ((rc = pool_get(ctx, std::max<size_t>(skel_elems, 1) * sizeof(int), &job.skel, fs))) return rc;
     if ((rc = pool_get(ctx, std::max<size_t>(feed_recs, 1) * sizeof(Rec), &job.feed, fs))) return rc;
     if ((rc = pool_get(ctx, std::max(strips, 1) * sizeof(StripRes), &job.sres, fs))) return rc;
+    if (getenv("GX_LCS_ALONE"))   // (diagnostics: no fill writes the strip results, so they must not be pool garbage)
+        HIPCHK(hipMemsetAsync(job.sres.p, 0, std::max(strips, 1) * sizeof(StripRes), fs));
     // one buffer [PairRes x P | band counter + status (64 B) | band progress]:
     // one memset before the launch, one copy of the results and status after
     // it (each small copy or memset on the stream costs a runtime round trip

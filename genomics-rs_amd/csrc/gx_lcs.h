@@ -336,7 +336,9 @@ __device__ __forceinline__ void lcs_workgroup(const PairDev& P, const int wg, co
 // steps of one wave, against the 64x traffic of keeping every row.
 __device__ __forceinline__ int lcs_matches(const PairDev& P, const int i, const int j, const int lane) {
     const int wd = __builtin_amdgcn_readfirstlane(P.lwords);
-    if (wd <= 0 || !P.lbits || i < 1 || j < 1) return 0;
+    // (a cell outside the table -- e.g. strip results a diagnostics launch
+    // never wrote, GX_LCS_ALONE -- reads nothing)
+    if (wd <= 0 || !P.lbits || i < 1 || i > P.n || j < 1 || j > P.m) return 0;
     const unsigned long long* const bits = uni_ptr(P.lbits);
     const int T = lcs_steps(wd);
     const int wj = (j + kLcsBits - 1) / kLcsBits;   // words of row i that count
@@ -361,19 +363,14 @@ __device__ __forceinline__ int lcs_matches(const PairDev& P, const int i, const 
         auto top_at = [&](int t0) -> unsigned long long {   // lane k < 8: the row above's word t0 + k
             return s > 0 && lane < 8 ? above[min(t0 + lane + 63, T - 1)] : ~0ull;
         };
-        v2i mn[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) mn[k] = __builtin_amdgcn_raw_buffer_load_b64(mrs, (int)vb, k * 8, 0);
-        unsigned long long tn = top_at(0);
         uint32_t c = 0, vl = ~0u, vh = ~0u;
-        for (int t0 = 0; t0 < tend; t0 += 8) {
-            uint32_t mlo[8], mhi[8];
+        // (groups of 8 steps; the loads of group t0 + 24 go out before group
+        // t0 runs, into four register sets in rotation, as in lcs_workgroup)
+        auto grp = [&](const int t0, const v2i (&mc)[8], const unsigned long long tc, v2i (&mn)[8],
+                       unsigned long long& tn) __attribute__((always_inline)) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) { mlo[k] = (uint32_t)mn[k][0]; mhi[k] = (uint32_t)mn[k][1]; }
-            const unsigned long long tc = tn;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) mn[k] = __builtin_amdgcn_raw_buffer_load_b64(mrs, (int)vb, (t0 + 8 + k) * 8, 0);
-            tn = top_at(t0 + 8);
+            for (int k = 0; k < 8; ++k) mn[k] = __builtin_amdgcn_raw_buffer_load_b64(mrs, (int)vb, (t0 + 24 + k) * 8, 0);
+            tn = top_at(t0 + 24);
             uint32_t ol[8], oh[8];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -382,7 +379,7 @@ __device__ __forceinline__ int lcs_matches(const PairDev& P, const int i, const 
                 for (int k = 0; k < 4; ++k) {
                     a[k] = __builtin_amdgcn_readlane((uint32_t)tc, 4 * h + k);
                     bh[k] = __builtin_amdgcn_readlane((uint32_t)(tc >> 32), 4 * h + k);
-                    ml[k] = mlo[4 * h + k]; mh[k] = mhi[4 * h + k];
+                    ml[k] = (uint32_t)mc[4 * h + k][0]; mh[k] = (uint32_t)mc[4 * h + k][1];
                 }
                 lcs_block4(a, bh, ml, mh, o1, o2, vl, vh, c);
 #pragma unroll
@@ -399,6 +396,20 @@ __device__ __forceinline__ int lcs_matches(const PairDev& P, const int i, const 
                     ones += __popcll(x);
                 }
             }
+        };
+        v2i mA[8], mB[8], mC[8], mD[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            mA[k] = __builtin_amdgcn_raw_buffer_load_b64(mrs, (int)vb, k * 8, 0);
+            mB[k] = __builtin_amdgcn_raw_buffer_load_b64(mrs, (int)vb, (8 + k) * 8, 0);
+            mC[k] = __builtin_amdgcn_raw_buffer_load_b64(mrs, (int)vb, (16 + k) * 8, 0);
+        }
+        unsigned long long tA = top_at(0), tB = top_at(8), tC = top_at(16), tD = 0;
+        for (int t0 = 0; t0 < tend; t0 += 32) {   // (steps past tend: harmless, nothing counted)
+            grp(t0, mA, tA, mD, tD);
+            grp(t0 + 8, mB, tB, mA, tA);
+            grp(t0 + 16, mC, tC, mB, tB);
+            grp(t0 + 24, mD, tD, mC, tC);
         }
     }
     for (int off = 32; off > 0; off >>= 1) ones += __shfl_xor(ones, off);

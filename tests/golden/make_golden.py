@@ -187,7 +187,7 @@ def related_pair(k: int, length: int):
 # Synthetic batches digested by --synthetic: BASELINE configs[1]'s shape (the
 # bench's own 30k pairs, rank 0's 80 at N = 1) and configs[4] (1024 x 1k, and
 # samples of the 4k / 16k / 64k batches).
-SYNTH_SETS = {30000: 80, 1024: 1024, 4096: 64, 16384: 8, 65536: 1}
+SYNTH_SETS = {30000: 80, 1024: 1024, 4096: 256, 16384: 256, 65536: 1}
 
 
 def _synth_job(job):
