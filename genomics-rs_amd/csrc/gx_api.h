@@ -58,6 +58,7 @@ hipError_t launch_fill_skew(int W, bool local, bool planes, bool tbl, bool trace
                             int total_bands, int* d_counter, StripRes* d_sres, PairRes* d_pres, Scores32 sc, int grid,
                             int lcs_blocks, hipStream_t st);
 int skew_lcs_blocks(int W, int n, int m);
+int skew_lcs_sweep(int W);
 hipError_t launch_skew_max_col(const PairDev* d_pairs, int npairs, int mmax, PairRes* d_pres, int gshift, hipStream_t st);
 bool skew_traced(bool planes, bool trace, bool track);
 hipError_t launch_skew_codes(const PairDev* d_pairs, int npairs, int mmax, Scores32 sc, bool tbl, hipStream_t st);
@@ -324,6 +325,7 @@ struct FillJob {
     DevBuf chars, planes, codes, skel, feed, progress, sres, pres, pairs, counter, ccodes;
     DevBuf lcs;                    // layout-3 tracked fills: LCS masks, hand-offs and bit rows (gx_lcs.h)
     bool lcs_rows = false;         // max_matches lives in PairDev.lbits (not in an LCS plane)
+    size_t ltrace_off = 0, ltrace_bytes = 0;   // (GX_LCS_TRACE diagnostics: the stamps' place in `lcs`)
     bool pairs_borrowed = false;   // pairs is a pipeline slot's cached descriptor block (not pooled)
     bool pres_held = false;        // pres is held by its pipeline slot until fill_collect
     std::vector<PairDev> pd;

@@ -416,7 +416,7 @@ int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
         // fill; the fill results (with a tracked fill's max cell and
         // matches_at_max, which do not move the start) are collected on the
         // host only for the labelling (no host round trip between fill and
-        // traceback; tracked Covid 5.10 -> 4.83 ms a step at 4.71 ms fill)
+        // traceback; tracked Covid 5.10 -> 4.89 ms a step at a 4.74 ms fill)
         for (size_t q = 0; q < idx.size(); ++q) starts[q] = TbStart{dph[q].n >= 1 && dph[q].m >= 1 ? (int)dph[q].n : 0,
                                                                      (int)dph[q].m, 0};
         // the walk stays on the fill's stream: the fill's buffers return to

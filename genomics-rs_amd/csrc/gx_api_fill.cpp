@@ -324,7 +324,7 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
             d.lwords = ceil_div(d.m, kLcsBits);
             // sweeping workgroups (GX_LCS_WAVES, GX_LCS_WGS override: diagnostics)
             const int nwg = getenv("GX_LCS_WGS") ? std::max(1, atoi(getenv("GX_LCS_WGS"))) : skew_lcs_blocks(W, d.n, d.m);
-            d.lcs_waves = (getenv("GX_LCS_WAVES") ? atoi(getenv("GX_LCS_WAVES")) : 0) | (nwg << 8) |   // (0: all that fit)
+            d.lcs_waves = (getenv("GX_LCS_WAVES") ? atoi(getenv("GX_LCS_WAVES")) : skew_lcs_sweep(W)) | (nwg << 8) |
                           (lcs ? 1 << 16 : 0);   // every row (the matches planes of a table) or the strips' last
             d.lcs_base = lcs_blocks;
             lcs_blocks += nwg;
@@ -333,13 +333,24 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
             ro[p] = rbytes;
             rbytes += feed_words * (lcs ? kWave : 1) * sizeof(unsigned long long);
         }
-        if ((rc = pool_get(ctx, zbytes + rbytes, &job.lcs, fs))) return rc;
+        // (GX_LCS_TRACE=file, diagnostics: each strip's s_memrealtime stamps, after the zeroed region)
+        const char* ltrace_file = getenv("GX_LCS_TRACE");
+        size_t tbytes = 0;
+        if (ltrace_file && *ltrace_file)
+            for (size_t p = 0; p < P; ++p) tbytes += (size_t)ceil_div(job.pd[p].n, kWave) * 4 * sizeof(unsigned long long);
+        if ((rc = pool_get(ctx, zbytes + rbytes + tbytes, &job.lcs, fs))) return rc;
+        size_t to = 0;
         for (size_t p = 0; p < P; ++p) {
             PairDev& d = job.pd[p];
             d.lmask = (unsigned long long*)((char*)job.lcs.p + zo[p]);
             d.llink = d.lmask + 256 * ((size_t)d.lwords + 2 * kLcsMaskPad);
             d.lbits = (unsigned long long*)((char*)job.lcs.p + zbytes + ro[p]);
+            d.ltrace = tbytes ? (unsigned long long*)((char*)job.lcs.p + zbytes + rbytes + to) : nullptr;
+            if (tbytes) to += (size_t)ceil_div(d.n, kWave) * 4 * sizeof(unsigned long long);
         }
+        if (tbytes) HIPCHK(hipMemsetAsync((char*)job.lcs.p + zbytes + rbytes, 0, tbytes, fs));
+        job.ltrace_off = zbytes + rbytes;
+        job.ltrace_bytes = tbytes;
         HIPCHK(hipMemsetAsync(job.lcs.p, 0, zbytes, fs));
     }
     const char* trace_file = slot < 0 ? getenv("GX_TRACE_FILE") : nullptr;
@@ -444,6 +455,18 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
         for (size_t p = 0; p < P; ++p) mmax = std::max(mmax, job.pd[p].m);
         HIPCHK(launch_skew_max_col((const PairDev*)job.pairs.p, (int)P, mmax, (PairRes*)job.pres.p,
                                    is_local ? 0 : sc.g, fs));
+    }
+    if (job.ltrace_bytes) {   // (GX_LCS_TRACE: pair, strip, start / first group / end stamps (100 MHz), workgroup * 64 + wave)
+        std::vector<unsigned long long> h(job.ltrace_bytes / sizeof(unsigned long long));
+        HIPCHK(hipStreamSynchronize(fs));
+        HIPCHK(hipMemcpy(h.data(), (char*)job.lcs.p + job.ltrace_off, job.ltrace_bytes, hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(getenv("GX_LCS_TRACE"), "a")) {
+            size_t o = 0;
+            for (size_t p = 0; p < P; ++p)
+                for (int s = 0; s < ceil_div(job.pd[p].n, kWave); ++s, o += 4)
+                    fprintf(f, "%zu,%d,%llu,%llu,%llu,%llu\n", p, s, h[o], h[o + 1], h[o + 2], h[o + 3]);
+            fclose(f);
+        }
     }
     // the local twin fill tracks each row's maximum only: the last column of
     // the chosen row from its plane codes (gx_kernels.hip local_col_kernel)

@@ -157,14 +157,15 @@ struct __attribute__((aligned(16))) PairDev {   // 16-B multiple: the pinned sta
                          // before and after (index j - 1 + 64 for column j; gx_skew.hip)
     // layout-3 tracked fills: max_matches as bit-parallel LCS rows (gx_lcs.h),
     // computed beside the fill by the launch's leading workgroups
-    unsigned long long* lbits;   // row i's LCS difference bits V_i (bit k of word w: column 63 w + k + 1),
-                                 // [strip][step][lane] (gx_lcs.h lcs_word_index)
+    unsigned long long* lbits;   // row i's LCS difference bits V_i (bit k of word w: column 64 w + k + 1),
+                                 // [strip][step][lane] (gx_lcs.h lcs_word_index), or each strip's last row
     unsigned long long* lmask;   // [256][lwords + 128] match masks of each byte against s2 (zeroed before the launch)
     unsigned long long* llink;   // [strips][lcs_steps][2] the strips' bottom rows, tagged halves (zeroed before the launch)
+    unsigned long long* ltrace;  // diagnostics (GX_LCS_TRACE): [strip][4] s_memrealtime stamps, or nullptr
     int lwords;                  // words per bit row, ceil(m / kLcsBits); 0 = no LCS rows
-    int lcs_waves;               // sweeping waves per LCS workgroup | (the pair's LCS workgroups << 8)
+    int lcs_waves;               // sweeping waves per LCS workgroup | (workgroups << 8) | (every row << 16)
     int lcs_base;                // the pair's first LCS workgroup (blockIdx.x)
-    int lcs_pad[3];
+    int lcs_pad;
 };
 static_assert(sizeof(PairDev) % 16 == 0, "PairDev staging keeps the PairRes that follow it 16-B aligned");
 

@@ -235,21 +235,25 @@ __device__ __forceinline__ void lcs_workgroup(const PairDev& P, const int wg, co
                 if (have < (unsigned)(qT + need)) {
                     unsigned it = 0;
                     for (;;) {
-                        have = (unsigned)__hip_atomic_load(pub + wave - 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        have = (unsigned)__hip_atomic_load(pub + wave - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         if (have >= (unsigned)(qT + need)) break;
                         if (++it > kSpinLimit) { __hip_atomic_store((gint*)status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
                         if ((it & 4095u) == 4095u && __hip_atomic_load((gint*)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
                         __builtin_amdgcn_s_sleep(1);
                     }
                 }
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);   // (LDS executes a wave's ops in order: the ring after the counter)
                 const int r0 = (qT + t0 + 63) & (kLcsRing - 1);
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     const unsigned long long x = rin[r0 + k];
                     tl[k] = (uint32_t)x; th[k] = (uint32_t)(x >> 32);
                 }
-                // (the reads are done before the counter moves: release)
-                if (lane == 0) __hip_atomic_store(con + wave - 1, qT + need, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                // (the counter moves after the reads, in LDS order; no release
+                // fence -- at workgroup scope it would wait for every load and
+                // store in flight, the mask prefetch included)
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                if (lane == 0) __hip_atomic_store(con + wave - 1, qT + need, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             } else {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) { tl[k] = ~0u; th[k] = ~0u; }
@@ -295,7 +299,7 @@ __device__ __forceinline__ void lcs_workgroup(const PairDev& P, const int wg, co
                 if ((int)conc < G + 8 - kLcsRing) {
                     unsigned it = 0;
                     for (;;) {
-                        conc = (unsigned)__hip_atomic_load(con + wave, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        conc = (unsigned)__hip_atomic_load(con + wave, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         if ((int)conc >= G + 8 - kLcsRing) break;
                         if (++it > kSpinLimit) { __hip_atomic_store((gint*)status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); break; }
                         if ((it & 4095u) == 4095u && __hip_atomic_load((gint*)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
@@ -310,10 +314,15 @@ __device__ __forceinline__ void lcs_workgroup(const PairDev& P, const int wg, co
                         rout[r0 + k] = x;
                         if (r0 == 0) rout[kLcsRing + k] = x;
                     }
-                    __hip_atomic_store(pub + wave, G + 8, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    // (the ring words land before the counter: LDS order, and the
+                    // compiler may not sink them past it)
+                    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                    __hip_atomic_store(pub + wave, G + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
         };
+        unsigned long long* const ltr = P.ltrace;   // (diagnostics: strip start, first group done, end)
+        if (ltr && lane == 0) ltr[(size_t)s * 4] = __builtin_amdgcn_s_memrealtime();
         v2i mA[8], mB[8], mC[8], mD[8];
         unsigned long long fA = 0, fB = 0, fC = 0, fD = 0;
 #pragma unroll
@@ -321,9 +330,14 @@ __device__ __forceinline__ void lcs_workgroup(const PairDev& P, const int wg, co
         if (hbm_in) { fA = feed_at(0); fB = feed_at(8); fC = feed_at(16); }
         for (int t0 = 0; t0 < T; t0 += 32) {   // (T: a multiple of 32)
             group(t0, mA, fA, mD, fD);
+            if (ltr && t0 == 0 && lane == 0) ltr[(size_t)s * 4 + 1] = __builtin_amdgcn_s_memrealtime();
             group(t0 + 8, mB, fB, mA, fA);
             group(t0 + 16, mC, fC, mB, fB);
             group(t0 + 24, mD, fD, mC, fC);
+        }
+        if (ltr && lane == 0) {
+            ltr[(size_t)s * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+            ltr[(size_t)s * 4 + 3] = (unsigned long long)(wg * 64 + wave);
         }
     }
 }

@@ -877,12 +877,16 @@ static hipError_t launch_skew_w(int W, const PairDev* d_pairs, int npairs, int t
     return hipErrorInvalidValue;
 }
 
-// LCS workgroups of a tracked launch (gx_lcs.h): sweeping waves a workgroup
-// (all of them, as many as the LDS of the fill's core -> side rings holds
-// rings for), and enough workgroups that about T / 64 + 1 strips are swept
-// at once -- a strip starts ~71 steps after the one above, so that many
-// keep up with the dependence chain -- and no more than the strips.
-int skew_lcs_sweep(int W) { return std::min(2 * W + 1, lcs_max_sweep((size_t)W * sizeof(SkHo))); }
+// LCS workgroups of a tracked launch (gx_lcs.h): four sweeping waves a
+// workgroup, one a SIMD (at five, two share a SIMD and every strip's pace
+// drops: Covid's sweep alone 4.56 ms with 5 x 2 workgroups, 3.92 with 4 x 3,
+// 3.77 with 2 x 5 -- but then more strips cross workgroups through HBM --
+// tools/lcs_trace.py, gpurun_out/r06t_waves.log), within what the LDS of the
+// fill's core -> side rings holds rings for; and enough workgroups that
+// about T / 64 + 1 strips are swept at once -- a strip starts ~80 steps after
+// the one above, so that many keep up with the dependence chain -- and no
+// more than the strips.
+int skew_lcs_sweep(int W) { return std::min(std::min(4, 2 * W + 1), lcs_max_sweep((size_t)W * sizeof(SkHo))); }
 int skew_lcs_blocks(int W, int n, int m) {
     const int T = lcs_steps(ceil_div(m, kLcsBits)), S = ceil_div(n, kWave);
     const int waves = std::min(S, ceil_div(T, 64) + 1);
