@@ -458,6 +458,26 @@ std::vector<std::pair<size_t, size_t>> plan_chunks(gx_context* ctx, const std::v
                 ph.size(), plane_bpc, budget, fr, tot, ctx->free_list.size(), out.size());
     }
     if (out.size() > 1) {
+        // the same number of chunks, pairs dealt out evenly two at a time (a
+        // twin each): 1024 x 64k was 51 chunks of 20 and one of 4, whose lone
+        // twins ran 4-wave bands; now 44 of 20 and 8 of 18 -- kept if every
+        // chunk fits the budget
+        {
+            const size_t K = out.size(), P = ph.size(), twins = (P + 1) / 2;
+            std::vector<std::pair<size_t, size_t>> even;
+            size_t a = 0;
+            bool fits = twins >= K;
+            for (size_t c = 0; c < K && fits; ++c) {
+                const size_t b = std::min(P, a + 2 * (twins / K + (c < twins % K ? 1 : 0)));
+                double bytes = 0;
+                for (size_t p = a; p < b; ++p)
+                    bytes += (ph[p].n && ph[p].m) ? pair_device_bytes(ph[p].n, ph[p].m, plane_bpc) : 0.0;
+                fits = b > a && bytes <= budget;
+                even.emplace_back(a, b);
+                a = b;
+            }
+            if (fits && a == P) return even;
+        }
         double total = 0;
         for (size_t p = 0; p < ph.size(); ++p)
             total += (ph[p].n && ph[p].m) ? pair_device_bytes(ph[p].n, ph[p].m, plane_bpc) : 0.0;
