@@ -52,6 +52,16 @@ typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pmaxu(uint32_t a, uint32_t b) {
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(us2, a), __builtin_bit_cast(us2, b)));
 }
+// The same as an opaque v_pk_max_u16, for running maxima: LLVM reassociates
+// a chain of umax across the unrolled sub-block and holds every step's
+// operand until a tree at its end (the local row maximum, 4 groups x 2 rows:
+// 149 VGPRs against 123 this way -- and 3.5 % faster, so the local fill keeps
+// the reassociable form; GX_PK_LB_OPAQUE builds this one)
+__device__ __forceinline__ uint32_t pmaxu_acc(uint32_t a, uint32_t b) {
+    uint32_t d;
+    asm("v_pk_max_u16 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
 __device__ __forceinline__ uint32_t padd(uint32_t a, uint32_t b) { return as_u(as_s2(a) + as_s2(b)); }
 __device__ __forceinline__ uint32_t padds(uint32_t a, uint32_t b) { return padd(a, b); }
 __device__ __forceinline__ uint32_t psub(uint32_t a, uint32_t b) { return as_u(as_s2(a) - as_s2(b)); }
@@ -234,8 +244,13 @@ __device__ __forceinline__ void cell_pk(RowPk& st, const uint32_t dd_in, const u
     const uint32_t cDn = CODES ? pcode(st.cD, m2) : 0u;   // them from the plane codes, tb_w16_codes_kernel)
     const uint32_t SMpn = (TBL && !LOCAL) ? SMn : padds(SMn, k.smp);   // TBL: no offset (the tables hold s''; local: - K)
     oI = In; oD = Dn; oS = Sn; oIold = Ig;
-    if (LOCAL)      // the row's largest score_max (its last column: local_col_kernel, from the plane codes)
+    if (LOCAL) {    // the row's largest score_max (its last column: local_col_kernel, from the plane codes)
+#ifndef GX_PK_LB_OPAQUE
         st.lb = pmaxu(st.lb, MASKED ? bfi(act, SMn, k.Z) : SMn);
+#else   // (123 VGPRs instead of 149, but 3.5 % slower at 8-wave bands: DESIGN.md 10, item 3)
+        st.lb = pmaxu_acc(st.lb, MASKED ? bfi(act, SMn, k.Z) : SMn);
+#endif
+    }
     if (MASKED) {   // act: 0xFFFF in each half whose pair has this column
         st.I = bfi(act, In, st.I); st.Hx = bfi(act, Hxn, st.Hx); st.Dd = bfi(act, Ddn, st.Dd);
         st.SMp = bfi(act, SMpn, st.SMp);
@@ -861,6 +876,7 @@ static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int npa
 #define GX_PK(PL) hipLaunchKernelGGL((fill_pk_kernel<W0, PL>), dim3(grid), dim3((W0 + 1) * kWave), 0, st, d_pairs, \
                                      npairs, ntwins, total_bands, d_counter, d_pres, d_sres, sc)
         switch (planes) {
+#ifndef GX_PK_ONLY_LOCAL   // (register-allocation experiments: the local instantiation alone compiles in seconds)
             case 0: GX_PK(0); break;
             case 1: GX_PK(1); break;
             case 2: GX_PK(2); break;
@@ -871,6 +887,7 @@ static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int npa
             case 26: GX_PK(26); break;   // twin codes, no code words, no skeleton (tb_seq_kernel)
             case 30: GX_PK(30); break;
             case 58: GX_PK(58); break;   // local (Smith-Waterman): twin codes, no code words, no skeleton
+#endif
             case 62: GX_PK(62); break;
             default: return hipErrorInvalidValue;
         }
@@ -890,8 +907,12 @@ static hipError_t launch_pk_w(int W, int planes, const PairDev* d_pairs, int npa
 // pair into d_sres (finalize_kernel reduces them).
 hipError_t launch_fill_pk(int W, int planes, const PairDev* d_pairs, int npairs, int ntwins, int total_bands,
                           int* d_counter, PairRes* d_pres, StripRes* d_sres, Scores32 sc, int grid, hipStream_t st) {
+#ifndef GX_PK_ONLY_LOCAL
     return launch_pk_w<3, 4, 7, 8, 15>(W, planes, d_pairs, npairs, ntwins, total_bands, d_counter, d_pres, d_sres, sc,
                                        grid, st);
+#else
+    return launch_pk_w<7>(W, planes, d_pairs, npairs, ntwins, total_bands, d_counter, d_pres, d_sres, sc, grid, st);
+#endif
 }
 
 }  // namespace gx

@@ -154,6 +154,43 @@ def test_skew_lcs_rows(gx, ctx, oracle, monkeypatch, n, m):
         table.free()
 
 
+LCS_SWEEPS = [("1", "1"), ("1", "3"), ("2", "2"), ("3", "2"), ("4", "1"), ("4", "3")]
+
+
+@pytest.mark.parametrize("waves,wgs", LCS_SWEEPS, ids=[f"w{w}g{g}" for w, g in LCS_SWEEPS])
+def test_skew_lcs_strip_handoffs(gx, ctx, oracle, monkeypatch, waves, wgs):
+    """The LCS sweep's strip-to-strip hand-offs (gx_lcs.h) on pairs of 5-24
+    strips, with the sweeping waves a workgroup and the workgroups forced
+    (GX_LCS_WAVES / GX_LCS_WGS): one wave a workgroup sends every bottom row
+    through HBM, several waves hand off through the LDS ring and reuse it
+    block after block (counters across blocks), several workgroups pass
+    blocks between them.  Every row with GX_TABLE_MATCHES (each row kept) and
+    matches_at_max without it (only the strips' last rows kept; the max
+    cell's strip re-swept by lcs_matches), against the oracle."""
+    monkeypatch.setenv("GX_LAYOUT", "3")
+    monkeypatch.setenv("GX_LCS_WAVES", waves)
+    monkeypatch.setenv("GX_LCS_WGS", wgs)
+    rng = random.Random(int(waves) * 10 + int(wgs))
+    for n, m, alpha, rev in ((300, 1000, b"ACGT", False), (700, 200, b"AC", True), (1500, 5000, b"ACGT", False)):
+        a = bytes(rng.choice(alpha) for _ in range(n))
+        b = bytes(rng.choice(alpha) for _ in range(m))
+        cont = gx.SequenceContainer([gx.Sequence("a", a.decode()), gx.Sequence("b", b.decode())])
+        o = oracle.align(a, b, CONFIG_SCORES, rev=rev)
+        tag = (n, m, rev, waves, wgs)
+        table, mam = gx.alignment_table(cont, gx.Scores(*CONFIG_SCORES), False, rev, ctx=ctx, max_cell=True,
+                                        flags=gx.GX_TABLE_MATCHES)
+        assert ctx.fill_info()["layout"] == 3, ctx.fill_info()
+        assert mam == o.matches_at_max and table.info()["max_cell"] == o.max_cell, tag
+        L = oracle.lcs_rows(a, b, range(n + 1), rev=rev)
+        got = table.rows(3, 0, n + 1)
+        for i in range(n + 1):
+            assert np.array_equal(got[i], L[i]), (tag, i)
+        table.free()
+        table, mam = gx.alignment_table(cont, gx.Scores(*CONFIG_SCORES), False, rev, ctx=ctx, max_cell=True)
+        assert mam == o.matches_at_max and table.info()["max_cell"] == o.max_cell, (tag, "last rows only")
+        table.free()
+
+
 @pytest.mark.parametrize("scores,layout", [((1, -2, -1, -5), 3), ((2, -3, -2, -4), 3), ((5, -4, 0, -10), 3),
                                            ((1, -1, -1, 0), 3), ((3, 1, -1, -2), 3), ((1, -2, 1, -3), 3),
                                            ((2, -1, -1, 3), 1), ((1, -1, 0, 2), 1)])
