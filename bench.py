@@ -672,7 +672,7 @@ def simulate_world(args, gx, ctx):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs-per-gpu", type=int,
                     default=int(os.environ["GX_BENCH_PAIRS"]) if "GX_BENCH_PAIRS" in os.environ else None,
