@@ -4,7 +4,8 @@
 // rotation), K2 + one lane-63 store a step, K3 + a full-wave store a step,
 // K4 = K2 with each lane's mask row one of four (as for DNA: scattered
 // loads), K5 = K4 + the producer's LDS ring writes and counter each group;
-// K6 = K4 with five waves in the workgroup (one SIMD holds two).  Reports
+// K6 = K4 with five waves in the workgroup (one SIMD holds two); K7 = K4,
+// K8 = K2 and K9 = K0 with four waves (one a SIMD).  Reports
 // cycles (s_memtime) and ns (s_memrealtime, 100 MHz) per step.
 //   hipcc --offload-arch=gfx950 -O3 -I genomics-rs_amd/csrc -o var/lcs_step_probe tools/lcs_step_probe.hip
 #include <hip/hip_runtime.h>
@@ -25,10 +26,10 @@ __global__ void probe(unsigned long long* masks, unsigned long long* out, long l
     for (int k = 0; k < 8; ++k) {
         mA[k] = v2i{(int)(0x12345 * (lane + k)), k}; mB[k] = mA[k] ^ 5; mC[k] = mA[k] ^ 9; mD[k] = mA[k] ^ 3;
     }
-    const uint32_t vb = (uint32_t)((K >= 4 ? (lane & 3) * 640 : 0) + 64 - lane) * 8u;
+    const uint32_t vb = (uint32_t)(((K >= 4 && K != 8 && K != 9) ? (lane & 3) * 640 : 0) + 64 - lane) * 8u;
     const int wv = threadIdx.x >> 6;
     auto grp = [&](int t0, const v2i (&mc)[8], v2i (&mn)[8]) __attribute__((always_inline)) {
-        if (K >= 1) {
+        if (K >= 1 && K != 9) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) mn[k] = __builtin_amdgcn_raw_buffer_load_b64(mrs, (int)vb, ((t0 + 24 + k) & 1023) * 8, 0);
         }
@@ -49,7 +50,7 @@ __global__ void probe(unsigned long long* masks, unsigned long long* out, long l
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
             __hip_atomic_store(pubc + wv, t0 + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        if (K >= 2 && K != 3 && lane == 63) {
+        if (K >= 2 && K != 3 && K != 9 && lane == 63) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) __builtin_amdgcn_raw_buffer_store_b64(v2i{(int)ol[k], (int)oh[k]}, ors, 0, ((t0 + k) & 65535) * 8, 0);
         }
@@ -77,7 +78,7 @@ int main() {
     const int groups = 4096;
     long long h[2] = {0, 0};
     printf("{");
-    for (int k = 0; k <= 6; ++k) {
+    for (int k = 0; k <= 9; ++k) {
         for (int rep = 0; rep < 2; ++rep) {
             if (k == 0) hipLaunchKernelGGL(probe<0>, dim3(1), dim3(64), 0, 0, m, o, c, groups);
             if (k == 1) hipLaunchKernelGGL(probe<1>, dim3(1), dim3(64), 0, 0, m, o, c, groups);
@@ -86,6 +87,9 @@ int main() {
             if (k == 4) hipLaunchKernelGGL(probe<4>, dim3(1), dim3(64), 0, 0, m, o, c, groups);
             if (k == 5) hipLaunchKernelGGL(probe<5>, dim3(1), dim3(64), 0, 0, m, o, c, groups);
             if (k == 6) hipLaunchKernelGGL(probe<6>, dim3(1), dim3(320), 0, 0, m, o, c, groups);
+            if (k == 7) hipLaunchKernelGGL(probe<7>, dim3(1), dim3(256), 0, 0, m, o, c, groups);
+            if (k == 8) hipLaunchKernelGGL(probe<8>, dim3(1), dim3(256), 0, 0, m, o, c, groups);
+            if (k == 9) hipLaunchKernelGGL(probe<9>, dim3(1), dim3(256), 0, 0, m, o, c, groups);
             hipDeviceSynchronize();
         }
         hipMemcpy(h, c, 16, hipMemcpyDeviceToHost);
