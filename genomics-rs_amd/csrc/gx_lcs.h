@@ -186,6 +186,21 @@ __device__ __forceinline__ void lcs_workgroup(const PairDev& P, const int wg, co
 #else
         auto mask_at = [&](int t) -> v2i { return v2i{(int)vb ^ t, t}; };
 #endif
+        // a group's 8 mask words of this lane (consecutive words of its row)
+        auto mask_group = [&](int t, v2i (&m)[8]) {
+#if defined(GX_LCS_B128) && !defined(GX_DIAG_LCS_NOMASK)   // (as four 16-B loads a lane)
+            typedef int v4i __attribute__((ext_vector_type(4)));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const v4i x = __builtin_amdgcn_raw_buffer_load_b128(mrs, (int)vb, (t + 2 * k) * 8, 0);
+                m[2 * k] = v2i{x[0], x[1]};
+                m[2 * k + 1] = v2i{x[2], x[3]};
+            }
+#else
+#pragma unroll
+            for (int k = 0; k < 8; ++k) m[k] = mask_at(t + k);
+#endif
+        };
         // the feed words of the strip above's steps t0 + 63 .. t0 + 70 (clamped
         // to its last step): lane k < 16 loads half k & 1 of step t0 + 63 + k / 2
         auto feed_at = [&](int t0) -> unsigned long long {
@@ -202,8 +217,7 @@ __device__ __forceinline__ void lcs_workgroup(const PairDev& P, const int wg, co
         // on its load).
         auto group = [&](const int t0, v2i (&mc)[8], const unsigned long long fc, v2i (&mn)[8],
                          unsigned long long& fn) __attribute__((always_inline)) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) mn[k] = mask_at(t0 + 24 + k);
+            mask_group(t0 + 24, mn);
             if (hbm_in) fn = feed_at(t0 + 24);
             // lane 0's words of the row above (words t0 .. t0 + 7: the strip
             // above's steps t0 + 63 .. t0 + 70), or row 0 (all ones)
@@ -325,8 +339,7 @@ __device__ __forceinline__ void lcs_workgroup(const PairDev& P, const int wg, co
         if (ltr && lane == 0) ltr[(size_t)s * 4] = __builtin_amdgcn_s_memrealtime();
         v2i mA[8], mB[8], mC[8], mD[8];
         unsigned long long fA = 0, fB = 0, fC = 0, fD = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) { mA[k] = mask_at(k); mB[k] = mask_at(8 + k); mC[k] = mask_at(16 + k); }
+        mask_group(0, mA); mask_group(8, mB); mask_group(16, mC);
         if (hbm_in) { fA = feed_at(0); fB = feed_at(8); fC = feed_at(16); }
         for (int t0 = 0; t0 < T; t0 += 32) {   // (T: a multiple of 32)
             group(t0, mA, fA, mD, fD);
