@@ -186,9 +186,13 @@ __device__ __forceinline__ void lcs_workgroup(const PairDev& P, const int wg, co
 #else
         auto mask_at = [&](int t) -> v2i { return v2i{(int)vb ^ t, t}; };
 #endif
-        // a group's 8 mask words of this lane (consecutive words of its row)
+        // a group's 8 mask words of this lane -- consecutive words of its row,
+        // as four 16-B loads (against eight 8-B ones: the sweep's pace 101 ->
+        // 87.5 ns a step, Covid's sweep alone 3.93 -> 3.43 ms; the per-lane
+        // loads gather from up to four rows at once and are what bounds it,
+        // tools/lcs_step_probe.hip)
         auto mask_group = [&](int t, v2i (&m)[8]) {
-#if defined(GX_LCS_B128) && !defined(GX_DIAG_LCS_NOMASK)   // (as four 16-B loads a lane)
+#ifndef GX_DIAG_LCS_NOMASK
             typedef int v4i __attribute__((ext_vector_type(4)));
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
