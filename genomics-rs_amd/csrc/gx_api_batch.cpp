@@ -463,7 +463,11 @@ int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
         auto trace_dev = [&](int s) {
             if (wstream) {   // the walk on its own stream; the fill's buffers held until it is collected
 #ifndef GX_MUT_NO_FDONE_WAIT   // (mutation build only: tests/test_gpu_atsize.py must catch its absence)
-                if (hipStreamWaitEvent(ctx->tstream, ctx->slots[s].fdone, 0) != hipSuccess) return fail(GX_EHIP, "walk stream wait");
+                // (on the fill kernel's own end event: the walk needs its planes
+                // and end cell only, not the reductions queued after it -- a
+                // tracked fill's max column and matches_at_max -- nor the
+                // checksums of a staged parity pass)
+                if (hipStreamWaitEvent(ctx->tstream, ctx->slots[s].fe, 0) != hipSuccess) return fail(GX_EHIP, "walk stream wait");
 #endif
                 jheld[s] = true;
                 const int r = run_traceback(ctx, std::vector<const FillJob*>{&jobs[s]}, starts, ctx->slots[s].out, s, false,
