@@ -255,6 +255,12 @@ struct gx_context {
     hipStream_t cstream = nullptr;   // pipelined path: traceback record copies (D2H) off the fill stream
     hipStream_t stream2 = nullptr;   // overlapped batches (batch_core_overlap): the second group's fills
     hipStream_t tstream = nullptr;   // ... and the walks
+    // the three-slot pipeline with the walk on its own stream (which holds a
+    // pass's buffers until it is collected): a fill's reductions -- strip
+    // results, a tracked fill's max column and matches_at_max, a parity
+    // pass's checksums -- run on pstream beside the next pass's fill
+    hipStream_t pstream = nullptr;
+    bool post_aside = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
     std::mutex mu;
     std::vector<DevBuf> free_list;

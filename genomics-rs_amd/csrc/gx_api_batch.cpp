@@ -500,7 +500,12 @@ int batch_core_steps(gx_context* ctx, const std::vector<PairHost>& ph,
             auto t = clk::now();
             while (!rc && queued < std::min(nsteps, k + 3)) {
                 const int q = queued++;
-                if ((rc = fill_at(q % 3, q & 1))) break;
+                // (a pass's reductions beside the next fill only once the walk's
+                // stream is settled: it holds the pass's buffers until collected)
+                ctx->post_aside = wstream && q > 0;
+                rc = fill_at(q % 3, q & 1);
+                ctx->post_aside = false;
+                if (rc) break;
                 // two fill workgroups a CU (7-wave bands, run_fill) leave the
                 // walks no room beside the fill: the walk stays on its stream
                 if (q == 0 && ctx->last_W == 7) wstream = false;

@@ -155,6 +155,7 @@ extern "C" int gx_context_create(int device, gx_context** out) {
     HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->tstream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->pstream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
     HIPCHK(hipEventCreate(&c->ev2));
@@ -215,6 +216,7 @@ extern "C" void gx_context_destroy(gx_context* ctx) {
     if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
     if (ctx->stream2) (void)hipStreamDestroy(ctx->stream2);
     if (ctx->tstream) (void)hipStreamDestroy(ctx->tstream);
+    if (ctx->pstream) (void)hipStreamDestroy(ctx->pstream);
     delete ctx;
 }
 

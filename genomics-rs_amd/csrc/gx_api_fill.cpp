@@ -439,26 +439,34 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
         HIPCHK(launch_fill(W, lay, is_local != 0, planes ? (d8 ? 2 : 1) : 0, track, lcs, tbl, (const PairDev*)job.pairs.p, (int)P, bands,
                            counter, (StripRes*)job.sres.p, (PairRes*)job.pres.p, scl, grid, fs));
     HIPCHK(hipEventRecord(eve, fs));   // evb..eve brackets the fill kernel alone
+    // the reductions after the fill: on the fill stream, or (pipelined, the
+    // walk on its own stream, gx_context.post_aside) on pstream beside the
+    // next pass's fill, which would otherwise queue behind them (~50 us a
+    // tracked Covid pass)
+    const bool aside = !collect && slot >= 0 && ctx->post_aside && bands > 0 &&
+                       ((ctx->sums_dst && planes) || track || is_local);
+    hipStream_t const ps = aside ? ctx->pstream : fs;
+    if (aside) HIPCHK(hipStreamWaitEvent(ps, eve, 0));
     if (ctx->sums_dst && planes && bands > 0) {   // staged checksum run: this pass's plane sums
-        HIPCHK(enqueue_plane_sums(ctx, job, sc, ctx->sums_dst, fs));
+        HIPCHK(enqueue_plane_sums(ctx, job, sc, ctx->sums_dst, ps));
         ctx->sums_dst += 3 * P;
     }
     // strip results exist only for the tracked and local fills (the untracked
     // global fill writes end_SM / end_E itself): no reduction launch otherwise
     if (bands > 0 && (track || is_local))
         HIPCHK(launch_finalize((const PairDev*)job.pairs.p, (int)P, (const StripRes*)job.sres.p,
-                               (PairRes*)job.pres.p, fs));
+                               (PairRes*)job.pres.p, ps));
     // tracked layout-3 fills with planes track each row's largest value only:
     // the first column holding the maximum from the planes, then matches_at_max
     if (bands > 0 && lay == 3 && track && planes) {
         int mmax = 0;
         for (size_t p = 0; p < P; ++p) mmax = std::max(mmax, job.pd[p].m);
         HIPCHK(launch_skew_max_col((const PairDev*)job.pairs.p, (int)P, mmax, (PairRes*)job.pres.p,
-                                   is_local ? 0 : sc.g, fs));
+                                   is_local ? 0 : sc.g, ps));
     }
     if (job.ltrace_bytes) {   // (GX_LCS_TRACE: pair, strip, start / first group / end stamps (100 MHz), workgroup * 64 + wave)
         std::vector<unsigned long long> h(job.ltrace_bytes / sizeof(unsigned long long));
-        HIPCHK(hipStreamSynchronize(fs));
+        HIPCHK(hipStreamSynchronize(ps));
         HIPCHK(hipMemcpy(h.data(), (char*)job.lcs.p + job.ltrace_off, job.ltrace_bytes, hipMemcpyDeviceToHost));
         if (FILE* f = fopen(getenv("GX_LCS_TRACE"), "a")) {
             size_t o = 0;
@@ -471,7 +479,7 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
     // the local twin fill tracks each row's maximum only: the last column of
     // the chosen row from its plane codes (gx_kernels.hip local_col_kernel)
     if (bands > 0 && twin && is_local)
-        HIPCHK(launch_local_col((const PairDev*)job.pairs.p, (int)P, (PairRes*)job.pres.p, sc.h, sc.g, fs));
+        HIPCHK(launch_local_col((const PairDev*)job.pairs.p, (int)P, (PairRes*)job.pres.p, sc.h, sc.g, ps));
     job.res.assign(P, PairRes{});
     int status[2] = {0, 0};
     PairRes* pin_res = (PairRes*)(pin + P * sizeof(PairDev) + ord_bytes);
@@ -485,7 +493,7 @@ int run_fill(gx_context* ctx, const std::vector<std::pair<const uint8_t*, const 
         // on the copy engine after a long transfer, 1024 x 1k); the block
         // stays held by the slot until that copy is collected
         auto& sl = ctx->slots[slot];
-        HIPCHK(hipEventRecord(sl.fdone, fs));
+        HIPCHK(hipEventRecord(sl.fdone, ps));   // (the fill and its reductions)
         HIPCHK(hipStreamWaitEvent(ctx->cstream, sl.fdone, 0));
         HIPCHK(hipMemcpyAsync(pin_res, job.pres.p, res_bytes + sizeof status, hipMemcpyDeviceToHost, ctx->cstream));
         HIPCHK(hipEventRecord(sl.fres, ctx->cstream));
