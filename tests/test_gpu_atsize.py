@@ -294,6 +294,9 @@ SHORT_PIPELINES = {
     # 2 x 512 pairs of 1k: the walk on its own stream beside the next passes' fills (fill buffers held
     # until the walk is collected, gx_api_batch.cpp trace_dev)
     "1k_walk_stream": (1024, 512, lambda W: W != 7),
+    # the same on a 64-workgroup fill grid: most CUs stay free, so a walk that did not wait for its
+    # fill (or read a buffer handed back too early) would run while the fill still writes
+    "1k_walk_stream_grid64": (1024, 512, lambda W: W != 7),
     # 2 x 32 pairs of 4k on the twin fill at 7-wave bands (forced: 32 pairs alone take the scalar
     # fill), two workgroups a CU as at 1024 x 4k, so the walk stays on the fill's stream
     "4k_w7_fill_stream": (4096, 32, lambda W: W == 7),
@@ -316,6 +319,8 @@ def test_short_pipeline_alternating_sets(gx, ctx, monkeypatch, shape, poison):
     pass's plane checksums and results, and each set's last alignments,
     against the oracle digests (tests/golden/synthetic_L{1024,4096}.json)."""
     L, H, w_ok = SHORT_PIPELINES[shape]
+    if shape.endswith("grid64"):
+        monkeypatch.setenv("GX_FILL_GRID", "64")
     if L == 4096:
         monkeypatch.setenv("GX_TWIN", "1")
         monkeypatch.setenv("GX_BAND_WAVES", "7")
